@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""Throughput bench of the MI355X Ed25519 verify engine (BASELINE.json metric).
+
+    python bench.py [--gpus N --steps K --warmup W] [--config c2|c5] [--n PER_GPU]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A "step" = one verify pass over the whole per-GPU batch (inputs resident in HBM), plus — for N > 1 —
+the RCCL all-gather of the verdict bitmaps that feeds the notary commit step.  Weak scaling: every
+rank verifies its own N_PER_GPU signatures.  value = all signatures verified by all ranks / the max
+over ranks of the timed region.
+
+Default workload (N=1): BASELINE config C2 — 1,000,000 single-signer Ed25519 signatures over
+300-byte messages, distinct key per signature, generated on the GPU by the engine's signer.
+
+Extra fields on the JSON line:
+  roofline      VALU-issue roofline of the verify kernel (algorithmic 2.28e5 32x32->64 MACs per
+                verify) against the measured v_mad_i64_i32 peak of this GPU
+  cpu_baseline  oracle/ C restatement of eddsa-0.1.0 verify (rank 0, N=1 only, bounded sample)
+  notary        p50/p99 end-to-end latency of a 4096-signature notary batch (host buffers in and
+                out, 1/16 adversarial), GPU vs the CPU restatement on the same batch
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from corda_amd import native, workload  # noqa: E402
+
+W_MAC_PER_VERIFY = 2.28e5       # algorithmic 32x32->64 MACs per verify (32-byte msg)
+MSG_BYTES = {"c2": 300, "c5": 32}
+CONFIG_NAME = {
+    "c2": "C2: 1M single-signer Ed25519 txs, 300-byte msg, distinct keys, SoA batch",
+    "c5": "C5 shard: 8M single-signer sigs per GPU over 32-byte tx ids",
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(batch, rank_device: int, seconds: float):
+    """Times the C restatement (oracle/, test infrastructure) on a bounded sample of the same batch."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import cv_oracle  # noqa: E402
+
+    threads = int(os.environ.get("CV_CPU_THREADS", "16"))
+    # 1-thread probe sizes the sample so the multi-thread leg runs ~`seconds`
+    n1 = 1024
+    pk, sig, arena, off, ln = batch.to_host(0, n1)
+    t = time.perf_counter()
+    v1, _ = cv_oracle.verify_batch(pk, sig, arena, off, ln, 1)
+    rate1 = n1 / (time.perf_counter() - t)
+    ns = int(min(batch.n, max(4096, rate1 * threads * seconds)))
+    pk, sig, arena, off, ln = batch.to_host(0, ns)
+    t = time.perf_counter()
+    vm, _ = cv_oracle.verify_batch(pk, sig, arena, off, ln, threads)
+    ratem = ns / (time.perf_counter() - t)
+    return {"value": ratem, "unit": "verifies/s", "cores": threads, "kind": "port",
+            "single_thread_value": rate1,
+            "sample": f"first {ns} signatures of the same batch ({batch.msg_len}-byte msgs) on {threads} host "
+                      f"threads; single-thread rate from the first {n1}",
+            "accepted_fraction": float(vm.mean())}
+
+
+def notary_latency(eng, device: int, reps: int, cpu: bool):
+    """C4 at 4096: host-buffer verify (H2D + kernel + D2H) + per-tx AND, p50/p99 over reps."""
+    b = workload.make_batch(eng, device, 4096, 32, seed=4096)
+    expect = workload.corrupt_fraction(b, 16).cpu().numpy()
+    pk, sig, arena, off, ln = b.to_host()
+    tx_begin = np.arange(0, 4097, 8, dtype=np.uint32)            # 8 signers per tx (512 txs)
+    lat = []
+    for r in range(reps + 5):
+        t = time.perf_counter()
+        bitmap, _ = eng.verify_batch(pk, sig, arena, off, ln, want_status=False)
+        txok = native.tx_verdicts(bitmap, tx_begin)
+        dt = time.perf_counter() - t
+        if r >= 5:
+            lat.append(dt)
+    got = native.bitmap_to_bools(bitmap, 4096)
+    assert np.array_equal(got, expect), "notary batch verdicts wrong"
+    out = {"batch": 4096, "p50_ms": float(np.percentile(lat, 50) * 1e3), "p99_ms": float(np.percentile(lat, 99) * 1e3),
+           "reps": reps, "txs": 512, "tx_ok": int(txok.sum())}
+    if cpu:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import cv_oracle  # noqa: E402
+        threads = int(os.environ.get("CV_CPU_THREADS", "16"))
+        cl = []
+        for r in range(3):
+            t = time.perf_counter()
+            v, _ = cv_oracle.verify_batch(pk, sig, arena, off, ln, threads)
+            cl.append(time.perf_counter() - t)
+        assert np.array_equal(v.astype(bool), expect)
+        out["cpu_p50_ms"] = float(np.median(cl) * 1e3)
+        out["cpu_threads"] = threads
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c2", choices=sorted(MSG_BYTES))
+    ap.add_argument("--n", type=int, default=0, help="signatures per GPU (default 1M for c2, 8M for c5)")
+    ap.add_argument("--key-pool", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-notary", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    n = args.n or (1_000_000 if args.config == "c2" else 8_000_000)
+    msg_len = MSG_BYTES[args.config]
+
+    eng = native.Engine(1 << local)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    t0 = time.perf_counter()
+    batch = workload.make_batch(eng, local, n, msg_len, seed=20261015 + 7919 * rank,
+                                key_pool=args.key_pool or None, stream=sh)
+    log(f"[rank {rank}] generated {n} signatures on GPU in {time.perf_counter() - t0:.2f}s")
+    words = (n + 63) // 64
+    bitmap = torch.zeros(words, dtype=torch.int64, device=dev)
+    gathered = torch.zeros(words * world, dtype=torch.int64, device=dev) if world > 1 else None
+
+    def step():
+        eng.verify_device(local, n, batch.pk.data_ptr(), batch.sig.data_ptr(), batch.arena.data_ptr(),
+                          batch.off.data_ptr(), batch.len.data_ptr(), bitmap.data_ptr(), 0, sh)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, bitmap)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    # correctness of the timed configuration: every generated signature is honest
+    full = torch.full_like(bitmap, -1)
+    if n % 64:
+        full[-1] = (1 << (n % 64)) - 1
+    assert torch.equal(bitmap, full), "verify rejected an honest signature"
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        eng.verify_device(local, n, batch.pk.data_ptr(), batch.sig.data_ptr(), batch.arena.data_ptr(),
+                          batch.off.data_ptr(), batch.len.data_ptr(), bitmap.data_ptr(), 0, sh)
+        ev[k][1].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, bitmap)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        tt = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(tt[0]), float(tt[1])
+        assert torch.equal(gathered.view(world, words)[rank], bitmap)
+    value = world * n * args.steps / elapsed
+
+    if rank == 0:
+        mad_rate, femul_rate = eng.calibrate(local)
+        achieved = n * W_MAC_PER_VERIFY / (kern_ms * 1e-3)
+        result = {
+            "metric": "Ed25519 verifies/sec (node)",
+            "value": value,
+            "unit": "verifies/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32/int64 (GF(2^255-19) radix 2^25.5 limbs)",
+            "data": "synthetic (keys, messages, signatures generated on-GPU from seeded RNG, RFC 8032 signing)",
+            "config": {"workload": CONFIG_NAME[args.config], "sigs_per_gpu": n, "msg_bytes": msg_len,
+                       "key_pool": args.key_pool or "distinct", "parallelism": f"shard-by-signature x{world}",
+                       "collective": "RCCL all_gather of verdict bitmaps" if world > 1 else "none"},
+            "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": mad_rate / 1e12, "unit": "Tmac/s",
+                         "frac": achieved / mad_rate, "traffic": None,
+                         "kernel": "cv_verify_kernel", "kernel_ms": kern_ms,
+                         "work_per_unit": f"{W_MAC_PER_VERIFY:.3g} 32x32->64 MAC per verify (SURVEY.md 8d)",
+                         "fe_mul_per_s": femul_rate},
+        }
+        if world == 1 and not args.no_cpu:
+            result["cpu_baseline"] = cpu_baseline(batch, local, args.cpu_seconds)
+        if not args.no_notary:
+            result["notary"] = notary_latency(eng, local, 50, cpu=(world == 1 and not args.no_cpu))
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

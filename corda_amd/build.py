@@ -1,0 +1,67 @@
+"""Builds the in-tree native library corda_amd/libcordaverify.so for gfx950.
+
+    python -m corda_amd.build          # or __graft_entry__.build()
+
+hipcc cross-compiles here without a GPU; the .so is git-ignored but travels to the GPU box with the
+gpurun snapshot.  Objects are rebuilt only when a source or header is newer than the library.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libcordaverify.so")
+OBJDIR = os.path.join(HERE, "_obj")
+ARCH = os.environ.get("CV_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+SOURCES = ["cv_kernels.hip", "cv_api.cpp"]
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+          "-Wno-unused-variable"]
+
+
+def _deps():
+    return glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(REPO, "include", "*.h"))
+
+
+def _stale(target: str, inputs) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(p) > t for p in inputs)
+
+
+def build(verbose: bool = False, force: bool = False) -> str:
+    os.makedirs(OBJDIR, exist_ok=True)
+    tables = os.path.join(CSRC, "cv_tables.h")
+    gen = os.path.join(CSRC, "gen_tables.py")
+    if force or _stale(tables, [gen]):
+        subprocess.run([sys.executable, gen], check=True)
+    objs = []
+    deps = _deps()
+    for src in SOURCES:
+        sp = os.path.join(CSRC, src)
+        op = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
+        objs.append(op)
+        if force or _stale(op, [sp] + deps):
+            cmd = [HIPCC] + CFLAGS + ["-c", sp, "-o", op]
+            if src.endswith(".cpp"):
+                cmd = [HIPCC, "-x", "hip"] + CFLAGS + ["-c", sp, "-o", op]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
+    if force or _stale(LIB, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + ["-lpthread"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True, force="--force" in sys.argv))

@@ -1,0 +1,239 @@
+// cv_sha.h — SHA-512 (Ed25519 challenge hash) and SHA-256 (Merkle leaves / nodes) for one lane.
+//
+// Each lane hashes its own record; the message bytes are read from the device arena with byte
+// loads (records are variable length and unaligned — the reads are a rounding error next to the
+// ~2.4e5 multiply-accumulates of a verify, see DESIGN.md roofline).
+#pragma once
+#include "cv_field.h"
+
+#define CV_K512_INIT { \
+    0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL, \
+    0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL, \
+    0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL, \
+    0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL, \
+    0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL, \
+    0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL, \
+    0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL, \
+    0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL, \
+    0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL, \
+    0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL, \
+    0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL, \
+    0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL, \
+    0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL, \
+    0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL, \
+    0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL, \
+    0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL, \
+    0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL, \
+    0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL, \
+    0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL, \
+    0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL}
+__device__ __constant__ static const uint64_t CV_K512_D[80] = CV_K512_INIT;
+static const uint64_t CV_K512_H[80] = CV_K512_INIT;
+
+#define CV_K256_INIT { \
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5, \
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174, \
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da, \
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967, \
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85, \
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070, \
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3, \
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2}
+__device__ __constant__ static const uint32_t CV_K256_D[64] = CV_K256_INIT;
+static const uint32_t CV_K256_H[64] = CV_K256_INIT;
+
+// Round constants: the __constant__ copy on the GPU, the host copy when the same code runs in the
+// CPU test harness (tests/host_harness.cpp).
+CV_HD uint64_t cv_k512(int i) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return CV_K512_D[i];
+#else
+    return CV_K512_H[i];
+#endif
+}
+CV_HD uint32_t cv_k256(int i) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return CV_K256_D[i];
+#else
+    return CV_K256_H[i];
+#endif
+}
+
+CV_HD uint64_t cv_ror64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+CV_HD uint32_t cv_ror32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+CV_HD uint32_t cv_bswap32(uint32_t x) {
+    return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
+}
+
+CV_HD void sha512_init(uint64_t st[8]) {
+    st[0] = 0x6a09e667f3bcc908ULL; st[1] = 0xbb67ae8584caa73bULL;
+    st[2] = 0x3c6ef372fe94f82bULL; st[3] = 0xa54ff53a5f1d36f1ULL;
+    st[4] = 0x510e527fade682d1ULL; st[5] = 0x9b05688c2b3e6c1fULL;
+    st[6] = 0x1f83d9abfb41bd6bULL; st[7] = 0x5be0cd19137e2179ULL;
+}
+
+// One compression; w[16] = big-endian message words (clobbered: used as the schedule ring).
+__host__ __device__ inline void sha512_compress(uint64_t st[8], uint64_t w[16]) {
+    uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll 16
+    for (int i = 0; i < 80; i++) {
+        uint64_t wi;
+        if (i < 16) {
+            wi = w[i & 15];
+        } else {
+            const uint64_t x15 = w[(i - 15) & 15], x2 = w[(i - 2) & 15];
+            const uint64_t s0 = cv_ror64(x15, 1) ^ cv_ror64(x15, 8) ^ (x15 >> 7);
+            const uint64_t s1 = cv_ror64(x2, 19) ^ cv_ror64(x2, 61) ^ (x2 >> 6);
+            wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+            w[i & 15] = wi;
+        }
+        const uint64_t t1 = h + (cv_ror64(e, 14) ^ cv_ror64(e, 18) ^ cv_ror64(e, 41)) + ((e & f) ^ (~e & g)) +
+                            cv_k512(i) + wi;
+        const uint64_t t2 = (cv_ror64(a, 28) ^ cv_ror64(a, 34) ^ cv_ror64(a, 39)) + ((a & b) ^ (a & c) ^ (b & c));
+        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// Byte t of the stream (pre || msg || 0x80 || 0.. || len128_be) where pre is 64 bytes given as 16
+// LE uint32 words (R || Abyte, or prefix || unused), total = 64 + mlen bytes of data.
+__host__ __device__ inline uint32_t sha512_stream_byte(const uint32_t pre[16], int npre, const uint8_t *msg, uint32_t mlen,
+                                              uint32_t t, uint32_t total_padded) {
+    const uint32_t data = npre + mlen;
+    if (t < (uint32_t)npre) return (pre[t >> 2] >> ((t & 3) * 8)) & 0xffu;
+    if (t < data) return msg[t - npre];
+    if (t == data) return 0x80u;
+    // 128-bit big-endian bit length in the last 16 bytes (only the low 64 bits can be non-zero)
+    if (t >= total_padded - 8) {
+        const uint64_t bits = (uint64_t)data * 8;
+        const int sh = 8 * (int)(total_padded - 1 - t);
+        return (uint32_t)(bits >> sh) & 0xffu;
+    }
+    return 0;
+}
+
+// SHA-512(pre[0:npre] || msg[0:mlen]) with npre in {32, 64} (pre as LE words); out = 16 LE words
+// of the 64-byte digest (byte order as produced by the hash, i.e. digest byte k = out[k/4] >> 8(k%4)).
+__host__ __device__ inline void sha512_pre_msg(uint32_t out[16], const uint32_t pre[16], int npre, const uint8_t *msg,
+                                      uint32_t mlen) {
+    uint64_t st[8];
+    sha512_init(st);
+    const uint32_t data = npre + mlen;
+    const uint32_t nblocks = (data + 1 + 16 + 127) / 128;
+    const uint32_t total = nblocks * 128;
+    for (uint32_t blk = 0; blk < nblocks; blk++) {
+        uint64_t w[16];
+        const uint32_t base = blk * 128;
+        if (blk == 0 && npre == 64) {
+            // words 0..7 come straight from the prefix words
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                w[j] = ((uint64_t)cv_bswap32(pre[2 * j]) << 32) | cv_bswap32(pre[2 * j + 1]);
+#pragma unroll
+            for (int j = 8; j < 16; j++) {
+                uint64_t v = 0;
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    v = (v << 8) | sha512_stream_byte(pre, npre, msg, mlen, base + 8 * j + q, total);
+                w[j] = v;
+            }
+        } else {
+            for (int j = 0; j < 16; j++) {
+                uint64_t v = 0;
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    v = (v << 8) | sha512_stream_byte(pre, npre, msg, mlen, base + 8 * j + q, total);
+                w[j] = v;
+            }
+        }
+        sha512_compress(st, w);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        out[2 * i] = cv_bswap32((uint32_t)(st[i] >> 32));
+        out[2 * i + 1] = cv_bswap32((uint32_t)st[i]);
+    }
+}
+
+// ---------------------------------------------------------------- SHA-256
+CV_HD void sha256_init(uint32_t st[8]) {
+    st[0] = 0x6a09e667; st[1] = 0xbb67ae85; st[2] = 0x3c6ef372; st[3] = 0xa54ff53a;
+    st[4] = 0x510e527f; st[5] = 0x9b05688c; st[6] = 0x1f83d9ab; st[7] = 0x5be0cd19;
+}
+
+__host__ __device__ inline void sha256_compress(uint32_t st[8], uint32_t w[16]) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll 16
+    for (int i = 0; i < 64; i++) {
+        uint32_t wi;
+        if (i < 16) {
+            wi = w[i & 15];
+        } else {
+            const uint32_t x15 = w[(i - 15) & 15], x2 = w[(i - 2) & 15];
+            const uint32_t s0 = cv_ror32(x15, 7) ^ cv_ror32(x15, 18) ^ (x15 >> 3);
+            const uint32_t s1 = cv_ror32(x2, 17) ^ cv_ror32(x2, 19) ^ (x2 >> 10);
+            wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+            w[i & 15] = wi;
+        }
+        const uint32_t t1 = h + (cv_ror32(e, 6) ^ cv_ror32(e, 11) ^ cv_ror32(e, 25)) + ((e & f) ^ (~e & g)) +
+                            cv_k256(i) + wi;
+        const uint32_t t2 = (cv_ror32(a, 2) ^ cv_ror32(a, 13) ^ cv_ror32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// SHA-256 of an arbitrary byte string in device memory; out = 8 big-endian state words.
+// Full 64-byte blocks are assembled from byte loads; the tail block(s) carry the padding.
+__host__ __device__ inline void sha256_bytes(uint32_t out[8], const uint8_t *p, uint32_t n) {
+    uint32_t st[8];
+    sha256_init(st);
+    const uint32_t nblocks = (n + 1 + 8 + 63) / 64;
+    const uint32_t total = nblocks * 64;
+    for (uint32_t blk = 0; blk < nblocks; blk++) {
+        uint32_t w[16];
+        const uint32_t base = blk * 64;
+        if (base + 64 <= n) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const uint8_t *q = p + base + 4 * j;
+                w[j] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+            }
+        } else {
+            for (int j = 0; j < 16; j++) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t t = base + 4 * j + k;
+                    uint32_t byte;
+                    if (t < n) byte = p[t];
+                    else if (t == n) byte = 0x80;
+                    else if (t >= total - 8) byte = (uint32_t)(((uint64_t)n * 8) >> (8 * (total - 1 - t))) & 0xff;
+                    else byte = 0;
+                    v = (v << 8) | byte;
+                }
+                w[j] = v;
+            }
+        }
+        sha256_compress(st, w);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) out[i] = st[i];
+}
+
+// SHA-256(left32 || right32) for two digests held as 8 big-endian state words each (Merkle node).
+__host__ __device__ inline void sha256_node(uint32_t out[8], const uint32_t l[8], const uint32_t r[8]) {
+    uint32_t st[8], w[16];
+    sha256_init(st);
+#pragma unroll
+    for (int i = 0; i < 8; i++) { w[i] = l[i]; w[8 + i] = r[i]; }
+    sha256_compress(st, w);
+    // padding block for a 64-byte message
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = 0;
+    w[0] = 0x80000000u;
+    w[15] = 512;
+    sha256_compress(st, w);
+#pragma unroll
+    for (int i = 0; i < 8; i++) out[i] = st[i];
+}

@@ -1,0 +1,249 @@
+"""ctypes binding of the C-ABI in include/cordaverify.h (corda_amd/libcordaverify.so).
+
+This is the product path: there is no CPU fallback.  If the library is missing or no GPU is
+present, the calls raise `NativeUnavailable` — loudly — instead of computing anything elsewhere.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcordaverify.so")
+
+CV_OK = 0
+CV_SIG_OK = 0
+CV_SIG_BAD_KEY = 1
+CV_TX_OK = 0
+CV_TX_EMPTY = 1
+
+# every symbol include/cordaverify.h declares (tests check the library exports all of them)
+EXPORTED = (
+    "cv_open", "cv_close", "cv_strerror", "cv_version", "cv_device_count",
+    "cv_ed25519_verify_batch", "cv_merkle_tx_ids", "cv_merkle_tx_ids_ex", "cv_ed25519_sign_batch",
+    "cv_tx_verdicts", "cv_ed25519_verify_device", "cv_ed25519_sign_device", "cv_merkle_tx_ids_device",
+    "cv_synchronize", "cv_calibrate",
+)
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class CvError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        super().__init__(f"{what}: {_lib.cv_strerror(code).decode() if _lib else code} (code {code})")
+        self.code = code
+
+
+_lib = None
+_lock = threading.Lock()
+
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+
+
+def load():
+    """Load the shared library (does not touch the GPU)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeUnavailable(f"{LIB_PATH} is missing: build it with `python -m corda_amd.build`")
+        lib = ctypes.CDLL(LIB_PATH)
+        lib.cv_open.argtypes = [ctypes.c_uint32, ctypes.POINTER(_vp)]
+        lib.cv_open.restype = ctypes.c_int
+        lib.cv_close.argtypes = [_vp]
+        lib.cv_close.restype = None
+        lib.cv_strerror.argtypes = [ctypes.c_int]
+        lib.cv_strerror.restype = ctypes.c_char_p
+        lib.cv_version.argtypes = []
+        lib.cv_version.restype = ctypes.c_char_p
+        lib.cv_device_count.argtypes = [_vp]
+        lib.cv_device_count.restype = ctypes.c_int
+        lib.cv_ed25519_verify_batch.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+        lib.cv_ed25519_verify_batch.restype = ctypes.c_int
+        lib.cv_merkle_tx_ids.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp]
+        lib.cv_merkle_tx_ids.restype = ctypes.c_int
+        lib.cv_merkle_tx_ids_ex.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]
+        lib.cv_merkle_tx_ids_ex.restype = ctypes.c_int
+        lib.cv_ed25519_sign_batch.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]
+        lib.cv_ed25519_sign_batch.restype = ctypes.c_int
+        lib.cv_tx_verdicts.argtypes = [_sz, _vp, _vp, _vp]
+        lib.cv_tx_verdicts.restype = ctypes.c_int
+        lib.cv_ed25519_verify_device.argtypes = [_vp, ctypes.c_int, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+        lib.cv_ed25519_verify_device.restype = ctypes.c_int
+        lib.cv_ed25519_sign_device.argtypes = [_vp, ctypes.c_int, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+        lib.cv_ed25519_sign_device.restype = ctypes.c_int
+        lib.cv_merkle_tx_ids_device.argtypes = [_vp, ctypes.c_int, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+        lib.cv_merkle_tx_ids_device.restype = ctypes.c_int
+        lib.cv_synchronize.argtypes = [_vp, ctypes.c_int]
+        lib.cv_synchronize.restype = ctypes.c_int
+        lib.cv_calibrate.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+        lib.cv_calibrate.restype = ctypes.c_int
+        _lib = lib
+        return lib
+
+
+def _p(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(_vp)
+
+
+def _u8(a, shape_last=None) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    return a
+
+
+def _check(rc: int, what: str):
+    if rc != CV_OK:
+        raise CvError(rc, what)
+
+
+class Engine:
+    """One context over a set of GPUs (bit d of device_mask = HIP device d; 0 = all).
+
+    Host-buffer methods mirror the JVM drop-in (synchronous); *_device methods take device pointers
+    (ints, e.g. torch.Tensor.data_ptr()) and an optional hipStream_t (int), and return immediately.
+    """
+
+    def __init__(self, device_mask: int = 0):
+        lib = load()
+        h = _vp()
+        rc = lib.cv_open(ctypes.c_uint32(device_mask), ctypes.byref(h))
+        if rc != CV_OK:
+            raise NativeUnavailable(f"cv_open failed: {lib.cv_strerror(rc).decode()} (code {rc})")
+        self._lib = lib
+        self._h = h
+        self.mu = threading.Lock()
+
+    def close(self):
+        if self._h:
+            self._lib.cv_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def device_count(self) -> int:
+        return self._lib.cv_device_count(self._h)
+
+    # ------------------------------------------------------------ host-buffer API
+    def verify_batch(self, pk, sig, arena, off, ln, want_status: bool = True) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+        """pk (n,32) u8, sig (n,64) u8, arena u8, off u64[n], ln u32[n] -> (bitmap u64[ceil(n/64)], status u8[n])."""
+        pk = _u8(pk)
+        sig = _u8(sig)
+        n = pk.shape[0]
+        if pk.size != n * 32 or sig.size != n * 64:
+            raise ValueError("pk must be (n,32) and sig (n,64)")
+        arena = _u8(arena) if arena is not None and np.asarray(arena).size else np.zeros(16, np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        ln = np.ascontiguousarray(ln, dtype=np.uint32)
+        if off.shape[0] != n or ln.shape[0] != n:
+            raise ValueError("off/len must have n entries")
+        if n and int((off + ln).max()) > arena.size:
+            raise ValueError("message range exceeds the arena")
+        bitmap = np.zeros((n + 63) // 64, np.uint64)
+        status = np.zeros(n, np.uint8) if want_status else None
+        with self.mu:
+            _check(self._lib.cv_ed25519_verify_batch(self._h, n, _p(pk), _p(sig), _p(arena), _p(off), _p(ln),
+                                                     _p(bitmap), _p(status)), "cv_ed25519_verify_batch")
+        return bitmap, status
+
+    def sign_batch(self, seeds, arena, off, ln) -> Tuple[np.ndarray, np.ndarray]:
+        seeds = _u8(seeds)
+        n = seeds.shape[0]
+        arena = _u8(arena) if arena is not None and np.asarray(arena).size else np.zeros(16, np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        ln = np.ascontiguousarray(ln, dtype=np.uint32)
+        pk = np.zeros((n, 32), np.uint8)
+        sig = np.zeros((n, 64), np.uint8)
+        with self.mu:
+            _check(self._lib.cv_ed25519_sign_batch(self._h, n, _p(seeds), _p(arena), _p(off), _p(ln), _p(pk),
+                                                   _p(sig)), "cv_ed25519_sign_batch")
+        return pk, sig
+
+    def merkle_tx_ids(self, arena, leaf_off, leaf_len, tx_leaf_begin) -> Tuple[np.ndarray, np.ndarray]:
+        tx_leaf_begin = np.ascontiguousarray(tx_leaf_begin, dtype=np.uint32)
+        ntx = tx_leaf_begin.shape[0] - 1
+        arena = _u8(arena) if arena is not None and np.asarray(arena).size else np.zeros(16, np.uint8)
+        leaf_off = np.ascontiguousarray(leaf_off, dtype=np.uint64)
+        leaf_len = np.ascontiguousarray(leaf_len, dtype=np.uint32)
+        if leaf_off.size == 0:
+            leaf_off = np.zeros(1, np.uint64)
+            leaf_len = np.zeros(1, np.uint32)
+        ids = np.zeros((max(ntx, 0), 32), np.uint8)
+        st = np.zeros(max(ntx, 0), np.uint8)
+        with self.mu:
+            _check(self._lib.cv_merkle_tx_ids_ex(self._h, ntx, _p(arena), _p(leaf_off), _p(leaf_len),
+                                                 _p(tx_leaf_begin), _p(ids), _p(st)), "cv_merkle_tx_ids_ex")
+        return ids, st
+
+    # ------------------------------------------------------------ device-resident API
+    def verify_device(self, device: int, n: int, d_pk: int, d_sig: int, d_arena: int, d_off: int, d_len: int,
+                      d_bitmap: int, d_status: int = 0, stream: int = 0):
+        _check(self._lib.cv_ed25519_verify_device(self._h, device, n, d_pk, d_sig, d_arena, d_off, d_len, d_bitmap,
+                                                  d_status or None, stream or None), "cv_ed25519_verify_device")
+
+    def sign_device(self, device: int, n: int, d_seed: int, d_arena: int, d_off: int, d_len: int, d_pk: int,
+                    d_sig: int, stream: int = 0):
+        _check(self._lib.cv_ed25519_sign_device(self._h, device, n, d_seed, d_arena, d_off, d_len, d_pk, d_sig,
+                                                stream or None), "cv_ed25519_sign_device")
+
+    def merkle_device(self, device: int, ntx: int, nleaves: int, d_arena: int, d_off: int, d_len: int,
+                      d_tx_begin: int, d_workspace: int, d_ids: int, d_status: int = 0, stream: int = 0):
+        _check(self._lib.cv_merkle_tx_ids_device(self._h, device, ntx, nleaves, d_arena, d_off, d_len, d_tx_begin,
+                                                 d_workspace, d_ids, d_status or None, stream or None),
+               "cv_merkle_tx_ids_device")
+
+    def calibrate(self, device: int) -> Tuple[float, float]:
+        """(v_mad_i64_i32 per second, fe_mul per second) measured on `device` (roofline peak)."""
+        a, b = ctypes.c_double(0), ctypes.c_double(0)
+        _check(self._lib.cv_calibrate(self._h, device, ctypes.byref(a), ctypes.byref(b)), "cv_calibrate")
+        return a.value, b.value
+
+    def synchronize(self, device: int):
+        _check(self._lib.cv_synchronize(self._h, device), "cv_synchronize")
+
+
+def tx_verdicts(bitmap: np.ndarray, tx_sig_begin) -> np.ndarray:
+    lib = load()
+    tx_sig_begin = np.ascontiguousarray(tx_sig_begin, dtype=np.uint32)
+    ntx = tx_sig_begin.shape[0] - 1
+    out = np.zeros(max(ntx, 0), np.uint8)
+    bitmap = np.ascontiguousarray(bitmap, dtype=np.uint64)
+    if bitmap.size == 0:
+        bitmap = np.zeros(1, np.uint64)
+    _check(lib.cv_tx_verdicts(ntx, _p(bitmap), _p(tx_sig_begin), _p(out)), "cv_tx_verdicts")
+    return out
+
+
+def bitmap_to_bools(bitmap: np.ndarray, n: int) -> np.ndarray:
+    bits = np.unpackbits(np.ascontiguousarray(bitmap, dtype="<u8").view(np.uint8), bitorder="little")
+    return bits[:n].astype(bool)
+
+
+_default: Optional[Engine] = None
+
+
+def default_engine() -> Engine:
+    """Process-wide engine on all visible GPUs (the JVM shim's "one ctx per process")."""
+    global _default
+    with _lock:
+        if _default is None:
+            _default = Engine(0)
+        return _default

@@ -1,0 +1,125 @@
+/*
+ * cordaverify.h — C-ABI of the MI355X batched signature-verification engine for Corda's
+ * transaction-validation hot path.  Plain pointers and sizes only (no C++ / torch types), so the
+ * JVM binds it directly through JNA or JNI (binding stubs: INTEGRATION.md).
+ *
+ * What each entry point replaces in the reference (MarioAriasC/corda @ 0.7-SNAPSHOT):
+ *
+ *   cv_ed25519_verify_batch   N x  PublicKey.verifyWithECDSA(content, signature)
+ *                                 core/src/main/kotlin/net/corda/core/crypto/CryptoUtilities.kt:90-96
+ *                             i.e. net.i2p.crypto:eddsa:0.1.0 EdDSAEngine.initVerify/update/verify
+ *                             (jar pinned at core/build.gradle:80), looped sequentially by
+ *                             SignedTransaction.checkSignaturesAreValid()
+ *                                 core/src/main/kotlin/net/corda/core/transactions/SignedTransaction.kt:82-87
+ *                             and by the notary / resolve flows (NotaryFlow.kt:97-113,
+ *                             ValidatingNotaryFlow.kt:24-45, ResolveTransactionsFlow.kt:105-111).
+ *                             Verdicts are bit-exact with eddsa-0.1.0, adversarial inputs included.
+ *   cv_merkle_tx_ids          N x  WireTransaction.id  (= MerkleTree.getMerkleTree(leafHashes).hash)
+ *                                 core/src/main/kotlin/net/corda/core/transactions/WireTransaction.kt:45-52
+ *                                 core/src/main/kotlin/net/corda/core/transactions/MerkleTransaction.kt:26-38,66-99
+ *                             leaf hash = SecureHash.sha256(leaf bytes)  (core/.../crypto/SecureHash.kt:33)
+ *   cv_ed25519_sign_batch     N x  PrivateKey.signWithECDSA(bytes) after entropyToKeyPair/seed
+ *                                 CryptoUtilities.kt:63-73,123-130 (deterministic RFC 8032; used to
+ *                                 generate synthetic workloads, not on the validation path)
+ *   cv_tx_verdicts            per-transaction AND of signature verdicts (the "all sigs valid" half of
+ *                                 SignedTransaction.verifySignatures, SignedTransaction.kt:58-72)
+ *
+ * Conventions
+ *   - Return codes: CV_OK (0) or a negative CV_E* code; nothing throws, aborts or longjmps across
+ *     the ABI.  cv_strerror() gives a static message.
+ *   - Host-buffer calls are synchronous; the caller owns every buffer.  A cv_ctx may be used by one
+ *     thread at a time (the JVM shim holds one ctx per process behind a mutex).
+ *   - Record layout (structure-of-arrays): pk[n][32], sig[n][64] (R || S), message i is
+ *     msg_arena[msg_off[i] .. msg_off[i] + msg_len[i]).
+ *   - verdict_bitmap: ceil(n/64) uint64 words, bit (i % 64) of word (i / 64) = signature i valid.
+ *   - status (optional, may be NULL): one byte per signature, CV_SIG_OK or CV_SIG_BAD_KEY (the key
+ *     bytes are not a valid point: the reference throws IllegalArgumentException when building the
+ *     EdDSAPublicKey).  Length errors (sig != 64 B -> SignatureException, key != 32 B) cannot be
+ *     expressed in these fixed-width records; the host shim rejects them before the call.
+ *   - Multi-GPU: cv_open(mask) with several bits set shards host-buffer batches by contiguous
+ *     signature ranges (multiples of 64) over the devices, one host thread + one HIP stream each.
+ */
+#ifndef CORDAVERIFY_H
+#define CORDAVERIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CV_OK 0
+#define CV_E_NO_DEVICE (-1)   /* no HIP device matches the mask */
+#define CV_E_HIP (-2)         /* a HIP runtime call failed */
+#define CV_E_ARGS (-3)        /* null pointer / bad size */
+#define CV_E_OOM (-4)         /* device allocation failed */
+#define CV_E_TOO_LARGE (-5)   /* more than 2^32-1 records in one shard */
+
+#define CV_SIG_OK 0
+#define CV_SIG_BAD_KEY 1
+#define CV_TX_OK 0
+#define CV_TX_EMPTY 1         /* no leaves: MerkleTreeException("Cannot calculate Merkle root on empty hash list.") */
+
+typedef struct cv_ctx cv_ctx;
+
+/* Open a context on the devices in device_mask (bit d = HIP device ordinal d; 0 = all devices). */
+int cv_open(uint32_t device_mask, cv_ctx **out);
+void cv_close(cv_ctx *ctx);
+const char *cv_strerror(int code);
+const char *cv_version(void);
+/* Number of devices in the context. */
+int cv_device_count(const cv_ctx *ctx);
+
+/* ---------------------------------------------------------------- host-buffer API (JVM drop-in) */
+
+int cv_ed25519_verify_batch(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint8_t *sig,
+                            const uint8_t *msg_arena, const uint64_t *msg_off, const uint32_t *msg_len,
+                            uint64_t *verdict_bitmap, uint8_t *status);
+
+int cv_merkle_tx_ids(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
+                     const uint32_t *leaf_len, const uint32_t *tx_leaf_begin /* ntx+1 */, uint8_t *ids /* ntx*32 */);
+
+/* as cv_merkle_tx_ids, with per-transaction status (CV_TX_OK / CV_TX_EMPTY) */
+int cv_merkle_tx_ids_ex(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
+                        const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, uint8_t *ids, uint8_t *tx_status);
+
+int cv_ed25519_sign_batch(cv_ctx *ctx, size_t n, const uint8_t *seed /* n*32 */, const uint8_t *msg_arena,
+                          const uint64_t *msg_off, const uint32_t *msg_len, uint8_t *pk_out /* n*32 */,
+                          uint8_t *sig_out /* n*64 */);
+
+/* tx_ok[t] = AND of verdict bits [tx_sig_begin[t], tx_sig_begin[t+1]); a transaction with no
+ * signatures is not ok (SignedTransaction requires sigs.isNotEmpty(), SignedTransaction.kt:27-29). */
+int cv_tx_verdicts(size_t ntx, const uint64_t *verdict_bitmap, const uint32_t *tx_sig_begin, uint8_t *tx_ok);
+
+/* ---------------------------------------------------------------- device-resident API
+ * All pointers are device pointers on HIP device `device` (which must be in the context); work is
+ * enqueued on `stream` (a hipStream_t, NULL = the context's stream for that device) and the call
+ * returns without synchronising.  These are the entry points bench.py times (inputs resident in HBM).
+ */
+int cv_ed25519_verify_device(cv_ctx *ctx, int device, size_t n, const void *d_pk, const void *d_sig,
+                             const void *d_arena, const void *d_off, const void *d_len, void *d_bitmap,
+                             void *d_status, void *stream);
+
+int cv_ed25519_sign_device(cv_ctx *ctx, int device, size_t n, const void *d_seed, const void *d_arena,
+                           const void *d_off, const void *d_len, void *d_pk, void *d_sig, void *stream);
+
+/* d_workspace: nleaves * 32 bytes (leaf digests, overwritten) */
+int cv_merkle_tx_ids_device(cv_ctx *ctx, int device, size_t ntx, size_t nleaves, const void *d_arena,
+                            const void *d_leaf_off, const void *d_leaf_len, const void *d_tx_leaf_begin,
+                            void *d_workspace, void *d_ids, void *d_tx_status, void *stream);
+
+/* Block until all work the context enqueued on `device` has finished. */
+int cv_synchronize(cv_ctx *ctx, int device);
+
+/* ---------------------------------------------------------------- roofline calibration
+ * Measures, on `device`, the chip-wide issue rate of the 32x32->64 multiply-accumulate
+ * (v_mad_i64_i32) the field arithmetic is built on, and the practical GF(2^255-19) multiply rate of
+ * the engine's fe_mul.  Either output pointer may be NULL.  Used by bench.py for roofline.peak.
+ */
+int cv_calibrate(cv_ctx *ctx, int device, double *mad_per_s, double *femul_per_s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CORDAVERIFY_H */

@@ -1,0 +1,160 @@
+// host_harness.cpp — TEST INFRASTRUCTURE: runs the product's per-lane device code (corda_amd/csrc/
+// cv_verify.h and friends, all __host__ __device__) on the CPU so its logic can be checked against
+// the oracle without a GPU.  Built by tests/conftest.py into tests/_build/libcvhost.so.
+#include <cstring>
+
+#include "../corda_amd/csrc/cv_verify.h"
+
+static void words_from_bytes(uint32_t *w, const uint8_t *b, int nwords) {
+    for (int i = 0; i < nwords; i++) memcpy(&w[i], b + 4 * i, 4);
+}
+static void bytes_from_words(uint8_t *b, const uint32_t *w, int nwords) {
+    for (int i = 0; i < nwords; i++) memcpy(b + 4 * i, &w[i], 4);
+}
+
+extern "C" {
+
+// verdict (0/1); *status = 0 ok / 1 bad key
+int cvh_verify(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, uint32_t mlen, int *status) {
+    uint32_t aw[8], rw[8], sw[8];
+    words_from_bytes(aw, pk, 8);
+    words_from_bytes(rw, sig, 8);
+    words_from_bytes(sw, sig + 32, 8);
+    bool key_ok = false;
+    const bool ok = cv_verify_one(CV_BTAB_H, aw, rw, sw, msg, mlen, &key_ok);
+    *status = key_ok ? 0 : 1;
+    return ok ? 1 : 0;
+}
+
+void cvh_sign(const uint8_t *seed, const uint8_t *msg, uint32_t mlen, uint8_t *pk, uint8_t *sig) {
+    uint32_t sd[8], pw[8], sg[16];
+    words_from_bytes(sd, seed, 8);
+    cv_sign_one(CV_BTAB_H, sd, msg, mlen, pw, sg);
+    bytes_from_words(pk, pw, 8);
+    bytes_from_words(sig, sg, 16);
+}
+
+// field element round trips: in = 32 bytes (value < 2^255), ops on canonical encodings
+void cvh_fe_mul(const uint8_t *a, const uint8_t *b, uint8_t *out) {
+    uint32_t aw[8], bw[8], ow[8];
+    words_from_bytes(aw, a, 8);
+    words_from_bytes(bw, b, 8);
+    fe fa, fb, fo;
+    fe_from_words(fa, aw);
+    fe_from_words(fb, bw);
+    fe_mul(fo, fa, fb);
+    fe_to_words(ow, fo);
+    bytes_from_words(out, ow, 8);
+}
+void cvh_fe_sq(const uint8_t *a, uint8_t *out, int dbl) {
+    uint32_t aw[8], ow[8];
+    words_from_bytes(aw, a, 8);
+    fe fa, fo;
+    fe_from_words(fa, aw);
+    if (dbl) fe_sq2(fo, fa); else fe_sq(fo, fa);
+    fe_to_words(ow, fo);
+    bytes_from_words(out, ow, 8);
+}
+void cvh_fe_invert(const uint8_t *a, uint8_t *out) {
+    uint32_t aw[8], ow[8];
+    words_from_bytes(aw, a, 8);
+    fe fa, fo;
+    fe_from_words(fa, aw);
+    fe_invert(fo, fa);
+    fe_to_words(ow, fo);
+    bytes_from_words(out, ow, 8);
+}
+// mul of raw limb vectors (bounds stress): a, b = 10 int32 limbs each
+void cvh_fe_mul_limbs(const int32_t *a, const int32_t *b, uint8_t *out) {
+    fe fa, fb, fo;
+    memcpy(fa.v, a, 40);
+    memcpy(fb.v, b, 40);
+    fe_mul(fo, fa, fb);
+    uint32_t ow[8];
+    fe_to_words(ow, fo);
+    bytes_from_words(out, ow, 8);
+}
+void cvh_fe_sq_limbs(const int32_t *a, uint8_t *out) {
+    fe fa, fo;
+    memcpy(fa.v, a, 40);
+    fe_sq(fo, fa);
+    uint32_t ow[8];
+    fe_to_words(ow, fo);
+    bytes_from_words(out, ow, 8);
+}
+void cvh_fe_to_bytes_limbs(const int32_t *a, uint8_t *out) {
+    fe fa;
+    memcpy(fa.v, a, 40);
+    uint32_t ow[8];
+    fe_to_words(ow, fa);
+    bytes_from_words(out, ow, 8);
+}
+
+void cvh_sc_reduce(const uint8_t *in64, uint8_t *out32) {
+    uint32_t x[16], o[8];
+    words_from_bytes(x, in64, 16);
+    sc_reduce512(o, x);
+    bytes_from_words(out32, o, 8);
+}
+void cvh_sc_muladd(const uint8_t *a, const uint8_t *b, const uint8_t *c, uint8_t *out) {
+    uint32_t aw[8], bw[8], cw[8], o[8];
+    words_from_bytes(aw, a, 8);
+    words_from_bytes(bw, b, 8);
+    words_from_bytes(cw, c, 8);
+    sc_muladd(o, aw, bw, cw);
+    bytes_from_words(out, o, 8);
+}
+int cvh_slide_drops(const uint8_t *s) {
+    uint32_t w[8];
+    words_from_bytes(w, s, 8);
+    return slide_drops_carry(w) ? 1 : 0;
+}
+void cvh_effective_s(const uint8_t *s, uint8_t *out) {
+    uint32_t w[8], o[8];
+    words_from_bytes(w, s, 8);
+    sc_effective_s(o, w);
+    bytes_from_words(out, o, 8);
+}
+int cvh_digit16(const uint8_t *s, int k) {
+    uint32_t w[8];
+    words_from_bytes(w, s, 8);
+    return digit16(w, k);
+}
+int cvh_digit256(const uint8_t *s, int k) {
+    uint32_t w[8];
+    words_from_bytes(w, s, 8);
+    return digit256(w, k);
+}
+void cvh_sha512(const uint8_t *pre, int npre, const uint8_t *msg, uint32_t mlen, uint8_t *out) {
+    uint32_t p[16] = {0}, o[16];
+    words_from_bytes(p, pre, npre / 4);
+    sha512_pre_msg(o, p, npre, msg, mlen);
+    bytes_from_words(out, o, 16);
+}
+void cvh_sha256(const uint8_t *msg, uint32_t n, uint8_t *out) {
+    uint32_t o[8];
+    sha256_bytes(o, msg, n);
+    for (int i = 0; i < 8; i++) {
+        const uint32_t v = cv_bswap32(o[i]);
+        memcpy(out + 4 * i, &v, 4);
+    }
+}
+// Merkle root over leaf digests (bytes, cnt x 32); returns 0 for empty
+int cvh_merkle_root(const uint8_t *leaves, uint32_t cnt, uint8_t *out) {
+    uint32_t *lvl = new uint32_t[8 * (cnt ? cnt : 1)];
+    for (uint32_t i = 0; i < 8 * cnt; i++) {
+        uint32_t v;
+        memcpy(&v, leaves + 4 * i, 4);
+        lvl[i] = cv_bswap32(v);
+    }
+    uint32_t root[8];
+    const bool ok = cv_merkle_root_inplace(lvl, cnt, root);
+    for (int i = 0; i < 8; i++) {
+        const uint32_t v = cv_bswap32(root[i]);
+        memcpy(out + 4 * i, &v, 4);
+    }
+    delete[] lvl;
+    return ok ? 1 : 0;
+}
+
+}  // extern "C"

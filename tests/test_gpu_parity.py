@@ -1,0 +1,178 @@
+"""GPU parity tests: the HIP engine (through the C-ABI) against the oracle and the golden fixtures.
+
+Bit-exact bar: every verdict, every key-status byte, every tx id.  Sizes: the golden corpus and
+oracle-checked random batches at sizes the oracle finishes in seconds; BASELINE sizes (1M) through
+size-independent properties (all honest accepted, an exact corruption pattern rejected).
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from corda_amd import native  # noqa: E402
+
+
+def _bits(bitmap, n):
+    return native.bitmap_to_bools(bitmap, n)
+
+
+def test_golden_corpus_verdicts(engine, corpus, manifest):
+    bitmap, status = engine.verify_batch(corpus["pk"], corpus["sig"], corpus["arena"], corpus["off"], corpus["len"])
+    got = _bits(bitmap, len(corpus["pk"]))
+    exp = corpus["verdict"].astype(bool)
+    bad = np.where(got != exp)[0]
+    classes = manifest["classes"]
+    assert bad.size == 0, f"mismatches in classes {sorted({classes[corpus['cls'][i]] for i in bad})}"
+    assert np.array_equal(status, corpus["status"])
+
+
+def test_golden_corpus_per_class_and_shuffled(engine, corpus, manifest):
+    """Same corpus in a shuffled order, tiled 10x: verdicts must follow the records (no cross-lane leaks)."""
+    n = len(corpus["pk"])
+    rng = np.random.default_rng(1)
+    perm = np.concatenate([rng.permutation(n) for _ in range(10)])
+    bitmap, status = engine.verify_batch(corpus["pk"][perm], corpus["sig"][perm], corpus["arena"], corpus["off"][perm],
+                                         corpus["len"][perm])
+    assert np.array_equal(_bits(bitmap, perm.size), corpus["verdict"][perm].astype(bool))
+    assert np.array_equal(status, corpus["status"][perm])
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 127, 129, 255, 256, 257, 1000])
+def test_ragged_sizes(engine, corpus, n):
+    idx = np.arange(n) % len(corpus["pk"])
+    bitmap, status = engine.verify_batch(corpus["pk"][idx], corpus["sig"][idx], corpus["arena"], corpus["off"][idx],
+                                         corpus["len"][idx])
+    assert bitmap.size == (n + 63) // 64
+    assert np.array_equal(_bits(bitmap, n), corpus["verdict"][idx].astype(bool))
+    # bits past n in the last word stay clear
+    if n % 64:
+        assert int(bitmap[-1]) >> (n % 64) == 0
+
+
+def test_empty_batch(engine):
+    bitmap, status = engine.verify_batch(np.zeros((0, 32), np.uint8), np.zeros((0, 64), np.uint8), np.zeros(0, np.uint8),
+                                         np.zeros(0, np.uint64), np.zeros(0, np.uint32))
+    assert bitmap.size == 0 and status.size == 0
+
+
+def test_gpu_signer_matches_oracle(engine):
+    import ed25519_ref as E
+    rng = np.random.default_rng(7)
+    n = 48
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    lens = rng.integers(0, 400, n).astype(np.uint32)
+    lens[:4] = [0, 32, 300, 111]
+    msgs = [rng.integers(0, 256, int(l), dtype=np.uint8).tobytes() for l in lens]
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1])
+    arena = np.frombuffer(b"".join(msgs) + b"\0" * 16, np.uint8)
+    pk, sig = engine.sign_batch(seeds, arena, off, lens)
+    for i in range(n):
+        s = seeds[i].tobytes()
+        assert pk[i].tobytes() == E.public_key_of(s)
+        assert sig[i].tobytes() == E.sign(s, msgs[i])
+    # entropyToKeyPair seeds of the reference's test keys (DUMMY_NOTARY_KEY = 20, CASH_ISSUER = 10)
+    for ent in (20, 10):
+        s = np.frombuffer(E.entropy_to_seed(ent), np.uint8)[None]
+        m = np.frombuffer(b"\x07" * 32, np.uint8)
+        p2, s2 = engine.sign_batch(s, m, np.zeros(1, np.uint64), np.array([32], np.uint32))
+        assert s2[0].tobytes() == E.sign(E.entropy_to_seed(ent), b"\x07" * 32)
+
+
+def test_random_batch_vs_c_oracle(engine, oracle_c):
+    rng = np.random.default_rng(11)
+    n = 8192
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    lens = rng.integers(0, 320, n).astype(np.uint32)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1])
+    arena = rng.integers(0, 256, int(lens.sum()) + 16, dtype=np.uint8)
+    pk, sig = engine.sign_batch(seeds, arena, off, lens)
+    # corruptions of every kind at known positions
+    sig[1::7, rng.integers(0, 64)] ^= 0x10
+    pk[2::11, 3] ^= 0x01
+    sig[3::13, 63] |= 0x80                     # S >= 2^255 (slide carry-loss territory)
+    arena[off[5::17].astype(np.int64)] ^= 0xFF  # message byte (where len > 0)
+    bitmap, status = engine.verify_batch(pk, sig, arena, off, lens)
+    ref, rst = oracle_c.verify_batch(pk, sig, arena, off, lens, nthreads=8)
+    assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
+    assert np.array_equal(status, rst)
+    assert 0.5 < ref.mean() < 0.95
+
+
+def test_baseline_size_all_honest_and_exact_pattern(engine):
+    """C2 at full size (1M, 300-byte messages): every honest signature accepted, and after flipping
+    one S bit in every 16th signature exactly those are rejected (size-independent properties)."""
+    import torch
+    from corda_amd import workload
+    n = 1_000_000
+    b = workload.make_batch(engine, 0, n, 300, seed=99)
+    bm = torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda:0")
+    st = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+    engine.verify_device(0, n, b.pk.data_ptr(), b.sig.data_ptr(), b.arena.data_ptr(), b.off.data_ptr(),
+                         b.len.data_ptr(), bm.data_ptr(), st.data_ptr())
+    engine.synchronize(0)
+    got = native.bitmap_to_bools(bm.cpu().numpy().view(np.uint64), n)
+    assert got.all()
+    assert int(st.sum()) == 0
+    expect = workload.corrupt_fraction(b, 16).cpu().numpy()
+    engine.verify_device(0, n, b.pk.data_ptr(), b.sig.data_ptr(), b.arena.data_ptr(), b.off.data_ptr(),
+                         b.len.data_ptr(), bm.data_ptr(), 0)
+    engine.synchronize(0)
+    got = native.bitmap_to_bools(bm.cpu().numpy().view(np.uint64), n)
+    assert np.array_equal(got, expect)
+
+
+def test_key_pool_batch(engine, oracle_c):
+    """1,024-key pool variant: repeated keys across lanes."""
+    from corda_amd import workload
+    n = 4096
+    b = workload.make_batch(engine, 0, n, 32, seed=5, key_pool=1024)
+    pk, sig, arena, off, ln = b.to_host()
+    assert len({bytes(r) for r in pk}) == 1024
+    bitmap, _ = engine.verify_batch(pk, sig, arena, off, ln)
+    assert _bits(bitmap, n).all()
+
+
+def test_merkle_golden(engine, merkle_cases):
+    m = merkle_cases
+    ids, st = engine.merkle_tx_ids(m["arena"], m["leaf_off"], m["leaf_len"], m["tx_leaf_begin"])
+    assert np.array_equal(st, m["status"])
+    assert np.array_equal(ids, m["ids"])
+    assert ids[0].tobytes().hex().upper() == "F6D8FB3720114F8D040D64F633B0D9178EB09A55AA7D62FAE1A070D1BF561051"
+
+
+def test_merkle_sha256_multiblock_kat(engine):
+    """One-leaf tx over the 71,644-byte prospectus jar: id = SHA-256(jar) = decd0986... (SellerFlow.kt:23)."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    data = np.fromfile(os.path.join(here, "golden", "bank-of-london-cp.jar.bin"), np.uint8)
+    ids, st = engine.merkle_tx_ids(data, np.zeros(1, np.uint64), np.array([data.size], np.uint32),
+                                   np.array([0, 1], np.uint32))
+    assert ids[0].tobytes().hex() == "decd098666b9657314870e192ced0c3519c2c9d395507a238338f8d003929de9"
+
+
+def test_merkle_random_vs_oracle(engine, oracle_c):
+    rng = np.random.default_rng(3)
+    ntx = 3000
+    counts = rng.integers(0, 12, ntx)
+    counts[:5] = [0, 1, 2, 3, 64]
+    begin = np.zeros(ntx + 1, np.uint32)
+    begin[1:] = np.cumsum(counts)
+    nl = int(begin[-1])
+    lens = rng.integers(0, 700, nl).astype(np.uint32)
+    off = np.zeros(nl, np.uint64)
+    off[1:] = np.cumsum(lens[:-1])
+    arena = rng.integers(0, 256, int(lens.sum()) + 16, dtype=np.uint8)
+    ids, st = engine.merkle_tx_ids(arena, off, lens, begin)
+    rids, rst = oracle_c.merkle_tx_ids(arena, off, lens, begin)
+    assert np.array_equal(st, rst)
+    assert np.array_equal(ids, rids)
+
+
+def test_tx_verdicts_and():
+    bitmap = np.array([0xFFFFFFFFFFFFFFF0, 0x1], np.uint64)
+    begin = np.array([0, 4, 8, 64, 65, 65, 66], np.uint32)
+    assert native.tx_verdicts(bitmap, begin).tolist() == [0, 1, 1, 1, 0, 0]
