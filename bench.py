@@ -130,8 +130,12 @@ def main():
     msg_len = MSG_BYTES[args.config]
 
     eng = native.Engine(1 << local)
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated (non-null) stream: the verify kernels, the HIP events that time them and the RCCL
+    # all-gather are all ordered on it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
+    assert sh != 0
     t0 = time.perf_counter()
     batch = workload.make_batch(eng, local, n, msg_len, seed=20261015 + 7919 * rank,
                                 key_pool=args.key_pool or None, stream=sh)
