@@ -1,0 +1,62 @@
+"""The drop-in boundary on CPU: the C-ABI library loads, exports every symbol include/*.h declares,
+and fails loudly (no silent fallback) when there is no GPU."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from corda_amd import native
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_functions():
+    names = set()
+    for h in os.listdir(os.path.join(REPO, "include")):
+        if h.endswith(".h"):
+            src = open(os.path.join(REPO, "include", h)).read()
+            src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+            names |= set(re.findall(r"\b(cv_[a-z0-9_]+)\s*\(", src))
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = native.load()
+    declared = _header_functions()
+    assert len(declared) >= 14
+    for name in declared:
+        assert hasattr(lib, name), f"{name} declared in include/ but not exported"
+    assert set(native.EXPORTED) == declared
+
+
+def test_version_and_strerror():
+    lib = native.load()
+    assert b"gfx950" in lib.cv_version()
+    assert lib.cv_strerror(0) == b"ok"
+    assert lib.cv_strerror(-1).startswith(b"no HIP device")
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure mode")
+def test_no_gpu_fails_loudly():
+    with pytest.raises(native.NativeUnavailable):
+        native.Engine(0)
+
+
+def test_null_context_rejected():
+    lib = native.load()
+    assert lib.cv_ed25519_verify_batch(None, 1, None, None, None, None, None, None, None) == -3
+    assert lib.cv_merkle_tx_ids(None, 1, None, None, None, None, None) == -3
+    assert lib.cv_close(None) is None
+
+
+def test_tx_verdicts_host_only():
+    bm = np.array([0b1011], np.uint64)
+    assert native.tx_verdicts(bm, np.array([0, 2, 4, 4], np.uint32)).tolist() == [1, 0, 0]
+
+
+def test_bitmap_to_bools():
+    bm = np.array([1 | (1 << 63), 2], np.uint64)
+    b = native.bitmap_to_bools(bm, 66)
+    assert b[0] and b[63] and b[65] and not b[64] and b.sum() == 3

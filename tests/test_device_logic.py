@@ -1,0 +1,175 @@
+"""The product's per-lane device code (corda_amd/csrc/*.h, __host__ __device__) run on the CPU via
+tests/host_harness.cpp and checked against the oracle: catches logic and limb-bound bugs without a
+GPU.  The GPU parity tests (test_gpu_parity.py) then check the compiled kernels themselves."""
+import ctypes
+import os
+import random
+
+import numpy as np
+import pytest
+
+import ed25519_ref as E
+
+P, L = E.P, E.L
+
+
+def _b(x: bytes):
+    return (ctypes.c_uint8 * max(1, len(x))).from_buffer_copy(x + b"\0")
+
+
+def _out(n):
+    return (ctypes.c_uint8 * n)()
+
+
+def _int(o):
+    return int.from_bytes(bytes(o), "little")
+
+
+def test_field_ops_random_and_extreme(host_harness):
+    H = host_harness
+    rng = random.Random(1)
+    vals = [0, 1, 2, 19, P - 1, P, P + 1, P + 18, 2**255 - 1, 2**254, 2**128 + 7] + \
+           [rng.randrange(2**255) for _ in range(300)]
+    for a in vals:
+        c = rng.choice(vals)
+        o = _out(32)
+        H.cvh_fe_mul(_b(a.to_bytes(32, "little")), _b(c.to_bytes(32, "little")), o)
+        assert _int(o) == a * c % P
+        H.cvh_fe_sq(_b(a.to_bytes(32, "little")), o, 0)
+        assert _int(o) == a * a % P
+        H.cvh_fe_sq(_b(a.to_bytes(32, "little")), o, 1)
+        assert _int(o) == 2 * a * a % P
+        H.cvh_fe_invert(_b(a.to_bytes(32, "little")), o)
+        assert _int(o) == pow(a, P - 2, P)
+
+
+OFF = [0, 26, 51, 77, 102, 128, 153, 179, 204, 230]
+
+
+def _limb_val(v):
+    return sum(x * (1 << o) for x, o in zip(v, OFF))
+
+
+def test_field_mul_at_limb_bounds(host_harness):
+    """Inputs at the documented precondition edge (|limb| = 1.65 * 2^w) must not overflow."""
+    H = host_harness
+    rng = random.Random(2)
+    W = [26, 25] * 5
+    for trial in range(400):
+        a = [int(rng.choice([1, -1]) * rng.choice([1.65, 1.5, 1.0, rng.random() * 1.65]) * (1 << W[i]))
+             for i in range(10)]
+        b = [int(rng.choice([1, -1]) * rng.choice([1.65, 1.5, 1.0, rng.random() * 1.65]) * (1 << W[i]))
+             for i in range(10)]
+        A = (ctypes.c_int32 * 10)(*a)
+        B = (ctypes.c_int32 * 10)(*b)
+        o = _out(32)
+        H.cvh_fe_mul_limbs(A, B, o)
+        assert _int(o) == _limb_val(a) * _limb_val(b) % P
+        H.cvh_fe_sq_limbs(A, o)
+        assert _int(o) == _limb_val(a) ** 2 % P
+
+
+def test_sc_reduce(host_harness):
+    H = host_harness
+    rng = random.Random(3)
+    cases = [bytes(64), b"\xff" * 64, L.to_bytes(64, "little"), (L - 1).to_bytes(64, "little"),
+             (2 * L).to_bytes(64, "little"), (2**512 - L).to_bytes(64, "little")]
+    cases += [rng.getrandbits(512).to_bytes(64, "little") for _ in range(3000)]
+    for x in cases:
+        o = _out(32)
+        H.cvh_sc_reduce(_b(x), o)
+        assert _int(o) == int.from_bytes(x, "little") % L
+
+
+def test_sc_muladd(host_harness):
+    H = host_harness
+    rng = random.Random(4)
+    for _ in range(500):
+        a, b, c = (rng.getrandbits(256) for _ in range(3))
+        o = _out(32)
+        H.cvh_sc_muladd(_b(a.to_bytes(32, "little")), _b(b.to_bytes(32, "little")), _b(c.to_bytes(32, "little")), o)
+        assert _int(o) == (a * b + c) % L
+
+
+def test_slide_replay_and_effective_scalar(host_harness):
+    H = host_harness
+    rng = random.Random(5)
+    for i in range(1500):
+        s = rng.getrandbits(256)
+        if i % 3 == 0:
+            s |= 1 << 255
+        if i % 7 == 0:
+            s |= ((1 << rng.randrange(1, 40)) - 1) << (256 - 40)
+        sb = s.to_bytes(32, "little")
+        assert H.cvh_slide_drops(_b(sb)) == int(E.slide_drops_carry(sb))
+        o = _out(32)
+        H.cvh_effective_s(_b(sb), o)
+        assert _int(o) == E.slide_value(sb) % L
+
+
+def test_signed_digits(host_harness):
+    H = host_harness
+    rng = random.Random(6)
+    for _ in range(200):
+        s = rng.getrandbits(255).to_bytes(32, "little")
+        assert sum(H.cvh_digit16(_b(s), k) * 16**k for k in range(64)) == int.from_bytes(s, "little")
+        assert sum(H.cvh_digit256(_b(s), k) * 256**k for k in range(32)) == int.from_bytes(s, "little")
+        assert all(-8 <= H.cvh_digit16(_b(s), k) <= 8 for k in range(64))
+        assert all(-128 <= H.cvh_digit256(_b(s), k) <= 128 for k in range(32))
+
+
+def test_sha512_and_sha256(host_harness):
+    import hashlib
+    H = host_harness
+    rng = random.Random(7)
+    for ln in [0, 1, 31, 47, 48, 49, 63, 64, 111, 112, 113, 127, 128, 200, 300, 1000]:
+        pre = bytes(rng.randrange(256) for _ in range(64))
+        m = bytes(rng.randrange(256) for _ in range(ln))
+        o = _out(64)
+        H.cvh_sha512(_b(pre), 64, _b(m), ln, o)
+        assert bytes(o) == hashlib.sha512(pre + m).digest()
+        H.cvh_sha512(_b(pre[:32]), 32, _b(m), ln, o)
+        assert bytes(o) == hashlib.sha512(pre[:32] + m).digest()
+        o2 = _out(32)
+        H.cvh_sha256(_b(m), ln, o2)
+        assert bytes(o2) == hashlib.sha256(m).digest()
+
+
+def test_verify_logic_on_golden_corpus(host_harness, corpus, manifest):
+    H = host_harness
+    bad = []
+    for i in range(len(corpus["pk"])):
+        m = corpus["arena"][corpus["off"][i]:corpus["off"][i] + corpus["len"][i]].tobytes()
+        st = ctypes.c_int(0)
+        v = H.cvh_verify(_b(corpus["pk"][i].tobytes()), _b(corpus["sig"][i].tobytes()), _b(m), len(m),
+                         ctypes.byref(st))
+        if v != corpus["verdict"][i] or st.value != corpus["status"][i]:
+            bad.append(manifest["classes"][corpus["cls"][i]])
+    assert not bad, sorted(set(bad))
+
+
+def test_sign_logic_matches_oracle(host_harness):
+    H = host_harness
+    rng = random.Random(8)
+    for i in range(12):
+        seed = bytes(rng.randrange(256) for _ in range(32))
+        m = bytes(rng.randrange(256) for _ in range(rng.randrange(0, 320)))
+        pk, sg = _out(32), _out(64)
+        H.cvh_sign(_b(seed), _b(m), len(m), pk, sg)
+        assert bytes(pk) == E.public_key_of(seed)
+        assert bytes(sg) == E.sign(seed, m)
+
+
+def test_merkle_logic(host_harness, merkle_cases):
+    import hashlib
+    H = host_harness
+    m = merkle_cases
+    for t in range(len(m["ids"])):
+        b, e = int(m["tx_leaf_begin"][t]), int(m["tx_leaf_begin"][t + 1])
+        leaves = b"".join(hashlib.sha256(m["arena"][m["leaf_off"][k]:m["leaf_off"][k] + m["leaf_len"][k]].tobytes())
+                          .digest() for k in range(b, e))
+        o = _out(32)
+        ok = H.cvh_merkle_root(_b(leaves), e - b, o)
+        assert ok == (1 - int(m["status"][t]))
+        if ok:
+            assert bytes(o) == m["ids"][t].tobytes()

@@ -1,0 +1,182 @@
+"""The host-side mirror of the reference API, end to end on the GPU engine.  Each test restates a
+reference test (file:line in the docstring) with the same expectations."""
+import numpy as np
+import pytest
+
+import ed25519_ref as E
+from corda_amd import native
+from corda_amd.crypto import (CompositeKey, DigitalSignature, DummyPublicKey, EdDSAPublicKey, IllegalArgumentException,
+                              InvalidKeyException, NullPublicKey, NullSignature, SignatureException, verify_with_ecdsa)
+from corda_amd.notary import (BatchingNotary, Conflict, SignaturesMissing, SignRequest, TransactionInvalid)
+from corda_amd.transactions import (IllegalStateException, SecureHash, SignaturesMissingException, SignedTransaction,
+                                    WireTransaction, compute_ids, verify_signatures_batch)
+
+pytestmark = pytest.mark.gpu
+
+
+def seed(i):
+    return bytes([i % 251 + 1]) * 32
+
+
+def keypair(i):
+    s = seed(i)
+    return s, EdDSAPublicKey(E.public_key_of(s))
+
+
+def sign(s, msg):
+    return E.sign(s, msg)
+
+
+def make_stx(engine, signer_idx, must_idx=None, inputs=(b"in-0",), outputs=(b"out-0",), commands=(b"cmd",),
+             extra_must=()):
+    must_idx = signer_idx if must_idx is None else must_idx
+    must = [keypair(i)[1].composite for i in must_idx] + list(extra_must)
+    wtx = WireTransaction(inputs=inputs, outputs=outputs, commands=commands, must_sign=must,
+                          command_descriptions={m: f"cmd-{i}" for i, m in zip(must_idx, must)})
+    txid = wtx.id
+    sigs = [DigitalSignature.WithKey(keypair(i)[1], sign(keypair(i)[0], txid.bytes)) for i in signer_idx]
+    return SignedTransaction(wtx, sigs, txid)
+
+
+def test_sign_verify_round_trip_kryo_tests(engine):
+    """KryoTests.kt:61-75: 4-byte message round trip; wrong message throws."""
+    s, pk = keypair(1)
+    bits = b"\x00\x01\x02\x03"
+    sig = DigitalSignature.WithKey(pk, sign(s, bits))
+    sig.verify_with_ecdsa(bits)
+    with pytest.raises(SignatureException, match="Signature did not match"):
+        sig.verify_with_ecdsa(b"\x00\x01\x02\x04")
+
+
+def test_signed_data_wrong_key(engine):
+    """SignedDataTest.kt:12-29: a signature by key A claimed as key B fails."""
+    sa, pa = keypair(2)
+    sb, pb = keypair(3)
+    data = b"serialized-network-map-registration"
+    with pytest.raises(SignatureException):
+        verify_with_ecdsa(pb, data, DigitalSignature(sign(sa, data)))
+    verify_with_ecdsa(pa, data, DigitalSignature(sign(sa, data)))
+
+
+def test_non_eddsa_keys_and_lengths(engine):
+    """initVerify rejects NullPublicKey/DummyPublicKey; bad signature lengths throw SignatureException."""
+    with pytest.raises(InvalidKeyException):
+        NullSignature.verify_with_ecdsa(b"x")
+    with pytest.raises(InvalidKeyException):
+        verify_with_ecdsa(DummyPublicKey("x"), b"x", DigitalSignature(b"\x01" * 64))
+    s, pk = keypair(4)
+    with pytest.raises(SignatureException, match="length"):
+        verify_with_ecdsa(pk, b"m", DigitalSignature(sign(s, b"m")[:63]))
+    with pytest.raises(IllegalArgumentException):
+        DigitalSignature(b"")
+    with pytest.raises(IllegalArgumentException):
+        EdDSAPublicKey(b"\x00" * 31)
+
+
+def test_invalid_point_key(engine):
+    """A key whose bytes are not a point: the reference cannot build the EdDSAPublicKey."""
+    bad = bytes.fromhex("02" + "00" * 30 + "00")
+    st, _ = E.verify_ex(bad, b"", bytes(64))
+    assert st == E.ST_BAD_KEY
+    with pytest.raises(InvalidKeyException, match="GroupElement"):
+        verify_with_ecdsa(EdDSAPublicKey(bad), b"", DigitalSignature(bytes(64)))
+
+
+def test_transaction_tests_empty_and_missing(engine):
+    """TransactionTests.kt:25-58: empty sigs -> IllegalArgumentException; missing signer -> exact set;
+    allowedToBeMissing semantics."""
+    with pytest.raises(IllegalArgumentException):
+        SignedTransaction(WireTransaction(outputs=[b"o"]), [], SecureHash(bytes(32)))
+    stx = make_stx(engine, signer_idx=[5], must_idx=[5, 6, 7])
+    with pytest.raises(SignaturesMissingException) as ei:
+        stx.verify_signatures()
+    assert ei.value.missing == {keypair(6)[1].composite, keypair(7)[1].composite}
+    with pytest.raises(SignaturesMissingException) as ei:
+        stx.verify_signatures(keypair(6)[1].composite)
+    assert ei.value.missing == {keypair(7)[1].composite}
+    wtx = stx.verify_signatures(keypair(6)[1].composite, keypair(7)[1].composite)
+    assert wtx.id == stx.id
+
+
+def test_transaction_serialization_tests(engine):
+    """TransactionSerializationTests.kt:62-103: valid sigs verify; mutating id.bytes[5] -> SignatureException;
+    signatures from another transaction -> SignatureException."""
+    stx = make_stx(engine, signer_idx=[8, 9])
+    stx.verify_signatures()
+    mutated = bytearray(stx.id.bytes)
+    mutated[5] ^= 1
+    bad = SignedTransaction(stx._wtx, stx.sigs, SecureHash(bytes(mutated)))
+    with pytest.raises(SignatureException):
+        bad.verify_signatures()
+    other = make_stx(engine, signer_idx=[8, 9], outputs=(b"out-other",))
+    foreign = SignedTransaction(stx._wtx, other.sigs, stx.id)
+    with pytest.raises(SignatureException):
+        foreign.check_signatures_are_valid()
+
+
+def test_first_bad_signature_ordering(engine):
+    """checkSignaturesAreValid throws for the FIRST bad signature in list order."""
+    stx = make_stx(engine, signer_idx=[10, 11, 12])
+    sigs = list(stx.sigs)
+    sigs[1] = DigitalSignature.WithKey(sigs[1].by, b"\x00" * 64)
+    sigs[2] = DigitalSignature.WithKey(NullPublicKey, b"\x00" * 64)
+    s2 = SignedTransaction(stx._wtx, sigs, stx.id)
+    with pytest.raises(SignatureException, match="did not match"):
+        s2.check_signatures_are_valid()
+
+
+def test_id_mismatch_is_illegal_state(engine):
+    stx = make_stx(engine, signer_idx=[13])
+    other = WireTransaction(inputs=[b"x"], outputs=[b"y"], must_sign=stx._wtx.must_sign)
+    tampered = SignedTransaction(other, stx.sigs, stx.id)       # sigs are over the claimed id
+    tampered.check_signatures_are_valid()
+    with pytest.raises(IllegalStateException):
+        tampered.tx
+
+
+def test_batch_verify_matches_sequential(engine):
+    stxs = [make_stx(engine, signer_idx=[i, i + 1], must_idx=[i, i + 1, i + 2] if i % 5 == 0 else None,
+                     outputs=(bytes([i]) * 40,)) for i in range(20, 60)]
+    stxs[3] = SignedTransaction(stxs[3]._wtx, [DigitalSignature.WithKey(stxs[3].sigs[0].by, b"\x01" * 64)], stxs[3].id)
+    batch = verify_signatures_batch(stxs)
+    for stx, got in zip(stxs, batch):
+        try:
+            stx.verify_signatures()
+            exp = None
+        except Exception as e:  # noqa: BLE001
+            exp = e
+        assert type(got) is type(exp)
+
+
+def test_compute_ids_golden():
+    """PartialMerkleTreeTest.kt:23-26 through the WireTransaction mirror (leaves = Kryo chars a..f)."""
+    w = WireTransaction(outputs=[bytes([7, 0, ord(c)]) for c in "abcdef"])
+    compute_ids([w])
+    assert repr(w.id) == "F6D8FB3720114F8D040D64F633B0D9178EB09A55AA7D62FAE1A070D1BF561051"
+
+
+def test_notary_batch(engine):
+    """NotaryServiceTests / ValidatingNotaryServiceTests: valid txs get a notary signature over stx.id
+    that verifies; conflicts; missing signatures -> SignaturesMissing; bad signatures -> TransactionInvalid."""
+    notary = BatchingNotary(E.entropy_to_seed(20), validating=True, engine=engine)
+    assert notary.public_key.encoded == E.public_key_of(E.entropy_to_seed(20))
+    reqs = []
+    for i in range(8):
+        reqs.append(SignRequest(make_stx(engine, signer_idx=[70 + i], inputs=(b"state-%d" % i,)), caller=f"party{i}"))
+    reqs.append(SignRequest(make_stx(engine, signer_idx=[90], inputs=(b"state-0",)), caller="double-spender"))
+    reqs.append(SignRequest(make_stx(engine, signer_idx=[91], must_idx=[91, 92], inputs=(b"s-91",)), caller="p"))
+    bad = make_stx(engine, signer_idx=[93], inputs=(b"s-93",))
+    reqs.append(SignRequest(SignedTransaction(bad._wtx, [DigitalSignature.WithKey(bad.sigs[0].by, b"\x05" * 64)],
+                                              bad.id), caller="p"))
+    res = notary.notarise(reqs)
+    for i in range(8):
+        assert res[i].ok
+        res[i].sig.verify_with_ecdsa(reqs[i].stx.id.bytes)
+        assert res[i].sig.bits == E.sign(E.entropy_to_seed(20), reqs[i].stx.id.bytes)
+    assert isinstance(res[8].error, Conflict)
+    assert isinstance(res[9].error, SignaturesMissing)
+    assert isinstance(res[10].error, TransactionInvalid)
+    # the notary's own key is allowed to be missing (verifySignatures(notaryKey))
+    r2 = notary.notarise([SignRequest(make_stx(engine, signer_idx=[94], inputs=(b"s-94",),
+                                               extra_must=(notary.owning_key,)), caller="q")])
+    assert r2[0].ok
