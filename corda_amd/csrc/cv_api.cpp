@@ -13,7 +13,8 @@
 
 extern "C" {
 hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off,
-                      const uint32_t *len, uint64_t *bitmap, uint8_t *status, hipStream_t stream);
+                      const uint32_t *len, uint64_t *bitmap, uint8_t *status, uint32_t *ws_hs, uint32_t *ws_tab,
+                      uint32_t *ws_R, uint8_t *ws_ok, uint32_t ws_cap, hipStream_t stream);
 hipError_t cvk_sign(uint32_t n, const uint8_t *seed, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
                     uint8_t *pk, uint8_t *sig, hipStream_t stream);
 hipError_t cvk_merkle(uint32_t ntx, uint32_t nleaves, const uint8_t *arena, const uint64_t *leaf_off,
@@ -53,7 +54,32 @@ struct Device {
     int ordinal = 0;
     hipStream_t stream = nullptr;
     DevBuf pk, sig, arena, off, len, bitmap, status, seed, tx_begin, digest, ids;
+    DevBuf ws_hs, ws_tab, ws_R, ws_ok;   // verify workspace (hs 64 B + tab 1280 B + R 128 B + ok 1 B per signature)
+    uint32_t ws_cap = 0;
 };
+
+// Verify workspace capacity: batches above it run in chunks of this many signatures.
+constexpr uint32_t kVerifyChunk = 1u << 21;
+
+hipError_t ensure_verify_ws(Device &d, size_t n) {
+    uint32_t want = (uint32_t)std::min<size_t>(kVerifyChunk, (n + 511) / 512 * 512);
+    if (want <= d.ws_cap) return hipSuccess;
+    hipError_t e;
+    if ((e = d.ws_hs.ensure((size_t)want * 64)) != hipSuccess) return e;
+    if ((e = d.ws_tab.ensure((size_t)want * 1280)) != hipSuccess) return e;
+    if ((e = d.ws_R.ensure((size_t)want * 128)) != hipSuccess) return e;
+    if ((e = d.ws_ok.ensure((size_t)want)) != hipSuccess) return e;
+    d.ws_cap = want;
+    return hipSuccess;
+}
+
+hipError_t launch_verify(Device &d, uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
+                         const uint64_t *off, const uint32_t *len, uint64_t *bitmap, uint8_t *status, hipStream_t s) {
+    hipError_t e = ensure_verify_ws(d, n);
+    if (e != hipSuccess) return e;
+    return cvk_verify(n, pk, sig, arena, off, len, bitmap, status, d.ws_hs.as<uint32_t>(), d.ws_tab.as<uint32_t>(),
+                      d.ws_R.as<uint32_t>(), d.ws_ok.as<uint8_t>(), d.ws_cap, s);
+}
 
 int hip_rc(hipError_t e) {
     if (e == hipSuccess) return CV_OK;
@@ -121,7 +147,7 @@ void cv_close(cv_ctx *ctx) {
         (void)hipSetDevice(d.ordinal);
         if (d.stream) (void)hipStreamSynchronize(d.stream);
         for (DevBuf *b : {&d.pk, &d.sig, &d.arena, &d.off, &d.len, &d.bitmap, &d.status, &d.seed, &d.tx_begin,
-                          &d.digest, &d.ids})
+                          &d.digest, &d.ids, &d.ws_hs, &d.ws_tab, &d.ws_R, &d.ws_ok})
             b->release();
         if (d.stream) (void)hipStreamDestroy(d.stream);
     }
@@ -166,9 +192,9 @@ static int verify_shard(Device &d, size_t b, size_t e, const uint8_t *pk, const 
     if (hi > lo) CV_TRY(hipMemcpyAsync(d.arena.p, arena + lo, hi - lo, hipMemcpyHostToDevice, s));
     CV_TRY(hipMemcpyAsync(d.off.p, off + b, n * 8, hipMemcpyHostToDevice, s));
     CV_TRY(hipMemcpyAsync(d.len.p, len + b, n * 4, hipMemcpyHostToDevice, s));
-    CV_TRY(cvk_verify((uint32_t)n, d.pk.as<uint8_t>(), d.sig.as<uint8_t>(), d.arena.as<uint8_t>() - lo,
-                      d.off.as<uint64_t>(), d.len.as<uint32_t>(), d.bitmap.as<uint64_t>(),
-                      status ? d.status.as<uint8_t>() : nullptr, s));
+    CV_TRY(launch_verify(d, (uint32_t)n, d.pk.as<uint8_t>(), d.sig.as<uint8_t>(), d.arena.as<uint8_t>() - lo,
+                         d.off.as<uint64_t>(), d.len.as<uint32_t>(), d.bitmap.as<uint64_t>(),
+                         status ? d.status.as<uint8_t>() : nullptr, s));
     CV_TRY(hipMemcpyAsync(bitmap + b / 64, d.bitmap.p, words * 8, hipMemcpyDeviceToHost, s));
     if (status) CV_TRY(hipMemcpyAsync(status + b, d.status.p, n, hipMemcpyDeviceToHost, s));
     CV_TRY(hipStreamSynchronize(s));
@@ -322,10 +348,10 @@ int cv_ed25519_verify_device(cv_ctx *ctx, int device, size_t n, const void *d_pk
     if (!d || !d_pk || !d_sig || !d_arena || !d_off || !d_len || !d_bitmap) return CV_E_ARGS;
     CV_TRY(hipSetDevice(d->ordinal));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : d->stream;
-    CV_TRY(cvk_verify((uint32_t)n, static_cast<const uint8_t *>(d_pk), static_cast<const uint8_t *>(d_sig),
-                      static_cast<const uint8_t *>(d_arena), static_cast<const uint64_t *>(d_off),
-                      static_cast<const uint32_t *>(d_len), static_cast<uint64_t *>(d_bitmap),
-                      static_cast<uint8_t *>(d_status), s));
+    CV_TRY(launch_verify(*d, (uint32_t)n, static_cast<const uint8_t *>(d_pk), static_cast<const uint8_t *>(d_sig),
+                         static_cast<const uint8_t *>(d_arena), static_cast<const uint64_t *>(d_off),
+                         static_cast<const uint32_t *>(d_len), static_cast<uint64_t *>(d_bitmap),
+                         static_cast<uint8_t *>(d_status), s));
     return CV_OK;
 }
 

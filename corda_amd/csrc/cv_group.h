@@ -1,6 +1,6 @@
 // cv_group.h — edwards25519 group operations (a = -1 twisted Edwards, extended coordinates).
 //
-// Representations (HWCD'08 extended coordinates; names follow the usual ed25519 conventions):
+// Representations (HWCD'08 extended coordinates):
 //   p2     (X:Y:Z)            x = X/Z, y = Y/Z
 //   p3     (X:Y:Z:T)          + T = XY/Z
 //   p1p1   ((X:Z),(Y:T))      "completed": x = X/Z, y = Y/T — output of add/dbl before conversion
@@ -9,6 +9,11 @@
 // The unified addition is complete for d non-square, so every routine below is exact group
 // arithmetic on ALL curve points, torsion included — which is what makes the GPU's fixed-window
 // schedule produce the same point (hence the same verdict) as eddsa-0.1.0's slide()-based one.
+//
+// Limb bounds (units of M, cv_field.h): every p2/p3 coordinate is tight (T) at rest.  p1p1 from
+// add/madd: X=E<=3.01, Y=H<=2.02, Z=G<=3.03, T=F<=4.02; from dbl: E<=3.01, H'=T, G<=3.01, F'<=5.01.
+// Conversions therefore always pass p1p1.T as the unrestricted `f` operand of fe_mul (<= 8) and the
+// other coordinate as `g` (<= 3.3).
 #pragma once
 #include "cv_field.h"
 
@@ -18,10 +23,10 @@ struct ge_p1p1 { fe X, Y, Z, T; };
 struct ge_cached { fe YplusX, YminusX, Z, T2d; };
 struct ge_precomp { fe yplusx, yminusx, xy2d; };
 
-// curve constants in radix-2^25.5 limbs (values checked against the oracle by the host tests)
-#define CV_FE_D   {-10913610, 13857413, -15372611, 6949391, 114729, -8787816, -6275908, -3247719, -18696448, -12055116}
-#define CV_FE_D2  {-21827239, -5839606, -30745221, 13898782, 229458, 15978800, -12551817, -6495438, 29715968, 9444199}
-#define CV_FE_SQRTM1 {-32595792, -7943725, 9377950, 3500415, 12389472, -272473, -25146209, -2005654, 326686, 11406482}
+// curve constants, canonical limbs (< M_i), generated and checked by the host tests
+#define CV_FE_D   {56195235, 13857412, 51736253, 6949390, 114729, 24766616, 60832955, 30306712, 48412415, 21499315}
+#define CV_FE_D2  {45281625, 27714825, 36363642, 13898781, 229458, 15978800, 54557047, 27058993, 29715967, 9444199}
+#define CV_FE_SQRTM1 {34513072, 25610706, 9377949, 3500415, 12389472, 33281959, 41962654, 31548777, 326685, 11406482}
 
 CV_HD void fe_const_d(fe &h) { const fe c = {CV_FE_D}; h = c; }
 CV_HD void fe_const_d2(fe &h) { const fe c = {CV_FE_D2}; h = c; }
@@ -33,14 +38,14 @@ CV_HD void ge_cached_identity(ge_cached &r) { fe_one(r.YplusX); fe_one(r.YminusX
 CV_HD void ge_precomp_identity(ge_precomp &r) { fe_one(r.yplusx); fe_one(r.yminusx); fe_zero(r.xy2d); }
 
 CV_HD void ge_p1p1_to_p2(ge_p2 &r, const ge_p1p1 &p) {
-    fe_mul(r.X, p.X, p.T);
+    fe_mul(r.X, p.T, p.X);
     fe_mul(r.Y, p.Y, p.Z);
-    fe_mul(r.Z, p.Z, p.T);
+    fe_mul(r.Z, p.T, p.Z);
 }
 CV_HD void ge_p1p1_to_p3(ge_p3 &r, const ge_p1p1 &p) {
-    fe_mul(r.X, p.X, p.T);
+    fe_mul(r.X, p.T, p.X);
     fe_mul(r.Y, p.Y, p.Z);
-    fe_mul(r.Z, p.Z, p.T);
+    fe_mul(r.Z, p.T, p.Z);
     fe_mul(r.T, p.X, p.Y);
 }
 CV_HD void ge_p3_to_p2(ge_p2 &r, const ge_p3 &p) { r.X = p.X; r.Y = p.Y; r.Z = p.Z; }
@@ -48,24 +53,25 @@ CV_HD void ge_p3_to_cached(ge_cached &r, const ge_p3 &p) {
     fe d2;
     fe_const_d2(d2);
     fe_add(r.YplusX, p.Y, p.X);
-    fe_sub(r.YminusX, p.Y, p.X);
+    fe_sub<2>(r.YminusX, p.Y, p.X);
     r.Z = p.Z;
     fe_mul(r.T2d, p.T, d2);
 }
 
-// r = 2p: 4 squarings.  Output p1p1 coordinates are the negated (E, -H, G, -F) form, which names
-// the same projective point after conversion.
+// r = 2p: 4 squarings.  p1p1 = (E, H', G, F') with E = 2XY, H' = X^2+Y^2, G = Y^2-X^2,
+// F' = 2Z^2-G: the negated (E, -H, G, -F) form of HWCD's doubling, which names the same point.
 CV_HD void ge_p2_dbl(ge_p1p1 &r, const ge_p2 &p) {
-    fe t0;
-    fe_sq(r.X, p.X);            // XX
-    fe_sq(r.Z, p.Y);            // YY
-    fe_sq2(r.T, p.Z);           // 2ZZ
-    fe_add(r.Y, p.X, p.Y);
-    fe_sq(t0, r.Y);             // (X+Y)^2
-    fe_add(r.Y, r.Z, r.X);      // YY + XX
-    fe_sub(r.Z, r.Z, r.X);      // YY - XX
-    fe_sub(r.X, t0, r.Y);       // 2XY
-    fe_sub(r.T, r.T, r.Z);      // 2ZZ - (YY - XX)
+    fe xx, yy, zz2, a, aa, hs;
+    fe_sq(xx, p.X);
+    fe_sq(yy, p.Y);
+    fe_sq2(zz2, p.Z);
+    fe_add(a, p.X, p.Y);
+    fe_sq(aa, a);
+    fe_add(hs, yy, xx);
+    fe_carry(r.Y, hs);            // H' (tight: it is subtracted below with a 2p bias)
+    fe_sub<2>(r.Z, yy, xx);       // G  <= 3.01
+    fe_sub<2>(r.X, aa, r.Y);      // E  <= 3.01
+    fe_sub<4>(r.T, zz2, r.Z);     // F' <= 5.01
 }
 CV_HD void ge_p3_dbl(ge_p1p1 &r, const ge_p3 &p) {
     ge_p2 q;
@@ -73,53 +79,38 @@ CV_HD void ge_p3_dbl(ge_p1p1 &r, const ge_p3 &p) {
     ge_p2_dbl(r, q);
 }
 
-// r = p + q (q cached)
+// r = p + q (q cached, possibly conditionally negated)
 CV_HD void ge_add(ge_p1p1 &r, const ge_p3 &p, const ge_cached &q) {
-    fe t0;
-    fe_add(r.X, p.Y, p.X);
-    fe_sub(r.Y, p.Y, p.X);
-    fe_mul(r.Z, r.X, q.YplusX);
-    fe_mul(r.Y, r.Y, q.YminusX);
-    fe_mul(r.T, q.T2d, p.T);
-    fe_mul(r.X, p.Z, q.Z);
-    fe_add(t0, r.X, r.X);
-    fe_sub(r.X, r.Z, r.Y);
-    fe_add(r.Y, r.Z, r.Y);
-    fe_add(r.Z, t0, r.T);
-    fe_sub(r.T, t0, r.T);
-}
-// r = p - q (q cached)
-CV_HD void ge_sub(ge_p1p1 &r, const ge_p3 &p, const ge_cached &q) {
-    fe t0;
-    fe_add(r.X, p.Y, p.X);
-    fe_sub(r.Y, p.Y, p.X);
-    fe_mul(r.Z, r.X, q.YminusX);
-    fe_mul(r.Y, r.Y, q.YplusX);
-    fe_mul(r.T, q.T2d, p.T);
-    fe_mul(r.X, p.Z, q.Z);
-    fe_add(t0, r.X, r.X);
-    fe_sub(r.X, r.Z, r.Y);
-    fe_add(r.Y, r.Z, r.Y);
-    fe_sub(r.Z, t0, r.T);
-    fe_add(r.T, t0, r.T);
+    fe s, d, a, b, c, dd;
+    fe_add(s, p.Y, p.X);          // <= 2.02
+    fe_sub<2>(d, p.Y, p.X);       // <= 3.01
+    fe_mul(a, q.YplusX, s);
+    fe_mul(b, q.YminusX, d);
+    fe_mul(c, q.T2d, p.T);
+    fe_mul(dd, p.Z, q.Z);
+    fe_add(dd, dd, dd);
+    fe_sub<2>(r.X, a, b);         // E <= 3.01
+    fe_add(r.Y, a, b);            // H <= 2.02
+    fe_add(r.Z, dd, c);           // G <= 3.03
+    fe_sub<2>(r.T, dd, c);        // F <= 4.02
 }
 // r = p + q (q affine precomp)
 CV_HD void ge_madd(ge_p1p1 &r, const ge_p3 &p, const ge_precomp &q) {
-    fe t0;
-    fe_add(r.X, p.Y, p.X);
-    fe_sub(r.Y, p.Y, p.X);
-    fe_mul(r.Z, r.X, q.yplusx);
-    fe_mul(r.Y, r.Y, q.yminusx);
-    fe_mul(r.T, q.xy2d, p.T);
-    fe_add(t0, p.Z, p.Z);
-    fe_sub(r.X, r.Z, r.Y);
-    fe_add(r.Y, r.Z, r.Y);
-    fe_add(r.Z, t0, r.T);
-    fe_sub(r.T, t0, r.T);
+    fe s, d, a, b, c, dd;
+    fe_add(s, p.Y, p.X);
+    fe_sub<2>(d, p.Y, p.X);
+    fe_mul(a, q.yplusx, s);
+    fe_mul(b, q.yminusx, d);
+    fe_mul(c, q.xy2d, p.T);
+    fe_add(dd, p.Z, p.Z);
+    fe_sub<2>(r.X, a, b);
+    fe_add(r.Y, a, b);
+    fe_add(r.Z, dd, c);
+    fe_sub<2>(r.T, dd, c);
 }
 
 // Conditional negation of a table entry, branch-free: -(x,y) = (-x, y) swaps Y+X <-> Y-X and
-// negates T.
+// negates T (2p - T, still within the g <= 3.3 budget).
 CV_HD void ge_cached_cneg(ge_cached &r, bool neg) {
     fe a = r.YplusX, b = r.YminusX, t;
     fe_sel(r.YplusX, a, b, neg);
@@ -147,19 +138,36 @@ __host__ __device__ inline void ge_p2_encode(uint32_t w[8], const ge_p2 &p) {
     w[7] |= (xw[0] & 1u) << 31;
 }
 
+// EdDSAPublicKey.getAbyte() (= A.toByteArray() after decoding) WITHOUT the square root: the decoded
+// y is the key's 255-bit value mod p, and the decoded x has isNegative(x) == bit 255 unless x = 0,
+// which happens exactly when y = +-1.  (For keys that fail to decode the value is irrelevant: the
+// verdict is forced false.)
+CV_HD void ge_abyte_from_key(uint32_t abyte[8], const uint32_t w[8]) {
+    fe y;
+    fe_from_words(y, w);
+    fe_to_words(abyte, y);
+    uint32_t one_or = abyte[0] ^ 1u, m1_or = abyte[0] ^ 0xffffffecu;     // y == 1, y == p - 1
+#pragma unroll
+    for (int q = 1; q < 7; q++) { one_or |= abyte[q]; m1_or |= abyte[q] ^ 0xffffffffu; }
+    one_or |= abyte[7];
+    m1_or |= abyte[7] ^ 0x7fffffffu;
+    const bool x_zero = (one_or == 0) | (m1_or == 0);
+    abyte[7] |= (x_zero ? 0u : (w[7] & 0x80000000u));
+}
+
 // eddsa-0.1.0 GroupElement(curve, bytes) decode of a public key given as 8 LE words.
 // Returns false where the reference throws IllegalArgumentException("not a valid GroupElement").
 // y keeps its non-reduced value; x is negated when isNegative(x) != bit 255 (x = 0 with the sign
-// bit set is therefore accepted as x = 0).
+// bit set is therefore accepted as x = 0).  All output coordinates are tight.
 __host__ __device__ inline bool ge_decode_0_1_0(ge_p3 &A, const uint32_t w[8]) {
     fe y, yy, u, v, v3, x, vxx, chk, one, d;
     fe_from_words(y, w);
     fe_one(one);
     fe_const_d(d);
     fe_sq(yy, y);
-    fe_sub(u, yy, one);          // u = y^2 - 1
+    fe_sub<2>(u, yy, one);       // u = y^2 - 1         (<= 3.01)
     fe_mul(v, yy, d);
-    fe_add(v, v, one);           // v = d y^2 + 1
+    fe_add(v, v, one);           // v = d y^2 + 1       (<= 1.02)
     fe_sq(v3, v);
     fe_mul(v3, v3, v);           // v^3
     fe_sq(x, v3);
@@ -170,7 +178,7 @@ __host__ __device__ inline bool ge_decode_0_1_0(ge_p3 &A, const uint32_t w[8]) {
     fe_mul(x, x, u);             // u v^3 (u v^7)^((p-5)/8)
     fe_sq(vxx, x);
     fe_mul(vxx, vxx, v);
-    fe_sub(chk, vxx, u);
+    fe_sub<4>(chk, vxx, u);
     bool ok = true;
     if (!fe_is_zero(chk)) {
         fe_add(chk, vxx, u);
@@ -183,6 +191,7 @@ __host__ __device__ inline bool ge_decode_0_1_0(ge_p3 &A, const uint32_t w[8]) {
     const int sign = (int)(w[7] >> 31);
     fe nx;
     fe_neg(nx, x);
+    fe_carry(nx, nx);
     fe_sel(x, x, nx, fe_is_negative(x) != sign);
     A.X = x;
     A.Y = y;

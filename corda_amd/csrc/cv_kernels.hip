@@ -22,7 +22,7 @@
 
 #define CV_BLOCK 256
 
-__device__ __forceinline__ void stage_btab(int32_t *lds) {
+__device__ __forceinline__ void stage_btab(uint32_t *lds) {
     for (int i = threadIdx.x; i < CV_BTAB_ENTRIES * CV_BTAB_STRIDE; i += blockDim.x) lds[i] = CV_BTAB[i];
     __syncthreads();
 }
@@ -34,32 +34,66 @@ __device__ __forceinline__ void load_words8(uint32_t w[8], const uint8_t *p) {
     w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
 }
 
-// ---------------------------------------------------------------- verify
+// ---------------------------------------------------------------- verify (three kernels)
 // SoA records: pk[n][32], sig[n][64]; message i = arena[off[i] .. off[i]+len[i]).
-// bitmap[i/64] bit (i%64) = verdict; status[i] (optional) = 0 ok, 1 key is not a valid point.
-__global__ __launch_bounds__(CV_BLOCK, 2) void cv_verify_kernel(
-    uint32_t n, const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig,
-    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ off, const uint32_t *__restrict__ len,
-    uint64_t *__restrict__ bitmap, uint8_t *__restrict__ status) {
-    __shared__ __attribute__((aligned(16))) int32_t btab[CV_BTAB_ENTRIES * CV_BTAB_STRIDE];
-    stage_btab(btab);
+// Workspace per signature: hs (16 words), tab (320 words, per-lane contiguous so each table
+// lookup is ten 16-B loads of one lane's own entry), R record (32 words), ok byte.
 
-    const uint32_t gid = blockIdx.x * CV_BLOCK + threadIdx.x;
-    const uint32_t wave_base = gid & ~63u;
-    if (wave_base >= n) return;                       // whole wave past the end
-    const bool active = gid < n;
-    const uint32_t i = active ? gid : n - 1;          // inactive lanes recompute a valid record
+__device__ __forceinline__ void store_words(uint32_t *dst, const uint32_t *src, int nwords4) {
+    uint4 *d = reinterpret_cast<uint4 *>(dst);
+    for (int q = 0; q < nwords4; q++) d[q] = make_uint4(src[4 * q], src[4 * q + 1], src[4 * q + 2], src[4 * q + 3]);
+}
 
+__global__ __launch_bounds__(CV_BLOCK, 2) void cv_prep_kernel(
+    uint32_t n, const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint8_t *__restrict__ arena,
+    const uint64_t *__restrict__ off, const uint32_t *__restrict__ len, uint32_t *__restrict__ ws_hs,
+    uint32_t *__restrict__ ws_tab, uint8_t *__restrict__ ws_ok, uint8_t *__restrict__ status) {
+    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (i >= n) return;
     uint32_t aw[8], rw[8], sw[8];
     load_words8(aw, pk + (size_t)i * 32);
     load_words8(rw, sig + (size_t)i * 64);
     load_words8(sw, sig + (size_t)i * 64 + 32);
-    bool key_ok;
-    const bool ok = active && cv_verify_one(btab, aw, rw, sw, arena + off[i], len[i], &key_ok);
+    uint32_t hs[CV_HS_WORDS];
+    const bool ok = cv_verify_prep(aw, rw, sw, arena + off[i], len[i], hs, ws_tab + (size_t)i * CV_TAB_WORDS);
+    store_words(ws_hs + (size_t)i * CV_HS_WORDS, hs, CV_HS_WORDS / 4);
+    ws_ok[i] = ok ? 1 : 0;
+    if (status) status[i] = ok ? 0 : 1;
+}
 
-    const uint64_t mask = __ballot(ok);
-    if ((threadIdx.x & 63) == 0) bitmap[wave_base >> 6] = mask;
-    if (status && active) status[i] = key_ok ? 0 : 1;
+__global__ __launch_bounds__(CV_BLOCK, 2) void cv_straus_kernel(uint32_t n, const uint32_t *__restrict__ ws_hs,
+                                                                const uint32_t *__restrict__ ws_tab,
+                                                                uint32_t *__restrict__ ws_R) {
+    __shared__ __attribute__((aligned(16))) uint32_t btab[CV_BTAB_ENTRIES * CV_BTAB_STRIDE];
+    stage_btab(btab);
+    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    ge_p2 R;
+    cv_verify_straus(btab, ws_hs + (size_t)i * CV_HS_WORDS, ws_tab + (size_t)i * CV_TAB_WORDS, R);
+    uint32_t rec[CV_R_WORDS];
+    fe_store(rec, R.X);
+    fe_store(rec + 10, R.Y);
+    fe_store(rec + 20, R.Z);
+    rec[30] = rec[31] = 0;
+    store_words(ws_R + (size_t)i * CV_R_WORDS, rec, CV_R_WORDS / 4);
+}
+
+// lane j: signatures [8j, 8j+8) -> bitmap byte j (bytes past n are written as zero)
+__global__ __launch_bounds__(CV_BLOCK) void cv_finish_kernel(uint32_t n, uint32_t nbytes,
+                                                             const uint8_t *__restrict__ sig,
+                                                             const uint32_t *__restrict__ ws_R,
+                                                             const uint8_t *__restrict__ ws_ok,
+                                                             uint8_t *__restrict__ bitmap_bytes) {
+    const uint32_t j = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (j >= nbytes) return;
+    const uint32_t b = j * CV_FIN_CHUNK;
+    uint32_t bits = 0;
+    if (b < n) {
+        const int cnt = (int)(n - b < CV_FIN_CHUNK ? n - b : CV_FIN_CHUNK);
+        bits = cv_verify_finish(ws_R + (size_t)b * CV_R_WORDS, reinterpret_cast<const uint32_t *>(sig + (size_t)b * 64),
+                                ws_ok + b, cnt);
+    }
+    bitmap_bytes[j] = (uint8_t)bits;
 }
 
 // ---------------------------------------------------------------- sign (synthetic inputs)
@@ -67,7 +101,7 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_sign_kernel(
     uint32_t n, const uint8_t *__restrict__ seed, const uint8_t *__restrict__ arena,
     const uint64_t *__restrict__ off, const uint32_t *__restrict__ len, uint8_t *__restrict__ pk_out,
     uint8_t *__restrict__ sig_out) {
-    __shared__ __attribute__((aligned(16))) int32_t btab[CV_BTAB_ENTRIES * CV_BTAB_STRIDE];
+    __shared__ __attribute__((aligned(16))) uint32_t btab[CV_BTAB_ENTRIES * CV_BTAB_STRIDE];
     stage_btab(btab);
     const uint32_t gid = blockIdx.x * CV_BLOCK + threadIdx.x;
     if (gid >= n) return;
@@ -115,12 +149,25 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_merkle_tree_kernel(uint32_t ntx, 
 // ---------------------------------------------------------------- launchers (internal ABI)
 extern "C" {
 
+// Verify n signatures with the workspace ws (capacity ws_cap signatures, a multiple of 512); the
+// batch is processed in chunks of ws_cap.  bitmap gets ceil(n/64) words.
 hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off,
-                      const uint32_t *len, uint64_t *bitmap, uint8_t *status, hipStream_t stream) {
+                      const uint32_t *len, uint64_t *bitmap, uint8_t *status, uint32_t *ws_hs, uint32_t *ws_tab,
+                      uint32_t *ws_R, uint8_t *ws_ok, uint32_t ws_cap, hipStream_t stream) {
     if (n == 0) return hipSuccess;
-    const uint32_t blocks = (n + CV_BLOCK - 1) / CV_BLOCK;
-    hipLaunchKernelGGL(cv_verify_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, n, pk, sig, arena, off, len,
-                       bitmap, status);
+    if (ws_cap == 0 || ws_cap % 512) return hipErrorInvalidValue;
+    for (uint32_t c0 = 0; c0 < n; c0 += ws_cap) {
+        const uint32_t m = (n - c0 < ws_cap) ? n - c0 : ws_cap;
+        const uint32_t blocks = (m + CV_BLOCK - 1) / CV_BLOCK;
+        hipLaunchKernelGGL(cv_prep_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, pk + (size_t)c0 * 32,
+                           sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_hs, ws_tab, ws_ok,
+                           status ? status + c0 : nullptr);
+        hipLaunchKernelGGL(cv_straus_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, ws_tab, ws_R);
+        const uint32_t nbytes = ((m + 63) / 64) * 8;
+        hipLaunchKernelGGL(cv_finish_kernel, dim3((nbytes + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, stream, m,
+                           nbytes, sig + (size_t)c0 * 64, ws_R, ws_ok,
+                           reinterpret_cast<uint8_t *>(bitmap) + (size_t)c0 / 8);
+    }
     return hipGetLastError();
 }
 
@@ -180,12 +227,12 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_femul_bench_kernel(uint32_t it
 #pragma unroll
     for (int k = 0; k < 4; k++)
 #pragma unroll
-        for (int i = 0; i < 10; i++) x[k].v[i] = (int32_t)((threadIdx.x * 977u + k * 131u + i * 7919u) & 0xffffff);
+        for (int i = 0; i < 10; i++) x[k].v[i] = (threadIdx.x * 977u + k * 131u + i * 7919u) & 0xffffff;
     for (uint32_t it = 0; it < iters; it++) {
 #pragma unroll
         for (int k = 0; k < 4; k++) fe_mul(x[k], x[k], x[(k + 1) & 3]);
     }
-    int32_t s = 0;
+    uint32_t s = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++)
 #pragma unroll

@@ -95,56 +95,51 @@ __host__ __device__ inline void sha512_compress(uint64_t st[8], uint64_t w[16]) 
     st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
-// Byte t of the stream (pre || msg || 0x80 || 0.. || len128_be) where pre is 64 bytes given as 16
-// LE uint32 words (R || Abyte, or prefix || unused), total = 64 + mlen bytes of data.
-__host__ __device__ inline uint32_t sha512_stream_byte(const uint32_t pre[16], int npre, const uint8_t *msg, uint32_t mlen,
-                                              uint32_t t, uint32_t total_padded) {
-    const uint32_t data = npre + mlen;
-    if (t < (uint32_t)npre) return (pre[t >> 2] >> ((t & 3) * 8)) & 0xffu;
-    if (t < data) return msg[t - npre];
-    if (t == data) return 0x80u;
-    // 128-bit big-endian bit length in the last 16 bytes (only the low 64 bits can be non-zero)
-    if (t >= total_padded - 8) {
-        const uint64_t bits = (uint64_t)data * 8;
-        const int sh = 8 * (int)(total_padded - 1 - t);
-        return (uint32_t)(bits >> sh) & 0xffu;
+// Little-endian dword of message bytes [t, t+4) (t a multiple of 4 relative to the message start),
+// with bytes past mlen replaced by the SHA padding (0x80 at mlen, zeros after).  Reads are aligned
+// dwords, and only dwords that contain at least one message byte are touched, so an unaligned
+// message ending at the very end of an allocation never reads past it.
+CV_HD uint32_t msg_dword_le(const uint8_t *msg, uint32_t mlen, uint32_t t) {
+    if (t > mlen) return 0;
+    const uintptr_t a = (uintptr_t)(msg + t);
+    const uint32_t sh = (uint32_t)(a & 3u);
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(a - sh);
+    const uint32_t lo = t < mlen ? p[0] : 0u;
+    const uint32_t hi = (sh != 0u && t + 4 - sh < mlen) ? p[1] : 0u;
+    uint32_t v = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * sh));
+    if (t + 4 > mlen) {
+        const uint32_t valid = mlen - t;                      // 0..3 bytes of message left
+        v = (v & ((1u << (8 * valid)) - 1u)) | (0x80u << (8 * valid));
     }
-    return 0;
+    return v;
 }
 
 // SHA-512(pre[0:npre] || msg[0:mlen]) with npre in {32, 64} (pre as LE words); out = 16 LE words
 // of the 64-byte digest (byte order as produced by the hash, i.e. digest byte k = out[k/4] >> 8(k%4)).
 __host__ __device__ inline void sha512_pre_msg(uint32_t out[16], const uint32_t pre[16], int npre, const uint8_t *msg,
-                                      uint32_t mlen) {
+                                               uint32_t mlen) {
     uint64_t st[8];
     sha512_init(st);
     const uint32_t data = npre + mlen;
     const uint32_t nblocks = (data + 1 + 16 + 127) / 128;
     const uint32_t total = nblocks * 128;
+    const uint64_t bits = (uint64_t)data * 8;
+#pragma nounroll
     for (uint32_t blk = 0; blk < nblocks; blk++) {
         uint64_t w[16];
-        const uint32_t base = blk * 128;
-        if (blk == 0 && npre == 64) {
-            // words 0..7 come straight from the prefix words
 #pragma unroll
-            for (int j = 0; j < 8; j++)
-                w[j] = ((uint64_t)cv_bswap32(pre[2 * j]) << 32) | cv_bswap32(pre[2 * j + 1]);
+        for (int j = 0; j < 16; j++) {
+            uint32_t d[2];
 #pragma unroll
-            for (int j = 8; j < 16; j++) {
-                uint64_t v = 0;
-#pragma unroll
-                for (int q = 0; q < 8; q++)
-                    v = (v << 8) | sha512_stream_byte(pre, npre, msg, mlen, base + 8 * j + q, total);
-                w[j] = v;
+            for (int hl = 0; hl < 2; hl++) {
+                const uint32_t u = blk * 128 + 8 * j + 4 * hl;    // stream offset of this dword
+                uint32_t le;
+                if (u < (uint32_t)npre) le = pre[u >> 2];
+                else le = msg_dword_le(msg, mlen, u - npre);
+                d[hl] = cv_bswap32(le);
+                if (u >= total - 8) d[hl] = (uint32_t)(bits >> (hl ? 0 : 32));
             }
-        } else {
-            for (int j = 0; j < 16; j++) {
-                uint64_t v = 0;
-#pragma unroll
-                for (int q = 0; q < 8; q++)
-                    v = (v << 8) | sha512_stream_byte(pre, npre, msg, mlen, base + 8 * j + q, total);
-                w[j] = v;
-            }
+            w[j] = ((uint64_t)d[0] << 32) | d[1];
         }
         sha512_compress(st, w);
     }

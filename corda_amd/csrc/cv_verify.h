@@ -10,13 +10,13 @@
 #include "cv_tables.h"
 
 // k*B for a signed digit k in [-128, 128] from the precomp table (LDS on the GPU)
-CV_HD void btab_select(ge_precomp &r, const int32_t *btab, int k) {
+CV_HD void btab_select(ge_precomp &r, const uint32_t *btab, int k) {
     const int m = k < 0 ? -k : k;
-    const int4 *row = reinterpret_cast<const int4 *>(btab + m * CV_BTAB_STRIDE);
-    int32_t t[32];
+    const uint4 *row = reinterpret_cast<const uint4 *>(btab + m * CV_BTAB_STRIDE);
+    uint32_t t[32];
 #pragma unroll
     for (int q = 0; q < 8; q++) {
-        const int4 v = row[q];
+        const uint4 v = row[q];
         t[4 * q] = v.x; t[4 * q + 1] = v.y; t[4 * q + 2] = v.z; t[4 * q + 3] = v.w;
     }
 #pragma unroll
@@ -29,7 +29,7 @@ CV_HD void btab_select(ge_precomp &r, const int32_t *btab, int k) {
 }
 
 // [k]B for a scalar k < 2^255: signed radix-256 digits from the table, 32 madds + 248 doublings.
-__host__ __device__ inline void ge_scalarmult_base(ge_p3 &R, const uint32_t k[8], const int32_t *btab) {
+__host__ __device__ inline void ge_scalarmult_base(ge_p3 &R, const uint32_t k[8], const uint32_t *btab) {
     ge_p3_identity(R);
     ge_p1p1 t;
     ge_p2 q;
@@ -57,104 +57,217 @@ CV_HD void ge_p3_encode(uint32_t w[8], const ge_p3 &p) {
     ge_p2_encode(w, q);
 }
 
-// ---------------------------------------------------------------- verify one signature
-// eddsa-0.1.0 EdDSAEngine.verify for one record (see cv_kernels.hip header for the schedule).
-// aw = public key words, rw / sw = R / S words (all 8 LE uint32), msg = message bytes.
-// Returns the verdict; *key_ok = false where the reference cannot even build the key.
-__host__ __device__ inline bool cv_verify_one(const int32_t *btab, const uint32_t aw[8], const uint32_t rw[8],
-                                              const uint32_t sw[8], const uint8_t *msg, uint32_t mlen,
-                                              bool *key_ok_out) {
-    // ---- key decode + canonical re-encoding (EdDSAPublicKey.Abyte)
-    ge_p3 A;
-    const bool key_ok = ge_decode_0_1_0(A, aw);
-    uint32_t abyte[8];
-    {
-        uint32_t xw[8];
-        fe_to_words(abyte, A.Y);
-        fe_to_words(xw, A.X);
-        abyte[7] |= (xw[0] & 1u) << 31;
+// ---------------------------------------------------------------- verify: three phases
+// eddsa-0.1.0 EdDSAEngine.verify, split so each GPU kernel keeps a small register working set:
+//   phase 1 (prep)   : decode A, Abyte, h = SHA-512(R||Abyte||M) mod L, s = effective S mod L,
+//                      table of k*(-A), k = 1..8 (cached form) -> workspace
+//   phase 2 (straus) : R' = [h](-A) + [s]B by joint fixed-window Straus -> (X:Y:Z) in workspace
+//   phase 3 (finish) : Z^-1 by Montgomery's trick over CV_FIN_CHUNK consecutive signatures per lane,
+//                      encode R', byte-compare with R, verdict bits
+// Invalid keys are replaced by the identity in phase 1 (verdict forced false) so that every Z
+// entering the batch inversion is a non-zero coordinate of a genuine curve point.
+
+#define CV_TAB_ENTRIES 8            // k*(-A), k = 1..8
+#define CV_TAB_WORDS (CV_TAB_ENTRIES * 40)
+#define CV_HS_WORDS 16              // h (8 words) || s (8 words)
+#define CV_R_WORDS 32               // X, Y, Z (10 limbs each) + 2 pad (16-B aligned records)
+#define CV_FIN_CHUNK 8              // signatures per lane in the finish phase
+
+CV_HD void fe_store(uint32_t *p, const fe &f) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) p[i] = f.v[i];
+}
+CV_HD void fe_load(fe &f, const uint32_t *p) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) f.v[i] = p[i];
+}
+CV_HD void ge_cached_store(uint32_t *p, const ge_cached &c) {
+    fe_store(p, c.YplusX);
+    fe_store(p + 10, c.YminusX);
+    fe_store(p + 20, c.Z);
+    fe_store(p + 30, c.T2d);
+}
+// 40 words, 16-byte aligned: ten 16-byte loads
+CV_HD void ge_cached_load(ge_cached &c, const uint32_t *p) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(p);
+    uint32_t t[40];
+#pragma unroll
+    for (int j = 0; j < 10; j++) {
+        const uint4 v = q[j];
+        t[4 * j] = v.x; t[4 * j + 1] = v.y; t[4 * j + 2] = v.z; t[4 * j + 3] = v.w;
     }
-    // ---- h = SHA-512(R || Abyte || M) mod L
-    uint32_t h[8];
+    fe_load(c.YplusX, t);
+    fe_load(c.YminusX, t + 10);
+    fe_load(c.Z, t + 20);
+    fe_load(c.T2d, t + 30);
+}
+
+// Phase 1.  Returns key_ok.  hs = h || s (16 words), tab = CV_TAB_WORDS words (16-B aligned).
+__host__ __device__ inline bool cv_verify_prep(const uint32_t aw[8], const uint32_t rw[8], const uint32_t sw[8],
+                                               const uint8_t *msg, uint32_t mlen, uint32_t *hs, uint32_t *tab) {
+    // hash first (its state is dead before the point decode starts: small live set)
     {
-        uint32_t pre[16], dig[16];
+        uint32_t pre[16], dig[16], h[8], abyte[8];
+        ge_abyte_from_key(abyte, aw);
 #pragma unroll
         for (int q = 0; q < 8; q++) { pre[q] = rw[q]; pre[8 + q] = abyte[q]; }
         sha512_pre_msg(dig, pre, 64, msg, mlen);
         sc_reduce512(h, dig);
+#pragma unroll
+        for (int q = 0; q < 8; q++) hs[q] = h[q];
     }
-    // ---- effective S (slide carry loss) reduced mod L
-    uint32_t s[8];
-    sc_effective_s(s, sw);
-
-    // ---- per-lane table: atab[k] = k * (-A), k = 0..8 (cached form)
-    ge_cached atab[9];
     {
-        ge_p3 nA, P;
-        fe_neg(nA.X, A.X);
-        nA.Y = A.Y;
-        nA.Z = A.Z;
-        fe_neg(nA.T, A.T);
-        ge_cached_identity(atab[0]);
-        ge_p3_to_cached(atab[1], nA);
-        ge_p1p1 t;
-        ge_p3_dbl(t, nA);
-        ge_p1p1_to_p3(P, t);
-        ge_p3_to_cached(atab[2], P);
-#pragma unroll 1
-        for (int k = 3; k <= 8; k++) {
-            ge_add(t, P, atab[1]);
-            ge_p1p1_to_p3(P, t);
-            ge_p3_to_cached(atab[k], P);
-        }
+        uint32_t s[8];
+        sc_effective_s(s, sw);
+#pragma unroll
+        for (int q = 0; q < 8; q++) hs[8 + q] = s[q];
     }
+    ge_p3 A;
+    const bool key_ok = ge_decode_0_1_0(A, aw);
+    if (!key_ok) ge_p3_identity(A);
+    ge_p3 nA, P;
+    fe_neg(nA.X, A.X);
+    fe_carry(nA.X, nA.X);
+    nA.Y = A.Y;
+    nA.Z = A.Z;
+    fe_neg(nA.T, A.T);
+    fe_carry(nA.T, nA.T);
+    ge_cached c1, c;
+    ge_p3_to_cached(c1, nA);
+    ge_cached_store(tab, c1);
+    ge_p1p1 t;
+    ge_p3_dbl(t, nA);
+    ge_p1p1_to_p3(P, t);
+    ge_p3_to_cached(c, P);
+    ge_cached_store(tab + 40, c);
+#pragma unroll 1
+    for (int k = 3; k <= 8; k++) {
+        ge_add(t, P, c1);
+        ge_p1p1_to_p3(P, t);
+        ge_p3_to_cached(c, P);
+        ge_cached_store(tab + 40 * (k - 1), c);
+    }
+    return key_ok;
+}
 
-    // ---- joint Straus: R' = sum_w 16^w (a_w * (-A) + [w even] b_{w/2} * B)
-    ge_p3 R;
-    ge_p3_identity(R);
+// Phase 2: R' = sum_w 16^w (a_w * (-A) + [w even] b_{w/2} * B) as (X:Y:Z).
+// Each window: 4 doublings (3 end in p2, the last in p3 for the add), the -A add, and every other
+// window the B madd; the window always ends in p2 (no T needed by the next doubling).
+__host__ __device__ inline void cv_verify_straus(const uint32_t *btab, const uint32_t *hs, const uint32_t *tab,
+                                                 ge_p2 &out) {
+    uint32_t h[8], s[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) { h[q] = hs[q]; s[q] = hs[8 + q]; }
+    ge_p2 R;
+    ge_p2_identity(R);
 #pragma unroll 1
     for (int w = 63; w >= 0; w--) {
         ge_p1p1 t;
+        ge_p3 R3;
         if (w != 63) {
-            ge_p2 q;
-            ge_p3_to_p2(q, R);
-            ge_p2_dbl(t, q);
-            ge_p1p1_to_p2(q, t);
-            ge_p2_dbl(t, q);
-            ge_p1p1_to_p2(q, t);
-            ge_p2_dbl(t, q);
-            ge_p1p1_to_p2(q, t);
-            ge_p2_dbl(t, q);
-            ge_p1p1_to_p3(R, t);
+            ge_p2_dbl(t, R);
+            ge_p1p1_to_p2(R, t);
+            ge_p2_dbl(t, R);
+            ge_p1p1_to_p2(R, t);
+            ge_p2_dbl(t, R);
+            ge_p1p1_to_p2(R, t);
+            ge_p2_dbl(t, R);
+            ge_p1p1_to_p3(R3, t);
+        } else {
+            ge_p3_identity(R3);
         }
         {
             const int a = digit16(h, w);
-            ge_cached e = atab[a < 0 ? -a : a];
+            ge_cached e;
+            const int m = a < 0 ? -a : a;
+            if (m) {
+                ge_cached_load(e, tab + 40 * (m - 1));
+            } else {
+                ge_cached_identity(e);
+            }
             ge_cached_cneg(e, a < 0);
-            ge_add(t, R, e);
-            ge_p1p1_to_p3(R, t);
+            ge_add(t, R3, e);
         }
         if ((w & 1) == 0) {
+            ge_p1p1_to_p3(R3, t);
             ge_precomp e;
             btab_select(e, btab, digit256(s, w >> 1));
-            ge_madd(t, R, e);
-            ge_p1p1_to_p3(R, t);
+            ge_madd(t, R3, e);
+        }
+        ge_p1p1_to_p2(R, t);
+    }
+    out = R;
+}
+
+// Phase 3 for `cnt` (<= CV_FIN_CHUNK) consecutive signatures: Rs = their (X,Y,Z) records
+// (CV_R_WORDS apart), rws = their R words (16 words apart: the sig records), ok = key_ok flags.
+// Returns the verdict bits (bit k = signature k).
+__host__ __device__ inline uint32_t cv_verify_finish(const uint32_t *Rs, const uint32_t *sigw, const uint8_t *ok,
+                                                     int cnt) {
+    fe pre[CV_FIN_CHUNK];
+    fe acc;
+    fe_one(acc);
+#pragma unroll
+    for (int k = 0; k < CV_FIN_CHUNK; k++) {
+        if (k < cnt) {
+            fe z;
+            fe_load(z, Rs + k * CV_R_WORDS + 20);
+            fe_mul(acc, z, acc);
+        }
+        pre[k] = acc;
+    }
+    fe inv;
+    fe_invert(inv, acc);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int k = CV_FIN_CHUNK - 1; k >= 0; k--) {
+        if (k < cnt) {
+            fe zi, z, x, y;
+            if (k) fe_mul(zi, inv, pre[k - 1]);
+            else zi = inv;
+            fe_load(z, Rs + k * CV_R_WORDS + 20);
+            fe_mul(inv, z, inv);
+            fe_load(x, Rs + k * CV_R_WORDS);
+            fe_load(y, Rs + k * CV_R_WORDS + 10);
+            fe_mul(x, x, zi);
+            fe_mul(y, y, zi);
+            uint32_t yw[8], xw[8];
+            fe_to_words(yw, y);
+            fe_to_words(xw, x);
+            yw[7] |= (xw[0] & 1u) << 31;
+            uint32_t diff = 0;
+#pragma unroll
+            for (int q = 0; q < 8; q++) diff |= yw[q] ^ sigw[16 * k + q];
+            if (diff == 0 && ok[k]) bits |= 1u << k;
         }
     }
+    return bits;
+}
 
-    // ---- encode R' and byte-compare with the signature's R
-    uint32_t enc[8];
-    ge_p3_encode(enc, R);
-    uint32_t diff = 0;
+// Single-signature convenience (host harness): the three phases back to back.
+__host__ __device__ inline bool cv_verify_one(const uint32_t *btab, const uint32_t aw[8], const uint32_t rw[8],
+                                              const uint32_t sw[8], const uint8_t *msg, uint32_t mlen,
+                                              bool *key_ok_out) {
+    uint32_t hs[CV_HS_WORDS];
+    alignas(16) uint32_t tab[CV_TAB_WORDS];
+    alignas(16) uint32_t Rrec[CV_R_WORDS];
+    const bool key_ok = cv_verify_prep(aw, rw, sw, msg, mlen, hs, tab);
+    ge_p2 R;
+    cv_verify_straus(btab, hs, tab, R);
+    fe_store(Rrec, R.X);
+    fe_store(Rrec + 10, R.Y);
+    fe_store(Rrec + 20, R.Z);
+    uint32_t sigw[16];
 #pragma unroll
-    for (int q = 0; q < 8; q++) diff |= enc[q] ^ rw[q];
+    for (int q = 0; q < 8; q++) { sigw[q] = rw[q]; sigw[8 + q] = sw[q]; }
+    const uint8_t okb = key_ok ? 1 : 0;
     *key_ok_out = key_ok;
-    return key_ok && diff == 0;
+    return cv_verify_finish(Rrec, sigw, &okb, 1) & 1u;
 }
 
 // ---------------------------------------------------------------- keygen + sign one message
 // EdDSAPrivateKeySpec(seed) + EdDSAEngine.sign (RFC 8032): pk = [a]B, R = [r]B, S = r + k a.
-__host__ __device__ inline void cv_sign_one(const int32_t *btab, const uint32_t seed[8], const uint8_t *msg,
+__host__ __device__ inline void cv_sign_one(const uint32_t *btab, const uint32_t seed[8], const uint8_t *msg,
                                             uint32_t mlen, uint32_t pk_out[8], uint32_t sig_out[16]) {
     uint32_t sd[16], hd[16];
 #pragma unroll

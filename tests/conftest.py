@@ -49,7 +49,7 @@ def host_harness():
                     if f.endswith(".h")]
     if not os.path.exists(lib) or any(os.path.getmtime(d) > os.path.getmtime(lib) for d in deps):
         os.makedirs(os.path.dirname(lib), exist_ok=True)
-        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17", "-fPIC", "-shared", src,
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17", "-DCV_BOUNDS_CHECK", "-fPIC", "-shared", src,
                         "-o", lib], check=True)
     return ctypes.CDLL(lib)
 

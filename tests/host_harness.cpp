@@ -1,6 +1,7 @@
 // host_harness.cpp — TEST INFRASTRUCTURE: runs the product's per-lane device code (corda_amd/csrc/
 // cv_verify.h and friends, all __host__ __device__) on the CPU so its logic can be checked against
 // the oracle without a GPU.  Built by tests/conftest.py into tests/_build/libcvhost.so.
+#include <cstdlib>
 #include <cstring>
 
 #include "../corda_amd/csrc/cv_verify.h"
@@ -24,6 +25,41 @@ int cvh_verify(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, uint32
     const bool ok = cv_verify_one(CV_BTAB_H, aw, rw, sw, msg, mlen, &key_ok);
     *status = key_ok ? 0 : 1;
     return ok ? 1 : 0;
+}
+
+// The GPU kernels' organisation on the host: prep + straus per signature, finish in lane chunks of
+// CV_FIN_CHUNK consecutive signatures.  verdict[i] = 0/1, status[i] = 0 ok / 1 bad key.
+void cvh_verify_batch(uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off,
+                      const uint32_t *len, uint8_t *verdict, uint8_t *status) {
+    uint32_t *hs = new uint32_t[(size_t)n * CV_HS_WORDS + 16];
+    uint32_t *tab = static_cast<uint32_t *>(aligned_alloc(16, ((size_t)n * CV_TAB_WORDS + 4) * 4));
+    uint32_t *R = static_cast<uint32_t *>(aligned_alloc(16, ((size_t)n * CV_R_WORDS + 4) * 4));
+    uint8_t *ok = new uint8_t[n + 1];
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t aw[8], rw[8], sw[8];
+        words_from_bytes(aw, pk + 32 * (size_t)i, 8);
+        words_from_bytes(rw, sig + 64 * (size_t)i, 8);
+        words_from_bytes(sw, sig + 64 * (size_t)i + 32, 8);
+        ok[i] = cv_verify_prep(aw, rw, sw, arena + off[i], len[i], hs + (size_t)i * CV_HS_WORDS,
+                               tab + (size_t)i * CV_TAB_WORDS) ? 1 : 0;
+        status[i] = ok[i] ? 0 : 1;
+        ge_p2 Rp;
+        cv_verify_straus(CV_BTAB_H, hs + (size_t)i * CV_HS_WORDS, tab + (size_t)i * CV_TAB_WORDS, Rp);
+        fe_store(R + (size_t)i * CV_R_WORDS, Rp.X);
+        fe_store(R + (size_t)i * CV_R_WORDS + 10, Rp.Y);
+        fe_store(R + (size_t)i * CV_R_WORDS + 20, Rp.Z);
+    }
+    for (uint32_t b = 0; b < n; b += CV_FIN_CHUNK) {
+        const int cnt = (int)(n - b < CV_FIN_CHUNK ? n - b : CV_FIN_CHUNK);
+        uint32_t sigw[16 * CV_FIN_CHUNK];
+        words_from_bytes(sigw, sig + 64 * (size_t)b, 16 * cnt);
+        const uint32_t bits = cv_verify_finish(R + (size_t)b * CV_R_WORDS, sigw, ok + b, cnt);
+        for (int k = 0; k < cnt; k++) verdict[b + k] = (bits >> k) & 1u;
+    }
+    delete[] hs;
+    free(tab);
+    free(R);
+    delete[] ok;
 }
 
 void cvh_sign(const uint8_t *seed, const uint8_t *msg, uint32_t mlen, uint8_t *pk, uint8_t *sig) {
@@ -65,7 +101,7 @@ void cvh_fe_invert(const uint8_t *a, uint8_t *out) {
     bytes_from_words(out, ow, 8);
 }
 // mul of raw limb vectors (bounds stress): a, b = 10 int32 limbs each
-void cvh_fe_mul_limbs(const int32_t *a, const int32_t *b, uint8_t *out) {
+void cvh_fe_mul_limbs(const uint32_t *a, const uint32_t *b, uint8_t *out) {
     fe fa, fb, fo;
     memcpy(fa.v, a, 40);
     memcpy(fb.v, b, 40);
@@ -74,7 +110,7 @@ void cvh_fe_mul_limbs(const int32_t *a, const int32_t *b, uint8_t *out) {
     fe_to_words(ow, fo);
     bytes_from_words(out, ow, 8);
 }
-void cvh_fe_sq_limbs(const int32_t *a, uint8_t *out) {
+void cvh_fe_sq_limbs(const uint32_t *a, uint8_t *out) {
     fe fa, fo;
     memcpy(fa.v, a, 40);
     fe_sq(fo, fa);
@@ -82,7 +118,7 @@ void cvh_fe_sq_limbs(const int32_t *a, uint8_t *out) {
     fe_to_words(ow, fo);
     bytes_from_words(out, ow, 8);
 }
-void cvh_fe_to_bytes_limbs(const int32_t *a, uint8_t *out) {
+void cvh_fe_to_bytes_limbs(const uint32_t *a, uint8_t *out) {
     fe fa;
     memcpy(fa.v, a, 40);
     uint32_t ow[8];

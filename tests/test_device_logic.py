@@ -51,22 +51,30 @@ def _limb_val(v):
 
 
 def test_field_mul_at_limb_bounds(host_harness):
-    """Inputs at the documented precondition edge (|limb| = 1.65 * 2^w) must not overflow."""
+    """Unsigned limbs at the documented precondition edges (cv_field.h): mul f <= 8M, g <= 3.3M;
+    sq f <= 3.3M.  The harness is built with CV_BOUNDS_CHECK, so it also asserts the preconditions."""
     H = host_harness
     rng = random.Random(2)
     W = [26, 25] * 5
+
+    def limbs(mult):
+        return [min(int(rng.choice([mult, mult * 0.999, rng.random() * mult, 0.0]) * (1 << W[i])),
+                    int(mult * (1 << W[i])) - 1) for i in range(10)]
+
     for trial in range(400):
-        a = [int(rng.choice([1, -1]) * rng.choice([1.65, 1.5, 1.0, rng.random() * 1.65]) * (1 << W[i]))
-             for i in range(10)]
-        b = [int(rng.choice([1, -1]) * rng.choice([1.65, 1.5, 1.0, rng.random() * 1.65]) * (1 << W[i]))
-             for i in range(10)]
-        A = (ctypes.c_int32 * 10)(*a)
-        B = (ctypes.c_int32 * 10)(*b)
+        a = limbs(8.0)
+        b = limbs(3.29)
+        c = limbs(3.29)
+        A = (ctypes.c_uint32 * 10)(*a)
+        B = (ctypes.c_uint32 * 10)(*b)
+        C = (ctypes.c_uint32 * 10)(*c)
         o = _out(32)
         H.cvh_fe_mul_limbs(A, B, o)
         assert _int(o) == _limb_val(a) * _limb_val(b) % P
-        H.cvh_fe_sq_limbs(A, o)
-        assert _int(o) == _limb_val(a) ** 2 % P
+        H.cvh_fe_sq_limbs(C, o)
+        assert _int(o) == _limb_val(c) ** 2 % P
+        H.cvh_fe_to_bytes_limbs(A, o)
+        assert _int(o) == _limb_val(a) % P
 
 
 def test_sc_reduce(host_harness):
@@ -133,6 +141,10 @@ def test_sha512_and_sha256(host_harness):
         o2 = _out(32)
         H.cvh_sha256(_b(m), ln, o2)
         assert bytes(o2) == hashlib.sha256(m).digest()
+        for shift in (1, 2, 3, 5):                       # unaligned message starts
+            buf = (ctypes.c_uint8 * (ln + 16)).from_buffer_copy(bytes(shift) + m + bytes(16 - shift))
+            H.cvh_sha512(_b(pre), 64, ctypes.byref(buf, shift), ln, o)
+            assert bytes(o) == hashlib.sha512(pre + m).digest()
 
 
 def test_verify_logic_on_golden_corpus(host_harness, corpus, manifest):
@@ -173,3 +185,25 @@ def test_merkle_logic(host_harness, merkle_cases):
         assert ok == (1 - int(m["status"][t]))
         if ok:
             assert bytes(o) == m["ids"][t].tobytes()
+
+
+def test_verify_batch_logic_chunks(host_harness, corpus, manifest):
+    """prep + straus + chunked finish (Montgomery batch inversion over 8 signatures per lane, invalid
+    keys mixed into the chunks, ragged tail) reproduces every golden verdict."""
+    H = host_harness
+    rng = np.random.default_rng(0)
+    for order in [np.arange(len(corpus["pk"])), rng.permutation(len(corpus["pk"]))[:613]]:
+        n = order.size
+        pk = np.ascontiguousarray(corpus["pk"][order])
+        sig = np.ascontiguousarray(corpus["sig"][order])
+        off = np.ascontiguousarray(corpus["off"][order])
+        ln = np.ascontiguousarray(corpus["len"][order])
+        arena = np.concatenate([corpus["arena"], np.zeros(16, np.uint8)])
+        verdict = np.zeros(n, np.uint8)
+        status = np.zeros(n, np.uint8)
+        vp = ctypes.c_void_p
+        H.cvh_verify_batch(ctypes.c_uint32(n), pk.ctypes.data_as(vp), sig.ctypes.data_as(vp), arena.ctypes.data_as(vp),
+                           off.ctypes.data_as(vp), ln.ctypes.data_as(vp), verdict.ctypes.data_as(vp),
+                           status.ctypes.data_as(vp))
+        assert np.array_equal(verdict, corpus["verdict"][order])
+        assert np.array_equal(status, corpus["status"][order])
