@@ -207,7 +207,8 @@ def main():
                        "collective": "RCCL all_gather of verdict bitmaps" if world > 1 else "none"},
             "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": mad_rate / 1e12, "unit": "Tmac/s",
                          "frac": achieved / mad_rate, "traffic": None,
-                         "kernel": "cv_verify_kernel", "kernel_ms": kern_ms,
+                         "kernel": "cv_prep_kernel + cv_straus_kernel + cv_finish_kernel (one verify launch group)",
+                         "kernel_ms": kern_ms,
                          "work_per_unit": f"{W_MAC_PER_VERIFY:.3g} 32x32->64 MAC per verify (SURVEY.md 8d)",
                          "fe_mul_per_s": femul_rate},
         }

@@ -238,12 +238,13 @@ def bitmap_to_bools(bitmap: np.ndarray, n: int) -> np.ndarray:
 
 
 _default: Optional[Engine] = None
+_default_lock = threading.Lock()
 
 
 def default_engine() -> Engine:
     """Process-wide engine on all visible GPUs (the JVM shim's "one ctx per process")."""
     global _default
-    with _lock:
+    with _default_lock:
         if _default is None:
             _default = Engine(0)
         return _default

@@ -42,6 +42,8 @@ def test_version_and_strerror():
 def test_no_gpu_fails_loudly():
     with pytest.raises(native.NativeUnavailable):
         native.Engine(0)
+    with pytest.raises(native.NativeUnavailable):      # and the process-wide engine neither hangs nor falls back
+        native.default_engine()
 
 
 def test_null_context_rejected():
