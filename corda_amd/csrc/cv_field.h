@@ -216,7 +216,7 @@ CV_HD void fe_sq2(fe &h, const fe &f) { fe_sq_impl(h, f, true); }
 // h = f^(2^n) (n >= 1).  A real loop keeps the code small; the trip count is hidden from the
 // optimiser so it cannot unroll the short chains into long straight-line blocks that the machine
 // scheduler then interleaves into VGPR spills.
-__host__ __device__ inline void fe_sqn(fe &h, const fe &f, int n) {
+__host__ __device__ __forceinline__ void fe_sqn(fe &h, const fe &f, int n) {
 #ifdef __HIP_DEVICE_COMPILE__
     asm volatile("" : "+s"(n));
 #endif
@@ -289,7 +289,7 @@ CV_HD int fe_is_negative(const fe &f) {
 }
 
 // z^(2^252 - 3)
-__host__ __device__ inline void fe_pow22523(fe &out, const fe &z) {
+__host__ __device__ __forceinline__ void fe_pow22523(fe &out, const fe &z) {
     fe t0, t1, t2;
     fe_sq(t0, z);            // z^2
     fe_sqn(t1, t0, 2);       // z^8
@@ -316,7 +316,7 @@ __host__ __device__ inline void fe_pow22523(fe &out, const fe &z) {
 }
 
 // z^(p-2) = z^(2^255 - 21)
-__host__ __device__ inline void fe_invert(fe &out, const fe &z) {
+__host__ __device__ __forceinline__ void fe_invert(fe &out, const fe &z) {
     fe t0, t1, t2, t3;
     fe_sq(t0, z);            // z^2
     fe_sqn(t1, t0, 2);       // z^8

@@ -127,7 +127,7 @@ CV_HD void ge_precomp_cneg(ge_precomp &r, bool neg) {
 }
 
 // GroupElement.toByteArray(): affine y (canonical) with the sign of x in bit 255, as 8 LE words.
-__host__ __device__ inline void ge_p2_encode(uint32_t w[8], const ge_p2 &p) {
+__host__ __device__ __forceinline__ void ge_p2_encode(uint32_t w[8], const ge_p2 &p) {
     fe zi, x, y;
     fe_invert(zi, p.Z);
     fe_mul(x, p.X, zi);
@@ -159,7 +159,7 @@ CV_HD void ge_abyte_from_key(uint32_t abyte[8], const uint32_t w[8]) {
 // Returns false where the reference throws IllegalArgumentException("not a valid GroupElement").
 // y keeps its non-reduced value; x is negated when isNegative(x) != bit 255 (x = 0 with the sign
 // bit set is therefore accepted as x = 0).  All output coordinates are tight.
-__host__ __device__ inline bool ge_decode_0_1_0(ge_p3 &A, const uint32_t w[8]) {
+__host__ __device__ __forceinline__ bool ge_decode_0_1_0(ge_p3 &A, const uint32_t w[8]) {
     fe y, yy, u, v, v3, x, vxx, chk, one, d;
     fe_from_words(y, w);
     fe_one(one);

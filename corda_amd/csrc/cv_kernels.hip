@@ -41,6 +41,7 @@ __device__ __forceinline__ void load_words8(uint32_t w[8], const uint8_t *p) {
 
 __device__ __forceinline__ void store_words(uint32_t *dst, const uint32_t *src, int nwords4) {
     uint4 *d = reinterpret_cast<uint4 *>(dst);
+#pragma unroll
     for (int q = 0; q < nwords4; q++) d[q] = make_uint4(src[4 * q], src[4 * q + 1], src[4 * q + 2], src[4 * q + 3]);
 }
 
@@ -61,9 +62,10 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_prep_kernel(
     if (status) status[i] = ok ? 0 : 1;
 }
 
-__global__ __launch_bounds__(CV_BLOCK, 2) void cv_straus_kernel(uint32_t n, const uint32_t *__restrict__ ws_hs,
-                                                                const uint32_t *__restrict__ ws_tab,
-                                                                uint32_t *__restrict__ ws_R) {
+template <int WAVES>
+__global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_straus_kernel(uint32_t n, const uint32_t *__restrict__ ws_hs,
+                                                                    const uint32_t *__restrict__ ws_tab,
+                                                                    uint32_t *__restrict__ ws_R) {
     __shared__ __attribute__((aligned(16))) uint32_t btab[CV_BTAB_ENTRIES * CV_BTAB_STRIDE];
     stage_btab(btab);
     const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
@@ -77,6 +79,14 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_straus_kernel(uint32_t n, cons
     rec[30] = rec[31] = 0;
     store_words(ws_R + (size_t)i * CV_R_WORDS, rec, CV_R_WORDS / 4);
 }
+template __global__ void cv_straus_kernel<2>(uint32_t, const uint32_t *, const uint32_t *, uint32_t *);
+template __global__ void cv_straus_kernel<3>(uint32_t, const uint32_t *, const uint32_t *, uint32_t *);
+template __global__ void cv_straus_kernel<4>(uint32_t, const uint32_t *, const uint32_t *, uint32_t *);
+
+// occupancy variant of the Straus kernel (waves per SIMD the register budget is built for);
+// tuned on the box with tools/ab_straus.py, default = the measured best
+static int g_straus_waves = 3;
+extern "C" void cvk_set_straus_waves(int w) { g_straus_waves = (w == 2 || w == 3 || w == 4) ? w : 3; }
 
 // lane j: signatures [8j, 8j+8) -> bitmap byte j (bytes past n are written as zero)
 __global__ __launch_bounds__(CV_BLOCK) void cv_finish_kernel(uint32_t n, uint32_t nbytes,
@@ -162,7 +172,12 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
         hipLaunchKernelGGL(cv_prep_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, pk + (size_t)c0 * 32,
                            sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_hs, ws_tab, ws_ok,
                            status ? status + c0 : nullptr);
-        hipLaunchKernelGGL(cv_straus_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, ws_tab, ws_R);
+        if (g_straus_waves == 2)
+            hipLaunchKernelGGL(cv_straus_kernel<2>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, ws_tab, ws_R);
+        else if (g_straus_waves == 4)
+            hipLaunchKernelGGL(cv_straus_kernel<4>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, ws_tab, ws_R);
+        else
+            hipLaunchKernelGGL(cv_straus_kernel<3>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, ws_tab, ws_R);
         const uint32_t nbytes = ((m + 63) / 64) * 8;
         hipLaunchKernelGGL(cv_finish_kernel, dim3((nbytes + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, stream, m,
                            nbytes, sig + (size_t)c0 * 64, ws_R, ws_ok,

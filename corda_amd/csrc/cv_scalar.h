@@ -38,7 +38,7 @@
     }
 
 // out = (x mod L), x given as 16 little-endian uint32 words (512 bits).
-__host__ __device__ inline void sc_reduce512(uint32_t out[8], const uint32_t x[16]) {
+__host__ __device__ __forceinline__ void sc_reduce512(uint32_t out[8], const uint32_t x[16]) {
     int64_t a[25];
     // 21-bit limbs; limb 24 holds the top 8 bits
 #pragma unroll
@@ -128,7 +128,7 @@ __host__ __device__ inline void sc_reduce512(uint32_t out[8], const uint32_t x[1
 }
 
 // (a * b + c) mod L for 256-bit a, b, c (signing only)
-__host__ __device__ inline void sc_muladd(uint32_t out[8], const uint32_t a[8], const uint32_t b[8],
+__host__ __device__ __forceinline__ void sc_muladd(uint32_t out[8], const uint32_t a[8], const uint32_t b[8],
                                           const uint32_t c[8]) {
     uint32_t x[16];
 #pragma unroll
@@ -159,7 +159,7 @@ CV_HD int bit_of(const uint32_t u[8], int i) { return (int)((u[i >> 5] >> (i & 3
 // (the Java loop that zeroes a run of ones and sets the next zero); a carry out of bit 255 is the
 // drop.  Fast path: with bit 255 clear no carry can leave the top (checked exhaustively on the top
 // bits and on 10^5 random scalars by tests/test_oracle.py::test_slide_drop_needs_bit255).
-__host__ __device__ inline bool slide_drops_carry(const uint32_t s[8]) {
+__host__ __device__ __forceinline__ bool slide_drops_carry(const uint32_t s[8]) {
     if (!(s[7] >> 31)) return false;
     uint32_t u[8];
 #pragma unroll
@@ -194,7 +194,7 @@ __host__ __device__ inline bool slide_drops_carry(const uint32_t s[8]) {
 }
 
 // Effective [S]B scalar of eddsa-0.1.0, reduced mod L: (S - 2^256 * drop) mod L.
-__host__ __device__ inline void sc_effective_s(uint32_t out[8], const uint32_t s[8]) {
+__host__ __device__ __forceinline__ void sc_effective_s(uint32_t out[8], const uint32_t s[8]) {
     const bool drop = slide_drops_carry(s);
     // -2^256 mod L = 16 (L - 2^252)
     const uint32_t K[5] = {0xcf5d3ed0u, 0x812631a5u, 0x2f79cd65u, 0x4def9deau, 0x1u};
@@ -213,17 +213,28 @@ __host__ __device__ inline void sc_effective_s(uint32_t out[8], const uint32_t s
 }
 
 // ---------------------------------------------------------------- digits
+// Word q (runtime, 0..7) of an 8-word register array through a select tree: keeps the array in
+// VGPRs (a dynamically indexed private array would be demoted to scratch memory).
+CV_HD uint32_t sel8(const uint32_t n[8], int q) {
+    const uint32_t a0 = (q & 1) ? n[1] : n[0], a1 = (q & 1) ? n[3] : n[2];
+    const uint32_t a2 = (q & 1) ? n[5] : n[4], a3 = (q & 1) ? n[7] : n[6];
+    const uint32_t b0 = (q & 2) ? a1 : a0, b1 = (q & 2) ? a3 : a2;
+    return (q & 4) ? b1 : b0;
+}
+// bit i (runtime, 0..255) of an 8-word scalar
+CV_HD int bit_of_sel(const uint32_t n[8], int i) { return (int)((sel8(n, i >> 5) >> (i & 31)) & 1u); }
+
 // Signed radix-16 digit k (0..63) of a scalar n < 2^255:  d_k in [-8, 8],  sum d_k 16^k = n.
 CV_HD int digit16(const uint32_t n[8], int k) {
-    const uint32_t nib = (n[k >> 3] >> ((k & 7) * 4)) & 15u;
+    const uint32_t nib = (sel8(n, k >> 3) >> ((k & 7) * 4)) & 15u;
     const int top = (int)(nib >> 3);
-    const int prev = k ? bit_of(n, 4 * k - 1) : 0;
+    const int prev = k ? bit_of_sel(n, 4 * k - 1) : 0;
     return (int)nib - 16 * top + prev;
 }
 // Signed radix-256 digit k (0..31) of a scalar n < 2^255:  d_k in [-128, 128].
 CV_HD int digit256(const uint32_t n[8], int k) {
-    const uint32_t byte = (n[k >> 2] >> ((k & 3) * 8)) & 255u;
+    const uint32_t byte = (sel8(n, k >> 2) >> ((k & 3) * 8)) & 255u;
     const int top = (int)(byte >> 7);
-    const int prev = k ? bit_of(n, 8 * k - 1) : 0;
+    const int prev = k ? bit_of_sel(n, 8 * k - 1) : 0;
     return (int)byte - 256 * top + prev;
 }

@@ -73,7 +73,7 @@ CV_HD void sha512_init(uint64_t st[8]) {
 }
 
 // One compression; w[16] = big-endian message words (clobbered: used as the schedule ring).
-__host__ __device__ inline void sha512_compress(uint64_t st[8], uint64_t w[16]) {
+__host__ __device__ __forceinline__ void sha512_compress(uint64_t st[8], uint64_t w[16]) {
     uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
 #pragma unroll 16
     for (int i = 0; i < 80; i++) {
@@ -116,7 +116,7 @@ CV_HD uint32_t msg_dword_le(const uint8_t *msg, uint32_t mlen, uint32_t t) {
 
 // SHA-512(pre[0:npre] || msg[0:mlen]) with npre in {32, 64} (pre as LE words); out = 16 LE words
 // of the 64-byte digest (byte order as produced by the hash, i.e. digest byte k = out[k/4] >> 8(k%4)).
-__host__ __device__ inline void sha512_pre_msg(uint32_t out[16], const uint32_t pre[16], int npre, const uint8_t *msg,
+__host__ __device__ __forceinline__ void sha512_pre_msg(uint32_t out[16], const uint32_t pre[16], int npre, const uint8_t *msg,
                                                uint32_t mlen) {
     uint64_t st[8];
     sha512_init(st);
@@ -156,7 +156,7 @@ CV_HD void sha256_init(uint32_t st[8]) {
     st[4] = 0x510e527f; st[5] = 0x9b05688c; st[6] = 0x1f83d9ab; st[7] = 0x5be0cd19;
 }
 
-__host__ __device__ inline void sha256_compress(uint32_t st[8], uint32_t w[16]) {
+__host__ __device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16]) {
     uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
 #pragma unroll 16
     for (int i = 0; i < 64; i++) {
@@ -180,7 +180,7 @@ __host__ __device__ inline void sha256_compress(uint32_t st[8], uint32_t w[16]) 
 
 // SHA-256 of an arbitrary byte string in device memory; out = 8 big-endian state words.
 // Full 64-byte blocks are assembled from byte loads; the tail block(s) carry the padding.
-__host__ __device__ inline void sha256_bytes(uint32_t out[8], const uint8_t *p, uint32_t n) {
+__host__ __device__ __forceinline__ void sha256_bytes(uint32_t out[8], const uint8_t *p, uint32_t n) {
     uint32_t st[8];
     sha256_init(st);
     const uint32_t nblocks = (n + 1 + 8 + 63) / 64;
@@ -217,7 +217,7 @@ __host__ __device__ inline void sha256_bytes(uint32_t out[8], const uint8_t *p, 
 }
 
 // SHA-256(left32 || right32) for two digests held as 8 big-endian state words each (Merkle node).
-__host__ __device__ inline void sha256_node(uint32_t out[8], const uint32_t l[8], const uint32_t r[8]) {
+__host__ __device__ __forceinline__ void sha256_node(uint32_t out[8], const uint32_t l[8], const uint32_t r[8]) {
     uint32_t st[8], w[16];
     sha256_init(st);
 #pragma unroll

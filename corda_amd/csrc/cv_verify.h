@@ -29,7 +29,7 @@ CV_HD void btab_select(ge_precomp &r, const uint32_t *btab, int k) {
 }
 
 // [k]B for a scalar k < 2^255: signed radix-256 digits from the table, 32 madds + 248 doublings.
-__host__ __device__ inline void ge_scalarmult_base(ge_p3 &R, const uint32_t k[8], const uint32_t *btab) {
+__host__ __device__ __forceinline__ void ge_scalarmult_base(ge_p3 &R, const uint32_t k[8], const uint32_t *btab) {
     ge_p3_identity(R);
     ge_p1p1 t;
     ge_p2 q;
@@ -103,7 +103,7 @@ CV_HD void ge_cached_load(ge_cached &c, const uint32_t *p) {
 }
 
 // Phase 1.  Returns key_ok.  hs = h || s (16 words), tab = CV_TAB_WORDS words (16-B aligned).
-__host__ __device__ inline bool cv_verify_prep(const uint32_t aw[8], const uint32_t rw[8], const uint32_t sw[8],
+__host__ __device__ __forceinline__ bool cv_verify_prep(const uint32_t aw[8], const uint32_t rw[8], const uint32_t sw[8],
                                                const uint8_t *msg, uint32_t mlen, uint32_t *hs, uint32_t *tab) {
     // hash first (its state is dead before the point decode starts: small live set)
     {
@@ -153,7 +153,7 @@ __host__ __device__ inline bool cv_verify_prep(const uint32_t aw[8], const uint3
 // Phase 2: R' = sum_w 16^w (a_w * (-A) + [w even] b_{w/2} * B) as (X:Y:Z).
 // Each window: 4 doublings (3 end in p2, the last in p3 for the add), the -A add, and every other
 // window the B madd; the window always ends in p2 (no T needed by the next doubling).
-__host__ __device__ inline void cv_verify_straus(const uint32_t *btab, const uint32_t *hs, const uint32_t *tab,
+__host__ __device__ __forceinline__ void cv_verify_straus(const uint32_t *btab, const uint32_t *hs, const uint32_t *tab,
                                                  ge_p2 &out) {
     uint32_t h[8], s[8];
 #pragma unroll
@@ -178,13 +178,14 @@ __host__ __device__ inline void cv_verify_straus(const uint32_t *btab, const uin
         }
         {
             const int a = digit16(h, w);
-            ge_cached e;
             const int m = a < 0 ? -a : a;
-            if (m) {
-                ge_cached_load(e, tab + 40 * (m - 1));
-            } else {
-                ge_cached_identity(e);
-            }
+            ge_cached e, id;
+            ge_cached_load(e, tab + 40 * (m ? m - 1 : 0));   // branch-free: always one lookup
+            ge_cached_identity(id);
+            fe_sel(e.YplusX, e.YplusX, id.YplusX, m == 0);
+            fe_sel(e.YminusX, e.YminusX, id.YminusX, m == 0);
+            fe_sel(e.Z, e.Z, id.Z, m == 0);
+            fe_sel(e.T2d, e.T2d, id.T2d, m == 0);
             ge_cached_cneg(e, a < 0);
             ge_add(t, R3, e);
         }
@@ -202,18 +203,19 @@ __host__ __device__ inline void cv_verify_straus(const uint32_t *btab, const uin
 // Phase 3 for `cnt` (<= CV_FIN_CHUNK) consecutive signatures: Rs = their (X,Y,Z) records
 // (CV_R_WORDS apart), rws = their R words (16 words apart: the sig records), ok = key_ok flags.
 // Returns the verdict bits (bit k = signature k).
-__host__ __device__ inline uint32_t cv_verify_finish(const uint32_t *Rs, const uint32_t *sigw, const uint8_t *ok,
-                                                     int cnt) {
+__host__ __device__ __forceinline__ uint32_t cv_verify_finish(const uint32_t *Rs, const uint32_t *sigw,
+                                                               const uint8_t *ok, int cnt) {
+    // slots past cnt use Z = 1 so every loop below has static indices (no private-memory arrays)
     fe pre[CV_FIN_CHUNK];
     fe acc;
     fe_one(acc);
 #pragma unroll
     for (int k = 0; k < CV_FIN_CHUNK; k++) {
-        if (k < cnt) {
-            fe z;
-            fe_load(z, Rs + k * CV_R_WORDS + 20);
-            fe_mul(acc, z, acc);
-        }
+        fe z, one;
+        fe_one(one);
+        if (k < cnt) fe_load(z, Rs + k * CV_R_WORDS + 20);
+        else z = one;
+        fe_mul(acc, z, acc);
         pre[k] = acc;
     }
     fe inv;
@@ -221,21 +223,28 @@ __host__ __device__ inline uint32_t cv_verify_finish(const uint32_t *Rs, const u
     uint32_t bits = 0;
 #pragma unroll
     for (int k = CV_FIN_CHUNK - 1; k >= 0; k--) {
+        fe zi, z, x, y, one;
+        fe_one(one);
+        if (k) fe_mul(zi, inv, pre[k - 1]);
+        else zi = inv;
         if (k < cnt) {
-            fe zi, z, x, y;
-            if (k) fe_mul(zi, inv, pre[k - 1]);
-            else zi = inv;
             fe_load(z, Rs + k * CV_R_WORDS + 20);
-            fe_mul(inv, z, inv);
             fe_load(x, Rs + k * CV_R_WORDS);
             fe_load(y, Rs + k * CV_R_WORDS + 10);
-            fe_mul(x, x, zi);
-            fe_mul(y, y, zi);
-            uint32_t yw[8], xw[8];
-            fe_to_words(yw, y);
-            fe_to_words(xw, x);
-            yw[7] |= (xw[0] & 1u) << 31;
-            uint32_t diff = 0;
+        } else {
+            z = one;
+            x = one;
+            y = one;
+        }
+        if (k) fe_mul(inv, z, inv);
+        fe_mul(x, x, zi);
+        fe_mul(y, y, zi);
+        uint32_t yw[8], xw[8];
+        fe_to_words(yw, y);
+        fe_to_words(xw, x);
+        yw[7] |= (xw[0] & 1u) << 31;
+        uint32_t diff = 0;
+        if (k < cnt) {
 #pragma unroll
             for (int q = 0; q < 8; q++) diff |= yw[q] ^ sigw[16 * k + q];
             if (diff == 0 && ok[k]) bits |= 1u << k;
@@ -245,7 +254,7 @@ __host__ __device__ inline uint32_t cv_verify_finish(const uint32_t *Rs, const u
 }
 
 // Single-signature convenience (host harness): the three phases back to back.
-__host__ __device__ inline bool cv_verify_one(const uint32_t *btab, const uint32_t aw[8], const uint32_t rw[8],
+__host__ __device__ __forceinline__ bool cv_verify_one(const uint32_t *btab, const uint32_t aw[8], const uint32_t rw[8],
                                               const uint32_t sw[8], const uint8_t *msg, uint32_t mlen,
                                               bool *key_ok_out) {
     uint32_t hs[CV_HS_WORDS];
@@ -267,7 +276,7 @@ __host__ __device__ inline bool cv_verify_one(const uint32_t *btab, const uint32
 
 // ---------------------------------------------------------------- keygen + sign one message
 // EdDSAPrivateKeySpec(seed) + EdDSAEngine.sign (RFC 8032): pk = [a]B, R = [r]B, S = r + k a.
-__host__ __device__ inline void cv_sign_one(const uint32_t *btab, const uint32_t seed[8], const uint8_t *msg,
+__host__ __device__ __forceinline__ void cv_sign_one(const uint32_t *btab, const uint32_t seed[8], const uint8_t *msg,
                                             uint32_t mlen, uint32_t pk_out[8], uint32_t sig_out[16]) {
     uint32_t sd[16], hd[16];
 #pragma unroll
@@ -303,7 +312,7 @@ __host__ __device__ inline void cv_sign_one(const uint32_t *btab, const uint32_t
 // ---------------------------------------------------------------- Merkle root of one transaction
 // MerkleTree.buildMerkleTree over cnt leaf digests (8 big-endian words each), in place.
 // Returns false for an empty leaf list (MerkleTreeException).  root = 8 big-endian words.
-__host__ __device__ inline bool cv_merkle_root_inplace(uint32_t *lvl, uint32_t cnt, uint32_t root[8]) {
+__host__ __device__ __forceinline__ bool cv_merkle_root_inplace(uint32_t *lvl, uint32_t cnt, uint32_t root[8]) {
     if (cnt == 0) {
 #pragma unroll
         for (int q = 0; q < 8; q++) root[q] = 0;
