@@ -179,36 +179,23 @@ __host__ __device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_
 }
 
 // SHA-256 of an arbitrary byte string in device memory; out = 8 big-endian state words.
-// Full 64-byte blocks are assembled from byte loads; the tail block(s) carry the padding.
+// Message words come from aligned dword loads (msg_dword_le, which also inserts the 0x80 pad).
 __host__ __device__ __forceinline__ void sha256_bytes(uint32_t out[8], const uint8_t *p, uint32_t n) {
     uint32_t st[8];
     sha256_init(st);
     const uint32_t nblocks = (n + 1 + 8 + 63) / 64;
     const uint32_t total = nblocks * 64;
+    const uint64_t bits = (uint64_t)n * 8;
+#pragma nounroll
     for (uint32_t blk = 0; blk < nblocks; blk++) {
         uint32_t w[16];
-        const uint32_t base = blk * 64;
-        if (base + 64 <= n) {
 #pragma unroll
-            for (int j = 0; j < 16; j++) {
-                const uint8_t *q = p + base + 4 * j;
-                w[j] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
-            }
-        } else {
-            for (int j = 0; j < 16; j++) {
-                uint32_t v = 0;
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t t = base + 4 * j + k;
-                    uint32_t byte;
-                    if (t < n) byte = p[t];
-                    else if (t == n) byte = 0x80;
-                    else if (t >= total - 8) byte = (uint32_t)(((uint64_t)n * 8) >> (8 * (total - 1 - t))) & 0xff;
-                    else byte = 0;
-                    v = (v << 8) | byte;
-                }
-                w[j] = v;
-            }
+        for (int j = 0; j < 16; j++) {
+            const uint32_t u = blk * 64 + 4 * j;
+            uint32_t v = cv_bswap32(msg_dword_le(p, n, u));
+            if (u == total - 8) v = (uint32_t)(bits >> 32);
+            if (u == total - 4) v = (uint32_t)bits;
+            w[j] = v;
         }
         sha256_compress(st, w);
     }

@@ -71,3 +71,59 @@ def corrupt_fraction(batch: SigBatch, every: int = 16) -> torch.Tensor:
     expect = torch.ones(batch.n, dtype=torch.bool, device=batch.sig.device)
     expect[idx] = False
     return expect
+
+
+@dataclass
+class TxBatch:
+    """C3-shaped transactions: leaf blobs (6 per tx: 2x120, 2x600, 2x300 bytes +-25 %), the claimed
+    ids (= Merkle roots, computed once on the GPU at generation time), and `signers` signatures per
+    transaction over its 32-byte id (SignedTransaction.kt:85: sigs cover id.bytes)."""
+    ntx: int
+    signers: int
+    leaf_arena: torch.Tensor
+    leaf_off: torch.Tensor
+    leaf_len: torch.Tensor
+    tx_begin: torch.Tensor       # (ntx+1,) int32
+    ids: torch.Tensor            # (ntx, 32) uint8 claimed ids
+    sigs: SigBatch               # ntx*signers records; message i = ids[i // signers]
+    sig_tx_begin: torch.Tensor   # (ntx+1,) int64
+
+
+LEAF_SHAPE = (120, 120, 600, 600, 300, 300)
+
+
+def make_tx_batch(engine: native.Engine, device: int, ntx: int, signers: int = 8, seed: int = 20261015,
+                  stream: int = 0) -> TxBatch:
+    dev = torch.device("cuda", device)
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    nleaf = len(LEAF_SHAPE)
+    base = torch.tensor(LEAF_SHAPE, dtype=torch.float32, device=dev).repeat(ntx)
+    scale = torch.rand(ntx * nleaf, device=dev, generator=g) * 0.5 + 0.75
+    leaf_len = (base * scale).to(torch.int32)
+    leaf_off = torch.zeros(ntx * nleaf, dtype=torch.int64, device=dev)
+    leaf_off[1:] = torch.cumsum(leaf_len[:-1].to(torch.int64), 0)
+    total = int(leaf_off[-1] + leaf_len[-1])
+    arena = torch.randint(0, 256, (total + 16,), dtype=torch.uint8, device=dev, generator=g)
+    tx_begin = torch.arange(0, ntx * nleaf + 1, nleaf, dtype=torch.int32, device=dev)
+    ids = torch.empty((ntx, 32), dtype=torch.uint8, device=dev)
+    ws = torch.empty(ntx * nleaf * 32, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+    engine.merkle_device(device, ntx, ntx * nleaf, arena.data_ptr(), leaf_off.data_ptr(), leaf_len.data_ptr(),
+                         tx_begin.data_ptr(), ws.data_ptr(), ids.data_ptr(), 0, stream)
+    engine.synchronize(device)
+    torch.cuda.synchronize(dev)
+    n = ntx * signers
+    key_seeds = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device=dev, generator=g)
+    off = (torch.arange(n, dtype=torch.int64, device=dev) // signers) * 32
+    ln = torch.full((n,), 32, dtype=torch.int32, device=dev)
+    pk = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    id_arena = torch.cat([ids.reshape(-1), torch.zeros(16, dtype=torch.uint8, device=dev)])
+    engine.sign_device(device, n, key_seeds.data_ptr(), id_arena.data_ptr(), off.data_ptr(), ln.data_ptr(),
+                       pk.data_ptr(), sig.data_ptr(), stream)
+    engine.synchronize(device)
+    torch.cuda.synchronize(dev)
+    sb = SigBatch(n, pk, sig, id_arena, off, ln, 32)
+    sig_tx_begin = torch.arange(0, n + 1, signers, dtype=torch.int64, device=dev)
+    return TxBatch(ntx, signers, arena, leaf_off, leaf_len, tx_begin, ids, sb, sig_tx_begin)
