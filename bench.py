@@ -15,7 +15,7 @@ Default workload (N=1): BASELINE config C2 — 1,000,000 single-signer Ed25519 s
 
 Extra fields on the JSON line:
   roofline      VALU-issue roofline of the verify kernel (algorithmic 2.28e5 32x32->64 MACs per
-                verify) against the measured v_mad_i64_i32 peak of this GPU
+                verify) against the measured v_mad_u64_u32 peak of this GPU
   cpu_baseline  oracle/ C restatement of eddsa-0.1.0 verify (rank 0, N=1 only, bounded sample)
   notary        p50/p99 end-to-end latency of a 4096-signature notary batch (host buffers in and
                 out, 1/16 adversarial), GPU vs the CPU restatement on the same batch
@@ -38,6 +38,9 @@ sys.path.insert(0, REPO)
 from corda_amd import distributed as D, native, workload  # noqa: E402
 
 W_MAC_PER_VERIFY = 2.28e5       # algorithmic 32x32->64 MACs per verify (32-byte msg)
+# Straus phase alone (cv_straus_kernel, the dominant kernel): 63 windows x (16 S + 13 M) + 64 -A adds x 7 M
+# + 32 B madds x 7 M = 1008 S + 1491 M, at S = 55 and M = 100 limb products (DESIGN.md "Roofline")
+W_MAC_STRAUS = 1008 * 55 + 1491 * 100
 MSG_BYTES = {"c2": 300, "c5": 32, "c3": 32}
 CONFIG_NAME = {
     "c2": "C2: 1M single-signer Ed25519 txs, 300-byte msg, distinct keys, SoA batch",
@@ -48,6 +51,17 @@ CONFIG_NAME = {
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def pmc_traffic(n: int):
+    """HBM bytes per cv_straus_kernel launch from the committed PMC pass (profiles/pmc_straus.json,
+    written by scripts/pmc.sh + tools/pmc_summary.py on the same build and workload), scaled to n."""
+    p = os.path.join(REPO, "profiles", "pmc_straus.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    return d["hbm_bytes_per_launch"] * n / d["n"]
 
 
 def cpu_baseline(batch, rank_device: int, seconds: float):
@@ -216,16 +230,17 @@ def main():
         step()
     torch.cuda.synchronize(dev)
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # Each step: the verify launch group on `stream`, timed kernel by kernel with HIP events recorded on
+    # that stream between the three launches (cv_ed25519_verify_device_timed waits for the last one).
+    phases = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        ev[k][0].record(stream)
-        eng.verify_device(local, n, batch.pk.data_ptr(), batch.sig.data_ptr(), batch.arena.data_ptr(),
-                          batch.off.data_ptr(), batch.len.data_ptr(), bitmap.data_ptr(), 0, sh)
-        ev[k][1].record(stream)
+        phases.append(eng.verify_device_timed(local, n, batch.pk.data_ptr(), batch.sig.data_ptr(),
+                                              batch.arena.data_ptr(), batch.off.data_ptr(), batch.len.data_ptr(),
+                                              bitmap.data_ptr(), sh))
         if world > 1:
             gathered = D.gather_bitmap(bitmap, world * n)     # RCCL all-gather into the commit step
     torch.cuda.synchronize(dev)
@@ -237,18 +252,20 @@ def main():
     if n % 64:
         full[-1] = (1 << (n % 64)) - 1
     assert torch.equal(bitmap, full), "verify rejected an honest signature"
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    ph = np.mean(np.array(phases), axis=0)
+    kern_ms, straus_ms = float(ph.sum()), float(ph[1])
     if world > 1:
-        tt = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed, kern_ms, straus_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(tt[0]), float(tt[1])
+        elapsed, kern_ms, straus_ms = float(tt[0]), float(tt[1]), float(tt[2])
         assert torch.equal(gathered.view(world, words)[rank], bitmap)
         assert bool((gathered == -1).all()), "a rank rejected an honest signature"
     value = world * n * args.steps / elapsed
 
     if rank == 0:
         mad_rate, femul_rate = eng.calibrate(local)
-        achieved = n * W_MAC_PER_VERIFY / (kern_ms * 1e-3)
+        achieved = n * W_MAC_STRAUS / (straus_ms * 1e-3)
+        group = n * W_MAC_PER_VERIFY / (kern_ms * 1e-3)
         result = {
             "metric": "Ed25519 verifies/sec (node)",
             "value": value,
@@ -260,16 +277,20 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int32/int64 (GF(2^255-19) radix 2^25.5 limbs)",
+            "dtype": "uint32/uint64 (GF(2^255-19) radix 2^25.5 limbs, v_mad_u64_u32)",
             "data": "synthetic (keys, messages, signatures generated on-GPU from seeded RNG, RFC 8032 signing)",
             "config": {"workload": CONFIG_NAME[args.config], "sigs_per_gpu": n, "msg_bytes": msg_len,
                        "key_pool": args.key_pool or "distinct", "parallelism": f"shard-by-signature x{world}",
                        "collective": "RCCL all_gather of verdict bitmaps" if world > 1 else "none"},
             "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": mad_rate / 1e12, "unit": "Tmac/s",
-                         "frac": achieved / mad_rate, "traffic": None,
-                         "kernel": "cv_prep_kernel + cv_straus_kernel + cv_finish_kernel (one verify launch group)",
-                         "kernel_ms": kern_ms,
-                         "work_per_unit": f"{W_MAC_PER_VERIFY:.3g} 32x32->64 MAC per verify (SURVEY.md 8d)",
+                         "frac": achieved / mad_rate, "traffic": pmc_traffic(n),
+                         "kernel": "cv_straus_kernel", "kernel_ms": straus_ms,
+                         "work_per_unit": f"{W_MAC_STRAUS} 32x32->64 MAC per verify in the Straus phase "
+                                          f"(1008 S + 1491 M)",
+                         "phase_ms": {"prep": float(ph[0]), "straus": float(ph[1]), "finish": float(ph[2])},
+                         "group": {"kernels": "prep + straus + finish", "kernel_ms": kern_ms,
+                                   "achieved": group / 1e12, "frac": group / mad_rate,
+                                   "work_per_unit": f"{W_MAC_PER_VERIFY:.3g} MAC per verify (SURVEY.md 8d)"},
                          "fe_mul_per_s": femul_rate},
         }
         if world == 1 and not args.no_cpu:

@@ -14,7 +14,7 @@
 extern "C" {
 hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off,
                       const uint32_t *len, uint64_t *bitmap, uint8_t *status, uint32_t *ws_hs, uint32_t *ws_tab,
-                      uint32_t *ws_R, uint8_t *ws_ok, uint32_t ws_cap, hipStream_t stream);
+                      uint32_t *ws_R, uint8_t *ws_ok, uint32_t ws_cap, hipStream_t stream, hipEvent_t *ev);
 hipError_t cvk_sign(uint32_t n, const uint8_t *seed, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
                     uint8_t *pk, uint8_t *sig, hipStream_t stream);
 hipError_t cvk_merkle(uint32_t ntx, uint32_t nleaves, const uint8_t *arena, const uint64_t *leaf_off,
@@ -74,11 +74,12 @@ hipError_t ensure_verify_ws(Device &d, size_t n) {
 }
 
 hipError_t launch_verify(Device &d, uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
-                         const uint64_t *off, const uint32_t *len, uint64_t *bitmap, uint8_t *status, hipStream_t s) {
+                         const uint64_t *off, const uint32_t *len, uint64_t *bitmap, uint8_t *status, hipStream_t s,
+                         hipEvent_t *ev = nullptr) {
     hipError_t e = ensure_verify_ws(d, n);
     if (e != hipSuccess) return e;
     return cvk_verify(n, pk, sig, arena, off, len, bitmap, status, d.ws_hs.as<uint32_t>(), d.ws_tab.as<uint32_t>(),
-                      d.ws_R.as<uint32_t>(), d.ws_ok.as<uint8_t>(), d.ws_cap, s);
+                      d.ws_R.as<uint32_t>(), d.ws_ok.as<uint8_t>(), d.ws_cap, s, ev);
 }
 
 int hip_rc(hipError_t e) {
@@ -353,6 +354,39 @@ int cv_ed25519_verify_device(cv_ctx *ctx, int device, size_t n, const void *d_pk
                          static_cast<const uint32_t *>(d_len), static_cast<uint64_t *>(d_bitmap),
                          static_cast<uint8_t *>(d_status), s));
     return CV_OK;
+}
+
+int cv_ed25519_verify_device_timed(cv_ctx *ctx, int device, size_t n, const void *d_pk, const void *d_sig,
+                                   const void *d_arena, const void *d_off, const void *d_len, void *d_bitmap,
+                                   void *stream, float *phase_ms) {
+    if (!ctx || !phase_ms) return CV_E_ARGS;
+    phase_ms[0] = phase_ms[1] = phase_ms[2] = 0.f;
+    if (n == 0) return CV_OK;
+    if (n > 0xffffffffull) return CV_E_TOO_LARGE;
+    Device *d = find_dev(ctx, device);
+    if (!d || !d_pk || !d_sig || !d_arena || !d_off || !d_len || !d_bitmap) return CV_E_ARGS;
+    CV_TRY(hipSetDevice(d->ordinal));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : d->stream;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipError_t e = hipSuccess;
+    for (int k = 0; k < 4 && e == hipSuccess; k++) e = hipEventCreate(&ev[k]);
+    // one workspace chunk at a time (chunk starts are multiples of 64: whole bitmap words)
+    for (size_t c0 = 0; c0 < n && e == hipSuccess; c0 += kVerifyChunk) {
+        const size_t m = std::min<size_t>(kVerifyChunk, n - c0);
+        e = launch_verify(*d, (uint32_t)m, static_cast<const uint8_t *>(d_pk) + c0 * 32,
+                          static_cast<const uint8_t *>(d_sig) + c0 * 64, static_cast<const uint8_t *>(d_arena),
+                          static_cast<const uint64_t *>(d_off) + c0, static_cast<const uint32_t *>(d_len) + c0,
+                          static_cast<uint64_t *>(d_bitmap) + c0 / 64, nullptr, s, ev);
+        if (e == hipSuccess) e = hipEventSynchronize(ev[3]);
+        for (int k = 0; k < 3 && e == hipSuccess; k++) {
+            float ms = 0.f;
+            e = hipEventElapsedTime(&ms, ev[k], ev[k + 1]);
+            phase_ms[k] += ms;
+        }
+    }
+    for (hipEvent_t x : ev)
+        if (x) (void)hipEventDestroy(x);
+    return hip_rc(e);
 }
 
 int cv_ed25519_sign_device(cv_ctx *ctx, int device, size_t n, const void *d_seed, const void *d_arena,

@@ -82,34 +82,6 @@ CV_HD void fe_sel(fe &h, const fe &f, const fe &g, bool b) {
     for (int i = 0; i < 10; i++) h.v[i] = b ? g.v[i] : f.v[i];
 }
 
-// Floor carry of ten 64-bit column sums (each < 2^64) into a tight element.  Order: two
-// interleaved chains (0..4, 4..9) and the 2^255 = 19 wrap, as in the classic 25.5-bit schedule.
-#define CV_FCARRY(h, i, nxt)              \
-    {                                     \
-        nxt += h[i] >> CV_W(i);           \
-        h[i] &= (uint64_t)CV_MASK(i);     \
-    }
-CV_HD void fe_reduce64(fe &out, uint64_t h[10]) {
-    CV_FCARRY(h, 0, h[1]);
-    CV_FCARRY(h, 4, h[5]);
-    CV_FCARRY(h, 1, h[2]);
-    CV_FCARRY(h, 5, h[6]);
-    CV_FCARRY(h, 2, h[3]);
-    CV_FCARRY(h, 6, h[7]);
-    CV_FCARRY(h, 3, h[4]);
-    CV_FCARRY(h, 7, h[8]);
-    CV_FCARRY(h, 4, h[5]);
-    CV_FCARRY(h, 8, h[9]);
-    {
-        const uint64_t c = h[9] >> 25;
-        h[9] &= 0x1ffffffu;
-        h[0] += c * 19;
-    }
-    CV_FCARRY(h, 0, h[1]);
-#pragma unroll
-    for (int i = 0; i < 10; i++) out.v[i] = (uint32_t)h[i];
-}
-
 // Renormalise an element whose limbs are < 2^31 to tight, with 32-bit ops only.
 CV_HD void fe_carry(fe &h, const fe &f) {
     uint32_t t[10];
@@ -143,75 +115,196 @@ CV_HD void fe_check_mul_in(const fe &f, const fe &g) {
 #endif
 }
 
-// h = f * g   (g is the operand multiplied by 19: g <= 3.3, f <= 8)
-CV_HD void fe_mul(fe &h, const fe &f, const fe &g) {
-    fe_check_mul_in(f, g);
-    const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
-    const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
-    const uint32_t g0 = g.v[0], g1 = g.v[1], g2 = g.v[2], g3 = g.v[3], g4 = g.v[4];
-    const uint32_t g5 = g.v[5], g6 = g.v[6], g7 = g.v[7], g8 = g.v[8], g9 = g.v[9];
-    // 19*g_j folds the 2^255 wrap; 2*f_i (odd i) pays the extra half bit of odd*odd offsets
-    const uint32_t g1_19 = 19 * g1, g2_19 = 19 * g2, g3_19 = 19 * g3, g4_19 = 19 * g4, g5_19 = 19 * g5;
-    const uint32_t g6_19 = 19 * g6, g7_19 = 19 * g7, g8_19 = 19 * g8, g9_19 = 19 * g9;
-    const uint32_t f1_2 = 2 * f1, f3_2 = 2 * f3, f5_2 = 2 * f5, f7_2 = 2 * f7, f9_2 = 2 * f9;
-    uint64_t h_[10];
-    h_[0] = mu64(f0, g0) + mu64(f1_2, g9_19) + mu64(f2, g8_19) + mu64(f3_2, g7_19) + mu64(f4, g6_19) +
-            mu64(f5_2, g5_19) + mu64(f6, g4_19) + mu64(f7_2, g3_19) + mu64(f8, g2_19) + mu64(f9_2, g1_19);
-    h_[1] = mu64(f0, g1) + mu64(f1, g0) + mu64(f2, g9_19) + mu64(f3, g8_19) + mu64(f4, g7_19) +
-            mu64(f5, g6_19) + mu64(f6, g5_19) + mu64(f7, g4_19) + mu64(f8, g3_19) + mu64(f9, g2_19);
-    h_[2] = mu64(f0, g2) + mu64(f1_2, g1) + mu64(f2, g0) + mu64(f3_2, g9_19) + mu64(f4, g8_19) +
-            mu64(f5_2, g7_19) + mu64(f6, g6_19) + mu64(f7_2, g5_19) + mu64(f8, g4_19) + mu64(f9_2, g3_19);
-    h_[3] = mu64(f0, g3) + mu64(f1, g2) + mu64(f2, g1) + mu64(f3, g0) + mu64(f4, g9_19) +
-            mu64(f5, g8_19) + mu64(f6, g7_19) + mu64(f7, g6_19) + mu64(f8, g5_19) + mu64(f9, g4_19);
-    h_[4] = mu64(f0, g4) + mu64(f1_2, g3) + mu64(f2, g2) + mu64(f3_2, g1) + mu64(f4, g0) +
-            mu64(f5_2, g9_19) + mu64(f6, g8_19) + mu64(f7_2, g7_19) + mu64(f8, g6_19) + mu64(f9_2, g5_19);
-    h_[5] = mu64(f0, g5) + mu64(f1, g4) + mu64(f2, g3) + mu64(f3, g2) + mu64(f4, g1) +
-            mu64(f5, g0) + mu64(f6, g9_19) + mu64(f7, g8_19) + mu64(f8, g7_19) + mu64(f9, g6_19);
-    h_[6] = mu64(f0, g6) + mu64(f1_2, g5) + mu64(f2, g4) + mu64(f3_2, g3) + mu64(f4, g2) +
-            mu64(f5_2, g1) + mu64(f6, g0) + mu64(f7_2, g9_19) + mu64(f8, g8_19) + mu64(f9_2, g7_19);
-    h_[7] = mu64(f0, g7) + mu64(f1, g6) + mu64(f2, g5) + mu64(f3, g4) + mu64(f4, g3) +
-            mu64(f5, g2) + mu64(f6, g1) + mu64(f7, g0) + mu64(f8, g9_19) + mu64(f9, g8_19);
-    h_[8] = mu64(f0, g8) + mu64(f1_2, g7) + mu64(f2, g6) + mu64(f3_2, g5) + mu64(f4, g4) +
-            mu64(f5_2, g3) + mu64(f6, g2) + mu64(f7_2, g1) + mu64(f8, g0) + mu64(f9_2, g9_19);
-    h_[9] = mu64(f0, g9) + mu64(f1, g8) + mu64(f2, g7) + mu64(f3, g6) + mu64(f4, g5) +
-            mu64(f5, g4) + mu64(f6, g3) + mu64(f7, g2) + mu64(f8, g1) + mu64(f9, g0);
-    fe_reduce64(h, h_);
+// Sequential-carry column accumulation: column k is accumulated on top of the carry out of column
+// k-1, so a carry costs only its shift (the first v_mad_u64_u32 of the next column adds it for
+// free) instead of shift + 64-bit add.  CV_MADC(acc, a, b): acc = a*b + acc as ONE v_mad_u64_u32,
+// written in asm so the compiler cannot reassociate the carry to the end of the column sum.
+// An asm result read by the very next instruction costs a conservative s_nop, so independent
+// multiplications are interleaved N ways (fe_mul_n / fe_sq_n): product k of chain m is followed by
+// product k of chain m+1, and a chain's next product comes N instructions later.
+#ifdef __HIP_DEVICE_COMPILE__
+#define CV_MADC(acc, a, b)                                                                   \
+    {                                                                                        \
+        uint64_t cc_;                                                                        \
+        asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc_) : "v"(a), "v"(b));     \
+    }
+#else
+#define CV_MADC(acc, a, b) ((acc) += (uint64_t)(a) * (uint64_t)(b))
+#endif
+
+// One product slot of N interleaved chains as ONE asm statement (N dependent-free mads back to back):
+// the compiler's conservative inline-asm hazard wait then costs one s_nop per N products.
+template <int N> CV_HD void cv_madc_n(uint64_t (&t)[N], const uint32_t (&a)[N], const uint32_t (&b)[N]) {
+#ifdef __HIP_DEVICE_COMPILE__
+    uint64_t cc;
+    if constexpr (N == 1) {
+        asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(t[0]), "=s"(cc) : "v"(a[0]), "v"(b[0]));
+    } else if constexpr (N == 2) {
+        asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\tv_mad_u64_u32 %1, %2, %5, %6, %1"
+            : "+v"(t[0]), "+v"(t[1]), "=s"(cc) : "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]));
+    } else {
+        // wider groups raise register pressure (all 2N operands live at once): issue pairs
+        static_assert(N == 3 || N == 4, "cv_madc_n: N in 1..4");
+        uint64_t t01[2] = {t[0], t[1]}, t23[2] = {t[2], N == 4 ? t[N - 1] : 0};
+        const uint32_t a01[2] = {a[0], a[1]}, b01[2] = {b[0], b[1]};
+        cv_madc_n<2>(t01, a01, b01);
+        if constexpr (N == 4) {
+            const uint32_t a23[2] = {a[2], a[N - 1]}, b23[2] = {b[2], b[N - 1]};
+            cv_madc_n<2>(t23, a23, b23);
+            t[N - 1] = t23[1];
+        } else {
+            uint64_t t2[1] = {t[2]};
+            const uint32_t a2[1] = {a[2]}, b2[1] = {b[2]};
+            cv_madc_n<1>(t2, a2, b2);
+            t23[0] = t2[0];
+        }
+        t[0] = t01[0]; t[1] = t01[1]; t[2] = t23[0];
+    }
+#else
+    for (int m = 0; m < N; m++) t[m] += (uint64_t)a[m] * (uint64_t)b[m];
+#endif
 }
 
-// h = f^2 (55 products); dbl gives h = 2 f^2 (columns doubled before the carry)
-CV_HD void fe_sq_impl(fe &h, const fe &f, bool dbl) {
-#if CV_CHECKING
-    for (int i = 0; i < 10; i++) CV_ASSERT((uint64_t)f.v[i] * 10 < ((uint64_t)33 << CV_W(i)), "fe_sq: limb > 3.3M");
-#endif
-    const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
-    const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
-    const uint32_t f0_2 = 2 * f0, f1_2 = 2 * f1, f2_2 = 2 * f2, f3_2 = 2 * f3, f4_2 = 2 * f4;
-    const uint32_t f5_2 = 2 * f5, f6_2 = 2 * f6, f7_2 = 2 * f7;
-    const uint32_t f5_38 = 38 * f5, f6_19 = 19 * f6, f7_38 = 38 * f7, f8_19 = 19 * f8, f9_38 = 38 * f9;
-    uint64_t h_[10];
-    h_[0] = mu64(f0, f0) + mu64(f1_2, f9_38) + mu64(f2_2, f8_19) + mu64(f3_2, f7_38) + mu64(f4_2, f6_19) +
-            mu64(f5, f5_38);
-    h_[1] = mu64(f0_2, f1) + mu64(f2, f9_38) + mu64(f3_2, f8_19) + mu64(f4, f7_38) + mu64(f5_2, f6_19);
-    h_[2] = mu64(f0_2, f2) + mu64(f1_2, f1) + mu64(f3_2, f9_38) + mu64(f4_2, f8_19) + mu64(f5_2, f7_38) +
-            mu64(f6, f6_19);
-    h_[3] = mu64(f0_2, f3) + mu64(f1_2, f2) + mu64(f4, f9_38) + mu64(f5_2, f8_19) + mu64(f6, f7_38);
-    h_[4] = mu64(f0_2, f4) + mu64(f1_2, f3_2) + mu64(f2, f2) + mu64(f5_2, f9_38) + mu64(f6_2, f8_19) +
-            mu64(f7, f7_38);
-    h_[5] = mu64(f0_2, f5) + mu64(f1_2, f4) + mu64(f2_2, f3) + mu64(f6, f9_38) + mu64(f7_2, f8_19);
-    h_[6] = mu64(f0_2, f6) + mu64(f1_2, f5_2) + mu64(f2_2, f4) + mu64(f3_2, f3) + mu64(f7_2, f9_38) +
-            mu64(f8, f8_19);
-    h_[7] = mu64(f0_2, f7) + mu64(f1_2, f6) + mu64(f2_2, f5) + mu64(f3_2, f4) + mu64(f8, f9_38);
-    h_[8] = mu64(f0_2, f8) + mu64(f1_2, f7_2) + mu64(f2_2, f6) + mu64(f3_2, f5_2) + mu64(f4, f4) +
-            mu64(f9, f9_38);
-    h_[9] = mu64(f0_2, f9) + mu64(f1_2, f8) + mu64(f2_2, f7) + mu64(f3_2, f6) + mu64(f4_2, f5);
-    if (dbl) {
+// Closing the sequential chain: the carry out of limb 9 (< 2^40) wraps into limb 0 as 19*c, and one
+// more carry takes limb 0 back under 2^26 (limb 1 stays < M_1 + 2^19: tight).
+CV_HD void fe_wrap_carry(fe &out, uint64_t c, uint32_t r[10]) {
+    c = c * 19 + r[0];
+    r[0] = (uint32_t)c & 0x3ffffffu;
+    r[1] += (uint32_t)(c >> 26);
 #pragma unroll
-        for (int i = 0; i < 10; i++) h_[i] += h_[i];
-    }
-    fe_reduce64(h, h_);
+    for (int i = 0; i < 10; i++) out.v[i] = r[i];
 }
-CV_HD void fe_sq(fe &h, const fe &f) { fe_sq_impl(h, f, false); }
-CV_HD void fe_sq2(fe &h, const fe &f) { fe_sq_impl(h, f, true); }
+
+// h[m] = f[m] * g[m] for m < N, interleaved (g[m] is the operand multiplied by 19: g <= 3.3, f <= 8).
+// Column k holds f_i g_j for i + j = k (mod 10): x2 when i and j are both odd (half-bit offsets),
+// x19 when i + j >= 10 (2^255 = 19).  Column sums stay < 2^63.7 (DESIGN.md "Field arithmetic").
+template <int N> CV_HD void fe_mul_n(fe (&h)[N], const fe (&f)[N], const fe (&g)[N]) {
+    uint32_t fd[N][10], g19[N][10];
+#pragma unroll
+    for (int m = 0; m < N; m++) {
+        fe_check_mul_in(f[m], g[m]);
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+            fd[m][i] = (i & 1) ? 2 * f[m].v[i] : f[m].v[i];
+            g19[m][i] = 19 * g[m].v[i];
+        }
+    }
+    uint64_t t[N];
+    uint32_t r[N][10];
+#pragma unroll
+    for (int m = 0; m < N; m++) t[m] = 0;
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+            const int j = (k - i + 10) % 10;
+            const bool dbl = (i & 1) && (j & 1);
+            const bool wrap = i + j >= 10;
+            uint32_t a[N], b[N];
+#pragma unroll
+            for (int m = 0; m < N; m++) {
+                a[m] = dbl ? fd[m][i] : f[m].v[i];
+                b[m] = wrap ? g19[m][j] : g[m].v[j];
+            }
+            cv_madc_n<N>(t, a, b);
+        }
+#pragma unroll
+        for (int m = 0; m < N; m++) {
+            r[m][k] = (uint32_t)t[m] & CV_MASK(k);
+            t[m] >>= CV_W(k);
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < N; m++) fe_wrap_carry(h[m], t[m], r[m]);
+}
+
+// Squaring: 55 products, column k as (left limb, left x1|x2, right limb, right x1|x2|x19|x38).
+// DBL bit m set: h[m] = 2 f[m]^2 (every left factor doubled; left factors stay < 2^29.7).
+// compile-time schedule (indices fold to constants inside the unrolled loops)
+CV_HD constexpr int cv_sq_cols(int k, int q, int field) {
+    // {l, lm, r, rm} of term q of column k; l = -1 marks an unused slot
+    constexpr int8_t T[10][6][4] = {
+        {{0, 1, 0, 1}, {1, 2, 9, 38}, {2, 2, 8, 19}, {3, 2, 7, 38}, {4, 2, 6, 19}, {5, 1, 5, 38}},
+        {{0, 2, 1, 1}, {2, 1, 9, 38}, {3, 2, 8, 19}, {4, 1, 7, 38}, {5, 2, 6, 19}, {-1, 0, 0, 0}},
+        {{0, 2, 2, 1}, {1, 2, 1, 1}, {3, 2, 9, 38}, {4, 2, 8, 19}, {5, 2, 7, 38}, {6, 1, 6, 19}},
+        {{0, 2, 3, 1}, {1, 2, 2, 1}, {4, 1, 9, 38}, {5, 2, 8, 19}, {6, 1, 7, 38}, {-1, 0, 0, 0}},
+        {{0, 2, 4, 1}, {1, 2, 3, 2}, {2, 1, 2, 1}, {5, 2, 9, 38}, {6, 2, 8, 19}, {7, 1, 7, 38}},
+        {{0, 2, 5, 1}, {1, 2, 4, 1}, {2, 2, 3, 1}, {6, 1, 9, 38}, {7, 2, 8, 19}, {-1, 0, 0, 0}},
+        {{0, 2, 6, 1}, {1, 2, 5, 2}, {2, 2, 4, 1}, {3, 2, 3, 1}, {7, 2, 9, 38}, {8, 1, 8, 19}},
+        {{0, 2, 7, 1}, {1, 2, 6, 1}, {2, 2, 5, 1}, {3, 2, 4, 1}, {8, 1, 9, 38}, {-1, 0, 0, 0}},
+        {{0, 2, 8, 1}, {1, 2, 7, 2}, {2, 2, 6, 1}, {3, 2, 5, 2}, {4, 1, 4, 1}, {9, 1, 9, 38}},
+        {{0, 2, 9, 1}, {1, 2, 8, 1}, {2, 2, 7, 1}, {3, 2, 6, 1}, {4, 2, 5, 1}, {-1, 0, 0, 0}},
+    };
+    return T[k][q][field];
+}
+
+template <int N, unsigned DBL = 0> CV_HD void fe_sq_n(fe (&h)[N], const fe (&f)[N]) {
+    // operand variants: left x1 / x2 (times 2 again for DBL chains), right x1 / x2 / x19 / x38
+    uint32_t l1[N][10], l2[N][10], r2[N][10], r19[N][10], r38[N][10];
+#pragma unroll
+    for (int m = 0; m < N; m++) {
+#if CV_CHECKING
+        for (int i = 0; i < 10; i++)
+            CV_ASSERT((uint64_t)f[m].v[i] * 10 < ((uint64_t)33 << CV_W(i)), "fe_sq: limb > 3.3M");
+#endif
+        const uint32_t k = (DBL >> m) & 1u;
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+            l1[m][i] = f[m].v[i] << k;
+            l2[m][i] = f[m].v[i] << (k + 1);
+            r2[m][i] = 2 * f[m].v[i];
+            r19[m][i] = 19 * f[m].v[i];
+            r38[m][i] = 38 * f[m].v[i];
+        }
+    }
+    uint64_t t[N];
+    uint32_t r[N][10];
+#pragma unroll
+    for (int m = 0; m < N; m++) t[m] = 0;
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+#pragma unroll
+        for (int q = 0; q < 6; q++) {
+            const int li = cv_sq_cols(k, q, 0), lm = cv_sq_cols(k, q, 1);
+            const int ri = cv_sq_cols(k, q, 2), rm = cv_sq_cols(k, q, 3);
+            if (li < 0) continue;
+            uint32_t a[N], b[N];
+#pragma unroll
+            for (int m = 0; m < N; m++) {
+                a[m] = lm == 2 ? l2[m][li] : l1[m][li];
+                b[m] = rm == 1 ? f[m].v[ri] : rm == 2 ? r2[m][ri] : rm == 19 ? r19[m][ri] : r38[m][ri];
+            }
+            cv_madc_n<N>(t, a, b);
+        }
+#pragma unroll
+        for (int m = 0; m < N; m++) {
+            r[m][k] = (uint32_t)t[m] & CV_MASK(k);
+            t[m] >>= CV_W(k);
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < N; m++) fe_wrap_carry(h[m], t[m], r[m]);
+}
+
+// single-operation forms
+CV_HD void fe_mul(fe &h, const fe &f, const fe &g) {
+    fe hh[1];
+    const fe ff[1] = {f}, gg[1] = {g};
+    fe_mul_n<1>(hh, ff, gg);
+    h = hh[0];
+}
+CV_HD void fe_sq(fe &h, const fe &f) {
+    fe hh[1];
+    const fe ff[1] = {f};
+    fe_sq_n<1, 0>(hh, ff);
+    h = hh[0];
+}
+CV_HD void fe_sq2(fe &h, const fe &f) {
+    fe hh[1];
+    const fe ff[1] = {f};
+    fe_sq_n<1, 1>(hh, ff);
+    h = hh[0];
+}
 
 // h = f^(2^n) (n >= 1).  A real loop keeps the code small; the trip count is hidden from the
 // optimiser so it cannot unroll the short chains into long straight-line blocks that the machine

@@ -37,16 +37,18 @@ CV_HD void ge_p2_identity(ge_p2 &r) { fe_zero(r.X); fe_one(r.Y); fe_one(r.Z); }
 CV_HD void ge_cached_identity(ge_cached &r) { fe_one(r.YplusX); fe_one(r.YminusX); fe_one(r.Z); fe_zero(r.T2d); }
 CV_HD void ge_precomp_identity(ge_precomp &r) { fe_one(r.yplusx); fe_one(r.yminusx); fe_zero(r.xy2d); }
 
+// Independent multiplications of one formula run interleaved (fe_mul_n, cv_field.h).
 CV_HD void ge_p1p1_to_p2(ge_p2 &r, const ge_p1p1 &p) {
-    fe_mul(r.X, p.T, p.X);
-    fe_mul(r.Y, p.Y, p.Z);
-    fe_mul(r.Z, p.T, p.Z);
+    fe h[3];
+    const fe f[3] = {p.T, p.Y, p.T}, g[3] = {p.X, p.Z, p.Z};
+    fe_mul_n<3>(h, f, g);
+    r.X = h[0]; r.Y = h[1]; r.Z = h[2];
 }
 CV_HD void ge_p1p1_to_p3(ge_p3 &r, const ge_p1p1 &p) {
-    fe_mul(r.X, p.T, p.X);
-    fe_mul(r.Y, p.Y, p.Z);
-    fe_mul(r.Z, p.T, p.Z);
-    fe_mul(r.T, p.X, p.Y);
+    fe h[4];
+    const fe f[4] = {p.T, p.Y, p.T, p.X}, g[4] = {p.X, p.Z, p.Z, p.Y};
+    fe_mul_n<4>(h, f, g);
+    r.X = h[0]; r.Y = h[1]; r.Z = h[2]; r.T = h[3];
 }
 CV_HD void ge_p3_to_p2(ge_p2 &r, const ge_p3 &p) { r.X = p.X; r.Y = p.Y; r.Z = p.Z; }
 CV_HD void ge_p3_to_cached(ge_cached &r, const ge_p3 &p) {
@@ -61,12 +63,11 @@ CV_HD void ge_p3_to_cached(ge_cached &r, const ge_p3 &p) {
 // r = 2p: 4 squarings.  p1p1 = (E, H', G, F') with E = 2XY, H' = X^2+Y^2, G = Y^2-X^2,
 // F' = 2Z^2-G: the negated (E, -H, G, -F) form of HWCD's doubling, which names the same point.
 CV_HD void ge_p2_dbl(ge_p1p1 &r, const ge_p2 &p) {
-    fe xx, yy, zz2, a, aa, hs;
-    fe_sq(xx, p.X);
-    fe_sq(yy, p.Y);
-    fe_sq2(zz2, p.Z);
+    fe a, hs, sq[4];
     fe_add(a, p.X, p.Y);
-    fe_sq(aa, a);
+    const fe in[4] = {p.X, p.Y, p.Z, a};
+    fe_sq_n<4, 0x4>(sq, in);      // X^2, Y^2, 2 Z^2, (X+Y)^2
+    const fe &xx = sq[0], &yy = sq[1], &zz2 = sq[2], &aa = sq[3];
     fe_add(hs, yy, xx);
     fe_carry(r.Y, hs);            // H' (tight: it is subtracted below with a 2p bias)
     fe_sub<2>(r.Z, yy, xx);       // G  <= 3.01
@@ -81,14 +82,14 @@ CV_HD void ge_p3_dbl(ge_p1p1 &r, const ge_p3 &p) {
 
 // r = p + q (q cached, possibly conditionally negated)
 CV_HD void ge_add(ge_p1p1 &r, const ge_p3 &p, const ge_cached &q) {
-    fe s, d, a, b, c, dd;
+    fe s, d, m[4];
     fe_add(s, p.Y, p.X);          // <= 2.02
     fe_sub<2>(d, p.Y, p.X);       // <= 3.01
-    fe_mul(a, q.YplusX, s);
-    fe_mul(b, q.YminusX, d);
-    fe_mul(c, q.T2d, p.T);
-    fe_mul(dd, p.Z, q.Z);
-    fe_add(dd, dd, dd);
+    const fe f[4] = {q.YplusX, q.YminusX, q.T2d, p.Z}, g[4] = {s, d, p.T, q.Z};
+    fe_mul_n<4>(m, f, g);
+    const fe &a = m[0], &b = m[1], &c = m[2];
+    fe dd;
+    fe_add(dd, m[3], m[3]);
     fe_sub<2>(r.X, a, b);         // E <= 3.01
     fe_add(r.Y, a, b);            // H <= 2.02
     fe_add(r.Z, dd, c);           // G <= 3.03
@@ -96,12 +97,12 @@ CV_HD void ge_add(ge_p1p1 &r, const ge_p3 &p, const ge_cached &q) {
 }
 // r = p + q (q affine precomp)
 CV_HD void ge_madd(ge_p1p1 &r, const ge_p3 &p, const ge_precomp &q) {
-    fe s, d, a, b, c, dd;
+    fe s, d, m[3], dd;
     fe_add(s, p.Y, p.X);
     fe_sub<2>(d, p.Y, p.X);
-    fe_mul(a, q.yplusx, s);
-    fe_mul(b, q.yminusx, d);
-    fe_mul(c, q.xy2d, p.T);
+    const fe f[3] = {q.yplusx, q.yminusx, q.xy2d}, g[3] = {s, d, p.T};
+    fe_mul_n<3>(m, f, g);
+    const fe &a = m[0], &b = m[1], &c = m[2];
     fe_add(dd, p.Z, p.Z);
     fe_sub<2>(r.X, a, b);
     fe_add(r.Y, a, b);

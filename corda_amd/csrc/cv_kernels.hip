@@ -163,25 +163,30 @@ extern "C" {
 // batch is processed in chunks of ws_cap.  bitmap gets ceil(n/64) words.
 hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off,
                       const uint32_t *len, uint64_t *bitmap, uint8_t *status, uint32_t *ws_hs, uint32_t *ws_tab,
-                      uint32_t *ws_R, uint8_t *ws_ok, uint32_t ws_cap, hipStream_t stream) {
+                      uint32_t *ws_R, uint8_t *ws_ok, uint32_t ws_cap, hipStream_t stream, hipEvent_t *ev) {
     if (n == 0) return hipSuccess;
     if (ws_cap == 0 || ws_cap % 512) return hipErrorInvalidValue;
     for (uint32_t c0 = 0; c0 < n; c0 += ws_cap) {
         const uint32_t m = (n - c0 < ws_cap) ? n - c0 : ws_cap;
         const uint32_t blocks = (m + CV_BLOCK - 1) / CV_BLOCK;
+        // ev (optional, single-chunk batches): phase boundaries for live per-kernel timing
+        if (ev && c0 == 0) (void)hipEventRecord(ev[0], stream);
         hipLaunchKernelGGL(cv_prep_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, pk + (size_t)c0 * 32,
                            sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_hs, ws_tab, ws_ok,
                            status ? status + c0 : nullptr);
+        if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);
         if (g_straus_waves == 2)
             hipLaunchKernelGGL(cv_straus_kernel<2>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, ws_tab, ws_R);
         else if (g_straus_waves == 4)
             hipLaunchKernelGGL(cv_straus_kernel<4>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, ws_tab, ws_R);
         else
             hipLaunchKernelGGL(cv_straus_kernel<3>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, ws_tab, ws_R);
+        if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
         const uint32_t nbytes = ((m + 63) / 64) * 8;
         hipLaunchKernelGGL(cv_finish_kernel, dim3((nbytes + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, stream, m,
                            nbytes, sig + (size_t)c0 * 64, ws_R, ws_ok,
                            reinterpret_cast<uint8_t *>(bitmap) + (size_t)c0 / 8);
+        if (ev && c0 == 0) (void)hipEventRecord(ev[3], stream);
     }
     return hipGetLastError();
 }
@@ -212,25 +217,26 @@ hipError_t cvk_merkle(uint32_t ntx, uint32_t nleaves, const uint8_t *arena, cons
 
 // ---------------------------------------------------------------- calibration microbenchmarks
 // Peak rate of the multiply-accumulate instruction the field arithmetic is built on (roofline
-// denominator): 8 independent accumulators x 16 unrolled v_mad_i64_i32 per iteration, no other VALU.
-__global__ __launch_bounds__(CV_BLOCK) void cv_mad_bench_kernel(uint32_t iters, int64_t *out) {
-    int64_t acc[8];
-    int32_t a[8], b[8];
+// denominator): 8 independent accumulators x 16 unrolled v_mad_u64_u32 per iteration, no other VALU.
+// (cv_field.h accumulates every limb product with v_mad_u64_u32.)
+__global__ __launch_bounds__(CV_BLOCK) void cv_mad_bench_kernel(uint32_t iters, uint64_t *out) {
+    uint64_t acc[8];
+    uint32_t a[8], b[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
         acc[k] = threadIdx.x + k;
-        a[k] = (int32_t)(threadIdx.x * 2654435761u + k);
-        b[k] = (int32_t)(blockIdx.x * 40503u + 7 * k + 1);
+        a[k] = threadIdx.x * 2654435761u + k;
+        b[k] = blockIdx.x * 40503u + 7 * k + 1;
     }
     for (uint32_t it = 0; it < iters; it++) {
 #pragma unroll
         for (int r = 0; r < 16; r++) {
 #pragma unroll
             for (int k = 0; k < 8; k++)
-                asm volatile("v_mad_i64_i32 %0, vcc, %1, %2, %0" : "+v"(acc[k]) : "v"(a[k]), "v"(b[(k + r) & 7]) : "vcc");
+                asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc[k]) : "v"(a[k]), "v"(b[(k + r) & 7]) : "vcc");
         }
     }
-    int64_t s = 0;
+    uint64_t s = 0;
 #pragma unroll
     for (int k = 0; k < 8; k++) s ^= acc[k];
     if (s == 0x1234567) out[0] = s;   // keep the chains alive
@@ -258,7 +264,7 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_femul_bench_kernel(uint32_t it
 extern "C" hipError_t cvk_calibrate(uint32_t iters, int which, uint32_t blocks, void *scratch, hipStream_t stream) {
     if (which == 0)
         hipLaunchKernelGGL(cv_mad_bench_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, iters,
-                           static_cast<int64_t *>(scratch));
+                           static_cast<uint64_t *>(scratch));
     else
         hipLaunchKernelGGL(cv_femul_bench_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, iters,
                            static_cast<int32_t *>(scratch));

@@ -13,7 +13,8 @@ from typing import Optional, Tuple
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcordaverify.so")
+# CV_LIB_PATH: load an alternative build of the same ABI (A/B tooling, tools/ab_lib.sh)
+LIB_PATH = os.environ.get("CV_LIB_PATH") or os.path.join(HERE, "libcordaverify.so")
 
 CV_OK = 0
 CV_SIG_OK = 0
@@ -25,7 +26,7 @@ CV_TX_EMPTY = 1
 EXPORTED = (
     "cv_open", "cv_close", "cv_strerror", "cv_version", "cv_device_count",
     "cv_ed25519_verify_batch", "cv_merkle_tx_ids", "cv_merkle_tx_ids_ex", "cv_ed25519_sign_batch",
-    "cv_tx_verdicts", "cv_ed25519_verify_device", "cv_ed25519_sign_device", "cv_merkle_tx_ids_device",
+    "cv_tx_verdicts", "cv_ed25519_verify_device", "cv_ed25519_verify_device_timed", "cv_ed25519_sign_device", "cv_merkle_tx_ids_device",
     "cv_synchronize", "cv_calibrate",
 )
 
@@ -78,6 +79,10 @@ def load():
         lib.cv_tx_verdicts.restype = ctypes.c_int
         lib.cv_ed25519_verify_device.argtypes = [_vp, ctypes.c_int, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
         lib.cv_ed25519_verify_device.restype = ctypes.c_int
+        if hasattr(lib, "cv_ed25519_verify_device_timed"):      # absent only in pre-r01 A/B builds
+            lib.cv_ed25519_verify_device_timed.argtypes = [_vp, ctypes.c_int, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                                           ctypes.POINTER(ctypes.c_float)]
+            lib.cv_ed25519_verify_device_timed.restype = ctypes.c_int
         lib.cv_ed25519_sign_device.argtypes = [_vp, ctypes.c_int, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
         lib.cv_ed25519_sign_device.restype = ctypes.c_int
         lib.cv_merkle_tx_ids_device.argtypes = [_vp, ctypes.c_int, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
@@ -199,6 +204,14 @@ class Engine:
         _check(self._lib.cv_ed25519_verify_device(self._h, device, n, d_pk, d_sig, d_arena, d_off, d_len, d_bitmap,
                                                   d_status or None, stream or None), "cv_ed25519_verify_device")
 
+    def verify_device_timed(self, device: int, n: int, d_pk: int, d_sig: int, d_arena: int, d_off: int, d_len: int,
+                            d_bitmap: int, stream: int = 0) -> Tuple[float, float, float]:
+        """Synchronous verify; returns the (prep, straus, finish) kernel durations in ms (HIP events)."""
+        ms = (ctypes.c_float * 3)()
+        _check(self._lib.cv_ed25519_verify_device_timed(self._h, device, n, d_pk, d_sig, d_arena, d_off, d_len,
+                                                        d_bitmap, stream or None, ms), "cv_ed25519_verify_device_timed")
+        return ms[0], ms[1], ms[2]
+
     def sign_device(self, device: int, n: int, d_seed: int, d_arena: int, d_off: int, d_len: int, d_pk: int,
                     d_sig: int, stream: int = 0):
         _check(self._lib.cv_ed25519_sign_device(self._h, device, n, d_seed, d_arena, d_off, d_len, d_pk, d_sig,
@@ -211,7 +224,7 @@ class Engine:
                "cv_merkle_tx_ids_device")
 
     def calibrate(self, device: int) -> Tuple[float, float]:
-        """(v_mad_i64_i32 per second, fe_mul per second) measured on `device` (roofline peak)."""
+        """(v_mad_u64_u32 per second, fe_mul per second) measured on `device` (roofline peak)."""
         a, b = ctypes.c_double(0), ctypes.c_double(0)
         _check(self._lib.cv_calibrate(self._h, device, ctypes.byref(a), ctypes.byref(b)), "cv_calibrate")
         return a.value, b.value

@@ -101,6 +101,14 @@ int cv_ed25519_verify_device(cv_ctx *ctx, int device, size_t n, const void *d_pk
                              const void *d_arena, const void *d_off, const void *d_len, void *d_bitmap,
                              void *d_status, void *stream);
 
+/* Measurement entry point (bench.py): as cv_ed25519_verify_device (no status), but synchronous,
+ * and fills phase_ms[0..2] with the summed durations of the three verify kernels measured with HIP
+ * events on the launch stream: prep (key decode, challenge hash, -A table), Straus
+ * double-scalar multiplication, finish (batched inversion, encode, compare, bitmap). */
+int cv_ed25519_verify_device_timed(cv_ctx *ctx, int device, size_t n, const void *d_pk, const void *d_sig,
+                                   const void *d_arena, const void *d_off, const void *d_len, void *d_bitmap,
+                                   void *stream, float *phase_ms);
+
 int cv_ed25519_sign_device(cv_ctx *ctx, int device, size_t n, const void *d_seed, const void *d_arena,
                            const void *d_off, const void *d_len, void *d_pk, void *d_sig, void *stream);
 
@@ -114,7 +122,7 @@ int cv_synchronize(cv_ctx *ctx, int device);
 
 /* ---------------------------------------------------------------- roofline calibration
  * Measures, on `device`, the chip-wide issue rate of the 32x32->64 multiply-accumulate
- * (v_mad_i64_i32) the field arithmetic is built on, and the practical GF(2^255-19) multiply rate of
+ * (v_mad_u64_u32) the field arithmetic is built on, and the practical GF(2^255-19) multiply rate of
  * the engine's fe_mul.  Either output pointer may be NULL.  Used by bench.py for roofline.peak.
  */
 int cv_calibrate(cv_ctx *ctx, int device, double *mad_per_s, double *femul_per_s);

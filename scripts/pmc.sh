@@ -2,6 +2,7 @@
 # PMC passes over the verify kernel (one counter group per rocprofv3 run; see MI355X_MICROARCH.md).
 set -e
 OUT=${1:-gpurun_out/pmc}
+cd "${GRAFT_REPO_ROOT:-.}" || exit 1
 mkdir -p $OUT
 export TMPDIR=/tmp
 ARGS="--steps 2 --warmup 0 --no-cpu --no-notary --n ${CV_PMC_N:-1000000}"
