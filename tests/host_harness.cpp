@@ -110,6 +110,30 @@ void cvh_fe_mul_limbs(const uint32_t *a, const uint32_t *b, uint8_t *out) {
     fe_to_words(ow, fo);
     bytes_from_words(out, ow, 8);
 }
+// the interleaved forms used by the group formulas: 4 products / 4 squares (the third doubled)
+void cvh_fe_mul4_limbs(const uint32_t *a, const uint32_t *b, uint8_t *out) {
+    fe f[4], g[4], h[4];
+    for (int m = 0; m < 4; m++) {
+        memcpy(f[m].v, a + 10 * m, 40);
+        memcpy(g[m].v, b + 10 * m, 40);
+    }
+    fe_mul_n<4>(h, f, g);
+    for (int m = 0; m < 4; m++) {
+        uint32_t ow[8];
+        fe_to_words(ow, h[m]);
+        bytes_from_words(out + 32 * m, ow, 8);
+    }
+}
+void cvh_fe_sq4_limbs(const uint32_t *a, uint8_t *out) {
+    fe f[4], h[4];
+    for (int m = 0; m < 4; m++) memcpy(f[m].v, a + 10 * m, 40);
+    fe_sq_n<4, 0x4>(h, f);
+    for (int m = 0; m < 4; m++) {
+        uint32_t ow[8];
+        fe_to_words(ow, h[m]);
+        bytes_from_words(out + 32 * m, ow, 8);
+    }
+}
 void cvh_fe_sq_limbs(const uint32_t *a, uint8_t *out) {
     fe fa, fo;
     memcpy(fa.v, a, 40);

@@ -77,6 +77,32 @@ def test_field_mul_at_limb_bounds(host_harness):
         assert _int(o) == _limb_val(a) % P
 
 
+def test_interleaved_mul_sq_at_limb_bounds(host_harness):
+    """fe_mul_n<4> / fe_sq_n<4, DBL> (sequential-carry columns, the forms the group formulas use) at
+    the precondition edges: mul f <= 8M, g <= 3.3M; sq f <= 3.3M, chain 2 doubled."""
+    H = host_harness
+    rng = random.Random(12)
+    W = [26, 25] * 5
+
+    def limbs(mult):
+        return [min(int(rng.choice([mult, mult * 0.999, rng.random() * mult, 0.0]) * (1 << W[i])),
+                    int(mult * (1 << W[i])) - 1) for i in range(10)]
+
+    for trial in range(150):
+        a = [limbs(8.0) for _ in range(4)]
+        b = [limbs(3.29) for _ in range(4)]
+        A = (ctypes.c_uint32 * 40)(*sum(a, []))
+        B = (ctypes.c_uint32 * 40)(*sum(b, []))
+        o = _out(128)
+        H.cvh_fe_mul4_limbs(A, B, o)
+        for m in range(4):
+            assert int.from_bytes(bytes(o)[32 * m:32 * m + 32], "little") == _limb_val(a[m]) * _limb_val(b[m]) % P
+        H.cvh_fe_sq4_limbs(B, o)
+        for m in range(4):
+            exp = _limb_val(b[m]) ** 2 * (2 if m == 2 else 1) % P
+            assert int.from_bytes(bytes(o)[32 * m:32 * m + 32], "little") == exp
+
+
 def test_sc_reduce(host_harness):
     H = host_harness
     rng = random.Random(3)
