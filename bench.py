@@ -88,9 +88,11 @@ def cpu_baseline(batch, rank_device: int, seconds: float):
             "accepted_fraction": float(vm.mean())}
 
 
-def notary_latency(eng, device: int, reps: int, cpu: bool):
-    """C4 at 4096: host-buffer verify (H2D + kernel + D2H) + per-tx AND, p50/p99 over reps."""
-    b = workload.make_batch(eng, device, 4096, 32, seed=4096)
+def notary_latency(eng, device: int, reps: int, cpu: bool, key_pool=None):
+    """C4 at 4096: host-buffer verify (H2D + kernel + D2H) + per-tx AND, p50/p99 over reps.  With
+    key_pool, the batch's signers come from that many parties (the engine's host dedupe then takes the
+    keyed path; the key pool is warm after the first repetition, as on a running notary)."""
+    b = workload.make_batch(eng, device, 4096, 32, seed=4096, key_pool=key_pool)
     expect = workload.corrupt_fraction(b, 16).cpu().numpy()
     pk, sig, arena, off, ln = b.to_host()
     tx_begin = np.arange(0, 4097, 8, dtype=np.uint32)            # 8 signers per tx (512 txs)
@@ -105,7 +107,7 @@ def notary_latency(eng, device: int, reps: int, cpu: bool):
     got = native.bitmap_to_bools(bitmap, 4096)
     assert np.array_equal(got, expect), "notary batch verdicts wrong"
     out = {"batch": 4096, "p50_ms": float(np.percentile(lat, 50) * 1e3), "p99_ms": float(np.percentile(lat, 99) * 1e3),
-           "reps": reps, "txs": 512, "tx_ok": int(txok.sum())}
+           "reps": reps, "txs": 512, "tx_ok": int(txok.sum()), "signer_keys": key_pool or "distinct"}
     if cpu:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import cv_oracle  # noqa: E402
@@ -119,6 +121,27 @@ def notary_latency(eng, device: int, reps: int, cpu: bool):
         out["cpu_p50_ms"] = float(np.median(cl) * 1e3)
         out["cpu_threads"] = threads
     return out
+
+
+def keyed_rate(eng, device: int, n: int, msg_len: int, steps: int, sh: int, pool: int = 1024):
+    """Keyed path (per-key comb tables) on the same C2 shape with a `pool`-key
+    pool: each step resolves the keys against the device key pool and verifies all n signatures."""
+    b = workload.make_batch(eng, device, n, msg_len, seed=4242, key_pool=pool, stream=sh)
+    bm = torch.zeros((n + 63) // 64, dtype=torch.int64, device=torch.device("cuda", device))
+    args = (device, n, b.nkeys, b.pk.data_ptr(), b.key_index.data_ptr(), b.sig.data_ptr(), b.arena.data_ptr(),
+            b.off.data_ptr(), b.len.data_ptr(), bm.data_ptr(), 0, sh)
+    cold = eng.verify_device_keyed(*args, timed=True)            # first call computes the key tables
+    ph = []
+    t = time.perf_counter()
+    for _ in range(steps):
+        ph.append(eng.verify_device_keyed(*args, timed=True))
+    dt = time.perf_counter() - t
+    assert bool((bm == -1).all()) or n % 64, "keyed path rejected an honest signature"
+    m = np.mean(np.array(ph), axis=0)
+    return {"workload": f"C2 shape, {pool}-key pool, keyed device path", "value": n * steps / dt,
+            "unit": "verifies/s", "ms_per_step": dt / steps * 1e3,
+            "phase_ms": {"key_tables": float(m[0]), "hash": float(m[1]), "comb": float(m[2]), "finish": float(m[3])},
+            "cold_key_tables_ms": float(cold[0]), "comb_work_per_unit": "240 S + 915 M per verify (60 doublings)"}
 
 
 def run_c3(args, eng, local, rank, world, stream, sh, dev):
@@ -184,6 +207,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-notary", action="store_true")
+    ap.add_argument("--no-keyed", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -295,8 +319,11 @@ def main():
         }
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(batch, local, args.cpu_seconds)
+        if not args.no_keyed and world == 1:
+            result["keyed"] = keyed_rate(eng, local, n, msg_len, max(3, args.steps // 2), sh)
         if not args.no_notary:
             result["notary"] = notary_latency(eng, local, 50, cpu=(world == 1 and not args.no_cpu))
+            result["notary_keyed"] = notary_latency(eng, local, 50, cpu=False, key_pool=64)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

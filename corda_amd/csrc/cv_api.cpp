@@ -4,9 +4,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstring>
 #include <mutex>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/cordaverify.h"
@@ -21,6 +23,13 @@ hipError_t cvk_merkle(uint32_t ntx, uint32_t nleaves, const uint8_t *arena, cons
                       const uint32_t *leaf_len, const uint32_t *tx_begin, uint32_t *leaf_digest, uint8_t *ids,
                       uint8_t *status, hipStream_t stream);
 hipError_t cvk_calibrate(uint32_t iters, int which, uint32_t blocks, void *scratch, hipStream_t stream);
+hipError_t cvk_keyprep(uint32_t nk, const uint8_t *keys, const uint32_t *slots, uint32_t *ktab_pool, uint8_t *kok_pool,
+                       hipStream_t stream);
+hipError_t cvk_verify_keyed(uint32_t n, const uint8_t *keys, const uint32_t *key_index, const uint32_t *slot_of_key,
+                            const uint32_t *ktab_pool, const uint8_t *kok_pool, const uint8_t *sig,
+                            const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
+                            uint8_t *status, uint32_t *ws_hs, uint32_t *ws_R, uint8_t *ws_ok, uint32_t ws_cap,
+                            hipStream_t stream, hipEvent_t *ev);
 }
 
 namespace {
@@ -50,13 +59,38 @@ struct DevBuf {
     }
 };
 
+// Device-resident per-key comb tables (keyed verify), content-addressed by the
+// 32 key bytes.  A key's tables are computed once (cv_keyprep_kernel) and reused by every later
+// batch on that device; when the pool is full it is emptied (epoch reset) before new keys go in.
+struct KeyHash {
+    size_t operator()(const std::array<uint8_t, 32> &k) const {
+        size_t h;
+        std::memcpy(&h, k.data() + 8, sizeof h);   // key bytes are uniformly distributed curve points
+        return h;
+    }
+};
+struct KeyCache {
+    DevBuf ktab, kok, keys, slots, slot_of_key, key_index;
+    uint32_t cap = 0;
+    std::unordered_map<std::array<uint8_t, 32>, uint32_t, KeyHash> map;
+    uint64_t hits = 0, misses = 0, resets = 0;
+};
+
 struct Device {
     int ordinal = 0;
     hipStream_t stream = nullptr;
     DevBuf pk, sig, arena, off, len, bitmap, status, seed, tx_begin, digest, ids;
     DevBuf ws_hs, ws_tab, ws_R, ws_ok;   // verify workspace (hs 64 B + tab 1280 B + R 128 B + ok 1 B per signature)
     uint32_t ws_cap = 0;
+    KeyCache kc;
 };
+
+// key-table pool capacity per device (keys); 5 KB of tables per key
+constexpr uint32_t kDefaultKeyCap = 1u << 16;
+constexpr size_t kKtabBytes = 1280 * 4;
+// cv_ed25519_verify_batch dedupes keys on the host up to this batch size, and takes the keyed
+// (per-key comb) path when the batch has at least two signatures per distinct key on average
+constexpr size_t kAutoKeyedMax = 1u << 18;
 
 // Verify workspace capacity: batches above it run in chunks of this many signatures.
 constexpr uint32_t kVerifyChunk = 1u << 21;
@@ -99,6 +133,7 @@ int hip_rc(hipError_t e) {
 struct cv_ctx {
     std::vector<Device> devs;
     std::mutex mu;
+    uint32_t key_cap = kDefaultKeyCap;
 };
 
 extern "C" {
@@ -148,7 +183,8 @@ void cv_close(cv_ctx *ctx) {
         (void)hipSetDevice(d.ordinal);
         if (d.stream) (void)hipStreamSynchronize(d.stream);
         for (DevBuf *b : {&d.pk, &d.sig, &d.arena, &d.off, &d.len, &d.bitmap, &d.status, &d.seed, &d.tx_begin,
-                          &d.digest, &d.ids, &d.ws_hs, &d.ws_tab, &d.ws_R, &d.ws_ok})
+                          &d.digest, &d.ids, &d.ws_hs, &d.ws_tab, &d.ws_R, &d.ws_ok, &d.kc.ktab, &d.kc.kok,
+                          &d.kc.keys, &d.kc.slots, &d.kc.slot_of_key, &d.kc.key_index})
             b->release();
         if (d.stream) (void)hipStreamDestroy(d.stream);
     }
@@ -223,6 +259,131 @@ template <class F> static int for_each_shard(cv_ctx *ctx, size_t n, F fn) {
     return CV_OK;
 }
 
+// ---------------------------------------------------------------- keyed verify (per-key comb tables)
+// Makes the keys k (used[k] != 0, or all when used == nullptr) of keys[0..nk) resident in d's key
+// pool and fills slot_of_key[k]; one keyprep launch on s computes the tables of the new ones.
+static int key_resolve(Device &d, uint32_t cap, size_t nk, const uint8_t *keys, const uint8_t *used,
+                       std::vector<uint32_t> &slot_of_key, hipStream_t s) {
+    KeyCache &kc = d.kc;
+    size_t nused = 0;
+    for (size_t k = 0; k < nk; k++) nused += used ? (used[k] != 0) : 1;
+    const size_t need = std::max<size_t>(cap, nused);
+    if (kc.cap < need) {                      // (re)allocate the pool; resident tables are dropped
+        if (need > 0xffffffffull / 2) return CV_E_TOO_LARGE;
+        CV_TRY(hipStreamSynchronize(s));
+        kc.ktab.release();
+        kc.kok.release();
+        CV_TRY(kc.ktab.ensure(need * kKtabBytes));
+        CV_TRY(kc.kok.ensure(need));
+        kc.cap = (uint32_t)need;
+        kc.map.clear();
+    }
+    if (kc.map.size() + nused > kc.cap) {     // epoch reset: every key of this call gets a fresh slot
+        kc.map.clear();
+        kc.resets++;
+    }
+    std::vector<uint8_t> miss_keys;
+    std::vector<uint32_t> miss_slots;
+    std::array<uint8_t, 32> key;
+    slot_of_key.assign(nk, 0);
+    for (size_t k = 0; k < nk; k++) {
+        if (used && !used[k]) continue;
+        std::memcpy(key.data(), keys + 32 * k, 32);
+        auto it = kc.map.find(key);
+        if (it != kc.map.end()) {
+            slot_of_key[k] = it->second;
+            kc.hits++;
+            continue;
+        }
+        const uint32_t slot = (uint32_t)kc.map.size();
+        kc.map.emplace(key, slot);
+        slot_of_key[k] = slot;
+        miss_keys.insert(miss_keys.end(), key.begin(), key.end());
+        miss_slots.push_back(slot);
+        kc.misses++;
+    }
+    if (!miss_slots.empty()) {
+        const size_t m = miss_slots.size();
+        CV_TRY(kc.keys.ensure(m * 32));
+        CV_TRY(kc.slots.ensure(m * 4));
+        CV_TRY(hipMemcpyAsync(kc.keys.p, miss_keys.data(), m * 32, hipMemcpyHostToDevice, s));
+        CV_TRY(hipMemcpyAsync(kc.slots.p, miss_slots.data(), m * 4, hipMemcpyHostToDevice, s));
+        CV_TRY(cvk_keyprep((uint32_t)m, kc.keys.as<uint8_t>(), kc.slots.as<uint32_t>(), kc.ktab.as<uint32_t>(),
+                           kc.kok.as<uint8_t>(), s));
+    }
+    return CV_OK;
+}
+
+// One shard [b, e) of a keyed host-buffer batch on one device (b a multiple of 64).
+static int verify_shard_keyed(uint32_t cap, Device &d, size_t b, size_t e, size_t nkeys, const uint8_t *keys,
+                              const uint32_t *key_index, const uint8_t *sig, const uint8_t *arena,
+                              const uint64_t *off, const uint32_t *len, uint64_t *bitmap, uint8_t *status) {
+    const size_t n = e - b;
+    if (n == 0) return CV_OK;
+    if (n > 0xffffffffull || nkeys > 0xffffffffull) return CV_E_TOO_LARGE;
+    CV_TRY(hipSetDevice(d.ordinal));
+    std::vector<uint8_t> used(nkeys, 0);
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (size_t i = b; i < e; i++) {
+        if (key_index[i] >= nkeys) return CV_E_ARGS;
+        used[key_index[i]] = 1;
+        lo = std::min<uint64_t>(lo, off[i]);
+        hi = std::max<uint64_t>(hi, off[i] + len[i]);
+    }
+    if (hi < lo) hi = lo;
+    hipStream_t s = d.stream;
+    std::vector<uint32_t> sok;
+    int rc = key_resolve(d, cap, nkeys, keys, used.data(), sok, s);
+    if (rc != CV_OK) return rc;
+    const size_t words = (n + 63) / 64;
+    KeyCache &kc = d.kc;
+    CV_TRY(d.pk.ensure(nkeys * 32));
+    CV_TRY(kc.slot_of_key.ensure(nkeys * 4));
+    CV_TRY(kc.key_index.ensure(n * 4));
+    CV_TRY(d.sig.ensure(n * 64));
+    CV_TRY(d.arena.ensure(hi - lo + 16));
+    CV_TRY(d.off.ensure(n * 8));
+    CV_TRY(d.len.ensure(n * 4));
+    CV_TRY(d.bitmap.ensure(words * 8));
+    CV_TRY(d.status.ensure(n));
+    CV_TRY(hipMemcpyAsync(d.pk.p, keys, nkeys * 32, hipMemcpyHostToDevice, s));
+    CV_TRY(hipMemcpyAsync(kc.slot_of_key.p, sok.data(), nkeys * 4, hipMemcpyHostToDevice, s));
+    CV_TRY(hipMemcpyAsync(kc.key_index.p, key_index + b, n * 4, hipMemcpyHostToDevice, s));
+    CV_TRY(hipMemcpyAsync(d.sig.p, sig + b * 64, n * 64, hipMemcpyHostToDevice, s));
+    if (hi > lo) CV_TRY(hipMemcpyAsync(d.arena.p, arena + lo, hi - lo, hipMemcpyHostToDevice, s));
+    CV_TRY(hipMemcpyAsync(d.off.p, off + b, n * 8, hipMemcpyHostToDevice, s));
+    CV_TRY(hipMemcpyAsync(d.len.p, len + b, n * 4, hipMemcpyHostToDevice, s));
+    CV_TRY(ensure_verify_ws(d, n));
+    CV_TRY(cvk_verify_keyed((uint32_t)n, d.pk.as<uint8_t>(), kc.key_index.as<uint32_t>(), kc.slot_of_key.as<uint32_t>(),
+                            kc.ktab.as<uint32_t>(), kc.kok.as<uint8_t>(), d.sig.as<uint8_t>(),
+                            d.arena.as<uint8_t>() - lo, d.off.as<uint64_t>(), d.len.as<uint32_t>(),
+                            d.bitmap.as<uint64_t>(), status ? d.status.as<uint8_t>() : nullptr, d.ws_hs.as<uint32_t>(),
+                            d.ws_R.as<uint32_t>(), d.ws_ok.as<uint8_t>(), d.ws_cap, s, nullptr));
+    CV_TRY(hipMemcpyAsync(bitmap + b / 64, d.bitmap.p, words * 8, hipMemcpyDeviceToHost, s));
+    if (status) CV_TRY(hipMemcpyAsync(status + b, d.status.p, n, hipMemcpyDeviceToHost, s));
+    CV_TRY(hipStreamSynchronize(s));
+    return CV_OK;
+}
+
+// Host-side key dedupe for the plain entry point: keys[] = distinct key bytes, key_index[i] = its
+// index.  Returns false when the batch does not repeat keys enough for the keyed path to pay.
+static bool dedupe_keys(size_t n, const uint8_t *pk, std::vector<uint8_t> &keys, std::vector<uint32_t> &key_index) {
+    if (n < 64 || n > kAutoKeyedMax) return false;
+    std::unordered_map<std::array<uint8_t, 32>, uint32_t, KeyHash> idx;
+    idx.reserve(n);
+    key_index.resize(n);
+    std::array<uint8_t, 32> key;
+    for (size_t i = 0; i < n; i++) {
+        std::memcpy(key.data(), pk + 32 * i, 32);
+        auto r = idx.emplace(key, (uint32_t)idx.size());
+        key_index[i] = r.first->second;
+        if (r.second && 2 * idx.size() > n) return false;   // fewer than two signatures per key
+    }
+    keys.resize(32 * idx.size());
+    for (auto &kv : idx) std::memcpy(keys.data() + 32 * (size_t)kv.second, kv.first.data(), 32);
+    return true;
+}
+
 extern "C" {
 
 int cv_ed25519_verify_batch(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg_arena,
@@ -232,9 +393,50 @@ int cv_ed25519_verify_batch(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint
     if (n == 0) return CV_OK;
     if (!pk || !sig || !msg_off || !msg_len || !verdict_bitmap) return CV_E_ARGS;
     std::lock_guard<std::mutex> g(ctx->mu);
+    std::vector<uint8_t> keys;
+    std::vector<uint32_t> key_index;
+    if (dedupe_keys(n, pk, keys, key_index)) {
+        const size_t nk = keys.size() / 32;
+        return for_each_shard(ctx, n, [&](Device &d, size_t b, size_t e) {
+            return verify_shard_keyed(ctx->key_cap, d, b, e, nk, keys.data(), key_index.data(), sig, msg_arena, msg_off,
+                                      msg_len, verdict_bitmap, status);
+        });
+    }
     return for_each_shard(ctx, n, [&](Device &d, size_t b, size_t e) {
         return verify_shard(d, b, e, pk, sig, msg_arena, msg_off, msg_len, verdict_bitmap, status);
     });
+}
+
+int cv_ed25519_verify_batch_keyed(cv_ctx *ctx, size_t n, size_t nkeys, const uint8_t *keys, const uint32_t *key_index,
+                                  const uint8_t *sig, const uint8_t *msg_arena, const uint64_t *msg_off,
+                                  const uint32_t *msg_len, uint64_t *verdict_bitmap, uint8_t *status) {
+    if (!ctx) return CV_E_ARGS;
+    if (n == 0) return CV_OK;
+    if (!keys || !key_index || !sig || !msg_off || !msg_len || !verdict_bitmap || nkeys == 0) return CV_E_ARGS;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    return for_each_shard(ctx, n, [&](Device &d, size_t b, size_t e) {
+        return verify_shard_keyed(ctx->key_cap, d, b, e, nkeys, keys, key_index, sig, msg_arena, msg_off, msg_len,
+                                  verdict_bitmap, status);
+    });
+}
+
+int cv_key_cache_reserve(cv_ctx *ctx, size_t max_keys) {
+    if (!ctx || max_keys == 0 || max_keys > 0x7fffffffull) return CV_E_ARGS;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    ctx->key_cap = (uint32_t)max_keys;
+    return CV_OK;
+}
+
+int cv_key_cache_stats(cv_ctx *ctx, int device, uint64_t *out4) {
+    if (!ctx || !out4) return CV_E_ARGS;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    Device *d = find_dev(ctx, device);
+    if (!d) return CV_E_ARGS;
+    out4[0] = d->kc.map.size();
+    out4[1] = d->kc.cap;
+    out4[2] = d->kc.hits;
+    out4[3] = d->kc.misses;
+    return CV_OK;
 }
 
 // ---------------------------------------------------------------- sign (host buffers)
@@ -387,6 +589,51 @@ int cv_ed25519_verify_device_timed(cv_ctx *ctx, int device, size_t n, const void
     for (hipEvent_t x : ev)
         if (x) (void)hipEventDestroy(x);
     return hip_rc(e);
+}
+
+int cv_ed25519_verify_device_keyed(cv_ctx *ctx, int device, size_t n, size_t nkeys, const void *d_keys,
+                                   const void *d_key_index, const void *d_sig, const void *d_arena, const void *d_off,
+                                   const void *d_len, void *d_bitmap, void *d_status, void *stream, float *phase_ms) {
+    if (!ctx) return CV_E_ARGS;
+    if (n == 0) return CV_OK;
+    if (n > 0xffffffffull || nkeys > 0xffffffffull) return CV_E_TOO_LARGE;
+    Device *d = find_dev(ctx, device);
+    if (!d || nkeys == 0 || !d_keys || !d_key_index || !d_sig || !d_arena || !d_off || !d_len || !d_bitmap)
+        return CV_E_ARGS;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    CV_TRY(hipSetDevice(d->ordinal));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : d->stream;
+    // the key bytes come to the host (32 B per distinct key) to resolve them against the pool
+    std::vector<uint8_t> hkeys(nkeys * 32);
+    CV_TRY(hipMemcpyAsync(hkeys.data(), d_keys, nkeys * 32, hipMemcpyDeviceToHost, s));
+    CV_TRY(hipStreamSynchronize(s));
+    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    hipError_t e = hipSuccess;
+    if (phase_ms)
+        for (int k = 0; k < 5 && e == hipSuccess; k++) e = hipEventCreate(&ev[k]);
+    if (e == hipSuccess && phase_ms) e = hipEventRecord(ev[0], s);
+    std::vector<uint32_t> sok;
+    int rc = e == hipSuccess ? key_resolve(*d, ctx->key_cap, nkeys, hkeys.data(), nullptr, sok, s) : hip_rc(e);
+    KeyCache &kc = d->kc;
+    if (rc == CV_OK) rc = hip_rc(kc.slot_of_key.ensure(nkeys * 4));
+    if (rc == CV_OK) rc = hip_rc(hipMemcpyAsync(kc.slot_of_key.p, sok.data(), nkeys * 4, hipMemcpyHostToDevice, s));
+    if (rc == CV_OK) rc = hip_rc(ensure_verify_ws(*d, n));
+    if (rc == CV_OK)
+        rc = hip_rc(cvk_verify_keyed((uint32_t)n, static_cast<const uint8_t *>(d_keys),
+                                     static_cast<const uint32_t *>(d_key_index), kc.slot_of_key.as<uint32_t>(),
+                                     kc.ktab.as<uint32_t>(), kc.kok.as<uint8_t>(), static_cast<const uint8_t *>(d_sig),
+                                     static_cast<const uint8_t *>(d_arena), static_cast<const uint64_t *>(d_off),
+                                     static_cast<const uint32_t *>(d_len), static_cast<uint64_t *>(d_bitmap),
+                                     static_cast<uint8_t *>(d_status), d->ws_hs.as<uint32_t>(), d->ws_R.as<uint32_t>(),
+                                     d->ws_ok.as<uint8_t>(), d->ws_cap, s, phase_ms ? ev + 1 : nullptr));
+    if (rc == CV_OK && phase_ms) {
+        e = hipEventSynchronize(ev[4]);
+        for (int k = 0; k < 4 && e == hipSuccess; k++) e = hipEventElapsedTime(&phase_ms[k], ev[k], ev[k + 1]);
+        rc = hip_rc(e);
+    }
+    for (hipEvent_t x : ev)
+        if (x) (void)hipEventDestroy(x);
+    return rc;
 }
 
 int cv_ed25519_sign_device(cv_ctx *ctx, int device, size_t n, const void *d_seed, const void *d_arena,

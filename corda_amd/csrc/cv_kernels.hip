@@ -106,6 +106,69 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_finish_kernel(uint32_t n, uint32_
     bitmap_bytes[j] = (uint8_t)bits;
 }
 
+// ---------------------------------------------------------------- keyed verify (per-key comb, f2)
+// key precompute: one lane per key (decode + 4 comb row tables of 8 cached multiples) into its slot
+__global__ __launch_bounds__(CV_BLOCK) void cv_keyprep_kernel(uint32_t nk, const uint8_t *__restrict__ keys,
+                                                              const uint32_t *__restrict__ slots,
+                                                              uint32_t *__restrict__ ktab_pool,
+                                                              uint8_t *__restrict__ kok_pool) {
+    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (i >= nk) return;
+    uint32_t aw[8];
+    load_words8(aw, keys + (size_t)i * 32);
+    const uint32_t slot = slots[i];
+    const bool ok = cv_key_prep(aw, ktab_pool + (size_t)slot * CV_KTAB_WORDS);
+    kok_pool[slot] = ok ? 1 : 0;
+}
+
+// keyed phase 1: hash + scalar per signature; key validity from the key's slot
+__global__ __launch_bounds__(CV_BLOCK) void cv_keyed_prep_kernel(
+    uint32_t n, const uint8_t *__restrict__ keys, const uint32_t *__restrict__ key_index,
+    const uint32_t *__restrict__ slot_of_key, const uint8_t *__restrict__ kok_pool, const uint8_t *__restrict__ sig,
+    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ off, const uint32_t *__restrict__ len,
+    uint32_t *__restrict__ ws_hs, uint8_t *__restrict__ ws_ok, uint8_t *__restrict__ status) {
+    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t ki = key_index[i];
+    uint32_t aw[8], rw[8], sw[8];
+    load_words8(aw, keys + (size_t)ki * 32);
+    load_words8(rw, sig + (size_t)i * 64);
+    load_words8(sw, sig + (size_t)i * 64 + 32);
+    uint32_t hs[CV_HS_WORDS];
+    cv_keyed_hs(aw, rw, sw, arena + off[i], len[i], hs);
+    store_words(ws_hs + (size_t)i * CV_HS_WORDS, hs, CV_HS_WORDS / 4);
+    const uint8_t ok = kok_pool[slot_of_key[ki]];
+    ws_ok[i] = ok;
+    if (status) status[i] = ok ? 0 : 1;
+}
+
+// keyed phase 2: the 4-row comb; the basepoint comb tables (66 KB) are staged in LDS
+#define CV_BCOMB_WORDS (4 * CV_BTAB_ENTRIES * CV_BTAB_STRIDE)
+__global__ __launch_bounds__(CV_BLOCK, 2) void cv_comb_kernel(uint32_t n, const uint32_t *__restrict__ ws_hs,
+                                                              const uint32_t *__restrict__ key_index,
+                                                              const uint32_t *__restrict__ slot_of_key,
+                                                              const uint32_t *__restrict__ ktab_pool,
+                                                              uint32_t *__restrict__ ws_R) {
+    __shared__ __attribute__((aligned(16))) uint32_t bcomb[CV_BCOMB_WORDS];
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(CV_BCOMB);
+        uint4 *dst = reinterpret_cast<uint4 *>(bcomb);
+        for (int q = threadIdx.x; q < CV_BCOMB_WORDS / 4; q += blockDim.x) dst[q] = src[q];
+        __syncthreads();
+    }
+    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t slot = slot_of_key[key_index[i]];
+    ge_p2 R;
+    cv_comb_straus(bcomb, ws_hs + (size_t)i * CV_HS_WORDS, ktab_pool + (size_t)slot * CV_KTAB_WORDS, R);
+    uint32_t rec[CV_R_WORDS];
+    fe_store(rec, R.X);
+    fe_store(rec + 10, R.Y);
+    fe_store(rec + 20, R.Z);
+    rec[30] = rec[31] = 0;
+    store_words(ws_R + (size_t)i * CV_R_WORDS, rec, CV_R_WORDS / 4);
+}
+
 // ---------------------------------------------------------------- sign (synthetic inputs)
 __global__ __launch_bounds__(CV_BLOCK, 2) void cv_sign_kernel(
     uint32_t n, const uint8_t *__restrict__ seed, const uint8_t *__restrict__ arena,
@@ -181,6 +244,43 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             hipLaunchKernelGGL(cv_straus_kernel<4>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, ws_tab, ws_R);
         else
             hipLaunchKernelGGL(cv_straus_kernel<3>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, ws_tab, ws_R);
+        if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
+        const uint32_t nbytes = ((m + 63) / 64) * 8;
+        hipLaunchKernelGGL(cv_finish_kernel, dim3((nbytes + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, stream, m,
+                           nbytes, sig + (size_t)c0 * 64, ws_R, ws_ok,
+                           reinterpret_cast<uint8_t *>(bitmap) + (size_t)c0 / 8);
+        if (ev && c0 == 0) (void)hipEventRecord(ev[3], stream);
+    }
+    return hipGetLastError();
+}
+
+hipError_t cvk_keyprep(uint32_t nk, const uint8_t *keys, const uint32_t *slots, uint32_t *ktab_pool, uint8_t *kok_pool,
+                       hipStream_t stream) {
+    if (nk == 0) return hipSuccess;
+    hipLaunchKernelGGL(cv_keyprep_kernel, dim3((nk + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, stream, nk, keys,
+                       slots, ktab_pool, kok_pool);
+    return hipGetLastError();
+}
+
+// Keyed verify of n signatures (key i = keys[key_index[i]], its tables in slot slot_of_key[...]),
+// chunked by the workspace capacity like cvk_verify.  ev: as in cvk_verify.
+hipError_t cvk_verify_keyed(uint32_t n, const uint8_t *keys, const uint32_t *key_index, const uint32_t *slot_of_key,
+                            const uint32_t *ktab_pool, const uint8_t *kok_pool, const uint8_t *sig,
+                            const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
+                            uint8_t *status, uint32_t *ws_hs, uint32_t *ws_R, uint8_t *ws_ok, uint32_t ws_cap,
+                            hipStream_t stream, hipEvent_t *ev) {
+    if (n == 0) return hipSuccess;
+    if (ws_cap == 0 || ws_cap % 512) return hipErrorInvalidValue;
+    for (uint32_t c0 = 0; c0 < n; c0 += ws_cap) {
+        const uint32_t m = (n - c0 < ws_cap) ? n - c0 : ws_cap;
+        const uint32_t blocks = (m + CV_BLOCK - 1) / CV_BLOCK;
+        if (ev && c0 == 0) (void)hipEventRecord(ev[0], stream);
+        hipLaunchKernelGGL(cv_keyed_prep_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, keys, key_index + c0,
+                           slot_of_key, kok_pool, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_hs, ws_ok,
+                           status ? status + c0 : nullptr);
+        if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);
+        hipLaunchKernelGGL(cv_comb_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, key_index + c0,
+                           slot_of_key, ktab_pool, ws_R);
         if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
         const uint32_t nbytes = ((m + 63) / 64) * 8;
         hipLaunchKernelGGL(cv_finish_kernel, dim3((nbytes + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, stream, m,

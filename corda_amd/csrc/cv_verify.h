@@ -102,6 +102,35 @@ CV_HD void ge_cached_load(ge_cached &c, const uint32_t *p) {
     fe_load(c.T2d, t + 30);
 }
 
+CV_HD void ge_p3_neg(ge_p3 &r, const ge_p3 &a) {
+    fe_neg(r.X, a.X);
+    fe_carry(r.X, r.X);
+    r.Y = a.Y;
+    r.Z = a.Z;
+    fe_neg(r.T, a.T);
+    fe_carry(r.T, r.T);
+}
+
+// tab[k-1] = k * P (k = 1..8) in cached form, 40 words per entry (16-B aligned)
+__host__ __device__ __forceinline__ void ge_cached_multiples8(uint32_t *tab, const ge_p3 &P1) {
+    ge_cached c1, c;
+    ge_p3 P;
+    ge_p3_to_cached(c1, P1);
+    ge_cached_store(tab, c1);
+    ge_p1p1 t;
+    ge_p3_dbl(t, P1);
+    ge_p1p1_to_p3(P, t);
+    ge_p3_to_cached(c, P);
+    ge_cached_store(tab + 40, c);
+#pragma unroll 1
+    for (int k = 3; k <= 8; k++) {
+        ge_add(t, P, c1);
+        ge_p1p1_to_p3(P, t);
+        ge_p3_to_cached(c, P);
+        ge_cached_store(tab + 40 * (k - 1), c);
+    }
+}
+
 // Phase 1.  Returns key_ok.  hs = h || s (16 words), tab = CV_TAB_WORDS words (16-B aligned).
 __host__ __device__ __forceinline__ bool cv_verify_prep(const uint32_t aw[8], const uint32_t rw[8], const uint32_t sw[8],
                                                const uint8_t *msg, uint32_t mlen, uint32_t *hs, uint32_t *tab) {
@@ -122,31 +151,11 @@ __host__ __device__ __forceinline__ bool cv_verify_prep(const uint32_t aw[8], co
 #pragma unroll
         for (int q = 0; q < 8; q++) hs[8 + q] = s[q];
     }
-    ge_p3 A;
+    ge_p3 A, nA;
     const bool key_ok = ge_decode_0_1_0(A, aw);
     if (!key_ok) ge_p3_identity(A);
-    ge_p3 nA, P;
-    fe_neg(nA.X, A.X);
-    fe_carry(nA.X, nA.X);
-    nA.Y = A.Y;
-    nA.Z = A.Z;
-    fe_neg(nA.T, A.T);
-    fe_carry(nA.T, nA.T);
-    ge_cached c1, c;
-    ge_p3_to_cached(c1, nA);
-    ge_cached_store(tab, c1);
-    ge_p1p1 t;
-    ge_p3_dbl(t, nA);
-    ge_p1p1_to_p3(P, t);
-    ge_p3_to_cached(c, P);
-    ge_cached_store(tab + 40, c);
-#pragma unroll 1
-    for (int k = 3; k <= 8; k++) {
-        ge_add(t, P, c1);
-        ge_p1p1_to_p3(P, t);
-        ge_p3_to_cached(c, P);
-        ge_cached_store(tab + 40 * (k - 1), c);
-    }
+    ge_p3_neg(nA, A);
+    ge_cached_multiples8(tab, nA);
     return key_ok;
 }
 
@@ -272,6 +281,117 @@ __host__ __device__ __forceinline__ bool cv_verify_one(const uint32_t *btab, con
     const uint8_t okb = key_ok ? 1 : 0;
     *key_ok_out = key_ok;
     return cv_verify_finish(Rrec, sigw, &okb, 1) & 1u;
+}
+
+// ---------------------------------------------------------------- keyed verify (per-key comb)
+// For keys that repeat across a batch (notary / party keys) the key work is
+// done once per key: decode A (eddsa-0.1.0 rules) and the comb tables
+//     T_j[k-1] = k * 2^(64 j) * (-A),   j = 0..3, k = 1..8        (CV_KTAB_WORDS words per key)
+// Then [h](-A) = sum_j [h_j] 2^(64 j)(-A) over the four 64-bit rows of h's signed radix-16 digits
+// (digit w = 16 j + u uses row table j at row position u), and [s]B likewise from CV_BCOMB
+// (digit k = 8 j + u/2 of s at even row positions u): 15 x 4 = 60 doublings instead of 252, the
+// same 64 + 32 additions.  The sums are exact integer scalar multiples, so torsion components of
+// A come out exactly as in the single-key schedule (and eddsa-0.1.0's slide-based one).
+
+#define CV_COMB_ROWS 4
+#define CV_KTAB_WORDS (CV_COMB_ROWS * CV_TAB_WORDS)   // 1280 words = 5 KB per key
+
+// Returns key_ok; ktab = CV_KTAB_WORDS words (16-B aligned).  Invalid keys get identity tables.
+__host__ __device__ __forceinline__ bool cv_key_prep(const uint32_t aw[8], uint32_t *ktab) {
+    ge_p3 A, P;
+    const bool key_ok = ge_decode_0_1_0(A, aw);
+    if (!key_ok) ge_p3_identity(A);
+    ge_p3_neg(P, A);
+#pragma unroll 1
+    for (int j = 0; j < CV_COMB_ROWS; j++) {
+        ge_cached_multiples8(ktab + j * CV_TAB_WORDS, P);
+        if (j + 1 < CV_COMB_ROWS) {   // P <- 2^64 P
+            ge_p2 q;
+            ge_p1p1 t;
+            ge_p3_to_p2(q, P);
+#pragma unroll 1
+            for (int d = 0; d < 63; d++) {
+                ge_p2_dbl(t, q);
+                ge_p1p1_to_p2(q, t);
+            }
+            ge_p2_dbl(t, q);
+            ge_p1p1_to_p3(P, t);
+        }
+    }
+    return key_ok;
+}
+
+// Keyed phase 1 for one signature: only the hash and scalar (the key work is in the table).
+__host__ __device__ __forceinline__ void cv_keyed_hs(const uint32_t aw[8], const uint32_t rw[8], const uint32_t sw[8],
+                                                     const uint8_t *msg, uint32_t mlen, uint32_t *hs) {
+    uint32_t pre[16], dig[16], h[8], abyte[8], s[8];
+    ge_abyte_from_key(abyte, aw);
+#pragma unroll
+    for (int q = 0; q < 8; q++) { pre[q] = rw[q]; pre[8 + q] = abyte[q]; }
+    sha512_pre_msg(dig, pre, 64, msg, mlen);
+    sc_reduce512(h, dig);
+    sc_effective_s(s, sw);
+#pragma unroll
+    for (int q = 0; q < 8; q++) { hs[q] = h[q]; hs[8 + q] = s[q]; }
+}
+
+// table entry |d| of row table `tab` (identity for d = 0), negated for d < 0
+CV_HD void ktab_select(ge_cached &e, const uint32_t *tab, int d) {
+    const int m = d < 0 ? -d : d;
+    ge_cached id;
+    ge_cached_load(e, tab + 40 * (m ? m - 1 : 0));
+    ge_cached_identity(id);
+    fe_sel(e.YplusX, e.YplusX, id.YplusX, m == 0);
+    fe_sel(e.YminusX, e.YminusX, id.YminusX, m == 0);
+    fe_sel(e.Z, e.Z, id.Z, m == 0);
+    fe_sel(e.T2d, e.T2d, id.T2d, m == 0);
+    ge_cached_cneg(e, d < 0);
+}
+
+// Keyed phase 2: R' = [h](-A) + [s]B by the 4-row comb.  bcomb = CV_BCOMB (global or LDS copy).
+__host__ __device__ __forceinline__ void cv_comb_straus(const uint32_t *bcomb, const uint32_t *hs, const uint32_t *ktab,
+                                                        ge_p2 &out) {
+    uint32_t h[8], s[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) { h[q] = hs[q]; s[q] = hs[8 + q]; }
+    ge_p2 R;
+    ge_p2_identity(R);
+#pragma unroll 1
+    for (int u = 15; u >= 0; u--) {
+        ge_p1p1 t;
+        ge_p3 R3;
+        if (u != 15) {
+            ge_p2_dbl(t, R);
+            ge_p1p1_to_p2(R, t);
+            ge_p2_dbl(t, R);
+            ge_p1p1_to_p2(R, t);
+            ge_p2_dbl(t, R);
+            ge_p1p1_to_p2(R, t);
+            ge_p2_dbl(t, R);
+            ge_p1p1_to_p3(R3, t);
+        } else {
+            ge_p3_identity(R3);
+        }
+        const bool with_b = (u & 1) == 0;
+#pragma unroll
+        for (int j = 0; j < CV_COMB_ROWS; j++) {
+            ge_cached e;
+            ktab_select(e, ktab + j * CV_TAB_WORDS, digit16(h, 16 * j + u));
+            ge_add(t, R3, e);
+            if (j + 1 < CV_COMB_ROWS || with_b) ge_p1p1_to_p3(R3, t);
+        }
+        if (with_b) {
+#pragma unroll
+            for (int j = 0; j < CV_COMB_ROWS; j++) {
+                ge_precomp e;
+                btab_select(e, bcomb + j * CV_BTAB_ENTRIES * CV_BTAB_STRIDE, digit256(s, 8 * j + (u >> 1)));
+                ge_madd(t, R3, e);
+                if (j + 1 < CV_COMB_ROWS) ge_p1p1_to_p3(R3, t);
+            }
+        }
+        ge_p1p1_to_p2(R, t);
+    }
+    out = R;
 }
 
 // ---------------------------------------------------------------- keygen + sign one message

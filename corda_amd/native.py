@@ -27,7 +27,8 @@ EXPORTED = (
     "cv_open", "cv_close", "cv_strerror", "cv_version", "cv_device_count",
     "cv_ed25519_verify_batch", "cv_merkle_tx_ids", "cv_merkle_tx_ids_ex", "cv_ed25519_sign_batch",
     "cv_tx_verdicts", "cv_ed25519_verify_device", "cv_ed25519_verify_device_timed", "cv_ed25519_sign_device", "cv_merkle_tx_ids_device",
-    "cv_synchronize", "cv_calibrate",
+    "cv_synchronize", "cv_calibrate", "cv_ed25519_verify_batch_keyed", "cv_key_cache_reserve", "cv_key_cache_stats",
+    "cv_ed25519_verify_device_keyed",
 )
 
 
@@ -89,6 +90,16 @@ def load():
         lib.cv_merkle_tx_ids_device.restype = ctypes.c_int
         lib.cv_synchronize.argtypes = [_vp, ctypes.c_int]
         lib.cv_synchronize.restype = ctypes.c_int
+        lib.cv_ed25519_verify_batch_keyed.argtypes = [_vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+        lib.cv_ed25519_verify_batch_keyed.restype = ctypes.c_int
+        lib.cv_key_cache_reserve.argtypes = [_vp, _sz]
+        lib.cv_key_cache_reserve.restype = ctypes.c_int
+        lib.cv_key_cache_stats.argtypes = [_vp, ctypes.c_int, _vp]
+        lib.cv_key_cache_stats.restype = ctypes.c_int
+        if hasattr(lib, "cv_ed25519_verify_device_keyed"):      # absent only in pre-r01 A/B builds
+            lib.cv_ed25519_verify_device_keyed.argtypes = [_vp, ctypes.c_int, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp,
+                                                           _vp, _vp, _vp, ctypes.POINTER(ctypes.c_float)]
+            lib.cv_ed25519_verify_device_keyed.restype = ctypes.c_int
         lib.cv_calibrate.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         lib.cv_calibrate.restype = ctypes.c_int
         _lib = lib
@@ -169,6 +180,38 @@ class Engine:
                                                      _p(bitmap), _p(status)), "cv_ed25519_verify_batch")
         return bitmap, status
 
+    def verify_batch_keyed(self, keys, key_index, sig, arena, off, ln, want_status: bool = True):
+        """keys (nk,32) distinct keys, key_index u32[n] -> (bitmap, status) exactly as verify_batch."""
+        keys = _u8(keys)
+        nk = keys.shape[0]
+        key_index = np.ascontiguousarray(key_index, dtype=np.uint32)
+        sig = _u8(sig)
+        n = key_index.shape[0]
+        if keys.size != nk * 32 or sig.size != n * 64:
+            raise ValueError("keys must be (nk,32) and sig (n,64)")
+        if n and int(key_index.max()) >= nk:
+            raise ValueError("key_index out of range")
+        arena = _u8(arena) if arena is not None and np.asarray(arena).size else np.zeros(16, np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        ln = np.ascontiguousarray(ln, dtype=np.uint32)
+        if n and int((off + ln).max()) > arena.size:
+            raise ValueError("message range exceeds the arena")
+        bitmap = np.zeros((n + 63) // 64, np.uint64)
+        status = np.zeros(n, np.uint8) if want_status else None
+        with self.mu:
+            _check(self._lib.cv_ed25519_verify_batch_keyed(self._h, n, nk, _p(keys), _p(key_index), _p(sig), _p(arena),
+                                                           _p(off), _p(ln), _p(bitmap), _p(status)),
+                   "cv_ed25519_verify_batch_keyed")
+        return bitmap, status
+
+    def key_cache_reserve(self, max_keys: int):
+        _check(self._lib.cv_key_cache_reserve(self._h, max_keys), "cv_key_cache_reserve")
+
+    def key_cache_stats(self, device: int = 0) -> dict:
+        out = np.zeros(4, np.uint64)
+        _check(self._lib.cv_key_cache_stats(self._h, device, _p(out)), "cv_key_cache_stats")
+        return {"resident": int(out[0]), "capacity": int(out[1]), "hits": int(out[2]), "misses": int(out[3])}
+
     def sign_batch(self, seeds, arena, off, ln) -> Tuple[np.ndarray, np.ndarray]:
         seeds = _u8(seeds)
         n = seeds.shape[0]
@@ -211,6 +254,16 @@ class Engine:
         _check(self._lib.cv_ed25519_verify_device_timed(self._h, device, n, d_pk, d_sig, d_arena, d_off, d_len,
                                                         d_bitmap, stream or None, ms), "cv_ed25519_verify_device_timed")
         return ms[0], ms[1], ms[2]
+
+    def verify_device_keyed(self, device: int, n: int, nkeys: int, d_keys: int, d_key_index: int, d_sig: int,
+                            d_arena: int, d_off: int, d_len: int, d_bitmap: int, d_status: int = 0, stream: int = 0,
+                            timed: bool = False):
+        """Keyed device batch; with timed=True synchronous, returns (keyprep, hash, comb, finish) ms."""
+        ms = (ctypes.c_float * 4)() if timed else None
+        _check(self._lib.cv_ed25519_verify_device_keyed(self._h, device, n, nkeys, d_keys, d_key_index, d_sig, d_arena,
+                                                        d_off, d_len, d_bitmap, d_status or None, stream or None, ms),
+               "cv_ed25519_verify_device_keyed")
+        return tuple(ms) if timed else None
 
     def sign_device(self, device: int, n: int, d_seed: int, d_arena: int, d_off: int, d_len: int, d_pk: int,
                     d_sig: int, stream: int = 0):

@@ -29,6 +29,8 @@ class SigBatch:
     off: torch.Tensor      # (n,) int64 (read as uint64), device
     len: torch.Tensor      # (n,) int32 (read as uint32), device
     msg_len: int
+    key_index: Optional[torch.Tensor] = None   # (n,) int32: key of signature i (key-pool batches)
+    nkeys: int = 0                             # distinct keys = pk[:nkeys] (key-pool batches)
 
     def to_host(self, lo: int = 0, hi: Optional[int] = None):
         hi = self.n if hi is None else hi
@@ -60,6 +62,9 @@ def make_batch(engine: native.Engine, device: int, n: int, msg_len: int, seed: i
                        pk.data_ptr(), sig.data_ptr(), stream)
     engine.synchronize(device)
     torch.cuda.synchronize(dev)
+    if key_pool is not None:
+        kidx = (torch.arange(n, device=dev) % key_pool).to(torch.int32)
+        return SigBatch(n, pk, sig, arena, off, ln, msg_len, kidx, min(key_pool, n))
     return SigBatch(n, pk, sig, arena, off, ln, msg_len)
 
 

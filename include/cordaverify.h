@@ -77,6 +77,25 @@ int cv_ed25519_verify_batch(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint
                             const uint8_t *msg_arena, const uint64_t *msg_off, const uint32_t *msg_len,
                             uint64_t *verdict_bitmap, uint8_t *status);
 
+/* Keyed batch: the distinct keys once, keys[nkeys][32], and per signature
+ * key_index[n] into them.  Replaces the same N x PublicKey.verifyWithECDSA as
+ * cv_ed25519_verify_batch — identical verdicts and status — for batches whose keys repeat (a notary
+ * batch, a ResolveTransactionsFlow chain, a party's transactions): the engine keeps per-key tables
+ * (decoded A and comb multiples k * 2^(64j) * (-A), 5 KB per key) resident on each device, keyed by
+ * the 32 key bytes, so a key is decoded once and each verify needs 60 doublings instead of 252.
+ * cv_ed25519_verify_batch takes this path by itself (host-side dedupe) for batches of up to 2^18
+ * signatures with at least two signatures per distinct key. */
+int cv_ed25519_verify_batch_keyed(cv_ctx *ctx, size_t n, size_t nkeys, const uint8_t *keys, const uint32_t *key_index,
+                                  const uint8_t *sig, const uint8_t *msg_arena, const uint64_t *msg_off,
+                                  const uint32_t *msg_len, uint64_t *verdict_bitmap, uint8_t *status);
+
+/* Per-device key-table pool capacity in keys (default 65536 = 320 MB of HBM per device); takes
+ * effect at the next keyed call.  A pool that fills up is emptied before new keys go in. */
+int cv_key_cache_reserve(cv_ctx *ctx, size_t max_keys);
+
+/* out4 = {resident keys, capacity, lookups that hit, lookups that missed} for `device`. */
+int cv_key_cache_stats(cv_ctx *ctx, int device, uint64_t *out4);
+
 int cv_merkle_tx_ids(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
                      const uint32_t *leaf_len, const uint32_t *tx_leaf_begin /* ntx+1 */, uint8_t *ids /* ntx*32 */);
 
@@ -108,6 +127,16 @@ int cv_ed25519_verify_device(cv_ctx *ctx, int device, size_t n, const void *d_pk
 int cv_ed25519_verify_device_timed(cv_ctx *ctx, int device, size_t n, const void *d_pk, const void *d_sig,
                                    const void *d_arena, const void *d_off, const void *d_len, void *d_bitmap,
                                    void *stream, float *phase_ms);
+
+/* Keyed device-resident batch: d_keys[nkeys][32], d_key_index[n] (uint32), the rest as
+ * cv_ed25519_verify_device.  The nkeys key records are copied to the host (32 B each) to resolve
+ * them against the key pool; new keys' tables are computed on `stream` before the verify.  Keyed
+ * calls on one device must share one stream (the pool is reused across calls in stream order).
+ * phase_ms NULL: returns without synchronising; else the call is synchronous and fills
+ * phase_ms[0..3] = key tables, hash, comb, finish kernel durations (HIP events). */
+int cv_ed25519_verify_device_keyed(cv_ctx *ctx, int device, size_t n, size_t nkeys, const void *d_keys,
+                                   const void *d_key_index, const void *d_sig, const void *d_arena, const void *d_off,
+                                   const void *d_len, void *d_bitmap, void *d_status, void *stream, float *phase_ms);
 
 int cv_ed25519_sign_device(cv_ctx *ctx, int device, size_t n, const void *d_seed, const void *d_arena,
                            const void *d_off, const void *d_len, void *d_pk, void *d_sig, void *stream);

@@ -27,6 +27,29 @@ int cvh_verify(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, uint32
     return ok ? 1 : 0;
 }
 
+// Keyed (per-key comb) verify of one signature: key prep + hash + comb + finish.
+int cvh_verify_keyed(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, uint32_t mlen, int *status) {
+    uint32_t aw[8], rw[8], sw[8];
+    words_from_bytes(aw, pk, 8);
+    words_from_bytes(rw, sig, 8);
+    words_from_bytes(sw, sig + 32, 8);
+    static thread_local uint32_t ktab[CV_KTAB_WORDS] __attribute__((aligned(16)));
+    uint32_t hs[CV_HS_WORDS];
+    uint32_t Rrec[CV_R_WORDS] __attribute__((aligned(16)));
+    const bool key_ok = cv_key_prep(aw, ktab);
+    cv_keyed_hs(aw, rw, sw, msg, mlen, hs);
+    ge_p2 R;
+    cv_comb_straus(CV_BCOMB_H, hs, ktab, R);
+    fe_store(Rrec, R.X);
+    fe_store(Rrec + 10, R.Y);
+    fe_store(Rrec + 20, R.Z);
+    uint32_t sigw[16];
+    for (int q = 0; q < 8; q++) { sigw[q] = rw[q]; sigw[8 + q] = sw[q]; }
+    const uint8_t okb = key_ok ? 1 : 0;
+    *status = key_ok ? 0 : 1;
+    return (int)(cv_verify_finish(Rrec, sigw, &okb, 1) & 1u);
+}
+
 // The GPU kernels' organisation on the host: prep + straus per signature, finish in lane chunks of
 // CV_FIN_CHUNK consecutive signatures.  verdict[i] = 0/1, status[i] = 0 ok / 1 bad key.
 void cvh_verify_batch(uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off,

@@ -186,6 +186,21 @@ def test_verify_logic_on_golden_corpus(host_harness, corpus, manifest):
     assert not bad, sorted(set(bad))
 
 
+def test_keyed_comb_logic_on_golden_corpus(host_harness, corpus, manifest):
+    """The per-key comb path (cv_key_prep + cv_keyed_hs + cv_comb_straus: 4 rows of 64-bit digits,
+    60 doublings) reproduces every golden verdict, torsion / mixed-order / invalid keys included."""
+    H = host_harness
+    bad = []
+    for i in range(len(corpus["pk"])):
+        m = corpus["arena"][corpus["off"][i]:corpus["off"][i] + corpus["len"][i]].tobytes()
+        st = ctypes.c_int(0)
+        v = H.cvh_verify_keyed(_b(corpus["pk"][i].tobytes()), _b(corpus["sig"][i].tobytes()), _b(m), len(m),
+                               ctypes.byref(st))
+        if v != corpus["verdict"][i] or st.value != corpus["status"][i]:
+            bad.append(manifest["classes"][corpus["cls"][i]])
+    assert not bad, sorted(set(bad))
+
+
 def test_sign_logic_matches_oracle(host_harness):
     H = host_harness
     rng = random.Random(8)

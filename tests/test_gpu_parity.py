@@ -176,3 +176,95 @@ def test_tx_verdicts_and():
     bitmap = np.array([0xFFFFFFFFFFFFFFF0, 0x1], np.uint64)
     begin = np.array([0, 4, 8, 64, 65, 65, 66], np.uint32)
     assert native.tx_verdicts(bitmap, begin).tolist() == [0, 1, 1, 1, 0, 0]
+
+
+# ---------------------------------------------------------------- keyed path (per-key comb tables, f2)
+def _dedupe(pk):
+    keys, inv = np.unique(pk, axis=0, return_inverse=True)
+    return keys, inv.reshape(-1).astype(np.uint32)
+
+
+def test_keyed_golden_corpus(engine, corpus, manifest):
+    """Every golden verdict and key status through the keyed path (torsion, mixed-order, invalid and
+    non-canonical keys included), and again on a warm key pool (all hits)."""
+    keys, kidx = _dedupe(corpus["pk"])
+    for rep in range(2):
+        before = engine.key_cache_stats(0)
+        bitmap, status = engine.verify_batch_keyed(keys, kidx, corpus["sig"], corpus["arena"], corpus["off"],
+                                                   corpus["len"])
+        got = _bits(bitmap, len(kidx))
+        bad = np.where(got != corpus["verdict"].astype(bool))[0]
+        assert bad.size == 0, f"keyed mismatches in {sorted({manifest['classes'][corpus['cls'][i]] for i in bad})}"
+        assert np.array_equal(status, corpus["status"])
+        after = engine.key_cache_stats(0)
+        if rep == 1:
+            assert after["misses"] == before["misses"], "warm pool recomputed key tables"
+
+
+def test_auto_keyed_path_matches_plain(engine, corpus):
+    """cv_ed25519_verify_batch dedupes keys itself when they repeat (>= 2 signatures per key)."""
+    idx = np.tile(np.arange(len(corpus["pk"])), 4)
+    before = engine.key_cache_stats(0)
+    bitmap, status = engine.verify_batch(corpus["pk"][idx], corpus["sig"][idx], corpus["arena"], corpus["off"][idx],
+                                         corpus["len"][idx])
+    assert np.array_equal(_bits(bitmap, idx.size), corpus["verdict"][idx].astype(bool))
+    assert np.array_equal(status, corpus["status"][idx])
+    after = engine.key_cache_stats(0)
+    assert after["hits"] + after["misses"] > before["hits"] + before["misses"], "keyed path not taken"
+
+
+def test_keyed_random_pool_vs_c_oracle(engine, oracle_c):
+    rng = np.random.default_rng(21)
+    n, pool = 6000, 37
+    kseeds = rng.integers(0, 256, (pool, 32), dtype=np.uint8)
+    kidx = rng.integers(0, pool, n).astype(np.uint32)
+    lens = rng.integers(0, 200, n).astype(np.uint32)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(lens[:-1])
+    arena = rng.integers(0, 256, int(lens.sum()) + 16, dtype=np.uint8)
+    pk, sig = engine.sign_batch(kseeds[kidx], arena, off, lens)
+    keys = pk[np.unique(kidx, return_index=True)[1]]
+    keys_full = np.zeros((pool, 32), np.uint8)
+    keys_full[np.unique(kidx)] = keys
+    sig[1::5, 40] ^= 0x04
+    sig[2::9, 63] |= 0x80
+    sig[3::11, 5] ^= 0x01
+    bitmap, status = engine.verify_batch_keyed(keys_full, kidx, sig, arena, off, lens)
+    ref, rst = oracle_c.verify_batch(keys_full[kidx], sig, arena, off, lens, nthreads=8)
+    assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
+    assert np.array_equal(status, rst)
+    assert 0.4 < ref.mean() < 0.9
+
+
+def test_keyed_pool_epoch_reset(engine, corpus):
+    """A pool smaller than the working set is emptied and refilled between calls; verdicts stay exact."""
+    from corda_amd import native
+    e = native.Engine(1)
+    try:
+        e.key_cache_reserve(8)
+        keys, kidx = _dedupe(corpus["pk"])
+        for lo in range(0, len(kidx), 100):
+            sl = slice(lo, lo + 100)
+            bm, st = e.verify_batch_keyed(keys, kidx[sl], corpus["sig"][sl], corpus["arena"], corpus["off"][sl],
+                                          corpus["len"][sl])
+            assert np.array_equal(_bits(bm, len(kidx[sl])), corpus["verdict"][sl].astype(bool))
+            assert np.array_equal(st, corpus["status"][sl])
+    finally:
+        e.close()
+
+
+def test_keyed_device_baseline_size(engine):
+    """C2 shape with a 1,024-key pool at full size on the keyed device path: all honest accepted, the
+    1/16 corruption pattern exactly rejected."""
+    import torch
+    from corda_amd import workload
+    n = 1_000_000
+    b = workload.make_batch(engine, 0, n, 300, seed=77, key_pool=1024)
+    bm = torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda:0")
+    args = (0, n, b.nkeys, b.pk.data_ptr(), b.key_index.data_ptr(), b.sig.data_ptr(), b.arena.data_ptr(),
+            b.off.data_ptr(), b.len.data_ptr(), bm.data_ptr())
+    engine.verify_device_keyed(*args, timed=True)
+    assert native.bitmap_to_bools(bm.cpu().numpy().view(np.uint64), n).all()
+    expect = workload.corrupt_fraction(b, 16).cpu().numpy()
+    engine.verify_device_keyed(*args, timed=True)
+    assert np.array_equal(native.bitmap_to_bools(bm.cpu().numpy().view(np.uint64), n), expect)
