@@ -142,25 +142,20 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_keyed_prep_kernel(
     if (status) status[i] = ok ? 0 : 1;
 }
 
-// keyed phase 2: the 4-row comb; the basepoint comb tables (66 KB) are staged in LDS
+// keyed phase 2: the 4-row comb.  The basepoint comb tables (66 KB) are read from global memory
+// (L2-resident: every lane of the chip reads the same table) so LDS does not cap the occupancy.
 #define CV_BCOMB_WORDS (4 * CV_BTAB_ENTRIES * CV_BTAB_STRIDE)
-__global__ __launch_bounds__(CV_BLOCK, 2) void cv_comb_kernel(uint32_t n, const uint32_t *__restrict__ ws_hs,
-                                                              const uint32_t *__restrict__ key_index,
-                                                              const uint32_t *__restrict__ slot_of_key,
-                                                              const uint32_t *__restrict__ ktab_pool,
-                                                              uint32_t *__restrict__ ws_R) {
-    __shared__ __attribute__((aligned(16))) uint32_t bcomb[CV_BCOMB_WORDS];
-    {
-        const uint4 *src = reinterpret_cast<const uint4 *>(CV_BCOMB);
-        uint4 *dst = reinterpret_cast<uint4 *>(bcomb);
-        for (int q = threadIdx.x; q < CV_BCOMB_WORDS / 4; q += blockDim.x) dst[q] = src[q];
-        __syncthreads();
-    }
+template <int WAVES>
+__global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_comb_kernel(uint32_t n, const uint32_t *__restrict__ ws_hs,
+                                                                  const uint32_t *__restrict__ key_index,
+                                                                  const uint32_t *__restrict__ slot_of_key,
+                                                                  const uint32_t *__restrict__ ktab_pool,
+                                                                  uint32_t *__restrict__ ws_R) {
     const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint32_t slot = slot_of_key[key_index[i]];
     ge_p2 R;
-    cv_comb_straus(bcomb, ws_hs + (size_t)i * CV_HS_WORDS, ktab_pool + (size_t)slot * CV_KTAB_WORDS, R);
+    cv_comb_straus(CV_BCOMB, ws_hs + (size_t)i * CV_HS_WORDS, ktab_pool + (size_t)slot * CV_KTAB_WORDS, R);
     uint32_t rec[CV_R_WORDS];
     fe_store(rec, R.X);
     fe_store(rec + 10, R.Y);
@@ -168,6 +163,12 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_comb_kernel(uint32_t n, const 
     rec[30] = rec[31] = 0;
     store_words(ws_R + (size_t)i * CV_R_WORDS, rec, CV_R_WORDS / 4);
 }
+template __global__ void cv_comb_kernel<2>(uint32_t, const uint32_t *, const uint32_t *, const uint32_t *,
+                                           const uint32_t *, uint32_t *);
+template __global__ void cv_comb_kernel<3>(uint32_t, const uint32_t *, const uint32_t *, const uint32_t *,
+                                           const uint32_t *, uint32_t *);
+static int g_comb_waves = 3;
+extern "C" void cvk_set_comb_waves(int w) { g_comb_waves = (w == 2) ? 2 : 3; }
 
 // ---------------------------------------------------------------- sign (synthetic inputs)
 __global__ __launch_bounds__(CV_BLOCK, 2) void cv_sign_kernel(
@@ -279,8 +280,12 @@ hipError_t cvk_verify_keyed(uint32_t n, const uint8_t *keys, const uint32_t *key
                            slot_of_key, kok_pool, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_hs, ws_ok,
                            status ? status + c0 : nullptr);
         if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);
-        hipLaunchKernelGGL(cv_comb_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, key_index + c0,
-                           slot_of_key, ktab_pool, ws_R);
+        if (g_comb_waves == 2)
+            hipLaunchKernelGGL(cv_comb_kernel<2>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, key_index + c0,
+                               slot_of_key, ktab_pool, ws_R);
+        else
+            hipLaunchKernelGGL(cv_comb_kernel<3>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, key_index + c0,
+                               slot_of_key, ktab_pool, ws_R);
         if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
         const uint32_t nbytes = ((m + 63) / 64) * 8;
         hipLaunchKernelGGL(cv_finish_kernel, dim3((nbytes + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, stream, m,

@@ -6,6 +6,7 @@ alternately in separate processes on one box (tools/ab_lib.sh) to A/B a kernel c
     CV_LIB_PATH=ab/old/libcv_old.so python tools/ab_lib.py --tag old
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -23,8 +24,15 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--msg", type=int, default=300)
     ap.add_argument("--tag", default=os.environ.get("CV_LIB_PATH", "default"))
+    ap.add_argument("--keyed", type=int, default=0, help="key pool size: time the keyed device path")
     args = ap.parse_args()
     eng = native.Engine(1)
+    lib = native.load()
+    if os.environ.get("CV_COMB_WAVES") and hasattr(lib, "cvk_set_comb_waves"):
+        lib.cvk_set_comb_waves.argtypes = [ctypes.c_int]
+        lib.cvk_set_comb_waves(int(os.environ["CV_COMB_WAVES"]))
+    if args.keyed:
+        return keyed(eng, args)
     stream = torch.cuda.Stream(0)
     torch.cuda.set_stream(stream)
     b = workload.make_batch(eng, 0, args.n, args.msg, seed=1, stream=stream.cuda_stream)
@@ -48,6 +56,21 @@ def main():
               for _ in range(3)]
         out["phase_ms"] = [round(float(x), 3) for x in np.median(np.array(ph), axis=0)]
     print(json.dumps(out), flush=True)
+
+
+def keyed(eng, args):
+    stream = torch.cuda.Stream(0)
+    torch.cuda.set_stream(stream)
+    b = workload.make_batch(eng, 0, args.n, args.msg, seed=1, key_pool=args.keyed, stream=stream.cuda_stream)
+    bm = torch.zeros((args.n + 63) // 64, dtype=torch.int64, device="cuda:0")
+    a = (0, args.n, b.nkeys, b.pk.data_ptr(), b.key_index.data_ptr(), b.sig.data_ptr(), b.arena.data_ptr(),
+         b.off.data_ptr(), b.len.data_ptr(), bm.data_ptr(), 0, stream.cuda_stream)
+    eng.verify_device_keyed(*a, timed=True)
+    ph = np.array([eng.verify_device_keyed(*a, timed=True) for _ in range(args.rounds)])
+    assert bool((bm == -1).all()) or args.n % 64, "honest batch rejected"
+    med = np.median(ph, axis=0)
+    print(json.dumps({"tag": args.tag, "keyed_pool": args.keyed, "phase_ms": [round(float(x), 3) for x in med],
+                      "total_ms": float(med.sum()), "verifies_per_s": args.n / (med.sum() * 1e-3)}), flush=True)
 
 
 if __name__ == "__main__":
