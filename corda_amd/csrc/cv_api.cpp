@@ -23,8 +23,8 @@ hipError_t cvk_merkle(uint32_t ntx, uint32_t nleaves, const uint8_t *arena, cons
                       const uint32_t *leaf_len, const uint32_t *tx_begin, uint32_t *leaf_digest, uint8_t *ids,
                       uint8_t *status, hipStream_t stream);
 hipError_t cvk_calibrate(uint32_t iters, int which, uint32_t blocks, void *scratch, hipStream_t stream);
-hipError_t cvk_keyprep(uint32_t nk, const uint8_t *keys, const uint32_t *slots, uint32_t *ktab_pool, uint8_t *kok_pool,
-                       hipStream_t stream);
+hipError_t cvk_keyprep(uint32_t nk, const uint8_t *keys, const uint32_t *slots, uint32_t *scratch, uint32_t *ktab_pool,
+                       uint8_t *kok_pool, hipStream_t stream);
 hipError_t cvk_verify_keyed(uint32_t n, const uint8_t *keys, const uint32_t *key_index, const uint32_t *slot_of_key,
                             const uint32_t *ktab_pool, const uint8_t *kok_pool, const uint8_t *sig,
                             const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
@@ -70,7 +70,7 @@ struct KeyHash {
     }
 };
 struct KeyCache {
-    DevBuf ktab, kok, keys, slots, slot_of_key, key_index;
+    DevBuf ktab, kok, keys, slots, slot_of_key, key_index, scratch;
     uint32_t cap = 0;
     std::unordered_map<std::array<uint8_t, 32>, uint32_t, KeyHash> map;
     uint64_t hits = 0, misses = 0, resets = 0;
@@ -85,9 +85,9 @@ struct Device {
     KeyCache kc;
 };
 
-// key-table pool capacity per device (keys); 5 KB of tables per key
+// key-table pool capacity per device (keys); 4 KB of tables per key
 constexpr uint32_t kDefaultKeyCap = 1u << 16;
-constexpr size_t kKtabBytes = 1280 * 4;
+constexpr size_t kKtabBytes = 1024 * 4;   // CV_KTAB_WORDS
 // cv_ed25519_verify_batch dedupes keys on the host up to this batch size, and takes the keyed
 // (per-key comb) path when the batch has at least two signatures per distinct key on average
 constexpr size_t kAutoKeyedMax = 1u << 18;
@@ -184,7 +184,7 @@ void cv_close(cv_ctx *ctx) {
         if (d.stream) (void)hipStreamSynchronize(d.stream);
         for (DevBuf *b : {&d.pk, &d.sig, &d.arena, &d.off, &d.len, &d.bitmap, &d.status, &d.seed, &d.tx_begin,
                           &d.digest, &d.ids, &d.ws_hs, &d.ws_tab, &d.ws_R, &d.ws_ok, &d.kc.ktab, &d.kc.kok,
-                          &d.kc.keys, &d.kc.slots, &d.kc.slot_of_key, &d.kc.key_index})
+                          &d.kc.keys, &d.kc.slots, &d.kc.slot_of_key, &d.kc.key_index, &d.kc.scratch})
             b->release();
         if (d.stream) (void)hipStreamDestroy(d.stream);
     }
@@ -306,10 +306,11 @@ static int key_resolve(Device &d, uint32_t cap, size_t nk, const uint8_t *keys, 
         const size_t m = miss_slots.size();
         CV_TRY(kc.keys.ensure(m * 32));
         CV_TRY(kc.slots.ensure(m * 4));
+        CV_TRY(kc.scratch.ensure(m * kKtabBytes));
         CV_TRY(hipMemcpyAsync(kc.keys.p, miss_keys.data(), m * 32, hipMemcpyHostToDevice, s));
         CV_TRY(hipMemcpyAsync(kc.slots.p, miss_slots.data(), m * 4, hipMemcpyHostToDevice, s));
-        CV_TRY(cvk_keyprep((uint32_t)m, kc.keys.as<uint8_t>(), kc.slots.as<uint32_t>(), kc.ktab.as<uint32_t>(),
-                           kc.kok.as<uint8_t>(), s));
+        CV_TRY(cvk_keyprep((uint32_t)m, kc.keys.as<uint8_t>(), kc.slots.as<uint32_t>(), kc.scratch.as<uint32_t>(),
+                           kc.ktab.as<uint32_t>(), kc.kok.as<uint8_t>(), s));
     }
     return CV_OK;
 }

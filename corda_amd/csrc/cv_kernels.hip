@@ -110,6 +110,7 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_finish_kernel(uint32_t n, uint32_
 // key precompute: one lane per key (decode + 4 comb row tables of 8 cached multiples) into its slot
 __global__ __launch_bounds__(CV_BLOCK) void cv_keyprep_kernel(uint32_t nk, const uint8_t *__restrict__ keys,
                                                               const uint32_t *__restrict__ slots,
+                                                              uint32_t *__restrict__ scratch,
                                                               uint32_t *__restrict__ ktab_pool,
                                                               uint8_t *__restrict__ kok_pool) {
     const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
@@ -117,7 +118,7 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_keyprep_kernel(uint32_t nk, const
     uint32_t aw[8];
     load_words8(aw, keys + (size_t)i * 32);
     const uint32_t slot = slots[i];
-    const bool ok = cv_key_prep(aw, ktab_pool + (size_t)slot * CV_KTAB_WORDS);
+    const bool ok = cv_key_prep(aw, scratch + (size_t)i * CV_KTAB_WORDS, ktab_pool + (size_t)slot * CV_KTAB_WORDS);
     kok_pool[slot] = ok ? 1 : 0;
 }
 
@@ -255,11 +256,12 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
     return hipGetLastError();
 }
 
-hipError_t cvk_keyprep(uint32_t nk, const uint8_t *keys, const uint32_t *slots, uint32_t *ktab_pool, uint8_t *kok_pool,
-                       hipStream_t stream) {
+// scratch: nk * CV_KTAB_WORDS words
+hipError_t cvk_keyprep(uint32_t nk, const uint8_t *keys, const uint32_t *slots, uint32_t *scratch, uint32_t *ktab_pool,
+                       uint8_t *kok_pool, hipStream_t stream) {
     if (nk == 0) return hipSuccess;
     hipLaunchKernelGGL(cv_keyprep_kernel, dim3((nk + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, stream, nk, keys,
-                       slots, ktab_pool, kok_pool);
+                       slots, scratch, ktab_pool, kok_pool);
     return hipGetLastError();
 }
 

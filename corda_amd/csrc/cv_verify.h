@@ -286,25 +286,53 @@ __host__ __device__ __forceinline__ bool cv_verify_one(const uint32_t *btab, con
 // ---------------------------------------------------------------- keyed verify (per-key comb)
 // For keys that repeat across a batch (notary / party keys) the key work is
 // done once per key: decode A (eddsa-0.1.0 rules) and the comb tables
-//     T_j[k-1] = k * 2^(64 j) * (-A),   j = 0..3, k = 1..8        (CV_KTAB_WORDS words per key)
+//     T_j[k-1] = k * 2^(64 j) * (-A),   j = 0..3, k = 1..8     (affine, CV_KTAB_WORDS words per key)
 // Then [h](-A) = sum_j [h_j] 2^(64 j)(-A) over the four 64-bit rows of h's signed radix-16 digits
 // (digit w = 16 j + u uses row table j at row position u), and [s]B likewise from CV_BCOMB
 // (digit k = 8 j + u/2 of s at even row positions u): 15 x 4 = 60 doublings instead of 252, the
-// same 64 + 32 additions.  The sums are exact integer scalar multiples, so torsion components of
+// same 64 + 32 additions, all mixed (affine tables).  The sums are exact integer scalar multiples, so torsion components of
 // A come out exactly as in the single-key schedule (and eddsa-0.1.0's slide-based one).
 
 #define CV_COMB_ROWS 4
-#define CV_KTAB_WORDS (CV_COMB_ROWS * CV_TAB_WORDS)   // 1280 words = 5 KB per key
+#define CV_KENT_WORDS 32                                      // one affine entry: 30 words + pad (128 B)
+#define CV_KROW_WORDS (8 * CV_KENT_WORDS)                     // 8 multiples per row table
+#define CV_KTAB_WORDS (CV_COMB_ROWS * CV_KROW_WORDS)          // 1024 words = 4 KB per key
 
-// Returns key_ok; ktab = CV_KTAB_WORDS words (16-B aligned).  Invalid keys get identity tables.
-__host__ __device__ __forceinline__ bool cv_key_prep(const uint32_t aw[8], uint32_t *ktab) {
+// (X, Y, Z) of k * P, k = 1..8, into ext[(k-1) * CV_KENT_WORDS ..] (X 0..9, Y 10..19, Z 20..29)
+__host__ __device__ __forceinline__ void ge_p3_multiples8(uint32_t *ext, const ge_p3 &P1) {
+    ge_cached c1;
+    ge_p3 P;
+    ge_p1p1 t;
+    ge_p3_to_cached(c1, P1);
+    P = P1;
+#pragma unroll 1
+    for (int k = 1; k <= 8; k++) {
+        if (k == 2) {
+            ge_p3_dbl(t, P1);
+            ge_p1p1_to_p3(P, t);
+        } else if (k > 2) {
+            ge_add(t, P, c1);
+            ge_p1p1_to_p3(P, t);
+        }
+        fe_store(ext + (k - 1) * CV_KENT_WORDS, P.X);
+        fe_store(ext + (k - 1) * CV_KENT_WORDS + 10, P.Y);
+        fe_store(ext + (k - 1) * CV_KENT_WORDS + 20, P.Z);
+    }
+}
+
+// Key precompute: decode A (eddsa-0.1.0 rules) and the comb tables of -A in affine "precomp" form
+//     ktab[j][k-1] = (y+x, y-x, 2dxy) of k * 2^(64 j) * (-A),   j = 0..3, k = 1..8
+// The 32 multiples are computed in extended coordinates into `ext` (CV_KTAB_WORDS words of scratch)
+// and normalised with one inversion (Montgomery's trick), so every table addition of the verify is a
+// mixed addition (3 products instead of 4).  Returns key_ok; invalid keys get identity tables.
+__host__ __device__ __forceinline__ bool cv_key_prep(const uint32_t aw[8], uint32_t *ext, uint32_t *ktab) {
     ge_p3 A, P;
     const bool key_ok = ge_decode_0_1_0(A, aw);
     if (!key_ok) ge_p3_identity(A);
     ge_p3_neg(P, A);
 #pragma unroll 1
     for (int j = 0; j < CV_COMB_ROWS; j++) {
-        ge_cached_multiples8(ktab + j * CV_TAB_WORDS, P);
+        ge_p3_multiples8(ext + j * CV_KROW_WORDS, P);
         if (j + 1 < CV_COMB_ROWS) {   // P <- 2^64 P
             ge_p2 q;
             ge_p1p1 t;
@@ -317,6 +345,48 @@ __host__ __device__ __forceinline__ bool cv_key_prep(const uint32_t aw[8], uint3
             ge_p2_dbl(t, q);
             ge_p1p1_to_p3(P, t);
         }
+    }
+    // prefix products of the Z's, parked in the (not yet written) xy2d words of ktab's entries
+    const int NE = CV_COMB_ROWS * 8;
+    fe acc, z;
+    fe_load(acc, ext + 20);
+    fe_store(ktab + 20, acc);
+#pragma unroll 1
+    for (int k = 1; k < NE; k++) {
+        fe_load(z, ext + k * CV_KENT_WORDS + 20);
+        fe_mul(acc, acc, z);
+        fe_store(ktab + k * CV_KENT_WORDS + 20, acc);
+    }
+    fe inv, d2;
+    fe_invert(inv, acc);
+    fe_const_d2(d2);
+#pragma unroll 1
+    for (int k = NE - 1; k >= 0; k--) {
+        fe zi, x, y, t;
+        if (k > 0) {
+            fe pre;
+            fe_load(pre, ktab + (k - 1) * CV_KENT_WORDS + 20);
+            fe_mul(zi, inv, pre);
+            fe_load(z, ext + k * CV_KENT_WORDS + 20);
+            fe_mul(inv, inv, z);
+        } else {
+            zi = inv;
+        }
+        fe_load(x, ext + k * CV_KENT_WORDS);
+        fe_load(y, ext + k * CV_KENT_WORDS + 10);
+        fe_mul(x, x, zi);
+        fe_mul(y, y, zi);
+        uint32_t *e = ktab + k * CV_KENT_WORDS;
+        fe_add(t, y, x);
+        fe_carry(t, t);
+        fe_store(e, t);                      // y + x
+        fe_sub<2>(t, y, x);
+        fe_carry(t, t);
+        fe_store(e + 10, t);                 // y - x
+        fe_mul(t, x, y);
+        fe_mul(t, t, d2);
+        fe_store(e + 20, t);                 // 2 d x y
+        e[30] = e[31] = 0;
     }
     return key_ok;
 }
@@ -335,17 +405,25 @@ __host__ __device__ __forceinline__ void cv_keyed_hs(const uint32_t aw[8], const
     for (int q = 0; q < 8; q++) { hs[q] = h[q]; hs[8 + q] = s[q]; }
 }
 
-// table entry |d| of row table `tab` (identity for d = 0), negated for d < 0
-CV_HD void ktab_select(ge_cached &e, const uint32_t *tab, int d) {
+// affine entry |d| of one key row table (identity for d = 0), negated for d < 0
+CV_HD void krow_select(ge_precomp &e, const uint32_t *row, int d) {
     const int m = d < 0 ? -d : d;
-    ge_cached id;
-    ge_cached_load(e, tab + 40 * (m ? m - 1 : 0));
-    ge_cached_identity(id);
-    fe_sel(e.YplusX, e.YplusX, id.YplusX, m == 0);
-    fe_sel(e.YminusX, e.YminusX, id.YminusX, m == 0);
-    fe_sel(e.Z, e.Z, id.Z, m == 0);
-    fe_sel(e.T2d, e.T2d, id.T2d, m == 0);
-    ge_cached_cneg(e, d < 0);
+    const uint4 *q = reinterpret_cast<const uint4 *>(row + (m ? m - 1 : 0) * CV_KENT_WORDS);
+    uint32_t t[32];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const uint4 v = q[j];
+        t[4 * j] = v.x; t[4 * j + 1] = v.y; t[4 * j + 2] = v.z; t[4 * j + 3] = v.w;
+    }
+    fe_load(e.yplusx, t);
+    fe_load(e.yminusx, t + 10);
+    fe_load(e.xy2d, t + 20);
+    ge_precomp id;
+    ge_precomp_identity(id);
+    fe_sel(e.yplusx, e.yplusx, id.yplusx, m == 0);
+    fe_sel(e.yminusx, e.yminusx, id.yminusx, m == 0);
+    fe_sel(e.xy2d, e.xy2d, id.xy2d, m == 0);
+    ge_precomp_cneg(e, d < 0);
 }
 
 // Keyed phase 2: R' = [h](-A) + [s]B by the 4-row comb.  bcomb = CV_BCOMB (global or LDS copy).
@@ -375,9 +453,9 @@ __host__ __device__ __forceinline__ void cv_comb_straus(const uint32_t *bcomb, c
         const bool with_b = (u & 1) == 0;
 #pragma unroll
         for (int j = 0; j < CV_COMB_ROWS; j++) {
-            ge_cached e;
-            ktab_select(e, ktab + j * CV_TAB_WORDS, digit16(h, 16 * j + u));
-            ge_add(t, R3, e);
+            ge_precomp e;
+            krow_select(e, ktab + j * CV_KROW_WORDS, digit16(h, 16 * j + u));
+            ge_madd(t, R3, e);
             if (j + 1 < CV_COMB_ROWS || with_b) ge_p1p1_to_p3(R3, t);
         }
         if (with_b) {

@@ -81,7 +81,7 @@ int cv_ed25519_verify_batch(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint
  * key_index[n] into them.  Replaces the same N x PublicKey.verifyWithECDSA as
  * cv_ed25519_verify_batch — identical verdicts and status — for batches whose keys repeat (a notary
  * batch, a ResolveTransactionsFlow chain, a party's transactions): the engine keeps per-key tables
- * (decoded A and comb multiples k * 2^(64j) * (-A), 5 KB per key) resident on each device, keyed by
+ * (decoded A and comb multiples k * 2^(64j) * (-A), 4 KB per key, affine) resident on each device, keyed by
  * the 32 key bytes, so a key is decoded once and each verify needs 60 doublings instead of 252.
  * cv_ed25519_verify_batch takes this path by itself (host-side dedupe) for batches of up to 2^18
  * signatures with at least two signatures per distinct key. */
@@ -89,7 +89,7 @@ int cv_ed25519_verify_batch_keyed(cv_ctx *ctx, size_t n, size_t nkeys, const uin
                                   const uint8_t *sig, const uint8_t *msg_arena, const uint64_t *msg_off,
                                   const uint32_t *msg_len, uint64_t *verdict_bitmap, uint8_t *status);
 
-/* Per-device key-table pool capacity in keys (default 65536 = 320 MB of HBM per device); takes
+/* Per-device key-table pool capacity in keys (default 65536 = 256 MB of HBM per device); takes
  * effect at the next keyed call.  A pool that fills up is emptied before new keys go in. */
 int cv_key_cache_reserve(cv_ctx *ctx, size_t max_keys);
 

@@ -34,9 +34,10 @@ int cvh_verify_keyed(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, 
     words_from_bytes(rw, sig, 8);
     words_from_bytes(sw, sig + 32, 8);
     static thread_local uint32_t ktab[CV_KTAB_WORDS] __attribute__((aligned(16)));
+    static thread_local uint32_t ext[CV_KTAB_WORDS] __attribute__((aligned(16)));
     uint32_t hs[CV_HS_WORDS];
     uint32_t Rrec[CV_R_WORDS] __attribute__((aligned(16)));
-    const bool key_ok = cv_key_prep(aw, ktab);
+    const bool key_ok = cv_key_prep(aw, ext, ktab);
     cv_keyed_hs(aw, rw, sw, msg, mlen, hs);
     ge_p2 R;
     cv_comb_straus(CV_BCOMB_H, hs, ktab, R);
