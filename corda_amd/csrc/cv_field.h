@@ -306,6 +306,102 @@ CV_HD void fe_sq2(fe &h, const fe &f) {
     h = hh[0];
 }
 
+// Latency forms (the quad kernels, cv_quad.h, which run where the chip is under-occupied): ten
+// independent column chains, then the carry chain with 64-bit adds — more instructions than the
+// sequential-carry forms but no long dependent chain, which is what a lone wave per SIMD waits on.
+// Floor carry of ten 64-bit column sums (each < 2^64) into a tight element.  Order: two
+// interleaved chains (0..4, 4..9) and the 2^255 = 19 wrap, as in the classic 25.5-bit schedule.
+#define CV_FCARRY(h, i, nxt)              \
+    {                                     \
+        nxt += h[i] >> CV_W(i);           \
+        h[i] &= (uint64_t)CV_MASK(i);     \
+    }
+CV_HD void fe_reduce64(fe &out, uint64_t h[10]) {
+    CV_FCARRY(h, 0, h[1]);
+    CV_FCARRY(h, 4, h[5]);
+    CV_FCARRY(h, 1, h[2]);
+    CV_FCARRY(h, 5, h[6]);
+    CV_FCARRY(h, 2, h[3]);
+    CV_FCARRY(h, 6, h[7]);
+    CV_FCARRY(h, 3, h[4]);
+    CV_FCARRY(h, 7, h[8]);
+    CV_FCARRY(h, 4, h[5]);
+    CV_FCARRY(h, 8, h[9]);
+    {
+        const uint64_t c = h[9] >> 25;
+        h[9] &= 0x1ffffffu;
+        h[0] += c * 19;
+    }
+    CV_FCARRY(h, 0, h[1]);
+#pragma unroll
+    for (int i = 0; i < 10; i++) out.v[i] = (uint32_t)h[i];
+}
+
+CV_HD void fe_mul_ilp(fe &h, const fe &f, const fe &g) {
+    fe_check_mul_in(f, g);
+    const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
+    const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
+    const uint32_t g0 = g.v[0], g1 = g.v[1], g2 = g.v[2], g3 = g.v[3], g4 = g.v[4];
+    const uint32_t g5 = g.v[5], g6 = g.v[6], g7 = g.v[7], g8 = g.v[8], g9 = g.v[9];
+    // 19*g_j folds the 2^255 wrap; 2*f_i (odd i) pays the extra half bit of odd*odd offsets
+    const uint32_t g1_19 = 19 * g1, g2_19 = 19 * g2, g3_19 = 19 * g3, g4_19 = 19 * g4, g5_19 = 19 * g5;
+    const uint32_t g6_19 = 19 * g6, g7_19 = 19 * g7, g8_19 = 19 * g8, g9_19 = 19 * g9;
+    const uint32_t f1_2 = 2 * f1, f3_2 = 2 * f3, f5_2 = 2 * f5, f7_2 = 2 * f7, f9_2 = 2 * f9;
+    uint64_t h_[10];
+    h_[0] = mu64(f0, g0) + mu64(f1_2, g9_19) + mu64(f2, g8_19) + mu64(f3_2, g7_19) + mu64(f4, g6_19) +
+            mu64(f5_2, g5_19) + mu64(f6, g4_19) + mu64(f7_2, g3_19) + mu64(f8, g2_19) + mu64(f9_2, g1_19);
+    h_[1] = mu64(f0, g1) + mu64(f1, g0) + mu64(f2, g9_19) + mu64(f3, g8_19) + mu64(f4, g7_19) +
+            mu64(f5, g6_19) + mu64(f6, g5_19) + mu64(f7, g4_19) + mu64(f8, g3_19) + mu64(f9, g2_19);
+    h_[2] = mu64(f0, g2) + mu64(f1_2, g1) + mu64(f2, g0) + mu64(f3_2, g9_19) + mu64(f4, g8_19) +
+            mu64(f5_2, g7_19) + mu64(f6, g6_19) + mu64(f7_2, g5_19) + mu64(f8, g4_19) + mu64(f9_2, g3_19);
+    h_[3] = mu64(f0, g3) + mu64(f1, g2) + mu64(f2, g1) + mu64(f3, g0) + mu64(f4, g9_19) +
+            mu64(f5, g8_19) + mu64(f6, g7_19) + mu64(f7, g6_19) + mu64(f8, g5_19) + mu64(f9, g4_19);
+    h_[4] = mu64(f0, g4) + mu64(f1_2, g3) + mu64(f2, g2) + mu64(f3_2, g1) + mu64(f4, g0) +
+            mu64(f5_2, g9_19) + mu64(f6, g8_19) + mu64(f7_2, g7_19) + mu64(f8, g6_19) + mu64(f9_2, g5_19);
+    h_[5] = mu64(f0, g5) + mu64(f1, g4) + mu64(f2, g3) + mu64(f3, g2) + mu64(f4, g1) +
+            mu64(f5, g0) + mu64(f6, g9_19) + mu64(f7, g8_19) + mu64(f8, g7_19) + mu64(f9, g6_19);
+    h_[6] = mu64(f0, g6) + mu64(f1_2, g5) + mu64(f2, g4) + mu64(f3_2, g3) + mu64(f4, g2) +
+            mu64(f5_2, g1) + mu64(f6, g0) + mu64(f7_2, g9_19) + mu64(f8, g8_19) + mu64(f9_2, g7_19);
+    h_[7] = mu64(f0, g7) + mu64(f1, g6) + mu64(f2, g5) + mu64(f3, g4) + mu64(f4, g3) +
+            mu64(f5, g2) + mu64(f6, g1) + mu64(f7, g0) + mu64(f8, g9_19) + mu64(f9, g8_19);
+    h_[8] = mu64(f0, g8) + mu64(f1_2, g7) + mu64(f2, g6) + mu64(f3_2, g5) + mu64(f4, g4) +
+            mu64(f5_2, g3) + mu64(f6, g2) + mu64(f7_2, g1) + mu64(f8, g0) + mu64(f9_2, g9_19);
+    h_[9] = mu64(f0, g9) + mu64(f1, g8) + mu64(f2, g7) + mu64(f3, g6) + mu64(f4, g5) +
+            mu64(f5, g4) + mu64(f6, g3) + mu64(f7, g2) + mu64(f8, g1) + mu64(f9, g0);
+    fe_reduce64(h, h_);
+}
+
+CV_HD void fe_sq_ilp(fe &h, const fe &f, bool dbl) {
+#if CV_CHECKING
+    for (int i = 0; i < 10; i++) CV_ASSERT((uint64_t)f.v[i] * 10 < ((uint64_t)33 << CV_W(i)), "fe_sq: limb > 3.3M");
+#endif
+    const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
+    const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
+    const uint32_t f0_2 = 2 * f0, f1_2 = 2 * f1, f2_2 = 2 * f2, f3_2 = 2 * f3, f4_2 = 2 * f4;
+    const uint32_t f5_2 = 2 * f5, f6_2 = 2 * f6, f7_2 = 2 * f7;
+    const uint32_t f5_38 = 38 * f5, f6_19 = 19 * f6, f7_38 = 38 * f7, f8_19 = 19 * f8, f9_38 = 38 * f9;
+    uint64_t h_[10];
+    h_[0] = mu64(f0, f0) + mu64(f1_2, f9_38) + mu64(f2_2, f8_19) + mu64(f3_2, f7_38) + mu64(f4_2, f6_19) +
+            mu64(f5, f5_38);
+    h_[1] = mu64(f0_2, f1) + mu64(f2, f9_38) + mu64(f3_2, f8_19) + mu64(f4, f7_38) + mu64(f5_2, f6_19);
+    h_[2] = mu64(f0_2, f2) + mu64(f1_2, f1) + mu64(f3_2, f9_38) + mu64(f4_2, f8_19) + mu64(f5_2, f7_38) +
+            mu64(f6, f6_19);
+    h_[3] = mu64(f0_2, f3) + mu64(f1_2, f2) + mu64(f4, f9_38) + mu64(f5_2, f8_19) + mu64(f6, f7_38);
+    h_[4] = mu64(f0_2, f4) + mu64(f1_2, f3_2) + mu64(f2, f2) + mu64(f5_2, f9_38) + mu64(f6_2, f8_19) +
+            mu64(f7, f7_38);
+    h_[5] = mu64(f0_2, f5) + mu64(f1_2, f4) + mu64(f2_2, f3) + mu64(f6, f9_38) + mu64(f7_2, f8_19);
+    h_[6] = mu64(f0_2, f6) + mu64(f1_2, f5_2) + mu64(f2_2, f4) + mu64(f3_2, f3) + mu64(f7_2, f9_38) +
+            mu64(f8, f8_19);
+    h_[7] = mu64(f0_2, f7) + mu64(f1_2, f6) + mu64(f2_2, f5) + mu64(f3_2, f4) + mu64(f8, f9_38);
+    h_[8] = mu64(f0_2, f8) + mu64(f1_2, f7_2) + mu64(f2_2, f6) + mu64(f3_2, f5_2) + mu64(f4, f4) +
+            mu64(f9, f9_38);
+    h_[9] = mu64(f0_2, f9) + mu64(f1_2, f8) + mu64(f2_2, f7) + mu64(f3_2, f6) + mu64(f4_2, f5);
+    if (dbl) {
+#pragma unroll
+        for (int i = 0; i < 10; i++) h_[i] += h_[i];
+    }
+    fe_reduce64(h, h_);
+}
 // h = f^(2^n) (n >= 1).  A real loop keeps the code small; the trip count is hidden from the
 // optimiser so it cannot unroll the short chains into long straight-line blocks that the machine
 // scheduler then interleaves into VGPR spills.

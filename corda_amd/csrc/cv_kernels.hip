@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include "cv_verify.h"
+#include "cv_quad.h"
 
 #define CV_BLOCK 256
 
@@ -105,6 +106,39 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_finish_kernel(uint32_t n, uint32_
     }
     bitmap_bytes[j] = (uint8_t)bits;
 }
+
+// ---------------------------------------------------------------- quad (latency) Straus kernels
+// Four lanes per signature (cv_quad.h) for batches too small to fill the chip.  Grid: 4n lanes.
+__global__ __launch_bounds__(CV_BLOCK) void cv_straus_quad_kernel(uint32_t n, const uint32_t *__restrict__ ws_hs,
+                                                                  const uint32_t *__restrict__ ws_tab,
+                                                                  uint32_t *__restrict__ ws_R) {
+    __shared__ __attribute__((aligned(16))) uint32_t btab[CV_BTAB_ENTRIES * CV_BTAB_STRIDE];
+    stage_btab(btab);
+    const uint32_t i = (blockIdx.x * CV_BLOCK + threadIdx.x) >> 2;
+    const int r = threadIdx.x & 3;
+    if (i >= n) return;                       // whole quads leave together
+    fe P;
+    cv_quad_straus(btab, ws_hs + (size_t)i * CV_HS_WORDS, ws_tab + (size_t)i * CV_TAB_WORDS, r, P);
+    if (r < 3) fe_store(ws_R + (size_t)i * CV_R_WORDS + 10 * r, P);
+}
+
+__global__ __launch_bounds__(CV_BLOCK) void cv_comb_quad_kernel(uint32_t n, const uint32_t *__restrict__ ws_hs,
+                                                                const uint32_t *__restrict__ key_index,
+                                                                const uint32_t *__restrict__ slot_of_key,
+                                                                const uint32_t *__restrict__ ktab_pool,
+                                                                uint32_t *__restrict__ ws_R) {
+    const uint32_t i = (blockIdx.x * CV_BLOCK + threadIdx.x) >> 2;
+    const int r = threadIdx.x & 3;
+    if (i >= n) return;
+    const uint32_t slot = slot_of_key[key_index[i]];
+    fe P;
+    cv_quad_comb(CV_BCOMB, ws_hs + (size_t)i * CV_HS_WORDS, ktab_pool + (size_t)slot * CV_KTAB_WORDS, r, P);
+    if (r < 3) fe_store(ws_R + (size_t)i * CV_R_WORDS + 10 * r, P);
+}
+
+// Batches of at most this many signatures run the quad kernels (set by cvk_set_quad_max; 0 = never)
+static uint32_t g_quad_max = 32768;
+extern "C" void cvk_set_quad_max(uint32_t m) { g_quad_max = m; }
 
 // ---------------------------------------------------------------- keyed verify (per-key comb, f2)
 // key precompute: one lane per key (decode + 4 comb row tables of 8 cached multiples) into its slot
@@ -240,7 +274,10 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
                            sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_hs, ws_tab, ws_ok,
                            status ? status + c0 : nullptr);
         if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);
-        if (g_straus_waves == 2)
+        if (n <= g_quad_max)
+            hipLaunchKernelGGL(cv_straus_quad_kernel, dim3((4 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
+                               stream, m, ws_hs, ws_tab, ws_R);
+        else if (g_straus_waves == 2)
             hipLaunchKernelGGL(cv_straus_kernel<2>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, ws_tab, ws_R);
         else if (g_straus_waves == 4)
             hipLaunchKernelGGL(cv_straus_kernel<4>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, ws_tab, ws_R);
@@ -282,7 +319,10 @@ hipError_t cvk_verify_keyed(uint32_t n, const uint8_t *keys, const uint32_t *key
                            slot_of_key, kok_pool, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_hs, ws_ok,
                            status ? status + c0 : nullptr);
         if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);
-        if (g_comb_waves == 2)
+        if (n <= g_quad_max)
+            hipLaunchKernelGGL(cv_comb_quad_kernel, dim3((4 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, stream,
+                               m, ws_hs, key_index + c0, slot_of_key, ktab_pool, ws_R);
+        else if (g_comb_waves == 2)
             hipLaunchKernelGGL(cv_comb_kernel<2>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, key_index + c0,
                                slot_of_key, ktab_pool, ws_R);
         else

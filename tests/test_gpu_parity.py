@@ -268,3 +268,36 @@ def test_keyed_device_baseline_size(engine):
     expect = workload.corrupt_fraction(b, 16).cpu().numpy()
     engine.verify_device_keyed(*args, timed=True)
     assert np.array_equal(native.bitmap_to_bools(bm.cpu().numpy().view(np.uint64), n), expect)
+
+
+# ---------------------------------------------------------------- both Straus forms at every size
+@pytest.mark.parametrize("quad_max", [0, 1 << 30])
+def test_lane_and_quad_forms_agree(engine, corpus, oracle_c, quad_max):
+    """Small batches normally run the 4-lanes-per-signature (quad) Straus; force each form in turn
+    (internal switch cvk_set_quad_max) over the golden corpus, keyed and plain, and a random batch."""
+    import ctypes
+    lib = native.load()
+    lib.cvk_set_quad_max.argtypes = [ctypes.c_uint32]
+    lib.cvk_set_quad_max(quad_max)
+    try:
+        bitmap, status = engine.verify_batch(corpus["pk"], corpus["sig"], corpus["arena"], corpus["off"], corpus["len"])
+        assert np.array_equal(_bits(bitmap, len(corpus["pk"])), corpus["verdict"].astype(bool))
+        assert np.array_equal(status, corpus["status"])
+        keys, kidx = _dedupe(corpus["pk"])
+        bitmap, status = engine.verify_batch_keyed(keys, kidx, corpus["sig"], corpus["arena"], corpus["off"],
+                                                   corpus["len"])
+        assert np.array_equal(_bits(bitmap, len(kidx)), corpus["verdict"].astype(bool))
+        assert np.array_equal(status, corpus["status"])
+        rng = np.random.default_rng(31)
+        n = 3000
+        seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+        arena = rng.integers(0, 256, n * 32 + 16, dtype=np.uint8)
+        off = np.arange(n, dtype=np.uint64) * 32
+        ln = np.full(n, 32, np.uint32)
+        pk, sig = engine.sign_batch(seeds, arena, off, ln)
+        sig[::4, 33] ^= 2
+        bitmap, _ = engine.verify_batch(pk, sig, arena, off, ln)
+        ref, _ = oracle_c.verify_batch(pk, sig, arena, off, ln, nthreads=8)
+        assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
+    finally:
+        lib.cvk_set_quad_max(32768)

@@ -31,6 +31,9 @@ def main():
     if os.environ.get("CV_COMB_WAVES") and hasattr(lib, "cvk_set_comb_waves"):
         lib.cvk_set_comb_waves.argtypes = [ctypes.c_int]
         lib.cvk_set_comb_waves(int(os.environ["CV_COMB_WAVES"]))
+    if os.environ.get("CV_QUAD_MAX"):
+        lib.cvk_set_quad_max.argtypes = [ctypes.c_uint32]
+        lib.cvk_set_quad_max(int(os.environ["CV_QUAD_MAX"]))
     if args.keyed:
         return keyed(eng, args)
     stream = torch.cuda.Stream(0)
