@@ -367,21 +367,43 @@ static int verify_shard_keyed(uint32_t cap, Device &d, size_t b, size_t e, size_
 }
 
 // Host-side key dedupe for the plain entry point: keys[] = distinct key bytes, key_index[i] = its
-// index.  Returns false when the batch does not repeat keys enough for the keyed path to pay.
+// index.  Returns false when the batch does not repeat keys enough for the keyed path to pay (it
+// gives up as soon as more than n/2 distinct keys have been seen).  Flat open addressing on the key
+// bytes (they are uniformly distributed curve-point encodings), no per-key allocation.
 static bool dedupe_keys(size_t n, const uint8_t *pk, std::vector<uint8_t> &keys, std::vector<uint32_t> &key_index) {
     if (n < 64 || n > kAutoKeyedMax) return false;
-    std::unordered_map<std::array<uint8_t, 32>, uint32_t, KeyHash> idx;
-    idx.reserve(n);
+    size_t cap = 64;
+    while (cap < 2 * n) cap <<= 1;
+    std::vector<uint32_t> first(cap, UINT32_MAX);   // bucket -> first signature with that key
+    std::vector<uint32_t> uid(cap, 0);              // bucket -> distinct-key index
     key_index.resize(n);
-    std::array<uint8_t, 32> key;
+    uint32_t nuniq = 0;
+    std::vector<uint32_t> uniq_sig;
+    uniq_sig.reserve(n / 2 + 1);
     for (size_t i = 0; i < n; i++) {
-        std::memcpy(key.data(), pk + 32 * i, 32);
-        auto r = idx.emplace(key, (uint32_t)idx.size());
-        key_index[i] = r.first->second;
-        if (r.second && 2 * idx.size() > n) return false;   // fewer than two signatures per key
+        const uint8_t *k = pk + 32 * i;
+        uint64_t h;
+        std::memcpy(&h, k + 8, sizeof h);
+        size_t bkt = (size_t)(h * 0x9E3779B97F4A7C15ull >> 20) & (cap - 1);
+        for (;;) {
+            const uint32_t f = first[bkt];
+            if (f == UINT32_MAX) {
+                first[bkt] = (uint32_t)i;
+                uid[bkt] = nuniq;
+                key_index[i] = nuniq++;
+                uniq_sig.push_back((uint32_t)i);
+                if (2 * (size_t)nuniq > n) return false;   // fewer than two signatures per key
+                break;
+            }
+            if (std::memcmp(pk + 32 * (size_t)f, k, 32) == 0) {
+                key_index[i] = uid[bkt];
+                break;
+            }
+            bkt = (bkt + 1) & (cap - 1);
+        }
     }
-    keys.resize(32 * idx.size());
-    for (auto &kv : idx) std::memcpy(keys.data() + 32 * (size_t)kv.second, kv.first.data(), 32);
+    keys.resize(32 * (size_t)nuniq);
+    for (uint32_t u = 0; u < nuniq; u++) std::memcpy(keys.data() + 32 * (size_t)u, pk + 32 * (size_t)uniq_sig[u], 32);
     return true;
 }
 

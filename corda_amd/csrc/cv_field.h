@@ -402,16 +402,25 @@ CV_HD void fe_sq_ilp(fe &h, const fe &f, bool dbl) {
     }
     fe_reduce64(h, h_);
 }
+// Mode dispatch for the long single chains (key decoding, inversion): LAT = true selects the latency
+// forms above (small batches, a lone wave per SIMD), false the sequential-carry forms (throughput).
+template <bool LAT> CV_HD void fe_mul_m(fe &h, const fe &f, const fe &g) {
+    if constexpr (LAT) fe_mul_ilp(h, f, g); else fe_mul(h, f, g);
+}
+template <bool LAT> CV_HD void fe_sq_m(fe &h, const fe &f) {
+    if constexpr (LAT) fe_sq_ilp(h, f, false); else fe_sq(h, f);
+}
+
 // h = f^(2^n) (n >= 1).  A real loop keeps the code small; the trip count is hidden from the
 // optimiser so it cannot unroll the short chains into long straight-line blocks that the machine
 // scheduler then interleaves into VGPR spills.
-__host__ __device__ __forceinline__ void fe_sqn(fe &h, const fe &f, int n) {
+template <bool LAT = false> __host__ __device__ __forceinline__ void fe_sqn(fe &h, const fe &f, int n) {
 #ifdef __HIP_DEVICE_COMPILE__
     asm volatile("" : "+s"(n));
 #endif
-    fe_sq(h, f);
+    fe_sq_m<LAT>(h, f);
 #pragma nounroll
-    for (int i = 1; i < n; i++) fe_sq(h, h);
+    for (int i = 1; i < n; i++) fe_sq_m<LAT>(h, h);
 }
 
 // Parse 32 little-endian bytes given as 8 uint32 words.  Bit 255 is ignored and the value is NOT
@@ -478,55 +487,55 @@ CV_HD int fe_is_negative(const fe &f) {
 }
 
 // z^(2^252 - 3)
-__host__ __device__ __forceinline__ void fe_pow22523(fe &out, const fe &z) {
+template <bool LAT = false> __host__ __device__ __forceinline__ void fe_pow22523(fe &out, const fe &z) {
     fe t0, t1, t2;
-    fe_sq(t0, z);            // z^2
-    fe_sqn(t1, t0, 2);       // z^8
-    fe_mul(t1, z, t1);       // z^9
-    fe_mul(t0, t0, t1);      // z^11
-    fe_sq(t0, t0);           // z^22
-    fe_mul(t0, t1, t0);      // z^31 = z^(2^5-1)
-    fe_sqn(t1, t0, 5);
-    fe_mul(t0, t1, t0);      // z^(2^10-1)
-    fe_sqn(t1, t0, 10);
-    fe_mul(t1, t1, t0);      // z^(2^20-1)
-    fe_sqn(t2, t1, 20);
-    fe_mul(t1, t2, t1);      // z^(2^40-1)
-    fe_sqn(t1, t1, 10);
-    fe_mul(t0, t1, t0);      // z^(2^50-1)
-    fe_sqn(t1, t0, 50);
-    fe_mul(t1, t1, t0);      // z^(2^100-1)
-    fe_sqn(t2, t1, 100);
-    fe_mul(t1, t2, t1);      // z^(2^200-1)
-    fe_sqn(t1, t1, 50);
-    fe_mul(t0, t1, t0);      // z^(2^250-1)
-    fe_sqn(t0, t0, 2);       // z^(2^252-4)
-    fe_mul(out, t0, z);      // z^(2^252-3)
+    fe_sq_m<LAT>(t0, z);            // z^2
+    fe_sqn<LAT>(t1, t0, 2);       // z^8
+    fe_mul_m<LAT>(t1, z, t1);       // z^9
+    fe_mul_m<LAT>(t0, t0, t1);      // z^11
+    fe_sq_m<LAT>(t0, t0);           // z^22
+    fe_mul_m<LAT>(t0, t1, t0);      // z^31 = z^(2^5-1)
+    fe_sqn<LAT>(t1, t0, 5);
+    fe_mul_m<LAT>(t0, t1, t0);      // z^(2^10-1)
+    fe_sqn<LAT>(t1, t0, 10);
+    fe_mul_m<LAT>(t1, t1, t0);      // z^(2^20-1)
+    fe_sqn<LAT>(t2, t1, 20);
+    fe_mul_m<LAT>(t1, t2, t1);      // z^(2^40-1)
+    fe_sqn<LAT>(t1, t1, 10);
+    fe_mul_m<LAT>(t0, t1, t0);      // z^(2^50-1)
+    fe_sqn<LAT>(t1, t0, 50);
+    fe_mul_m<LAT>(t1, t1, t0);      // z^(2^100-1)
+    fe_sqn<LAT>(t2, t1, 100);
+    fe_mul_m<LAT>(t1, t2, t1);      // z^(2^200-1)
+    fe_sqn<LAT>(t1, t1, 50);
+    fe_mul_m<LAT>(t0, t1, t0);      // z^(2^250-1)
+    fe_sqn<LAT>(t0, t0, 2);       // z^(2^252-4)
+    fe_mul_m<LAT>(out, t0, z);      // z^(2^252-3)
 }
 
 // z^(p-2) = z^(2^255 - 21)
-__host__ __device__ __forceinline__ void fe_invert(fe &out, const fe &z) {
+template <bool LAT = false> __host__ __device__ __forceinline__ void fe_invert(fe &out, const fe &z) {
     fe t0, t1, t2, t3;
-    fe_sq(t0, z);            // z^2
-    fe_sqn(t1, t0, 2);       // z^8
-    fe_mul(t1, z, t1);       // z^9
-    fe_mul(t0, t0, t1);      // z^11
-    fe_sq(t2, t0);           // z^22
-    fe_mul(t1, t1, t2);      // z^31
-    fe_sqn(t2, t1, 5);
-    fe_mul(t1, t2, t1);      // 2^10-1
-    fe_sqn(t2, t1, 10);
-    fe_mul(t2, t2, t1);      // 2^20-1
-    fe_sqn(t3, t2, 20);
-    fe_mul(t2, t3, t2);      // 2^40-1
-    fe_sqn(t2, t2, 10);
-    fe_mul(t1, t2, t1);      // 2^50-1
-    fe_sqn(t2, t1, 50);
-    fe_mul(t2, t2, t1);      // 2^100-1
-    fe_sqn(t3, t2, 100);
-    fe_mul(t2, t3, t2);      // 2^200-1
-    fe_sqn(t2, t2, 50);
-    fe_mul(t1, t2, t1);      // 2^250-1
-    fe_sqn(t1, t1, 5);       // 2^255-32
-    fe_mul(out, t1, t0);     // 2^255-21
+    fe_sq_m<LAT>(t0, z);            // z^2
+    fe_sqn<LAT>(t1, t0, 2);       // z^8
+    fe_mul_m<LAT>(t1, z, t1);       // z^9
+    fe_mul_m<LAT>(t0, t0, t1);      // z^11
+    fe_sq_m<LAT>(t2, t0);           // z^22
+    fe_mul_m<LAT>(t1, t1, t2);      // z^31
+    fe_sqn<LAT>(t2, t1, 5);
+    fe_mul_m<LAT>(t1, t2, t1);      // 2^10-1
+    fe_sqn<LAT>(t2, t1, 10);
+    fe_mul_m<LAT>(t2, t2, t1);      // 2^20-1
+    fe_sqn<LAT>(t3, t2, 20);
+    fe_mul_m<LAT>(t2, t3, t2);      // 2^40-1
+    fe_sqn<LAT>(t2, t2, 10);
+    fe_mul_m<LAT>(t1, t2, t1);      // 2^50-1
+    fe_sqn<LAT>(t2, t1, 50);
+    fe_mul_m<LAT>(t2, t2, t1);      // 2^100-1
+    fe_sqn<LAT>(t3, t2, 100);
+    fe_mul_m<LAT>(t2, t3, t2);      // 2^200-1
+    fe_sqn<LAT>(t2, t2, 50);
+    fe_mul_m<LAT>(t1, t2, t1);      // 2^250-1
+    fe_sqn<LAT>(t1, t1, 5);       // 2^255-32
+    fe_mul_m<LAT>(out, t1, t0);     // 2^255-21
 }

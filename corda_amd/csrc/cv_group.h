@@ -160,25 +160,25 @@ CV_HD void ge_abyte_from_key(uint32_t abyte[8], const uint32_t w[8]) {
 // Returns false where the reference throws IllegalArgumentException("not a valid GroupElement").
 // y keeps its non-reduced value; x is negated when isNegative(x) != bit 255 (x = 0 with the sign
 // bit set is therefore accepted as x = 0).  All output coordinates are tight.
-__host__ __device__ __forceinline__ bool ge_decode_0_1_0(ge_p3 &A, const uint32_t w[8]) {
+template <bool LAT = false> __host__ __device__ __forceinline__ bool ge_decode_0_1_0(ge_p3 &A, const uint32_t w[8]) {
     fe y, yy, u, v, v3, x, vxx, chk, one, d;
     fe_from_words(y, w);
     fe_one(one);
     fe_const_d(d);
-    fe_sq(yy, y);
+    fe_sq_m<LAT>(yy, y);
     fe_sub<2>(u, yy, one);       // u = y^2 - 1         (<= 3.01)
-    fe_mul(v, yy, d);
+    fe_mul_m<LAT>(v, yy, d);
     fe_add(v, v, one);           // v = d y^2 + 1       (<= 1.02)
-    fe_sq(v3, v);
-    fe_mul(v3, v3, v);           // v^3
-    fe_sq(x, v3);
-    fe_mul(x, x, v);
-    fe_mul(x, x, u);             // u v^7
-    fe_pow22523(x, x);           // (u v^7)^((p-5)/8)
-    fe_mul(x, x, v3);
-    fe_mul(x, x, u);             // u v^3 (u v^7)^((p-5)/8)
-    fe_sq(vxx, x);
-    fe_mul(vxx, vxx, v);
+    fe_sq_m<LAT>(v3, v);
+    fe_mul_m<LAT>(v3, v3, v);           // v^3
+    fe_sq_m<LAT>(x, v3);
+    fe_mul_m<LAT>(x, x, v);
+    fe_mul_m<LAT>(x, x, u);             // u v^7
+    fe_pow22523<LAT>(x, x);           // (u v^7)^((p-5)/8)
+    fe_mul_m<LAT>(x, x, v3);
+    fe_mul_m<LAT>(x, x, u);             // u v^3 (u v^7)^((p-5)/8)
+    fe_sq_m<LAT>(vxx, x);
+    fe_mul_m<LAT>(vxx, vxx, v);
     fe_sub<4>(chk, vxx, u);
     bool ok = true;
     if (!fe_is_zero(chk)) {
@@ -186,7 +186,7 @@ __host__ __device__ __forceinline__ bool ge_decode_0_1_0(ge_p3 &A, const uint32_
         if (!fe_is_zero(chk)) ok = false;
         fe sqm1, xi;
         fe_const_sqrtm1(sqm1);
-        fe_mul(xi, x, sqm1);
+        fe_mul_m<LAT>(xi, x, sqm1);
         x = xi;
     }
     const int sign = (int)(w[7] >> 31);
@@ -197,6 +197,6 @@ __host__ __device__ __forceinline__ bool ge_decode_0_1_0(ge_p3 &A, const uint32_
     A.X = x;
     A.Y = y;
     fe_one(A.Z);
-    fe_mul(A.T, x, y);
+    fe_mul_m<LAT>(A.T, x, y);
     return ok;
 }

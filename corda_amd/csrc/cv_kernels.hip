@@ -46,6 +46,7 @@ __device__ __forceinline__ void store_words(uint32_t *dst, const uint32_t *src, 
     for (int q = 0; q < nwords4; q++) d[q] = make_uint4(src[4 * q], src[4 * q + 1], src[4 * q + 2], src[4 * q + 3]);
 }
 
+template <bool LAT>
 __global__ __launch_bounds__(CV_BLOCK, 2) void cv_prep_kernel(
     uint32_t n, const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint8_t *__restrict__ arena,
     const uint64_t *__restrict__ off, const uint32_t *__restrict__ len, uint32_t *__restrict__ ws_hs,
@@ -57,7 +58,7 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_prep_kernel(
     load_words8(rw, sig + (size_t)i * 64);
     load_words8(sw, sig + (size_t)i * 64 + 32);
     uint32_t hs[CV_HS_WORDS];
-    const bool ok = cv_verify_prep(aw, rw, sw, arena + off[i], len[i], hs, ws_tab + (size_t)i * CV_TAB_WORDS);
+    const bool ok = cv_verify_prep<LAT>(aw, rw, sw, arena + off[i], len[i], hs, ws_tab + (size_t)i * CV_TAB_WORDS);
     store_words(ws_hs + (size_t)i * CV_HS_WORDS, hs, CV_HS_WORDS / 4);
     ws_ok[i] = ok ? 1 : 0;
     if (status) status[i] = ok ? 0 : 1;
@@ -90,6 +91,7 @@ static int g_straus_waves = 3;
 extern "C" void cvk_set_straus_waves(int w) { g_straus_waves = (w == 2 || w == 3 || w == 4) ? w : 3; }
 
 // lane j: signatures [8j, 8j+8) -> bitmap byte j (bytes past n are written as zero)
+template <bool LAT>
 __global__ __launch_bounds__(CV_BLOCK) void cv_finish_kernel(uint32_t n, uint32_t nbytes,
                                                              const uint8_t *__restrict__ sig,
                                                              const uint32_t *__restrict__ ws_R,
@@ -101,7 +103,7 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_finish_kernel(uint32_t n, uint32_
     uint32_t bits = 0;
     if (b < n) {
         const int cnt = (int)(n - b < CV_FIN_CHUNK ? n - b : CV_FIN_CHUNK);
-        bits = cv_verify_finish(ws_R + (size_t)b * CV_R_WORDS, reinterpret_cast<const uint32_t *>(sig + (size_t)b * 64),
+        bits = cv_verify_finish<LAT>(ws_R + (size_t)b * CV_R_WORDS, reinterpret_cast<const uint32_t *>(sig + (size_t)b * 64),
                                 ws_ok + b, cnt);
     }
     bitmap_bytes[j] = (uint8_t)bits;
@@ -270,9 +272,15 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
         const uint32_t blocks = (m + CV_BLOCK - 1) / CV_BLOCK;
         // ev (optional, single-chunk batches): phase boundaries for live per-kernel timing
         if (ev && c0 == 0) (void)hipEventRecord(ev[0], stream);
-        hipLaunchKernelGGL(cv_prep_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, pk + (size_t)c0 * 32,
-                           sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_hs, ws_tab, ws_ok,
-                           status ? status + c0 : nullptr);
+        const bool lat = n <= g_quad_max;   // small batch: latency forms of the single chains
+        if (lat)
+            hipLaunchKernelGGL(cv_prep_kernel<true>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, pk + (size_t)c0 * 32,
+                               sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_hs, ws_tab, ws_ok,
+                               status ? status + c0 : nullptr);
+        else
+            hipLaunchKernelGGL(cv_prep_kernel<false>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, pk + (size_t)c0 * 32,
+                               sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_hs, ws_tab, ws_ok,
+                               status ? status + c0 : nullptr);
         if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);
         if (n <= g_quad_max)
             hipLaunchKernelGGL(cv_straus_quad_kernel, dim3((4 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
@@ -285,9 +293,14 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             hipLaunchKernelGGL(cv_straus_kernel<3>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, ws_tab, ws_R);
         if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
         const uint32_t nbytes = ((m + 63) / 64) * 8;
-        hipLaunchKernelGGL(cv_finish_kernel, dim3((nbytes + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, stream, m,
-                           nbytes, sig + (size_t)c0 * 64, ws_R, ws_ok,
-                           reinterpret_cast<uint8_t *>(bitmap) + (size_t)c0 / 8);
+        if (n <= g_quad_max)
+            hipLaunchKernelGGL(cv_finish_kernel<true>, dim3((nbytes + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
+                               stream, m, nbytes, sig + (size_t)c0 * 64, ws_R, ws_ok,
+                               reinterpret_cast<uint8_t *>(bitmap) + (size_t)c0 / 8);
+        else
+            hipLaunchKernelGGL(cv_finish_kernel<false>, dim3((nbytes + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
+                               stream, m, nbytes, sig + (size_t)c0 * 64, ws_R, ws_ok,
+                               reinterpret_cast<uint8_t *>(bitmap) + (size_t)c0 / 8);
         if (ev && c0 == 0) (void)hipEventRecord(ev[3], stream);
     }
     return hipGetLastError();
@@ -330,9 +343,14 @@ hipError_t cvk_verify_keyed(uint32_t n, const uint8_t *keys, const uint32_t *key
                                slot_of_key, ktab_pool, ws_R);
         if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
         const uint32_t nbytes = ((m + 63) / 64) * 8;
-        hipLaunchKernelGGL(cv_finish_kernel, dim3((nbytes + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, stream, m,
-                           nbytes, sig + (size_t)c0 * 64, ws_R, ws_ok,
-                           reinterpret_cast<uint8_t *>(bitmap) + (size_t)c0 / 8);
+        if (n <= g_quad_max)
+            hipLaunchKernelGGL(cv_finish_kernel<true>, dim3((nbytes + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
+                               stream, m, nbytes, sig + (size_t)c0 * 64, ws_R, ws_ok,
+                               reinterpret_cast<uint8_t *>(bitmap) + (size_t)c0 / 8);
+        else
+            hipLaunchKernelGGL(cv_finish_kernel<false>, dim3((nbytes + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
+                               stream, m, nbytes, sig + (size_t)c0 * 64, ws_R, ws_ok,
+                               reinterpret_cast<uint8_t *>(bitmap) + (size_t)c0 / 8);
         if (ev && c0 == 0) (void)hipEventRecord(ev[3], stream);
     }
     return hipGetLastError();

@@ -132,7 +132,7 @@ __host__ __device__ __forceinline__ void ge_cached_multiples8(uint32_t *tab, con
 }
 
 // Phase 1.  Returns key_ok.  hs = h || s (16 words), tab = CV_TAB_WORDS words (16-B aligned).
-__host__ __device__ __forceinline__ bool cv_verify_prep(const uint32_t aw[8], const uint32_t rw[8], const uint32_t sw[8],
+template <bool LAT = false> __host__ __device__ __forceinline__ bool cv_verify_prep(const uint32_t aw[8], const uint32_t rw[8], const uint32_t sw[8],
                                                const uint8_t *msg, uint32_t mlen, uint32_t *hs, uint32_t *tab) {
     // hash first (its state is dead before the point decode starts: small live set)
     {
@@ -152,7 +152,7 @@ __host__ __device__ __forceinline__ bool cv_verify_prep(const uint32_t aw[8], co
         for (int q = 0; q < 8; q++) hs[8 + q] = s[q];
     }
     ge_p3 A, nA;
-    const bool key_ok = ge_decode_0_1_0(A, aw);
+    const bool key_ok = ge_decode_0_1_0<LAT>(A, aw);
     if (!key_ok) ge_p3_identity(A);
     ge_p3_neg(nA, A);
     ge_cached_multiples8(tab, nA);
@@ -212,7 +212,7 @@ __host__ __device__ __forceinline__ void cv_verify_straus(const uint32_t *btab, 
 // Phase 3 for `cnt` (<= CV_FIN_CHUNK) consecutive signatures: Rs = their (X,Y,Z) records
 // (CV_R_WORDS apart), rws = their R words (16 words apart: the sig records), ok = key_ok flags.
 // Returns the verdict bits (bit k = signature k).
-__host__ __device__ __forceinline__ uint32_t cv_verify_finish(const uint32_t *Rs, const uint32_t *sigw,
+template <bool LAT = false> __host__ __device__ __forceinline__ uint32_t cv_verify_finish(const uint32_t *Rs, const uint32_t *sigw,
                                                                const uint8_t *ok, int cnt) {
     // slots past cnt use Z = 1 so every loop below has static indices (no private-memory arrays)
     fe pre[CV_FIN_CHUNK];
@@ -224,17 +224,17 @@ __host__ __device__ __forceinline__ uint32_t cv_verify_finish(const uint32_t *Rs
         fe_one(one);
         if (k < cnt) fe_load(z, Rs + k * CV_R_WORDS + 20);
         else z = one;
-        fe_mul(acc, z, acc);
+        fe_mul_m<LAT>(acc, z, acc);
         pre[k] = acc;
     }
     fe inv;
-    fe_invert(inv, acc);
+    fe_invert<LAT>(inv, acc);
     uint32_t bits = 0;
 #pragma unroll
     for (int k = CV_FIN_CHUNK - 1; k >= 0; k--) {
         fe zi, z, x, y, one;
         fe_one(one);
-        if (k) fe_mul(zi, inv, pre[k - 1]);
+        if (k) fe_mul_m<LAT>(zi, inv, pre[k - 1]);
         else zi = inv;
         if (k < cnt) {
             fe_load(z, Rs + k * CV_R_WORDS + 20);
@@ -245,9 +245,9 @@ __host__ __device__ __forceinline__ uint32_t cv_verify_finish(const uint32_t *Rs
             x = one;
             y = one;
         }
-        if (k) fe_mul(inv, z, inv);
-        fe_mul(x, x, zi);
-        fe_mul(y, y, zi);
+        if (k) fe_mul_m<LAT>(inv, z, inv);
+        fe_mul_m<LAT>(x, x, zi);
+        fe_mul_m<LAT>(y, y, zi);
         uint32_t yw[8], xw[8];
         fe_to_words(yw, y);
         fe_to_words(xw, x);
@@ -327,7 +327,7 @@ __host__ __device__ __forceinline__ void ge_p3_multiples8(uint32_t *ext, const g
 // mixed addition (3 products instead of 4).  Returns key_ok; invalid keys get identity tables.
 __host__ __device__ __forceinline__ bool cv_key_prep(const uint32_t aw[8], uint32_t *ext, uint32_t *ktab) {
     ge_p3 A, P;
-    const bool key_ok = ge_decode_0_1_0(A, aw);
+    const bool key_ok = ge_decode_0_1_0<true>(A, aw);
     if (!key_ok) ge_p3_identity(A);
     ge_p3_neg(P, A);
 #pragma unroll 1
@@ -354,11 +354,11 @@ __host__ __device__ __forceinline__ bool cv_key_prep(const uint32_t aw[8], uint3
 #pragma unroll 1
     for (int k = 1; k < NE; k++) {
         fe_load(z, ext + k * CV_KENT_WORDS + 20);
-        fe_mul(acc, acc, z);
+        fe_mul_m<true>(acc, acc, z);
         fe_store(ktab + k * CV_KENT_WORDS + 20, acc);
     }
     fe inv, d2;
-    fe_invert(inv, acc);
+    fe_invert<true>(inv, acc);
     fe_const_d2(d2);
 #pragma unroll 1
     for (int k = NE - 1; k >= 0; k--) {
@@ -366,16 +366,16 @@ __host__ __device__ __forceinline__ bool cv_key_prep(const uint32_t aw[8], uint3
         if (k > 0) {
             fe pre;
             fe_load(pre, ktab + (k - 1) * CV_KENT_WORDS + 20);
-            fe_mul(zi, inv, pre);
+            fe_mul_m<true>(zi, inv, pre);
             fe_load(z, ext + k * CV_KENT_WORDS + 20);
-            fe_mul(inv, inv, z);
+            fe_mul_m<true>(inv, inv, z);
         } else {
             zi = inv;
         }
         fe_load(x, ext + k * CV_KENT_WORDS);
         fe_load(y, ext + k * CV_KENT_WORDS + 10);
-        fe_mul(x, x, zi);
-        fe_mul(y, y, zi);
+        fe_mul_m<true>(x, x, zi);
+        fe_mul_m<true>(y, y, zi);
         uint32_t *e = ktab + k * CV_KENT_WORDS;
         fe_add(t, y, x);
         fe_carry(t, t);
@@ -383,8 +383,8 @@ __host__ __device__ __forceinline__ bool cv_key_prep(const uint32_t aw[8], uint3
         fe_sub<2>(t, y, x);
         fe_carry(t, t);
         fe_store(e + 10, t);                 // y - x
-        fe_mul(t, x, y);
-        fe_mul(t, t, d2);
+        fe_mul_m<true>(t, x, y);
+        fe_mul_m<true>(t, t, d2);
         fe_store(e + 20, t);                 // 2 d x y
         e[30] = e[31] = 0;
     }

@@ -90,13 +90,13 @@ def load():
         lib.cv_merkle_tx_ids_device.restype = ctypes.c_int
         lib.cv_synchronize.argtypes = [_vp, ctypes.c_int]
         lib.cv_synchronize.restype = ctypes.c_int
-        lib.cv_ed25519_verify_batch_keyed.argtypes = [_vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
-        lib.cv_ed25519_verify_batch_keyed.restype = ctypes.c_int
-        lib.cv_key_cache_reserve.argtypes = [_vp, _sz]
-        lib.cv_key_cache_reserve.restype = ctypes.c_int
-        lib.cv_key_cache_stats.argtypes = [_vp, ctypes.c_int, _vp]
-        lib.cv_key_cache_stats.restype = ctypes.c_int
-        if hasattr(lib, "cv_ed25519_verify_device_keyed"):      # absent only in pre-r01 A/B builds
+        if hasattr(lib, "cv_ed25519_verify_device_keyed"):      # absent only in older A/B builds
+            lib.cv_ed25519_verify_batch_keyed.argtypes = [_vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+            lib.cv_ed25519_verify_batch_keyed.restype = ctypes.c_int
+            lib.cv_key_cache_reserve.argtypes = [_vp, _sz]
+            lib.cv_key_cache_reserve.restype = ctypes.c_int
+            lib.cv_key_cache_stats.argtypes = [_vp, ctypes.c_int, _vp]
+            lib.cv_key_cache_stats.restype = ctypes.c_int
             lib.cv_ed25519_verify_device_keyed.argtypes = [_vp, ctypes.c_int, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp,
                                                            _vp, _vp, _vp, ctypes.POINTER(ctypes.c_float)]
             lib.cv_ed25519_verify_device_keyed.restype = ctypes.c_int
