@@ -41,6 +41,12 @@ W_MAC_PER_VERIFY = 2.28e5       # algorithmic 32x32->64 MACs p
 # Straus phase alone (cv_straus_kernel, the dominant kernel): 63 windows x (16 S + 13 M) + 64 -A adds x 7 M
 # + 32 B madds x 7 M = 1008 S + 1491 M, at S = 55 and M = 100 limb products (DESIGN.md "Roofline")
 W_MAC_STRAUS = 1008 * 55 + 1491 * 100
+# Half-size schedule (DESIGN.md "Half-size scalars"), cv_hs_straus_kernel at the typical 33 windows:
+# 32 x 4 doublings (16 S + 13 M) + 33 x (R add + A add: 15 M) + 16 x 2 B madds (14 M) = 512 S + 1135 M
+HS_NW = 33
+W_MAC_HS_STRAUS = (HS_NW - 1) * (16 * 55 + 13 * 100) + HS_NW * 15 * 100 + 16 * 14 * 100
+# whole half-size group: + 2 point decodes (254 S + 19 M each) + 2 odd-multiple tables (4 S + 59 M each)
+W_MAC_HS_GROUP = W_MAC_HS_STRAUS + 2 * (258 * 55 + 78 * 100)
 MSG_BYTES = {"c2": 300, "c5": 32, "c3": 32}
 CONFIG_NAME = {
     "c2": "C2: 1M single-signer Ed25519 txs, 300-byte msg, distinct keys, SoA batch",
@@ -53,10 +59,11 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(n: int):
-    """HBM bytes per cv_straus_kernel launch from the committed PMC pass (profiles/pmc_straus.json,
-    written by scripts/pmc.sh + tools/pmc_summary.py on the same build and workload), scaled to n."""
-    p = os.path.join(REPO, "profiles", "pmc_straus.json")
+def pmc_traffic(n: int, hs: bool):
+    """HBM bytes per launch of the dominant kernel from the committed PMC pass (profiles/pmc_hs_straus.json
+    or pmc_straus.json, written by scripts/pmc.sh + tools/pmc_summary.py on the same build and
+    workload), scaled to n."""
+    p = os.path.join(REPO, "profiles", "pmc_hs_straus.json" if hs else "pmc_straus.json")
     if not os.path.exists(p):
         return None
     with open(p) as f:
@@ -277,7 +284,8 @@ def main():
         full[-1] = (1 << (n % 64)) - 1
     assert torch.equal(bitmap, full), "verify rejected an honest signature"
     ph = np.mean(np.array(phases), axis=0)
-    kern_ms, straus_ms = float(ph.sum()), float(ph[1])
+    hs = native.verify_mode() == 1
+    kern_ms, straus_ms = float(ph.sum()), float(ph[2] if hs else ph[1])
     if world > 1:
         tt = torch.tensor([elapsed, kern_ms, straus_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -288,8 +296,21 @@ def main():
 
     if rank == 0:
         mad_rate, femul_rate = eng.calibrate(local)
-        achieved = n * W_MAC_STRAUS / (straus_ms * 1e-3)
-        group = n * W_MAC_PER_VERIFY / (kern_ms * 1e-3)
+        w_straus = W_MAC_HS_STRAUS if hs else W_MAC_STRAUS
+        w_group = W_MAC_HS_GROUP if hs else W_MAC_PER_VERIFY
+        achieved = n * w_straus / (straus_ms * 1e-3)
+        group = n * w_group / (kern_ms * 1e-3)
+        if hs:
+            phase_ms = {"prep": float(ph[0]), "hsprep": float(ph[1]), "hs_straus": float(ph[2])}
+            kname, gname = "cv_hs_straus_kernel", "prep + hsprep + hs_straus"
+            wdesc = (f"{w_straus} 32x32->64 MAC per verify in the half-size Straus phase at {HS_NW} windows "
+                     f"(512 S + 1135 M)")
+            gdesc = f"{w_group} MAC per verify (half-size schedule: Straus + 2 decodes + 2 tables)"
+        else:
+            phase_ms = {"prep": float(ph[0]), "straus": float(ph[1]), "finish": float(ph[2])}
+            kname, gname = "cv_straus_kernel", "prep + straus + finish"
+            wdesc = f"{w_straus} 32x32->64 MAC per verify in the Straus phase (1008 S + 1491 M)"
+            gdesc = f"{W_MAC_PER_VERIFY:.3g} MAC per verify (SURVEY.md 8d)"
         result = {
             "metric": "Ed25519 verifies/sec (node)",
             "value": value,
@@ -307,14 +328,11 @@ def main():
                        "key_pool": args.key_pool or "distinct", "parallelism": f"shard-by-signature x{world}",
                        "collective": "RCCL all_gather of verdict bitmaps" if world > 1 else "none"},
             "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": mad_rate / 1e12, "unit": "Tmac/s",
-                         "frac": achieved / mad_rate, "traffic": pmc_traffic(n),
-                         "kernel": "cv_straus_kernel", "kernel_ms": straus_ms,
-                         "work_per_unit": f"{W_MAC_STRAUS} 32x32->64 MAC per verify in the Straus phase "
-                                          f"(1008 S + 1491 M)",
-                         "phase_ms": {"prep": float(ph[0]), "straus": float(ph[1]), "finish": float(ph[2])},
-                         "group": {"kernels": "prep + straus + finish", "kernel_ms": kern_ms,
-                                   "achieved": group / 1e12, "frac": group / mad_rate,
-                                   "work_per_unit": f"{W_MAC_PER_VERIFY:.3g} MAC per verify (SURVEY.md 8d)"},
+                         "frac": achieved / mad_rate, "traffic": pmc_traffic(n, hs),
+                         "kernel": kname, "kernel_ms": straus_ms, "work_per_unit": wdesc,
+                         "phase_ms": phase_ms,
+                         "group": {"kernels": gname, "kernel_ms": kern_ms,
+                                   "achieved": group / 1e12, "frac": group / mad_rate, "work_per_unit": gdesc},
                          "fe_mul_per_s": femul_rate},
         }
         if world == 1 and not args.no_cpu:

@@ -16,7 +16,8 @@
 extern "C" {
 hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off,
                       const uint32_t *len, uint64_t *bitmap, uint8_t *status, uint32_t *ws_hs, uint32_t *ws_tab,
-                      uint32_t *ws_R, uint8_t *ws_ok, uint32_t ws_cap, hipStream_t stream, hipEvent_t *ev);
+                      uint32_t *ws_R, uint8_t *ws_ok, uint32_t *ws_dig, uint32_t ws_cap, hipStream_t stream,
+                      hipEvent_t *ev);
 hipError_t cvk_sign(uint32_t n, const uint8_t *seed, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
                     uint8_t *pk, uint8_t *sig, hipStream_t stream);
 hipError_t cvk_merkle(uint32_t ntx, uint32_t nleaves, const uint8_t *arena, const uint64_t *leaf_off,
@@ -80,7 +81,8 @@ struct Device {
     int ordinal = 0;
     hipStream_t stream = nullptr;
     DevBuf pk, sig, arena, off, len, bitmap, status, seed, tx_begin, digest, ids;
-    DevBuf ws_hs, ws_tab, ws_R, ws_ok;   // verify workspace (hs 64 B + tab 1280 B + R 128 B + ok 1 B per signature)
+    DevBuf ws_hs, ws_tab, ws_R, ws_ok, ws_dig;   // verify workspace per signature: hs 64 B, 2 tables 2560 B,
+                                         // R record 128 B, ok 1 B, half-size digits 260 B
     uint32_t ws_cap = 0;
     KeyCache kc;
 };
@@ -100,9 +102,10 @@ hipError_t ensure_verify_ws(Device &d, size_t n) {
     if (want <= d.ws_cap) return hipSuccess;
     hipError_t e;
     if ((e = d.ws_hs.ensure((size_t)want * 64)) != hipSuccess) return e;
-    if ((e = d.ws_tab.ensure((size_t)want * 1280)) != hipSuccess) return e;
+    if ((e = d.ws_tab.ensure((size_t)want * 2560)) != hipSuccess) return e;   // k*(-A) and k*R tables
     if ((e = d.ws_R.ensure((size_t)want * 128)) != hipSuccess) return e;
     if ((e = d.ws_ok.ensure((size_t)want)) != hipSuccess) return e;
+    if ((e = d.ws_dig.ensure((size_t)want * 65 * 4)) != hipSuccess) return e;   // CV_HS_DIGWORDS
     d.ws_cap = want;
     return hipSuccess;
 }
@@ -113,7 +116,7 @@ hipError_t launch_verify(Device &d, uint32_t n, const uint8_t *pk, const uint8_t
     hipError_t e = ensure_verify_ws(d, n);
     if (e != hipSuccess) return e;
     return cvk_verify(n, pk, sig, arena, off, len, bitmap, status, d.ws_hs.as<uint32_t>(), d.ws_tab.as<uint32_t>(),
-                      d.ws_R.as<uint32_t>(), d.ws_ok.as<uint8_t>(), d.ws_cap, s, ev);
+                      d.ws_R.as<uint32_t>(), d.ws_ok.as<uint8_t>(), d.ws_dig.as<uint32_t>(), d.ws_cap, s, ev);
 }
 
 int hip_rc(hipError_t e) {
@@ -183,7 +186,7 @@ void cv_close(cv_ctx *ctx) {
         (void)hipSetDevice(d.ordinal);
         if (d.stream) (void)hipStreamSynchronize(d.stream);
         for (DevBuf *b : {&d.pk, &d.sig, &d.arena, &d.off, &d.len, &d.bitmap, &d.status, &d.seed, &d.tx_begin,
-                          &d.digest, &d.ids, &d.ws_hs, &d.ws_tab, &d.ws_R, &d.ws_ok, &d.kc.ktab, &d.kc.kok,
+                          &d.digest, &d.ids, &d.ws_hs, &d.ws_tab, &d.ws_R, &d.ws_ok, &d.ws_dig, &d.kc.ktab, &d.kc.kok,
                           &d.kc.keys, &d.kc.slots, &d.kc.slot_of_key, &d.kc.key_index, &d.kc.scratch})
             b->release();
         if (d.stream) (void)hipStreamDestroy(d.stream);

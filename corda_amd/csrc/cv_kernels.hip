@@ -109,6 +109,76 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_finish_kernel(uint32_t n, uint32_
     bitmap_bytes[j] = (uint8_t)bits;
 }
 
+// ---------------------------------------------------------------- half-size verify (cv_verify.h)
+// hsprep: decode R canonically (r_ok folded into the key-ok byte), k*R table, lattice-reduced
+// (u, v, w) as packed per-window digit words, window-major: ws_dig[win * cap + i].
+template <bool LAT>
+__global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsprep_kernel(uint32_t n, uint32_t cap, const uint8_t *__restrict__ sig,
+                                                                const uint32_t *__restrict__ ws_hs,
+                                                                uint32_t *__restrict__ ws_dig,
+                                                                uint32_t *__restrict__ ws_tabR,
+                                                                uint8_t *__restrict__ ws_ok) {
+    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    uint32_t rw[8], hs[CV_HS_WORDS];
+    load_words8(rw, sig + (size_t)i * 64);
+    const uint4 *hp = reinterpret_cast<const uint4 *>(ws_hs + (size_t)i * CV_HS_WORDS);
+#pragma unroll
+    for (int q = 0; q < CV_HS_WORDS / 4; q++) {
+        const uint4 x = hp[q];
+        hs[4 * q] = x.x; hs[4 * q + 1] = x.y; hs[4 * q + 2] = x.z; hs[4 * q + 3] = x.w;
+    }
+    const bool r_ok = cv_hs_prep<LAT>(rw, hs, ws_dig + i, cap, ws_tabR + (size_t)i * CV_TAB_WORDS);
+    if (!r_ok) ws_ok[i] = 0;
+}
+
+// hs_straus: E = [v]R + [u]A + [w]B per lane over the wave's largest window count, the identity
+// test, and the verdict word by wave ballot (bit i of word i/64 = signature i).  Lanes past n
+// replay signature n-1 so the whole wave takes part in the window-count reduction.
+template <int WAVES>
+__global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_hs_straus_kernel(uint32_t n, uint32_t cap,
+                                                                       const uint32_t *__restrict__ ws_dig,
+                                                                       const uint32_t *__restrict__ ws_tab,
+                                                                       const uint32_t *__restrict__ ws_tabR,
+                                                                       const uint8_t *__restrict__ ws_ok,
+                                                                       uint64_t *__restrict__ bitmap) {
+    __shared__ __attribute__((aligned(16))) uint32_t btab[2 * CV_BTAB_ENTRIES * CV_BTAB_STRIDE];
+    constexpr int ROW = CV_BTAB_ENTRIES * CV_BTAB_STRIDE;
+    for (int k = threadIdx.x; k < ROW; k += blockDim.x) {
+        btab[k] = CV_BCOMB[k];                 // k * B
+        btab[ROW + k] = CV_BCOMB[2 * ROW + k]; // k * 2^128 * B
+    }
+    __syncthreads();
+    const uint32_t wave0 = blockIdx.x * CV_BLOCK + (threadIdx.x & ~63u);
+    if (wave0 >= n) return;                    // whole waves past the end leave together
+    const uint32_t i0 = wave0 + (threadIdx.x & 63u);
+    const uint32_t i = i0 < n ? i0 : n - 1;
+    int nw = (int)ws_dig[(size_t)64 * cap + i];
+    nw = nw < 32 ? 32 : nw;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const int x = __shfl_xor(nw, o);
+        nw = x > nw ? x : nw;
+    }
+    nw = __builtin_amdgcn_readfirstlane(nw);
+    const bool eq = cv_hs_straus(btab, btab + ROW, ws_dig + i, cap, ws_tab + (size_t)i * CV_TAB_WORDS,
+                                 ws_tabR + (size_t)i * CV_TAB_WORDS, nw);
+    const bool acc = eq && ws_ok[i] && i0 < n;
+    const uint64_t bits = __ballot(acc);
+    if ((threadIdx.x & 63u) == 0) bitmap[wave0 >> 6] = bits;
+}
+template __global__ void cv_hs_straus_kernel<2>(uint32_t, uint32_t, const uint32_t *, const uint32_t *,
+                                                const uint32_t *, const uint8_t *, uint64_t *);
+template __global__ void cv_hs_straus_kernel<3>(uint32_t, uint32_t, const uint32_t *, const uint32_t *,
+                                                const uint32_t *, const uint8_t *, uint64_t *);
+
+// 1 = half-size verify for throughput batches (default), 0 = the full-width prep/straus/finish group
+static int g_verify_mode = 1;
+static int g_hs_waves = 3;
+extern "C" void cvk_set_verify_mode(int m) { g_verify_mode = m ? 1 : 0; }
+extern "C" int cvk_get_verify_mode(void) { return g_verify_mode; }
+extern "C" void cvk_set_hs_waves(int w) { g_hs_waves = (w == 2) ? 2 : 3; }
+
 // ---------------------------------------------------------------- quad (latency) Straus kernels
 // Four lanes per signature (cv_quad.h) for batches too small to fill the chip.  Grid: 4n lanes.
 __global__ __launch_bounds__(CV_BLOCK) void cv_straus_quad_kernel(uint32_t n, const uint32_t *__restrict__ ws_hs,
@@ -261,10 +331,13 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_merkle_tree_kernel(uint32_t ntx, 
 extern "C" {
 
 // Verify n signatures with the workspace ws (capacity ws_cap signatures, a multiple of 512); the
-// batch is processed in chunks of ws_cap.  bitmap gets ceil(n/64) words.
+// batch is processed in chunks of ws_cap.  bitmap gets ceil(n/64) words.  ws_tab holds 2 * ws_cap
+// tables (k*(-A), then k*R for the half-size group); ws_dig CV_HS_DIGWORDS * ws_cap words.  ev phases: prep | straus | finish, or in the
+// half-size group prep | hsprep | hs_straus.
 hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off,
                       const uint32_t *len, uint64_t *bitmap, uint8_t *status, uint32_t *ws_hs, uint32_t *ws_tab,
-                      uint32_t *ws_R, uint8_t *ws_ok, uint32_t ws_cap, hipStream_t stream, hipEvent_t *ev) {
+                      uint32_t *ws_R, uint8_t *ws_ok, uint32_t *ws_dig, uint32_t ws_cap, hipStream_t stream,
+                      hipEvent_t *ev) {
     if (n == 0) return hipSuccess;
     if (ws_cap == 0 || ws_cap % 512) return hipErrorInvalidValue;
     for (uint32_t c0 = 0; c0 < n; c0 += ws_cap) {
@@ -282,6 +355,21 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
                                sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_hs, ws_tab, ws_ok,
                                status ? status + c0 : nullptr);
         if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);
+        if (!lat && g_verify_mode == 1) {
+            // half-size group: phases = prep | hsprep | hs_straus (verdict bits included)
+            uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
+            hipLaunchKernelGGL(cv_hsprep_kernel<false>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap,
+                               sig + (size_t)c0 * 64, ws_hs, ws_dig, ws_tabR, ws_ok);
+            if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
+            if (g_hs_waves == 2)
+                hipLaunchKernelGGL(cv_hs_straus_kernel<2>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, ws_dig,
+                                   ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
+            else
+                hipLaunchKernelGGL(cv_hs_straus_kernel<3>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, ws_dig,
+                                   ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
+            if (ev && c0 == 0) (void)hipEventRecord(ev[3], stream);
+            continue;
+        }
         if (n <= g_quad_max)
             hipLaunchKernelGGL(cv_straus_quad_kernel, dim3((4 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
                                stream, m, ws_hs, ws_tab, ws_R);

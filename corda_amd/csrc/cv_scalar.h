@@ -238,3 +238,187 @@ CV_HD int digit256(const uint32_t n[8], int k) {
     const int prev = k ? bit_of_sel(n, 8 * k - 1) : 0;
     return (int)byte - 256 * top + prev;
 }
+
+// ---------------------------------------------------------------- half-size scalars
+// For the verify equation R = [s]B - [h]A (eddsa-0.1.0, cofactorless) find u, v with
+//     u = v * h  (mod 8L),   v odd,   |u|, |v| ~ 2^128
+// by the extended Euclidean algorithm on (8L, h) stopped half-way (the lattice
+// {(u, v) : u = v h mod 8L} of determinant 8L, Lagrange/Gauss reduction in dimension 2).  Then
+//     [v] (R - [s]B + [h]A) = [v]R + [u]A + [w]B,    w = (-v s) mod L
+// because A's order divides 8L and B's is L; and since gcd(v, 8L) = 1 (v odd, 0 < |v| < L),
+// [v] is a bijection on E(F_p) (order 8L), so  R == [s]B - [h]A  <=>  [v]R + [u]A + [w]B == O.
+// The double-scalar multiplication then needs ~128 doublings instead of ~252.  Modulus 8L (not
+// L) keeps the identity exact for keys with a torsion component; v odd keeps it exact for R.
+// When no short odd-v vector turns up (rare), (u, v) = (h, 1) is returned with the full window count.
+
+#define CV_HS_MAXWIN 36                 // |u|, |v| < 2^140 -> at most 36 signed radix-16 windows
+#define CV_HS_MAXIT 200                 // Euclid steps (the Fibonacci worst case is ~185)
+
+CV_HD double cv_words_to_double(const uint32_t a[8]) {
+    double d = (double)a[7];
+#pragma unroll
+    for (int i = 6; i >= 0; i--) d = d * 4294967296.0 + (double)a[i];
+    return d;
+}
+// two's-complement 5-word signed value -> |value| as double
+CV_HD double cv_sw5_abs_double(const uint32_t t[5]) {
+    const bool neg = (int32_t)t[4] < 0;
+    double d = 0;
+#pragma unroll
+    for (int i = 4; i >= 0; i--) d = d * 4294967296.0 + (double)(neg ? ~t[i] : t[i]);
+    return neg ? d + 1.0 : d;
+}
+// a -= q * b (8 words, no underflow by construction)
+CV_HD void cv_submul8(uint32_t a[8], const uint32_t b[8], uint32_t q) {
+    uint64_t carry = 0;
+    int64_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint64_t p = (uint64_t)b[i] * q + carry;
+        carry = p >> 32;
+        const int64_t d = (int64_t)a[i] - (int64_t)(uint32_t)p + borrow;
+        a[i] = (uint32_t)d;
+        borrow = d >> 32;
+    }
+}
+// a -= q * b modulo 2^160 (two's complement: works for signed a, b)
+CV_HD void cv_submul5(uint32_t a[5], const uint32_t b[5], uint32_t q) {
+    uint64_t carry = 0;
+    int64_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+        const uint64_t p = (uint64_t)b[i] * q + carry;
+        carry = p >> 32;
+        const int64_t d = (int64_t)a[i] - (int64_t)(uint32_t)p + borrow;
+        a[i] = (uint32_t)d;
+        borrow = d >> 32;
+    }
+}
+CV_HD bool cv_lt8(const uint32_t a[8], const uint32_t b[8]) {
+    int64_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) borrow = ((int64_t)a[i] - (int64_t)b[i] + borrow) >> 32;
+    return borrow != 0;
+}
+CV_HD int cv_bitlen8(const uint32_t a[8]) {
+    int b = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        if (a[i]) b = 32 * i + 32 - __builtin_clz(a[i]);
+    return b;
+}
+
+// Outputs: u (8 words, u >= 0), v = |v| (8 words), v_neg, nwin = signed radix-16 windows that cover
+// both (digit16 k < nwin), w = (-v s) mod L.  Returns false when it fell back to (h, 1).
+__host__ __device__ __forceinline__ bool sc_halfsize(uint32_t u[8], uint32_t v[8], bool &v_neg, int &nwin,
+                                                     uint32_t w[8], const uint32_t h[8], const uint32_t s[8]) {
+    uint32_t r0[8] = {0xe7ae9f68u, 0xc09318d2u, 0x17bce6b2u, 0xa6f7cef5u, 0, 0, 0, 0x80000000u};   // 8L
+    uint32_t r1[8], t0[5] = {0, 0, 0, 0, 0}, t1[5] = {1, 0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 8; i++) r1[i] = h[i];
+    bool done = false;
+#pragma nounroll
+    for (int it = 0; it < CV_HS_MAXIT; it++) {
+        // keep r0 >= r1 (a quotient underestimate leaves r0 >= r1: the next step continues it)
+        const bool lt = cv_lt8(r0, r1);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t a = r0[i], b = r1[i];
+            r0[i] = lt ? b : a;
+            r1[i] = lt ? a : b;
+        }
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            const uint32_t a = t0[i], b = t1[i];
+            t0[i] = lt ? b : a;
+            t1[i] = lt ? a : b;
+        }
+        if ((r1[4] | r1[5] | r1[6] | r1[7]) == 0) {   // r1 < 2^128 <= r0: stop
+            done = true;
+            break;
+        }
+        // quotient estimate, never above floor(r0 / r1): the doubles carry < 2^-49 relative error
+        double q = (cv_words_to_double(r0) / cv_words_to_double(r1)) * (1.0 - 0x1p-44);
+        q = q < 1.0 ? 1.0 : (q > 4294967295.0 ? 4294967295.0 : q);
+        const uint32_t qi = (uint32_t)q;
+        cv_submul8(r0, r1, qi);
+        cv_submul5(t0, t1, qi);
+    }
+    // candidate: (r1, t1) if t1 is odd, else (r0 - k r1, t0 - k t1) balanced (t0 is then odd, and
+    // t0, t1 have opposite signs so |t0 - k t1| = |t0| + k |t1|)
+    bool ok = done;
+    uint32_t vt[5];
+    if ((t1[0] & 1u) != 0) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) u[i] = r1[i];
+#pragma unroll
+        for (int i = 0; i < 5; i++) vt[i] = t1[i];
+    } else {
+        double k = (cv_words_to_double(r0) - cv_sw5_abs_double(t0)) /
+                   (cv_words_to_double(r1) + cv_sw5_abs_double(t1)) * (1.0 - 0x1p-40);
+        if (!(k < 4294967295.0)) ok = false;
+        k = k < 0.0 ? 0.0 : (k > 4294967295.0 ? 4294967295.0 : k);
+        const uint32_t ki = (uint32_t)k;
+#pragma unroll
+        for (int i = 0; i < 8; i++) u[i] = r0[i];
+#pragma unroll
+        for (int i = 0; i < 5; i++) vt[i] = t0[i];
+        cv_submul8(u, r1, ki);
+        cv_submul5(vt, t1, ki);
+    }
+    v_neg = (int32_t)vt[4] < 0;
+    {
+        uint64_t c = v_neg ? 1 : 0;                            // |vt| = v_neg ? ~vt + 1 : vt
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            c += (uint64_t)(v_neg ? ~vt[i] : vt[i]);
+            v[i] = (uint32_t)c;
+            c >>= 32;
+        }
+    }
+    v[5] = v[6] = v[7] = 0;
+    // bit length of max(u, |v|) -> windows (digit16 of an x < 2^b needs floor(b/4) + 1 digits)
+    uint32_t m[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) m[i] = u[i] | v[i];
+    nwin = cv_bitlen8(m) / 4 + 1;
+    if (nwin > CV_HS_MAXWIN) ok = false;
+    if (!ok) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) { u[i] = h[i]; v[i] = i == 0; }
+        v_neg = false;
+        nwin = 64;
+    }
+    // w = (-v s) mod L
+    {
+        uint32_t x[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) x[i] = 0;
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            uint64_t carry = 0;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint64_t t = (uint64_t)v[i] * s[j] + x[i + j] + carry;
+                x[i + j] = (uint32_t)t;
+                carry = t >> 32;
+            }
+            x[i + 8] = (uint32_t)carry;
+        }
+        uint32_t mm[8];
+        sc_reduce512(mm, x);                                   // |v| s mod L
+        const uint32_t Lw[8] = {0x5cf5d3ed, 0x5812631a, 0xa2f79cd6, 0x14def9de, 0, 0, 0, 0x10000000};
+        uint32_t nz = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) nz |= mm[i];
+        int64_t br = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int64_t d = (int64_t)Lw[i] - (int64_t)mm[i] + br;
+            const uint32_t neg_i = nz ? (uint32_t)d : 0u;      // (L - m) mod L
+            br = d >> 32;
+            w[i] = v_neg ? mm[i] : neg_i;                      // v < 0: -v s = |v| s
+        }
+    }
+    return ok;
+}

@@ -533,3 +533,142 @@ __host__ __device__ __forceinline__ bool cv_merkle_root_inplace(uint32_t *lvl, u
     for (int q = 0; q < 8; q++) root[q] = lvl[q];
     return true;
 }
+
+// ---------------------------------------------------------------- half-size verify (throughput path)
+// Same verdict as phases 1-3 above with about half the doublings (sc_halfsize, cv_scalar.h):
+//   accept  <=>  key_ok  AND  R's bytes are the canonical encoding of a curve point
+//                        AND  [v]R + [u]A + [w]B == O
+// R' = [s]B - [h]A always encodes canonically (toByteArray), so the reference's byte compare accepts
+// exactly when R decodes canonically to the point R' (encoding is injective on points); the scaled
+// equation is equivalent to R == R' because gcd(v, 8L) = 1.
+//   hsprep : decode R (canonical), table k*R (k = 1..8, cached), (u, v, w) -> workspace
+//   straus : ~33 windows of 4 doublings; R and A digits every window, B digits every other window
+//            from two radix-256 tables (k*B and k*2^128*B: w's low and high 128 bits); the identity
+//            test needs no inversion, so the verdict bit comes straight out of this kernel.
+// hsprep leaves per window one packed digit word, window-major (dig[win * stride + i]: a wave reads
+// 256 contiguous bytes per window), two's-complement fields:  bits 0-4 = digit of A in [-8, 8] (sign
+// pre-flipped for the k*(-A) table), bits 5-9 = digit of R (sign of v folded in), bits 10-18 and
+// 19-27 = radix-256 digits in [-128, 128] of w for k*B and k*2^128*B (even windows < 32 only).
+// dig[64 * stride + i] = the lane's window count.
+CV_HD int cv_sfield(uint32_t w, int off, int width) { return (int)(w << (32 - off - width)) >> (32 - width); }
+#define CV_HS_DIGWORDS 65
+
+// Canonical decode of R: true iff the 8 words are exactly GroupElement.toByteArray() of a point.
+template <bool LAT = false> __host__ __device__ __forceinline__ bool ge_decode_canonical(ge_p3 &P, const uint32_t w[8]) {
+    bool ok = ge_decode_0_1_0<LAT>(P, w);
+    uint32_t enc[8], diff = 0;
+    ge_abyte_from_key(enc, w);          // y mod p, sign bit cleared when x = 0
+#pragma unroll
+    for (int q = 0; q < 8; q++) diff |= enc[q] ^ w[q];
+    return ok && diff == 0;
+}
+
+template <bool LAT = false> __host__ __device__ __forceinline__ bool cv_hs_prep(const uint32_t rw[8], const uint32_t *hs,
+                                                                               uint32_t *dig, size_t stride,
+                                                                               uint32_t *tabR) {
+    {
+        uint32_t h[8], s[8], u[8], v[8], w[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) { h[q] = hs[q]; s[q] = hs[8 + q]; }
+        bool v_neg;
+        int nwin;
+        sc_halfsize(u, v, v_neg, nwin, w, h, s);
+#pragma unroll 4
+        for (int win = 0; win < 64; win++) {
+            const int da = -digit16(u, win), dr = v_neg ? -digit16(v, win) : digit16(v, win);
+            const bool bw = (win & 1) == 0 && win < 32;
+            const int dlo = bw ? digit256(w, win >> 1) : 0, dhi = bw ? digit256(w, 16 + (win >> 1)) : 0;
+            dig[(size_t)win * stride] = ((uint32_t)da & 0x1fu) | (((uint32_t)dr & 0x1fu) << 5) |
+                                        (((uint32_t)dlo & 0x1ffu) << 10) | (((uint32_t)dhi & 0x1ffu) << 19);
+        }
+        dig[64 * stride] = (uint32_t)nwin;
+    }
+    ge_p3 R;
+    const bool r_ok = ge_decode_canonical<LAT>(R, rw);
+    if (!r_ok) ge_p3_identity(R);
+    ge_cached_multiples8(tabR, R);
+    return r_ok;
+}
+
+// entry |d| of a cached k*P table (identity for d = 0), negated for d < 0
+CV_HD void tab_cached_select(ge_cached &e, const uint32_t *tab, int d) {
+    const int m = d < 0 ? -d : d;
+    ge_cached id;
+    ge_cached_load(e, tab + 40 * (m ? m - 1 : 0));
+    ge_cached_identity(id);
+    fe_sel(e.YplusX, e.YplusX, id.YplusX, m == 0);
+    fe_sel(e.YminusX, e.YminusX, id.YminusX, m == 0);
+    fe_sel(e.Z, e.Z, id.Z, m == 0);
+    fe_sel(e.T2d, e.T2d, id.T2d, m == 0);
+    ge_cached_cneg(e, d < 0);
+}
+
+// E = [v]R + [u]A + [w]B from the packed digits (tabA = k*(-A), tabR = k*R); nw (>= 32, uniform
+// over the wave on the GPU) windows.  Returns E == O.
+__host__ __device__ __forceinline__ bool cv_hs_straus(const uint32_t *blo, const uint32_t *bhi, const uint32_t *dig,
+                                                      size_t stride, const uint32_t *tabA, const uint32_t *tabR, int nw) {
+    ge_p2 R;
+    ge_p2_identity(R);
+#pragma unroll 1
+    for (int win = nw - 1; win >= 0; win--) {
+        const uint32_t dw = dig[(size_t)win * stride];
+        ge_p1p1 t;
+        ge_p3 R3;
+        if (win != nw - 1) {
+            ge_p2_dbl(t, R);
+            ge_p1p1_to_p2(R, t);
+            ge_p2_dbl(t, R);
+            ge_p1p1_to_p2(R, t);
+            ge_p2_dbl(t, R);
+            ge_p1p1_to_p2(R, t);
+            ge_p2_dbl(t, R);
+            ge_p1p1_to_p3(R3, t);
+        } else {
+            ge_p3_identity(R3);
+        }
+        {
+            ge_cached e;
+            tab_cached_select(e, tabR, cv_sfield(dw, 5, 5));
+            ge_add(t, R3, e);
+        }
+        ge_p1p1_to_p3(R3, t);
+        {
+            ge_cached e;
+            tab_cached_select(e, tabA, cv_sfield(dw, 0, 5));
+            ge_add(t, R3, e);
+        }
+        if ((win & 1) == 0 && win < 32) {
+            ge_precomp e;
+            ge_p1p1_to_p3(R3, t);
+            btab_select(e, blo, cv_sfield(dw, 10, 9));
+            ge_madd(t, R3, e);
+            ge_p1p1_to_p3(R3, t);
+            btab_select(e, bhi, cv_sfield(dw, 19, 9));
+            ge_madd(t, R3, e);
+        }
+        ge_p1p1_to_p2(R, t);
+    }
+    // identity: X = 0 and Y = Z (Z != 0 for points of the complete formulas)
+    fe d;
+    fe_sub<2>(d, R.Y, R.Z);
+    return fe_is_zero(R.X) && fe_is_zero(d);
+}
+
+// Single-signature convenience (host harness): prep + hsprep + straus.  dig_out: 65 words or null.
+__host__ __device__ __forceinline__ bool cv_verify_one_hs(const uint32_t *bcomb, const uint32_t aw[8], const uint32_t rw[8],
+                                                          const uint32_t sw[8], const uint8_t *msg, uint32_t mlen,
+                                                          bool *key_ok_out, uint32_t *dig_out) {
+    uint32_t hs[CV_HS_WORDS];
+    alignas(16) uint32_t tab[CV_TAB_WORDS];
+    alignas(16) uint32_t tabR[CV_TAB_WORDS];
+    uint32_t dig[CV_HS_DIGWORDS];
+    const bool key_ok = cv_verify_prep(aw, rw, sw, msg, mlen, hs, tab);
+    const bool r_ok = cv_hs_prep(rw, hs, dig, 1, tabR);
+    int nw = (int)dig[64];
+    if (nw < 32) nw = 32;
+    const bool eq = cv_hs_straus(bcomb, bcomb + 2 * CV_BTAB_ENTRIES * CV_BTAB_STRIDE, dig, 1, tab, tabR, nw);
+    *key_ok_out = key_ok;
+    if (dig_out)
+        for (int q = 0; q < CV_HS_DIGWORDS; q++) dig_out[q] = dig[q];
+    return key_ok && r_ok && eq;
+}

@@ -32,6 +32,17 @@ EXPORTED = (
 )
 
 
+def verify_mode() -> int:
+    """Throughput verify schedule: 1 = half-size scalars (prep | hsprep | hs_straus), 0 = full width
+    (prep | straus | finish)."""
+    lib = load()
+    return int(lib.cvk_get_verify_mode()) if hasattr(lib, "cvk_get_verify_mode") else 0
+
+
+def set_verify_mode(mode: int) -> None:
+    load().cvk_set_verify_mode(int(mode))
+
+
 class NativeUnavailable(RuntimeError):
     pass
 
@@ -78,6 +89,11 @@ def load():
         lib.cv_ed25519_sign_batch.restype = ctypes.c_int
         lib.cv_tx_verdicts.argtypes = [_sz, _vp, _vp, _vp]
         lib.cv_tx_verdicts.restype = ctypes.c_int
+        if hasattr(lib, "cvk_set_verify_mode"):                 # internal tuning knobs (not C-ABI)
+            lib.cvk_set_verify_mode.argtypes = [ctypes.c_int]
+            lib.cvk_get_verify_mode.restype = ctypes.c_int
+            if os.environ.get("CV_VERIFY_MODE"):                 # A/B: 0 = full-width group, 1 = half-size
+                lib.cvk_set_verify_mode(int(os.environ["CV_VERIFY_MODE"]))
         lib.cv_ed25519_verify_device.argtypes = [_vp, ctypes.c_int, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
         lib.cv_ed25519_verify_device.restype = ctypes.c_int
         if hasattr(lib, "cv_ed25519_verify_device_timed"):      # absent only in pre-r01 A/B builds
@@ -249,7 +265,8 @@ class Engine:
 
     def verify_device_timed(self, device: int, n: int, d_pk: int, d_sig: int, d_arena: int, d_off: int, d_len: int,
                             d_bitmap: int, stream: int = 0) -> Tuple[float, float, float]:
-        """Synchronous verify; returns the (prep, straus, finish) kernel durations in ms (HIP events)."""
+        """Synchronous verify; returns three kernel durations in ms (HIP events): (prep, straus, finish),
+        or (prep, hsprep, hs_straus) in the half-size schedule (verify_mode() == 1)."""
         ms = (ctypes.c_float * 3)()
         _check(self._lib.cv_ed25519_verify_device_timed(self._h, device, n, d_pk, d_sig, d_arena, d_off, d_len,
                                                         d_bitmap, stream or None, ms), "cv_ed25519_verify_device_timed")

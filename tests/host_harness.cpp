@@ -241,4 +241,33 @@ int cvh_merkle_root(const uint8_t *leaves, uint32_t cnt, uint8_t *out) {
     return ok ? 1 : 0;
 }
 
+// Half-size-scalar verify of one signature (prep + hsprep + straus, identity test).  sc_out: 65 words.
+int cvh_verify_hs(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, uint32_t mlen, int *status,
+                  uint32_t *sc_out) {
+    uint32_t aw[8], rw[8], sw[8];
+    words_from_bytes(aw, pk, 8);
+    words_from_bytes(rw, sig, 8);
+    words_from_bytes(sw, sig + 32, 8);
+    bool key_ok = false;
+    const bool ok = cv_verify_one_hs(CV_BCOMB_H, aw, rw, sw, msg, mlen, &key_ok, sc_out);
+    *status = key_ok ? 0 : 1;
+    return ok ? 1 : 0;
+}
+
+// sc_halfsize on (h, s) given as 32 LE bytes each; out = u (32 B) | |v| (32 B) | w (32 B).
+int cvh_halfsize(const uint8_t *h, const uint8_t *s, uint8_t *out, int *v_neg, int *nwin) {
+    uint32_t hw[8], sw[8], u[8], v[8], w[8];
+    words_from_bytes(hw, h, 8);
+    words_from_bytes(sw, s, 8);
+    bool neg = false;
+    int nw = 0;
+    const bool ok = sc_halfsize(u, v, neg, nw, w, hw, sw);
+    bytes_from_words(out, u, 8);
+    bytes_from_words(out + 32, v, 8);
+    bytes_from_words(out + 64, w, 8);
+    *v_neg = neg ? 1 : 0;
+    *nwin = nw;
+    return ok ? 1 : 0;
+}
+
 }  // extern "C"

@@ -248,3 +248,51 @@ def test_verify_batch_logic_chunks(host_harness, corpus, manifest):
                            status.ctypes.data_as(vp))
         assert np.array_equal(verdict, corpus["verdict"][order])
         assert np.array_equal(status, corpus["status"][order])
+
+
+def test_halfsize_lattice_properties(host_harness):
+    """sc_halfsize: u = v h (mod 8L), v odd, w = -v s (mod L), |u|, |v| < 16^nwin; the fallback
+    (h, 1) only when no short odd-v vector exists.  Random h, s plus edge scalars."""
+    H = host_harness
+    rng = random.Random(7)
+    cases = [(0, 0), (1, 5), (L - 1, L - 1), (2**128 - 1, 3), (2**128, 1), (2**252, 7), (8, 9)]
+    cases += [(rng.randrange(L), rng.randrange(L)) for _ in range(3000)]
+    wins = []
+    fallbacks = 0
+    for ci, (h, s) in enumerate(cases):
+        out = _out(96)
+        vn, nw = ctypes.c_int(0), ctypes.c_int(0)
+        ok = H.cvh_halfsize(_b(h.to_bytes(32, "little")), _b(s.to_bytes(32, "little")), out, ctypes.byref(vn),
+                            ctypes.byref(nw))
+        o = bytes(out)
+        u, va, w = (int.from_bytes(o[32 * k:32 * k + 32], "little") for k in range(3))
+        v = -va if vn.value else va
+        assert v % 2 == 1
+        assert (u - v * h) % (8 * L) == 0
+        assert w == (-v * s) % L
+        assert u >= 0 and max(u, va) < 16 ** nw.value
+        if ok:
+            assert nw.value <= 36
+            wins.append(nw.value)
+        else:
+            fallbacks += 1
+            assert ci < 7, "fallback on a random scalar"    # only degenerate edge lattices fall back
+            assert (u, v, nw.value) == (h, 1, 64)
+    assert fallbacks <= 3
+    assert sum(wins) / len(wins) < 34.0
+
+
+def test_halfsize_verify_logic_on_golden_corpus(host_harness, corpus, manifest):
+    """The half-size verify ([v]R + [u]A + [w]B == O with canonical R decoding) reproduces every
+    golden verdict: non-canonical / off-curve / small-order R, torsion keys, S >= L, carry loss."""
+    H = host_harness
+    bad = []
+    sc = (ctypes.c_uint32 * 65)()
+    for i in range(len(corpus["pk"])):
+        m = corpus["arena"][corpus["off"][i]:corpus["off"][i] + corpus["len"][i]].tobytes()
+        st = ctypes.c_int(0)
+        v = H.cvh_verify_hs(_b(corpus["pk"][i].tobytes()), _b(corpus["sig"][i].tobytes()), _b(m), len(m),
+                            ctypes.byref(st), sc)
+        if v != corpus["verdict"][i] or st.value != corpus["status"][i]:
+            bad.append(manifest["classes"][corpus["cls"][i]])
+    assert not bad, sorted(set(bad))

@@ -301,3 +301,47 @@ def test_lane_and_quad_forms_agree(engine, corpus, oracle_c, quad_max):
         assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
     finally:
         lib.cvk_set_quad_max(32768)
+
+
+# ---------------------------------------------------------------- both throughput schedules
+@pytest.mark.parametrize("mode", [0, 1])
+def test_full_width_and_half_size_schedules_agree(engine, corpus, oracle_c, mode):
+    """The lane-form throughput path in each schedule (internal switch cvk_set_verify_mode: 0 = full
+    width prep/straus/finish, 1 = half-size scalars prep/hsprep/hs_straus with the wave-ballot
+    verdicts) over the golden corpus, ragged tails, and a corrupted random batch vs the C oracle."""
+    import ctypes
+    lib = native.load()
+    lib.cvk_set_quad_max.argtypes = [ctypes.c_uint32]
+    lib.cvk_set_quad_max(0)
+    native.set_verify_mode(mode)
+    try:
+        bitmap, status = engine.verify_batch(corpus["pk"], corpus["sig"], corpus["arena"], corpus["off"], corpus["len"])
+        assert np.array_equal(_bits(bitmap, len(corpus["pk"])), corpus["verdict"].astype(bool))
+        assert np.array_equal(status, corpus["status"])
+        for n in (1, 63, 65, 257, 699):
+            sel = np.arange(n) % len(corpus["pk"])
+            bitmap, status = engine.verify_batch(corpus["pk"][sel], corpus["sig"][sel], corpus["arena"],
+                                                 corpus["off"][sel], corpus["len"][sel])
+            assert np.array_equal(_bits(bitmap, n), corpus["verdict"][sel].astype(bool))
+            assert np.array_equal(status, corpus["status"][sel])
+        rng = np.random.default_rng(41)
+        n = 6000
+        seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+        lens = rng.integers(0, 200, n).astype(np.uint32)
+        off = np.zeros(n, np.uint64)
+        off[1:] = np.cumsum(lens[:-1])
+        arena = rng.integers(0, 256, int(lens.sum()) + 16, dtype=np.uint8)
+        pk, sig = engine.sign_batch(seeds, arena, off, lens)
+        sig[1::7, rng.integers(0, 32)] ^= 0x04          # R corrupted (mostly off-curve / wrong point)
+        sig[2::11, 31] |= 0x80                          # R sign bit forced
+        sig[3::13, 63] |= 0x80                          # S >= 2^255
+        sig[4::17, 40] ^= 0x01                          # S corrupted
+        pk[5::19, 7] ^= 0x20                            # key corrupted
+        bitmap, status = engine.verify_batch(pk, sig, arena, off, lens)
+        ref, rst = oracle_c.verify_batch(pk, sig, arena, off, lens, nthreads=8)
+        assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
+        assert np.array_equal(status, rst)
+        assert 0.4 < ref.mean() < 0.9
+    finally:
+        native.set_verify_mode(1)
+        lib.cvk_set_quad_max(32768)

@@ -2,7 +2,8 @@
 """Summarise rocprofv3 --pmc passes (scripts/pmc.sh) per kernel, and write the HBM-traffic record of
 the dominant kernel that bench.py reports as roofline.traffic.
 
-    python tools/pmc_summary.py gpurun_out/<tag>/pmc N_SIGNATURES [--out profiles/pmc_straus.json]
+    python tools/pmc_summary.py gpurun_out/<tag>/pmc N_SIGNATURES [--kernel cv_hs_straus_kernel]
+                                [--out profiles/pmc_hs_straus.json]
 
 Counter values are averaged over the dispatches of each kernel.  HBM bytes follow
 MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half
@@ -34,9 +35,10 @@ def main():
         print(k)
         for c, v in sorted(d.items()):
             print(f"    {c:28s} {v:.6g}")
-    key = next((k for k in data if "cv_straus_kernel" in k), None)
+    want = sys.argv[sys.argv.index("--kernel") + 1] if "--kernel" in sys.argv else "cv_straus_kernel"
+    key = next((k for k in data if want in k), None)
     if key is None:
-        print("no cv_straus_kernel dispatches found")
+        print(f"no {want} dispatches found")
         return
     d = data[key]
     rec = {"kernel": key, "n": n, "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (scripts/pmc.sh)",
