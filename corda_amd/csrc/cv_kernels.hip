@@ -117,7 +117,7 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsprep_kernel(uint32_t n, uint
                                                                 const uint32_t *__restrict__ ws_hs,
                                                                 uint32_t *__restrict__ ws_dig,
                                                                 uint32_t *__restrict__ ws_tabR,
-                                                                uint8_t *__restrict__ ws_ok) {
+                                                                uint8_t *__restrict__ ws_ok, int reduce) {
     const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
     if (i >= n) return;
     uint32_t rw[8], hs[CV_HS_WORDS];
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsprep_kernel(uint32_t n, uint
         const uint4 x = hp[q];
         hs[4 * q] = x.x; hs[4 * q + 1] = x.y; hs[4 * q + 2] = x.z; hs[4 * q + 3] = x.w;
     }
-    const bool r_ok = cv_hs_prep<LAT>(rw, hs, ws_dig + i, cap, ws_tabR + (size_t)i * CV_TAB_WORDS);
+    const bool r_ok = cv_hs_prep<LAT>(rw, hs, ws_dig + i, cap, ws_tabR + (size_t)i * CV_TAB_WORDS, reduce != 0);
     if (!r_ok) ws_ok[i] = 0;
 }
 
@@ -178,6 +178,13 @@ static int g_hs_waves = 3;
 extern "C" void cvk_set_verify_mode(int m) { g_verify_mode = m ? 1 : 0; }
 extern "C" int cvk_get_verify_mode(void) { return g_verify_mode; }
 extern "C" void cvk_set_hs_waves(int w) { g_hs_waves = (w == 2) ? 2 : 3; }
+// latency (ILP) field forms in the prep / hsprep kernels of throughput batches (2 waves per SIMD)
+static int g_prep_lat = 0, g_hsprep_lat = 0;
+// 0 = skip the lattice reduction ((u, v) = (h, 1), 64 windows: still exact) — A/B timing only
+static int g_hs_reduce = 1;
+extern "C" void cvk_set_hs_reduce(int v) { g_hs_reduce = v ? 1 : 0; }
+extern "C" void cvk_set_prep_lat(int v) { g_prep_lat = v ? 1 : 0; }
+extern "C" void cvk_set_hsprep_lat(int v) { g_hsprep_lat = v ? 1 : 0; }
 
 // ---------------------------------------------------------------- quad (latency) Straus kernels
 // Four lanes per signature (cv_quad.h) for batches too small to fill the chip.  Grid: 4n lanes.
@@ -346,7 +353,7 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
         // ev (optional, single-chunk batches): phase boundaries for live per-kernel timing
         if (ev && c0 == 0) (void)hipEventRecord(ev[0], stream);
         const bool lat = n <= g_quad_max;   // small batch: latency forms of the single chains
-        if (lat)
+        if (lat || g_prep_lat)
             hipLaunchKernelGGL(cv_prep_kernel<true>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, pk + (size_t)c0 * 32,
                                sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_hs, ws_tab, ws_ok,
                                status ? status + c0 : nullptr);
@@ -358,8 +365,12 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
         if (!lat && g_verify_mode == 1) {
             // half-size group: phases = prep | hsprep | hs_straus (verdict bits included)
             uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
-            hipLaunchKernelGGL(cv_hsprep_kernel<false>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap,
-                               sig + (size_t)c0 * 64, ws_hs, ws_dig, ws_tabR, ws_ok);
+            if (g_hsprep_lat)
+                hipLaunchKernelGGL(cv_hsprep_kernel<true>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap,
+                                   sig + (size_t)c0 * 64, ws_hs, ws_dig, ws_tabR, ws_ok, g_hs_reduce);
+            else
+                hipLaunchKernelGGL(cv_hsprep_kernel<false>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap,
+                                   sig + (size_t)c0 * 64, ws_hs, ws_dig, ws_tabR, ws_ok, g_hs_reduce);
             if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
             if (g_hs_waves == 2)
                 hipLaunchKernelGGL(cv_hs_straus_kernel<2>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, ws_dig,

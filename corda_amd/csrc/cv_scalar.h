@@ -251,6 +251,9 @@ CV_HD int digit256(const uint32_t n[8], int k) {
 // L) keeps the identity exact for keys with a torsion component; v odd keeps it exact for R.
 // When no short odd-v vector turns up (rare), (u, v) = (h, 1) is returned with the full window count.
 
+#ifndef CV_STAT
+#define CV_STAT(x)
+#endif
 #define CV_HS_MAXWIN 36                 // |u|, |v| < 2^140 -> at most 36 signed radix-16 windows
 #define CV_HS_MAXIT 200                 // Euclid steps (the Fibonacci worst case is ~185)
 
@@ -300,6 +303,36 @@ CV_HD bool cv_lt8(const uint32_t a[8], const uint32_t b[8]) {
     for (int i = 0; i < 8; i++) borrow = ((int64_t)a[i] - (int64_t)b[i] + borrow) >> 32;
     return borrow != 0;
 }
+// bits [sh, sh + 53) of an 8-word value below 2^(sh + 53), as an exact double (0 <= sh <= 203)
+CV_HD double cv_top53(const uint32_t a[8], int sh) {
+    const int ws = sh >> 5, bs = sh & 31;
+    const uint32_t w0 = sel8(a, ws), w1 = sel8(a, ws + 1), w2 = ws + 2 < 8 ? sel8(a, ws + 2) : 0u;
+    const uint32_t lo = (uint32_t)((((uint64_t)w1 << 32) | w0) >> bs);
+    const uint32_t hi = (uint32_t)((((uint64_t)w2 << 32) | w1) >> bs);
+    return (double)hi * 4294967296.0 + (double)lo;
+}
+// out = m0 a + m1 b over NW words (|m0|, |m1| < 2^30), two's complement, word NW (if kept) = sign
+template <int NW> CV_HD void cv_lincomb(uint32_t *out, const uint32_t *a, int64_t m0, const uint32_t *b, int64_t m1) {
+    int64_t carry = 0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+        const int64_t acc = (int64_t)a[i] * m0 + (int64_t)b[i] * m1 + carry;
+        out[i] = (uint32_t)acc;
+        carry = acc >> 32;
+    }
+    out[NW] = (uint32_t)carry;
+}
+// two's-complement negation of n words when neg
+template <int N> CV_HD void cv_cneg_words(uint32_t *x, bool neg) {
+    uint64_t c = neg ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        c += (uint64_t)(neg ? ~x[i] : x[i]);
+        x[i] = (uint32_t)c;
+        c >>= 32;
+    }
+}
+
 CV_HD int cv_bitlen8(const uint32_t a[8]) {
     int b = 0;
 #pragma unroll
@@ -311,14 +344,59 @@ CV_HD int cv_bitlen8(const uint32_t a[8]) {
 // Outputs: u (8 words, u >= 0), v = |v| (8 words), v_neg, nwin = signed radix-16 windows that cover
 // both (digit16 k < nwin), w = (-v s) mod L.  Returns false when it fell back to (h, 1).
 __host__ __device__ __forceinline__ bool sc_halfsize(uint32_t u[8], uint32_t v[8], bool &v_neg, int &nwin,
-                                                     uint32_t w[8], const uint32_t h[8], const uint32_t s[8]) {
+                                                     uint32_t w[8], const uint32_t h[8], const uint32_t s[8],
+                                                     bool reduce = true) {
     uint32_t r0[8] = {0xe7ae9f68u, 0xc09318d2u, 0x17bce6b2u, 0xa6f7cef5u, 0, 0, 0, 0x80000000u};   // 8L
     uint32_t r1[8], t0[5] = {0, 0, 0, 0, 0}, t1[5] = {1, 0, 0, 0, 0};
 #pragma unroll
     for (int i = 0; i < 8; i++) r1[i] = h[i];
     bool done = false;
+    // Lehmer phase: Euclid on the leading 53 bits in double precision (cosequence entries < 2^30),
+    // one exact multi-word application per ~26 bits.  Every applied matrix is unimodular, so the
+    // invariant r_i = t_i h (mod 8L) holds whatever the quotients; a quotient the truncation got
+    // wrong only shows up as a negative or out-of-order pair, normalised below.  The exact loop
+    // then finishes at the first remainder below 2^128.
 #pragma nounroll
-    for (int it = 0; it < CV_HS_MAXIT; it++) {
+    for (int outer = 0; outer < (reduce ? 6 : 0); outer++) {
+        if ((r1[4] | r1[5] | r1[6] | r1[7]) == 0) break;
+        const int sh = cv_bitlen8(r0) - 53;           // >= 76: r0 >= r1 >= 2^128
+        double x0 = cv_top53(r0, sh), x1 = cv_top53(r1, sh);
+        double a00 = 1, a01 = 0, a10 = 0, a11 = 1;
+        const double lim = sh >= 128 ? 1.0 : (double)(1ull << (128 - sh));   // full r1 stays >= 2^128
+        int steps = 0;
+#pragma nounroll
+        for (int k = 0; k < 40; k++) {
+            if (!(x1 >= 0x1p27)) break;
+            const double q = floor(x0 / x1);
+            const double nx = fma(-q, x1, x0);
+            const double n0 = fma(-q, a10, a00), n1 = fma(-q, a11, a01);
+            const double e = fabs(n0) + fabs(n1);
+            if (!(nx >= 0 && nx < x1 && e < 0x1p30 && nx >= lim)) break;
+            if (!(nx >= e + 1 && x1 - nx >= e + fabs(a10) + fabs(a11) + 1)) break;   // truncation-safe quotient
+            x0 = x1; x1 = nx;
+            a00 = a10; a01 = a11; a10 = n0; a11 = n1;
+            steps++;
+        }
+        CV_STAT(g_outer++; g_inner += steps;)
+        if (steps == 0) break;
+        uint32_t nr0[9], nr1[9], nt0[6], nt1[6];
+        const int64_t m00 = (int64_t)a00, m01 = (int64_t)a01, m10 = (int64_t)a10, m11 = (int64_t)a11;
+        cv_lincomb<8>(nr0, r0, m00, r1, m01);
+        cv_lincomb<8>(nr1, r0, m10, r1, m11);
+        cv_lincomb<5>(nt0, t0, m00, t1, m01);
+        cv_lincomb<5>(nt1, t0, m10, t1, m11);
+        const bool n0neg = (int32_t)nr0[8] < 0, n1neg = (int32_t)nr1[8] < 0;
+        cv_cneg_words<8>(nr0, n0neg);
+        cv_cneg_words<5>(nt0, n0neg);
+        cv_cneg_words<8>(nr1, n1neg);
+        cv_cneg_words<5>(nt1, n1neg);
+#pragma unroll
+        for (int i = 0; i < 8; i++) { r0[i] = nr0[i]; r1[i] = nr1[i]; }
+#pragma unroll
+        for (int i = 0; i < 5; i++) { t0[i] = nt0[i]; t1[i] = nt1[i]; }
+    }
+#pragma nounroll
+    for (int it = 0; it < (reduce ? CV_HS_MAXIT : 0); it++) {
         // keep r0 >= r1 (a quotient underestimate leaves r0 >= r1: the next step continues it)
         const bool lt = cv_lt8(r0, r1);
 #pragma unroll
@@ -337,6 +415,7 @@ __host__ __device__ __forceinline__ bool sc_halfsize(uint32_t u[8], uint32_t v[8
             done = true;
             break;
         }
+        CV_STAT(g_exact++;)
         // quotient estimate, never above floor(r0 / r1): the doubles carry < 2^-49 relative error
         double q = (cv_words_to_double(r0) / cv_words_to_double(r1)) * (1.0 - 0x1p-44);
         q = q < 1.0 ? 1.0 : (q > 4294967295.0 ? 4294967295.0 : q);

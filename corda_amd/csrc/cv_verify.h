@@ -565,14 +565,14 @@ template <bool LAT = false> __host__ __device__ __forceinline__ bool ge_decode_c
 
 template <bool LAT = false> __host__ __device__ __forceinline__ bool cv_hs_prep(const uint32_t rw[8], const uint32_t *hs,
                                                                                uint32_t *dig, size_t stride,
-                                                                               uint32_t *tabR) {
+                                                                               uint32_t *tabR, bool reduce = true) {
     {
         uint32_t h[8], s[8], u[8], v[8], w[8];
 #pragma unroll
         for (int q = 0; q < 8; q++) { h[q] = hs[q]; s[q] = hs[8 + q]; }
         bool v_neg;
         int nwin;
-        sc_halfsize(u, v, v_neg, nwin, w, h, s);
+        sc_halfsize(u, v, v_neg, nwin, w, h, s, reduce);
 #pragma unroll 4
         for (int win = 0; win < 64; win++) {
             const int da = -digit16(u, win), dr = v_neg ? -digit16(v, win) : digit16(v, win);

@@ -34,6 +34,11 @@ def main():
     if os.environ.get("CV_QUAD_MAX"):
         lib.cvk_set_quad_max.argtypes = [ctypes.c_uint32]
         lib.cvk_set_quad_max(int(os.environ["CV_QUAD_MAX"]))
+    # CV_KNOBS="cvk_set_hs_waves=2,cvk_set_prep_lat=1": any internal int setter of the library
+    for kv in filter(None, os.environ.get("CV_KNOBS", "").split(",")):
+        k, v = kv.split("=")
+        getattr(lib, k).argtypes = [ctypes.c_int]
+        getattr(lib, k)(int(v))
     if args.keyed:
         return keyed(eng, args)
     stream = torch.cuda.Stream(0)
