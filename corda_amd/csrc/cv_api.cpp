@@ -20,6 +20,10 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
                       hipEvent_t *ev);
 hipError_t cvk_sign(uint32_t n, const uint8_t *seed, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
                     uint8_t *pk, uint8_t *sig, hipStream_t stream);
+hipError_t cvk_pmt_verify(uint32_t ntrees, const uint8_t *kind, const uint32_t *left, const uint32_t *right,
+                          const uint8_t *leaf_hash, const uint32_t *tree_begin, const uint8_t *root, const uint8_t *check,
+                          const uint32_t *check_begin, uint32_t *dig, uint8_t *flag, uint8_t *verdict, uint8_t *status,
+                          hipStream_t stream);
 hipError_t cvk_merkle(uint32_t ntx, uint32_t nleaves, const uint8_t *arena, const uint64_t *leaf_off,
                       const uint32_t *leaf_len, const uint32_t *tx_begin, uint32_t *leaf_digest, uint8_t *ids,
                       uint8_t *status, hipStream_t stream);
@@ -81,6 +85,7 @@ struct Device {
     int ordinal = 0;
     hipStream_t stream = nullptr;
     DevBuf pk, sig, arena, off, len, bitmap, status, seed, tx_begin, digest, ids;
+    DevBuf pmt;                          // partial Merkle trees: inputs, outputs and workspace, packed
     DevBuf ws_hs, ws_tab, ws_R, ws_ok, ws_dig;   // verify workspace per signature: hs 64 B, 2 tables 2560 B,
                                          // R record 128 B, ok 1 B, half-size digits 260 B
     uint32_t ws_cap = 0;
@@ -186,7 +191,7 @@ void cv_close(cv_ctx *ctx) {
         (void)hipSetDevice(d.ordinal);
         if (d.stream) (void)hipStreamSynchronize(d.stream);
         for (DevBuf *b : {&d.pk, &d.sig, &d.arena, &d.off, &d.len, &d.bitmap, &d.status, &d.seed, &d.tx_begin,
-                          &d.digest, &d.ids, &d.ws_hs, &d.ws_tab, &d.ws_R, &d.ws_ok, &d.ws_dig, &d.kc.ktab, &d.kc.kok,
+                          &d.digest, &d.ids, &d.pmt, &d.ws_hs, &d.ws_tab, &d.ws_R, &d.ws_ok, &d.ws_dig, &d.kc.ktab, &d.kc.kok,
                           &d.kc.keys, &d.kc.slots, &d.kc.slot_of_key, &d.kc.key_index, &d.kc.scratch})
             b->release();
         if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -544,6 +549,55 @@ int cv_merkle_tx_ids_ex(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, cons
                       d.status.as<uint8_t>(), s));
     CV_TRY(hipMemcpyAsync(ids, d.ids.p, ntx * 32, hipMemcpyDeviceToHost, s));
     if (tx_status) CV_TRY(hipMemcpyAsync(tx_status, d.status.p, ntx, hipMemcpyDeviceToHost, s));
+    CV_TRY(hipStreamSynchronize(s));
+    return CV_OK;
+}
+
+int cv_partial_merkle_verify(cv_ctx *ctx, size_t ntrees, size_t nnodes, const uint8_t *kind, const uint32_t *left,
+                             const uint32_t *right, const uint8_t *leaf_hash, const uint32_t *tree_begin,
+                             const uint8_t *root, size_t ncheck, const uint8_t *check, const uint32_t *check_begin,
+                             uint8_t *verdict, uint8_t *status) {
+    if (!ctx) return CV_E_ARGS;
+    if (ntrees == 0) return CV_OK;
+    if (!tree_begin || !check_begin || !root || !verdict) return CV_E_ARGS;
+    if (nnodes && (!kind || !left || !right || !leaf_hash)) return CV_E_ARGS;
+    if (ncheck && !check) return CV_E_ARGS;
+    if (ntrees > 0xfffffffeull || nnodes > 0xfffffffeull || ncheck > 0xfffffffeull) return CV_E_TOO_LARGE;
+    // the ranges must be well formed for the kernel to stay inside the buffers
+    if (tree_begin[0] != 0 || tree_begin[ntrees] != nnodes || check_begin[0] != 0 || check_begin[ntrees] != ncheck)
+        return CV_E_ARGS;
+    for (size_t t = 0; t < ntrees; t++)
+        if (tree_begin[t + 1] < tree_begin[t] || check_begin[t + 1] < check_begin[t]) return CV_E_ARGS;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    Device &d = ctx->devs[0];
+    CV_TRY(hipSetDevice(d.ordinal));
+    auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const size_t o_kind = 0, o_left = up16(o_kind + nnodes), o_right = up16(o_left + 4 * nnodes);
+    const size_t o_hash = up16(o_right + 4 * nnodes), o_tb = up16(o_hash + 32 * nnodes);
+    const size_t o_root = up16(o_tb + 4 * (ntrees + 1)), o_check = up16(o_root + 32 * ntrees);
+    const size_t o_cb = up16(o_check + 32 * ncheck), o_verdict = up16(o_cb + 4 * (ntrees + 1));
+    const size_t o_status = up16(o_verdict + ntrees), o_dig = up16(o_status + ntrees);
+    const size_t o_flag = up16(o_dig + 32 * nnodes), total = up16(o_flag + nnodes + 1);
+    CV_TRY(d.pmt.ensure(total));
+    uint8_t *base = d.pmt.as<uint8_t>();
+    hipStream_t s = d.stream;
+    if (nnodes) {
+        CV_TRY(hipMemcpyAsync(base + o_kind, kind, nnodes, hipMemcpyHostToDevice, s));
+        CV_TRY(hipMemcpyAsync(base + o_left, left, 4 * nnodes, hipMemcpyHostToDevice, s));
+        CV_TRY(hipMemcpyAsync(base + o_right, right, 4 * nnodes, hipMemcpyHostToDevice, s));
+        CV_TRY(hipMemcpyAsync(base + o_hash, leaf_hash, 32 * nnodes, hipMemcpyHostToDevice, s));
+    }
+    CV_TRY(hipMemcpyAsync(base + o_tb, tree_begin, 4 * (ntrees + 1), hipMemcpyHostToDevice, s));
+    CV_TRY(hipMemcpyAsync(base + o_root, root, 32 * ntrees, hipMemcpyHostToDevice, s));
+    if (ncheck) CV_TRY(hipMemcpyAsync(base + o_check, check, 32 * ncheck, hipMemcpyHostToDevice, s));
+    CV_TRY(hipMemcpyAsync(base + o_cb, check_begin, 4 * (ntrees + 1), hipMemcpyHostToDevice, s));
+    CV_TRY(cvk_pmt_verify((uint32_t)ntrees, base + o_kind, reinterpret_cast<uint32_t *>(base + o_left),
+                          reinterpret_cast<uint32_t *>(base + o_right), base + o_hash,
+                          reinterpret_cast<uint32_t *>(base + o_tb), base + o_root, base + o_check,
+                          reinterpret_cast<uint32_t *>(base + o_cb), reinterpret_cast<uint32_t *>(base + o_dig),
+                          base + o_flag, base + o_verdict, base + o_status, s));
+    CV_TRY(hipMemcpyAsync(verdict, base + o_verdict, ntrees, hipMemcpyDeviceToHost, s));
+    if (status) CV_TRY(hipMemcpyAsync(status, base + o_status, ntrees, hipMemcpyDeviceToHost, s));
     CV_TRY(hipStreamSynchronize(s));
     return CV_OK;
 }

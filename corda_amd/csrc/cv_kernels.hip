@@ -334,6 +334,27 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_merkle_tree_kernel(uint32_t ntx, 
     if (status) status[gid] = ok ? 0 : 1;
 }
 
+// ---------------------------------------------------------------- partial Merkle trees (f3)
+// one lane per tree (FilteredTransaction.verify / PartialMerkleTree.verify, cv_verify.h)
+__global__ __launch_bounds__(CV_BLOCK) void cv_pmt_verify_kernel(uint32_t ntrees, const uint8_t *__restrict__ kind,
+                                                                 const uint32_t *__restrict__ left,
+                                                                 const uint32_t *__restrict__ right,
+                                                                 const uint8_t *__restrict__ leaf_hash,
+                                                                 const uint32_t *__restrict__ tree_begin,
+                                                                 const uint8_t *__restrict__ root,
+                                                                 const uint8_t *__restrict__ check,
+                                                                 const uint32_t *__restrict__ check_begin,
+                                                                 uint32_t *__restrict__ dig, uint8_t *__restrict__ flag,
+                                                                 uint8_t *__restrict__ verdict, uint8_t *__restrict__ status) {
+    const uint32_t t = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (t >= ntrees) return;
+    bool v = false;
+    const int st = cv_pmt_verify(tree_begin[t], tree_begin[t + 1], kind, left, right, leaf_hash, root + 32 * (size_t)t,
+                                 check, check_begin[t], check_begin[t + 1], dig, flag, v);
+    verdict[t] = v ? 1 : 0;
+    status[t] = (uint8_t)st;
+}
+
 // ---------------------------------------------------------------- launchers (internal ABI)
 extern "C" {
 
@@ -460,6 +481,16 @@ hipError_t cvk_sign(uint32_t n, const uint8_t *seed, const uint8_t *arena, const
     if (n == 0) return hipSuccess;
     const uint32_t blocks = (n + CV_BLOCK - 1) / CV_BLOCK;
     hipLaunchKernelGGL(cv_sign_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, n, seed, arena, off, len, pk, sig);
+    return hipGetLastError();
+}
+
+hipError_t cvk_pmt_verify(uint32_t ntrees, const uint8_t *kind, const uint32_t *left, const uint32_t *right,
+                          const uint8_t *leaf_hash, const uint32_t *tree_begin, const uint8_t *root, const uint8_t *check,
+                          const uint32_t *check_begin, uint32_t *dig, uint8_t *flag, uint8_t *verdict, uint8_t *status,
+                          hipStream_t stream) {
+    if (ntrees == 0) return hipSuccess;
+    hipLaunchKernelGGL(cv_pmt_verify_kernel, dim3((ntrees + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, stream, ntrees,
+                       kind, left, right, leaf_hash, tree_begin, root, check, check_begin, dig, flag, verdict, status);
     return hipGetLastError();
 }
 

@@ -672,3 +672,80 @@ __host__ __device__ __forceinline__ bool cv_verify_one_hs(const uint32_t *bcomb,
         for (int q = 0; q < CV_HS_DIGWORDS; q++) dig_out[q] = dig[q];
     return key_ok && r_ok && eq;
 }
+
+// ---------------------------------------------------------------- partial Merkle tree verify (f3)
+// PartialMerkleTree.verify (core/src/main/kotlin/net/corda/core/crypto/PartialMerkleTree.kt:117-144)
+// over the flat encoding of include/cordaverify.h (cv_partial_merkle_verify): nodes [b, e) of one
+// tree, kind 0 Leaf / 1 IncludedLeaf / 2 Node, children (absolute indices) before their parent,
+// root = node e-1.  The root is recomputed bottom-up with hashConcat = SHA-256(left32 || right32);
+// the included-leaf hashes must equal the check list as a multiset (the reference's groupBy
+// compare); verdict = multiset equal AND root equal.  Workspace: dig (8 words per node), flag (one
+// byte per node: bit 0 referenced as a child, bit 1 matched by a check hash).  Returns 0, or 2 when
+// [b, e) is not a tree encoding (empty, unknown kind, child not before its parent or outside the
+// tree, a node referenced twice or never): verdict false.
+#define CV_PMT_LEAF 0
+#define CV_PMT_INCLUDED 1
+#define CV_PMT_NODE 2
+
+CV_HD void cv_load_digest(uint32_t d[8], const uint8_t *p) {
+#pragma unroll
+    for (int q = 0; q < 8; q++)
+        d[q] = ((uint32_t)p[4 * q] << 24) | ((uint32_t)p[4 * q + 1] << 16) | ((uint32_t)p[4 * q + 2] << 8) | p[4 * q + 3];
+}
+
+__host__ __device__ inline int cv_pmt_verify(uint32_t b, uint32_t e, const uint8_t *kind, const uint32_t *left,
+                                             const uint32_t *right, const uint8_t *leaf_hash, const uint8_t *root,
+                                             const uint8_t *check, uint32_t cb, uint32_t ce, uint32_t *dig,
+                                             uint8_t *flag, bool &verdict) {
+    verdict = false;
+    if (e <= b) return 2;
+    for (uint32_t k = b; k < e; k++) flag[k] = 0;
+    uint32_t n_incl = 0;
+    for (uint32_t k = b; k < e; k++) {
+        const uint8_t kd = kind[k];
+        uint32_t o[8];
+        if (kd == CV_PMT_NODE) {
+            const uint32_t l = left[k], r = right[k];
+            if (l < b || l >= k || r < b || r >= k || l == r) return 2;
+            if ((flag[l] | flag[r]) & 1u) return 2;
+            flag[l] |= 1u;
+            flag[r] |= 1u;
+            uint32_t lw[8], rw[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) { lw[q] = dig[8 * (size_t)l + q]; rw[q] = dig[8 * (size_t)r + q]; }
+            sha256_node(o, lw, rw);
+        } else if (kd == CV_PMT_LEAF || kd == CV_PMT_INCLUDED) {
+            cv_load_digest(o, leaf_hash + 32 * (size_t)k);
+            n_incl += kd == CV_PMT_INCLUDED;
+        } else {
+            return 2;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++) dig[8 * (size_t)k + q] = o[q];
+    }
+    for (uint32_t k = b; k + 1 < e; k++)
+        if (!(flag[k] & 1u)) return 2;                 // every node but the root has a parent
+    if (ce - cb != n_incl) return 0;
+    for (uint32_t j = cb; j < ce; j++) {
+        uint32_t c[8];
+        cv_load_digest(c, check + 32 * (size_t)j);
+        bool found = false;
+        for (uint32_t k = b; k < e && !found; k++) {
+            if (kind[k] != CV_PMT_INCLUDED || (flag[k] & 2u)) continue;
+            uint32_t diff = 0;
+#pragma unroll
+            for (int q = 0; q < 8; q++) diff |= dig[8 * (size_t)k + q] ^ c[q];
+            if (diff == 0) {
+                flag[k] |= 2u;
+                found = true;
+            }
+        }
+        if (!found) return 0;
+    }
+    uint32_t rt[8], diff = 0;
+    cv_load_digest(rt, root);
+#pragma unroll
+    for (int q = 0; q < 8; q++) diff |= dig[8 * (size_t)(e - 1) + q] ^ rt[q];
+    verdict = diff == 0;
+    return 0;
+}

@@ -28,7 +28,7 @@ EXPORTED = (
     "cv_ed25519_verify_batch", "cv_merkle_tx_ids", "cv_merkle_tx_ids_ex", "cv_ed25519_sign_batch",
     "cv_tx_verdicts", "cv_ed25519_verify_device", "cv_ed25519_verify_device_timed", "cv_ed25519_sign_device", "cv_merkle_tx_ids_device",
     "cv_synchronize", "cv_calibrate", "cv_ed25519_verify_batch_keyed", "cv_key_cache_reserve", "cv_key_cache_stats",
-    "cv_ed25519_verify_device_keyed",
+    "cv_ed25519_verify_device_keyed", "cv_partial_merkle_verify",
 )
 
 
@@ -84,6 +84,8 @@ def load():
         lib.cv_merkle_tx_ids.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp]
         lib.cv_merkle_tx_ids.restype = ctypes.c_int
         lib.cv_merkle_tx_ids_ex.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]
+        lib.cv_partial_merkle_verify.argtypes = [_vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]
+        lib.cv_partial_merkle_verify.restype = ctypes.c_int
         lib.cv_merkle_tx_ids_ex.restype = ctypes.c_int
         lib.cv_ed25519_sign_batch.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]
         lib.cv_ed25519_sign_batch.restype = ctypes.c_int
@@ -256,6 +258,33 @@ class Engine:
             _check(self._lib.cv_merkle_tx_ids_ex(self._h, ntx, _p(arena), _p(leaf_off), _p(leaf_len),
                                                  _p(tx_leaf_begin), _p(ids), _p(st)), "cv_merkle_tx_ids_ex")
         return ids, st
+
+    def partial_merkle_verify(self, kind, left, right, leaf_hash, tree_begin, root, check, check_begin
+                              ) -> Tuple[np.ndarray, np.ndarray]:
+        """Flat partial Merkle trees (include/cordaverify.h) -> (verdict[ntrees], status[ntrees])."""
+        tree_begin = np.ascontiguousarray(tree_begin, dtype=np.uint32)
+        check_begin = np.ascontiguousarray(check_begin, dtype=np.uint32)
+        ntrees = tree_begin.shape[0] - 1
+        nnodes = int(tree_begin[-1]) if ntrees > 0 else 0
+        ncheck = int(check_begin[-1]) if ntrees > 0 else 0
+
+        def pad(a, dt, shape):
+            a = np.ascontiguousarray(a, dtype=dt)
+            return a if a.size else np.zeros(shape, dt)
+        kind = pad(kind, np.uint8, 1)
+        left = pad(left, np.uint32, 1)
+        right = pad(right, np.uint32, 1)
+        leaf_hash = pad(leaf_hash, np.uint8, (1, 32))
+        root = pad(root, np.uint8, (1, 32))
+        check = pad(check, np.uint8, (1, 32))
+        verdict = np.zeros(max(ntrees, 1), np.uint8)
+        status = np.zeros(max(ntrees, 1), np.uint8)
+        with self.mu:
+            _check(self._lib.cv_partial_merkle_verify(self._h, ntrees, nnodes, _p(kind), _p(left), _p(right),
+                                                      _p(leaf_hash), _p(tree_begin), _p(root), ncheck, _p(check),
+                                                      _p(check_begin), _p(verdict), _p(status)),
+                   "cv_partial_merkle_verify")
+        return verdict[:ntrees], status[:ntrees]
 
     # ------------------------------------------------------------ device-resident API
     def verify_device(self, device: int, n: int, d_pk: int, d_sig: int, d_arena: int, d_off: int, d_len: int,

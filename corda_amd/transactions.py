@@ -188,3 +188,177 @@ def verify_signatures_batch(stxs: Sequence[SignedTransaction], allowed_to_be_mis
         except Exception as e:  # noqa: BLE001 - mirrored reference exceptions
             out.append(e)
     return out
+
+
+# ---------------------------------------------------------------- filtered transactions
+# Prover side (host): the full MerkleTree with its DuplicatedLeaf marks and PartialMerkleTree.build
+# (MerkleTransaction.kt:49-101, PartialMerkleTree.kt:69-111) — object work the JVM does once per
+# tear-off.  Verifier side (GPU): PartialMerkleTree.verify for many trees in one call
+# (cv_partial_merkle_verify), the root recompute + multiset check of PartialMerkleTree.kt:117-144.
+def _hash_concat(a: bytes, b: bytes) -> bytes:
+    import hashlib
+    return hashlib.sha256(a + b).digest()
+
+
+class MerkleTree:
+    """MerkleTree.Leaf / Node / DuplicatedLeaf (MerkleTransaction.kt:49-57)."""
+    __slots__ = ("hash", "left", "right", "duplicated")
+
+    def __init__(self, h: SecureHash, left=None, right=None, duplicated: bool = False):
+        self.hash, self.left, self.right, self.duplicated = h, left, right, duplicated
+
+    @staticmethod
+    def get_merkle_tree(all_leaves_hashes: Sequence[SecureHash]) -> "MerkleTree":
+        """MerkleTree.getMerkleTree / buildMerkleTree (MerkleTransaction.kt:66-99)."""
+        lvl = [MerkleTree(h) for h in all_leaves_hashes]
+        if len(lvl) < 1:
+            raise MerkleTreeException("Cannot calculate Merkle root on empty hash list.")
+        while len(lvl) > 1:
+            n = len(lvl)
+            nxt = []
+            for i in range(0, n, 2):
+                left = lvl[i]
+                right = MerkleTree(lvl[n - 1].hash, duplicated=True) if i + 1 > n - 1 else lvl[i + 1]
+                nxt.append(MerkleTree(SecureHash(_hash_concat(left.hash.bytes, right.hash.bytes)), left, right))
+            lvl = nxt
+        return lvl[0]
+
+
+class PartialTree:
+    """PartialMerkleTree.PartialTree: IncludedLeaf / Leaf (hash set) or Node (children set)."""
+    __slots__ = ("hash", "included", "left", "right")
+
+    def __init__(self, h: Optional[SecureHash] = None, included: bool = False, left=None, right=None):
+        self.hash, self.included, self.left, self.right = h, included, left, right
+
+
+class PartialMerkleTree:
+    LEAF, INCLUDED, NODE = 0, 1, 2
+
+    def __init__(self, root: PartialTree):
+        self.root = root
+
+    @staticmethod
+    def build(merkle_root: MerkleTree, include_hashes: Sequence[SecureHash]) -> "PartialMerkleTree":
+        """PartialMerkleTree.build (PartialMerkleTree.kt:69-111)."""
+        include = list(include_hashes)
+        used: List[SecureHash] = []
+
+        def rec(node: MerkleTree):
+            if node.left is None:
+                if not node.duplicated and node.hash in include:
+                    used.append(node.hash)
+                    return True, PartialTree(node.hash, included=True)
+                return False, PartialTree(node.hash)
+            lf, lt = rec(node.left)
+            rf, rt = rec(node.right)
+            if lf or rf:
+                return True, PartialTree(left=lt, right=rt)
+            return False, PartialTree(node.hash)
+
+        _, tree = rec(merkle_root)
+        if len(include) != len(used):
+            raise MerkleTreeException("Some of the provided hashes are not in the tree.")
+        return PartialMerkleTree(tree)
+
+    def flatten(self, base: int = 0):
+        """Post-order flat encoding of include/cordaverify.h (absolute indices from `base`)."""
+        kind: List[int] = []
+        left: List[int] = []
+        right: List[int] = []
+        hashes: List[bytes] = []
+
+        def rec(n: PartialTree) -> int:
+            if n.left is not None:
+                li, ri = rec(n.left), rec(n.right)
+                kind.append(self.NODE); left.append(li); right.append(ri); hashes.append(bytes(32))
+            else:
+                kind.append(self.INCLUDED if n.included else self.LEAF)
+                left.append(0); right.append(0); hashes.append(n.hash.bytes)
+            return base + len(kind) - 1
+
+        rec(self.root)
+        return kind, left, right, hashes
+
+    def verify(self, merkle_root_hash: SecureHash, hashes_to_check: Sequence[SecureHash],
+               engine: Optional[native.Engine] = None) -> bool:
+        """PartialMerkleTree.verify (PartialMerkleTree.kt:117-124), on the GPU."""
+        return verify_partial_trees([(self, merkle_root_hash, list(hashes_to_check))], engine)[0]
+
+
+def verify_partial_trees(items, engine: Optional[native.Engine] = None) -> List[bool]:
+    """Many PartialMerkleTree.verify(root, hashesToCheck) in ONE GPU call.  items: (pmt, root, hashes)."""
+    kind: List[int] = []
+    left: List[int] = []
+    right: List[int] = []
+    hashes: List[bytes] = []
+    tb, cb = [0], [0]
+    roots: List[bytes] = []
+    checks: List[bytes] = []
+    for pmt, root, hs in items:
+        k, l, r, h = pmt.flatten(len(kind))
+        kind += k; left += l; right += r; hashes += h
+        tb.append(len(kind))
+        roots.append(root.bytes)
+        checks += [x.bytes for x in hs]
+        cb.append(len(checks))
+    eng = engine or native.default_engine()
+    v, st = eng.partial_merkle_verify(np.array(kind, np.uint8), np.array(left, np.uint32), np.array(right, np.uint32),
+                                      np.frombuffer(b"".join(hashes), np.uint8).reshape(-1, 32),
+                                      np.array(tb, np.uint32), np.frombuffer(b"".join(roots), np.uint8).reshape(-1, 32),
+                                      np.frombuffer(b"".join(checks), np.uint8).reshape(-1, 32) if checks
+                                      else np.zeros((0, 32), np.uint8), np.array(cb, np.uint32))
+    if (st != 0).any():
+        raise IllegalArgumentException("malformed partial Merkle tree encoding")
+    return [bool(x) for x in v]
+
+
+class FilteredLeaves:
+    """FilteredLeaves (MerkleTransaction.kt:105-119): the serialized leaves kept in the tear-off."""
+
+    def __init__(self, inputs: Sequence[bytes] = (), outputs: Sequence[bytes] = (), attachments: Sequence[bytes] = (),
+                 commands: Sequence[bytes] = ()):
+        self.inputs, self.outputs = list(inputs), list(outputs)
+        self.attachments, self.commands = list(attachments), list(commands)
+
+    def get_filtered_hashes(self) -> List[SecureHash]:
+        import hashlib
+        return [SecureHash(hashlib.sha256(b).digest())
+                for b in self.inputs + self.outputs + self.attachments + self.commands]
+
+
+class FilteredTransaction:
+    """FilteredTransaction (MerkleTransaction.kt:146-178)."""
+
+    def __init__(self, filtered_leaves: FilteredLeaves, partial_merkle_tree: PartialMerkleTree):
+        self.filtered_leaves = filtered_leaves
+        self.partial_merkle_tree = partial_merkle_tree
+
+    @staticmethod
+    def build_merkle_transaction(wtx: WireTransaction, filter_inputs=lambda b: False, filter_outputs=lambda b: False,
+                                 filter_attachments=lambda b: False, filter_commands=lambda b: False
+                                 ) -> "FilteredTransaction":
+        """FilteredTransaction.buildMerkleTransaction with FilterFuns over the serialized leaves."""
+        import hashlib
+        fl = FilteredLeaves([x for x in wtx.inputs if filter_inputs(x)], [x for x in wtx.outputs if filter_outputs(x)],
+                            [x for x in wtx.attachments if filter_attachments(x)],
+                            [x for x in wtx.commands if filter_commands(x)])
+        full = MerkleTree.get_merkle_tree([SecureHash(hashlib.sha256(b).digest()) for b in wtx.leaves])
+        return FilteredTransaction(fl, PartialMerkleTree.build(full, fl.get_filtered_hashes()))
+
+    def verify(self, merkle_root_hash: SecureHash, engine: Optional[native.Engine] = None) -> bool:
+        hashes = self.filtered_leaves.get_filtered_hashes()
+        if len(hashes) == 0:
+            raise MerkleTreeException("Transaction without included leaves.")
+        return self.partial_merkle_tree.verify(merkle_root_hash, hashes, engine)
+
+
+def verify_filtered_batch(items, engine: Optional[native.Engine] = None) -> List[bool]:
+    """FilteredTransaction.verify(root) for many tear-offs in one GPU call.  items: (ftx, root)."""
+    batch = []
+    for ftx, root in items:
+        hashes = ftx.filtered_leaves.get_filtered_hashes()
+        if len(hashes) == 0:
+            raise MerkleTreeException("Transaction without included leaves.")
+        batch.append((ftx.partial_merkle_tree, root, hashes))
+    return verify_partial_trees(batch, engine)

@@ -23,6 +23,10 @@
  *                                 generate synthetic workloads, not on the validation path)
  *   cv_tx_verdicts            per-transaction AND of signature verdicts (the "all sigs valid" half of
  *                                 SignedTransaction.verifySignatures, SignedTransaction.kt:58-72)
+ *   cv_partial_merkle_verify  N x  PartialMerkleTree.verify(merkleRootHash, hashesToCheck)
+ *                                 core/src/main/kotlin/net/corda/core/crypto/PartialMerkleTree.kt:117-144
+ *                             behind FilteredTransaction.verify (MerkleTransaction.kt:170-178; the
+ *                             oracle tear-off check of NodeInterestRates.kt:189-191)
  *
  * Conventions
  *   - Return codes: CV_OK (0) or a negative CV_E* code; nothing throws, aborts or longjmps across
@@ -102,6 +106,27 @@ int cv_merkle_tx_ids(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const u
 /* as cv_merkle_tx_ids, with per-transaction status (CV_TX_OK / CV_TX_EMPTY) */
 int cv_merkle_tx_ids_ex(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
                         const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, uint8_t *ids, uint8_t *tx_status);
+
+/* Partial Merkle trees (FilteredTransaction / PartialMerkleTree.verify), one verdict per tree.
+ * The shim flattens each PartialTree object in post-order and concatenates the trees: node k has
+ * kind[k] (CV_PMT_LEAF 0 = PartialTree.Leaf, CV_PMT_INCLUDED 1 = IncludedLeaf, CV_PMT_NODE 2 = Node),
+ * for a Node left[k] / right[k] = absolute indices of its children (smaller than k, inside the same
+ * tree), for a leaf leaf_hash[k][32] = its SecureHash bytes; tree t is nodes
+ * [tree_begin[t], tree_begin[t+1]) with its root last.  root[t][32] = merkleRootHash, the
+ * hashesToCheck of tree t are check[check_begin[t] .. check_begin[t+1]).
+ * verdict[t] = 1 iff hashConcat recomputation gives root[t] AND the IncludedLeaf hashes equal the
+ * check hashes as a multiset (the reference's groupBy compare).  status[t] (optional) = CV_PMT_OK,
+ * or CV_PMT_MALFORMED when the nodes are not a tree encoding (verdict 0; the shim throws
+ * IllegalArgumentException).  FilteredTransaction.verify's empty-check MerkleTreeException stays in
+ * the shim. */
+#define CV_PMT_OK 0
+#define CV_PMT_MALFORMED 2
+int cv_partial_merkle_verify(cv_ctx *ctx, size_t ntrees, size_t nnodes, const uint8_t *kind, const uint32_t *left,
+                             const uint32_t *right, const uint8_t *leaf_hash /* nnodes*32 */,
+                             const uint32_t *tree_begin /* ntrees+1 */, const uint8_t *root /* ntrees*32 */,
+                             size_t ncheck, const uint8_t *check /* ncheck*32 */,
+                             const uint32_t *check_begin /* ntrees+1 */, uint8_t *verdict /* ntrees */,
+                             uint8_t *status /* ntrees, optional */);
 
 int cv_ed25519_sign_batch(cv_ctx *ctx, size_t n, const uint8_t *seed /* n*32 */, const uint8_t *msg_arena,
                           const uint64_t *msg_off, const uint32_t *msg_len, uint8_t *pk_out /* n*32 */,

@@ -270,4 +270,14 @@ int cvh_halfsize(const uint8_t *h, const uint8_t *s, uint8_t *out, int *v_neg, i
     return ok ? 1 : 0;
 }
 
+// PartialMerkleTree.verify of tree t of a flat batch (cv_pmt_verify); returns status, *verdict.
+int cvh_pmt_verify(uint32_t b, uint32_t e, const uint8_t *kind, const uint32_t *left, const uint32_t *right,
+                   const uint8_t *leaf_hash, const uint8_t *root, const uint8_t *check, uint32_t cb, uint32_t ce,
+                   uint32_t *dig, uint8_t *flag, int *verdict) {
+    bool v = false;
+    const int st = cv_pmt_verify(b, e, kind, left, right, leaf_hash, root, check, cb, ce, dig, flag, v);
+    *verdict = v ? 1 : 0;
+    return st;
+}
+
 }  // extern "C"
