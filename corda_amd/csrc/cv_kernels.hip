@@ -132,6 +132,26 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsprep_kernel(uint32_t n, uint
     if (!r_ok) ws_ok[i] = 0;
 }
 
+// fused half-size prep (cv_hs_prep_fused): hash, scalars, lattice + digits, A and R decoded as one
+// interleaved pair, both odd-multiple tables; ws_ok = key_ok AND r_ok, status = key status.
+__global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsfused_prep_kernel(
+    uint32_t n, uint32_t cap, const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig,
+    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ off, const uint32_t *__restrict__ len,
+    uint32_t *__restrict__ ws_dig, uint32_t *__restrict__ ws_tab, uint32_t *__restrict__ ws_tabR,
+    uint8_t *__restrict__ ws_ok, uint8_t *__restrict__ status) {
+    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    uint32_t aw[8], rw[8], sw[8];
+    load_words8(aw, pk + (size_t)i * 32);
+    load_words8(rw, sig + (size_t)i * 64);
+    load_words8(sw, sig + (size_t)i * 64 + 32);
+    bool ok = false;
+    const bool key_ok = cv_hs_prep_fused(aw, rw, sw, arena + off[i], len[i], ws_dig + i, cap,
+                                         ws_tab + (size_t)i * CV_TAB_WORDS, ws_tabR + (size_t)i * CV_TAB_WORDS, ok);
+    ws_ok[i] = ok ? 1 : 0;
+    if (status) status[i] = key_ok ? 0 : 1;
+}
+
 // hs_straus: E = [v]R + [u]A + [w]B per lane over the wave's largest window count, the identity
 // test, and the verdict word by wave ballot (bit i of word i/64 = signature i).  Lanes past n
 // replay signature n-1 so the whole wave takes part in the window-count reduction.
@@ -182,6 +202,9 @@ extern "C" void cvk_set_hs_waves(int w) { g_hs_waves = (w == 2) ? 2 : 3; }
 static int g_prep_lat = 0, g_hsprep_lat = 0;
 // 0 = skip the lattice reduction ((u, v) = (h, 1), 64 windows: still exact) — A/B timing only
 static int g_hs_reduce = 1;
+// 1 = one fused prep kernel (interleaved A/R decodes), 0 = prep + hsprep
+static int g_hs_fused = 1;
+extern "C" void cvk_set_hs_fused(int v) { g_hs_fused = v ? 1 : 0; }
 extern "C" void cvk_set_hs_reduce(int v) { g_hs_reduce = v ? 1 : 0; }
 extern "C" void cvk_set_prep_lat(int v) { g_prep_lat = v ? 1 : 0; }
 extern "C" void cvk_set_hsprep_lat(int v) { g_hsprep_lat = v ? 1 : 0; }
@@ -374,6 +397,23 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
         // ev (optional, single-chunk batches): phase boundaries for live per-kernel timing
         if (ev && c0 == 0) (void)hipEventRecord(ev[0], stream);
         const bool lat = n <= g_quad_max;   // small batch: latency forms of the single chains
+        if (!lat && g_verify_mode == 1 && g_hs_fused) {
+            // fused half-size group: phases = fused prep | (empty) | hs_straus
+            uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
+            hipLaunchKernelGGL(cv_hsfused_prep_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap,
+                               pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_dig, ws_tab,
+                               ws_tabR, ws_ok, status ? status + c0 : nullptr);
+            if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);
+            if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
+            if (g_hs_waves == 2)
+                hipLaunchKernelGGL(cv_hs_straus_kernel<2>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, ws_dig,
+                                   ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
+            else
+                hipLaunchKernelGGL(cv_hs_straus_kernel<3>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, ws_dig,
+                                   ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
+            if (ev && c0 == 0) (void)hipEventRecord(ev[3], stream);
+            continue;
+        }
         if (lat || g_prep_lat)
             hipLaunchKernelGGL(cv_prep_kernel<true>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, pk + (size_t)c0 * 32,
                                sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_hs, ws_tab, ws_ok,

@@ -749,3 +749,62 @@ __host__ __device__ inline int cv_pmt_verify(uint32_t b, uint32_t e, const uint8
     verdict = diff == 0;
     return 0;
 }
+
+// ---------------------------------------------------------------- fused half-size prep
+// cv_verify_prep + cv_hs_prep in one pass: hash and scalars, lattice + packed digits, then the A and
+// R decodes interleaved (ge_decode2_0_1_0), then the two odd-multiple tables.  ok_out = key_ok AND
+// r_ok (the verdict mask); returns key_ok (the status byte).
+__host__ __device__ __forceinline__ bool cv_hs_prep_fused(const uint32_t aw[8], const uint32_t rw[8], const uint32_t sw[8],
+                                                          const uint8_t *msg, uint32_t mlen, uint32_t *dig, size_t stride,
+                                                          uint32_t *tabA, uint32_t *tabR, bool &ok_out) {
+    {
+        uint32_t hs[CV_HS_WORDS];
+        cv_keyed_hs(aw, rw, sw, msg, mlen, hs);            // h = SHA-512(R || Abyte || M) mod L, effective s
+        uint32_t h[8], s[8], u[8], v[8], w[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) { h[q] = hs[q]; s[q] = hs[8 + q]; }
+        bool v_neg;
+        int nwin;
+        sc_halfsize(u, v, v_neg, nwin, w, h, s);
+#pragma unroll 4
+        for (int win = 0; win < 64; win++) {
+            const int da = -digit16(u, win), dr = v_neg ? -digit16(v, win) : digit16(v, win);
+            const bool bw = (win & 1) == 0 && win < 32;
+            const int dlo = bw ? digit256(w, win >> 1) : 0, dhi = bw ? digit256(w, 16 + (win >> 1)) : 0;
+            dig[(size_t)win * stride] = ((uint32_t)da & 0x1fu) | (((uint32_t)dr & 0x1fu) << 5) |
+                                        (((uint32_t)dlo & 0x1ffu) << 10) | (((uint32_t)dhi & 0x1ffu) << 19);
+        }
+        dig[64 * stride] = (uint32_t)nwin;
+    }
+    ge_p3 P[2];
+    bool ok[2];
+    ge_decode2_0_1_0(P, ok, aw, rw);
+    uint32_t enc[8], diff = 0;
+    ge_abyte_from_key(enc, rw);                            // R canonical: its bytes re-encode to themselves
+#pragma unroll
+    for (int q = 0; q < 8; q++) diff |= enc[q] ^ rw[q];
+    const bool key_ok = ok[0], r_ok = ok[1] && diff == 0;
+    if (!key_ok) ge_p3_identity(P[0]);
+    if (!r_ok) ge_p3_identity(P[1]);
+    ge_p3 nA;
+    ge_p3_neg(nA, P[0]);
+    ge_cached_multiples8(tabA, nA);
+    ge_cached_multiples8(tabR, P[1]);
+    ok_out = key_ok && r_ok;
+    return key_ok;
+}
+
+// Single-signature convenience of the fused schedule (host harness).
+__host__ __device__ __forceinline__ bool cv_verify_one_hs_fused(const uint32_t *bcomb, const uint32_t aw[8],
+                                                                const uint32_t rw[8], const uint32_t sw[8],
+                                                                const uint8_t *msg, uint32_t mlen, bool *key_ok_out) {
+    alignas(16) uint32_t tab[CV_TAB_WORDS];
+    alignas(16) uint32_t tabR[CV_TAB_WORDS];
+    uint32_t dig[CV_HS_DIGWORDS];
+    bool ok = false;
+    *key_ok_out = cv_hs_prep_fused(aw, rw, sw, msg, mlen, dig, 1, tab, tabR, ok);
+    int nw = (int)dig[64];
+    if (nw < 32) nw = 32;
+    const bool eq = cv_hs_straus(bcomb, bcomb + 2 * CV_BTAB_ENTRIES * CV_BTAB_STRIDE, dig, 1, tab, tabR, nw);
+    return ok && eq;
+}
