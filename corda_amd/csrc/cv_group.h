@@ -206,45 +206,63 @@ template <bool LAT = false> __host__ __device__ __forceinline__ bool ge_decode_0
 // fused half-size prep): every field operation of the two square-root chains runs as a 2-way
 // interleaved pair (fe_mul_n<2> / fe_sq_n<2>), which doubles the independent work per instruction
 // window of a lane at the same instruction count.
-__host__ __device__ __forceinline__ void fe_sqn2(fe (&h)[2], const fe (&f)[2], int n) {
+// LAT = true: each element by the latency (ILP) forms instead (small batches, lone waves).
+template <bool LAT = false> CV_HD void fe_sq2(fe (&h)[2], const fe (&f)[2]) {
+    if constexpr (LAT) {
+        fe_sq_ilp(h[0], f[0], false);
+        fe_sq_ilp(h[1], f[1], false);
+    } else {
+        fe_sq_n<2, 0>(h, f);
+    }
+}
+template <bool LAT = false> __host__ __device__ __forceinline__ void fe_sqn2(fe (&h)[2], const fe (&f)[2], int n) {
 #ifdef __HIP_DEVICE_COMPILE__
     asm volatile("" : "+s"(n));
 #endif
-    fe_sq_n<2, 0>(h, f);
+    fe_sq2<LAT>(h, f);
 #pragma nounroll
-    for (int i = 1; i < n; i++) fe_sq_n<2, 0>(h, h);
+    for (int i = 1; i < n; i++) fe_sq2<LAT>(h, h);
 }
-CV_HD void fe_mul2(fe (&h)[2], const fe &f0, const fe &g0, const fe &f1, const fe &g1) {
-    const fe f[2] = {f0, f1}, g[2] = {g0, g1};
-    fe_mul_n<2>(h, f, g);
+template <bool LAT = false> CV_HD void fe_mul2(fe (&h)[2], const fe &f0, const fe &g0, const fe &f1, const fe &g1) {
+    if constexpr (LAT) {
+        fe a, b;
+        fe_mul_ilp(a, f0, g0);
+        fe_mul_ilp(b, f1, g1);
+        h[0] = a;
+        h[1] = b;
+    } else {
+        const fe f[2] = {f0, f1}, g[2] = {g0, g1};
+        fe_mul_n<2>(h, f, g);
+    }
 }
 // z^(2^252 - 3) for two elements
-__host__ __device__ __forceinline__ void fe_pow22523_2(fe (&out)[2], const fe (&z)[2]) {
+template <bool LAT = false> __host__ __device__ __forceinline__ void fe_pow22523_2(fe (&out)[2], const fe (&z)[2]) {
     fe t0[2], t1[2], t2[2];
-    fe_sq_n<2, 0>(t0, z);                                  // z^2
-    fe_sqn2(t1, t0, 2);                                    // z^8
-    fe_mul2(t1, z[0], t1[0], z[1], t1[1]);                 // z^9
-    fe_mul2(t0, t0[0], t1[0], t0[1], t1[1]);               // z^11
-    fe_sq_n<2, 0>(t0, t0);                                 // z^22
-    fe_mul2(t0, t1[0], t0[0], t1[1], t0[1]);               // z^31
-    fe_sqn2(t1, t0, 5);
-    fe_mul2(t0, t1[0], t0[0], t1[1], t0[1]);               // 2^10 - 1
-    fe_sqn2(t1, t0, 10);
-    fe_mul2(t1, t1[0], t0[0], t1[1], t0[1]);               // 2^20 - 1
-    fe_sqn2(t2, t1, 20);
-    fe_mul2(t1, t2[0], t1[0], t2[1], t1[1]);               // 2^40 - 1
-    fe_sqn2(t1, t1, 10);
-    fe_mul2(t0, t1[0], t0[0], t1[1], t0[1]);               // 2^50 - 1
-    fe_sqn2(t1, t0, 50);
-    fe_mul2(t1, t1[0], t0[0], t1[1], t0[1]);               // 2^100 - 1
-    fe_sqn2(t2, t1, 100);
-    fe_mul2(t1, t2[0], t1[0], t2[1], t1[1]);               // 2^200 - 1
-    fe_sqn2(t1, t1, 50);
-    fe_mul2(t0, t1[0], t0[0], t1[1], t0[1]);               // 2^250 - 1
-    fe_sqn2(t0, t0, 2);                                    // 2^252 - 4
-    fe_mul2(out, t0[0], z[0], t0[1], z[1]);                // 2^252 - 3
+    fe_sq2<LAT>(t0, z);                                  // z^2
+    fe_sqn2<LAT>(t1, t0, 2);                                    // z^8
+    fe_mul2<LAT>(t1, z[0], t1[0], z[1], t1[1]);                 // z^9
+    fe_mul2<LAT>(t0, t0[0], t1[0], t0[1], t1[1]);               // z^11
+    fe_sq2<LAT>(t0, t0);                                 // z^22
+    fe_mul2<LAT>(t0, t1[0], t0[0], t1[1], t0[1]);               // z^31
+    fe_sqn2<LAT>(t1, t0, 5);
+    fe_mul2<LAT>(t0, t1[0], t0[0], t1[1], t0[1]);               // 2^10 - 1
+    fe_sqn2<LAT>(t1, t0, 10);
+    fe_mul2<LAT>(t1, t1[0], t0[0], t1[1], t0[1]);               // 2^20 - 1
+    fe_sqn2<LAT>(t2, t1, 20);
+    fe_mul2<LAT>(t1, t2[0], t1[0], t2[1], t1[1]);               // 2^40 - 1
+    fe_sqn2<LAT>(t1, t1, 10);
+    fe_mul2<LAT>(t0, t1[0], t0[0], t1[1], t0[1]);               // 2^50 - 1
+    fe_sqn2<LAT>(t1, t0, 50);
+    fe_mul2<LAT>(t1, t1[0], t0[0], t1[1], t0[1]);               // 2^100 - 1
+    fe_sqn2<LAT>(t2, t1, 100);
+    fe_mul2<LAT>(t1, t2[0], t1[0], t2[1], t1[1]);               // 2^200 - 1
+    fe_sqn2<LAT>(t1, t1, 50);
+    fe_mul2<LAT>(t0, t1[0], t0[0], t1[1], t0[1]);               // 2^250 - 1
+    fe_sqn2<LAT>(t0, t0, 2);                                    // 2^252 - 4
+    fe_mul2<LAT>(out, t0[0], z[0], t0[1], z[1]);                // 2^252 - 3
 }
 // ge_decode_0_1_0 of w[0] and w[1] together; ok[k] as ge_decode_0_1_0's return value.
+template <bool LAT = false>
 __host__ __device__ __forceinline__ void ge_decode2_0_1_0(ge_p3 (&P)[2], bool (&ok)[2], const uint32_t *w0,
                                                           const uint32_t *w1) {
     fe y[2], yy[2], u[2], v[2], v3[2], x[2], vxx[2], one, d;
@@ -252,23 +270,23 @@ __host__ __device__ __forceinline__ void ge_decode2_0_1_0(ge_p3 (&P)[2], bool (&
     fe_from_words(y[1], w1);
     fe_one(one);
     fe_const_d(d);
-    fe_sq_n<2, 0>(yy, y);
-    fe_mul2(v, yy[0], d, yy[1], d);
+    fe_sq2<LAT>(yy, y);
+    fe_mul2<LAT>(v, yy[0], d, yy[1], d);
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         fe_sub<2>(u[k], yy[k], one);       // u = y^2 - 1
         fe_add(v[k], v[k], one);           // v = d y^2 + 1
     }
-    fe_sq_n<2, 0>(v3, v);
-    fe_mul2(v3, v3[0], v[0], v3[1], v[1]);                 // v^3
-    fe_sq_n<2, 0>(x, v3);
-    fe_mul2(x, x[0], v[0], x[1], v[1]);
-    fe_mul2(x, x[0], u[0], x[1], u[1]);                    // u v^7
-    fe_pow22523_2(x, x);
-    fe_mul2(x, x[0], v3[0], x[1], v3[1]);
-    fe_mul2(x, x[0], u[0], x[1], u[1]);                    // u v^3 (u v^7)^((p-5)/8)
-    fe_sq_n<2, 0>(vxx, x);
-    fe_mul2(vxx, vxx[0], v[0], vxx[1], v[1]);
+    fe_sq2<LAT>(v3, v);
+    fe_mul2<LAT>(v3, v3[0], v[0], v3[1], v[1]);                 // v^3
+    fe_sq2<LAT>(x, v3);
+    fe_mul2<LAT>(x, x[0], v[0], x[1], v[1]);
+    fe_mul2<LAT>(x, x[0], u[0], x[1], u[1]);                    // u v^7
+    fe_pow22523_2<LAT>(x, x);
+    fe_mul2<LAT>(x, x[0], v3[0], x[1], v3[1]);
+    fe_mul2<LAT>(x, x[0], u[0], x[1], u[1]);                    // u v^3 (u v^7)^((p-5)/8)
+    fe_sq2<LAT>(vxx, x);
+    fe_mul2<LAT>(vxx, vxx[0], v[0], vxx[1], v[1]);
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         const uint32_t *w = k ? w1 : w0;
@@ -293,7 +311,7 @@ __host__ __device__ __forceinline__ void ge_decode2_0_1_0(ge_p3 (&P)[2], bool (&
         fe_one(P[k].Z);
     }
     fe T[2];
-    fe_mul2(T, x[0], y[0], x[1], y[1]);
+    fe_mul2<LAT>(T, x[0], y[0], x[1], y[1]);
     P[0].T = T[0];
     P[1].T = T[1];
 }

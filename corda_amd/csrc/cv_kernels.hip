@@ -20,6 +20,7 @@
 
 #include "cv_verify.h"
 #include "cv_quad.h"
+#include "cv_hsquad.h"
 
 #define CV_BLOCK 256
 
@@ -134,6 +135,7 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsprep_kernel(uint32_t n, uint
 
 // fused half-size prep (cv_hs_prep_fused): hash, scalars, lattice + digits, A and R decoded as one
 // interleaved pair, both odd-multiple tables; ws_ok = key_ok AND r_ok, status = key status.
+template <bool LAT>
 __global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsfused_prep_kernel(
     uint32_t n, uint32_t cap, const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig,
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ off, const uint32_t *__restrict__ len,
@@ -146,7 +148,7 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsfused_prep_kernel(
     load_words8(rw, sig + (size_t)i * 64);
     load_words8(sw, sig + (size_t)i * 64 + 32);
     bool ok = false;
-    const bool key_ok = cv_hs_prep_fused(aw, rw, sw, arena + off[i], len[i], ws_dig + i, cap,
+    const bool key_ok = cv_hs_prep_fused<LAT>(aw, rw, sw, arena + off[i], len[i], ws_dig + i, cap,
                                          ws_tab + (size_t)i * CV_TAB_WORDS, ws_tabR + (size_t)i * CV_TAB_WORDS, ok);
     ws_ok[i] = ok ? 1 : 0;
     if (status) status[i] = key_ok ? 0 : 1;
@@ -204,6 +206,9 @@ static int g_prep_lat = 0, g_hsprep_lat = 0;
 static int g_hs_reduce = 1;
 // 1 = one fused prep kernel (interleaved A/R decodes), 0 = prep + hsprep
 static int g_hs_fused = 1;
+// 1 = small batches (<= g_quad_max) run the half-size quad kernel, 0 = the full-width quad group
+static int g_hs_quad = 1;
+extern "C" void cvk_set_hs_quad(int v) { g_hs_quad = v ? 1 : 0; }
 extern "C" void cvk_set_hs_fused(int v) { g_hs_fused = v ? 1 : 0; }
 extern "C" void cvk_set_hs_reduce(int v) { g_hs_reduce = v ? 1 : 0; }
 extern "C" void cvk_set_prep_lat(int v) { g_prep_lat = v ? 1 : 0; }
@@ -236,6 +241,38 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_comb_quad_kernel(uint32_t n, cons
     fe P;
     cv_quad_comb(CV_BCOMB, ws_hs + (size_t)i * CV_HS_WORDS, ktab_pool + (size_t)slot * CV_KTAB_WORDS, r, P);
     if (r < 3) fe_store(ws_R + (size_t)i * CV_R_WORDS + 10 * r, P);
+}
+
+// Half-size quad kernel (cv_hsquad.h): grid 4n lanes.  The chunk's bitmap words must be zero on
+// entry (the launcher clears them): each wave ORs its 16 verdict bits into its word.  Quads past n
+// replay signature n-1 (whole waves take part in the window-count reduction) and add no bits.
+__global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_quad_kernel(uint32_t n, uint32_t cap,
+                                                                     const uint32_t *__restrict__ ws_dig,
+                                                                     const uint32_t *__restrict__ ws_tab,
+                                                                     const uint32_t *__restrict__ ws_tabR,
+                                                                     const uint8_t *__restrict__ ws_ok,
+                                                                     uint64_t *__restrict__ bitmap) {
+    constexpr int ROW = CV_BTAB_ENTRIES * CV_BTAB_STRIDE;
+    const uint32_t lane0 = blockIdx.x * CV_BLOCK + (threadIdx.x & ~63u);
+    const uint32_t sig0 = lane0 >> 2;                        // first signature of this wave
+    if (sig0 >= n) return;                                   // whole waves leave together
+    const uint32_t i0 = (blockIdx.x * CV_BLOCK + threadIdx.x) >> 2;
+    const int r = threadIdx.x & 3;
+    const uint32_t i = i0 < n ? i0 : n - 1;
+    int nw = (int)ws_dig[(size_t)64 * cap + i];
+    nw = nw < 32 ? 32 : nw;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const int x = __shfl_xor(nw, o);
+        nw = x > nw ? x : nw;
+    }
+    nw = __builtin_amdgcn_readfirstlane(nw);
+    const bool eq = cv_quad_hs_straus(CV_BCOMB, CV_BCOMB + 2 * ROW, ws_dig + i, cap, ws_tab + (size_t)i * CV_TAB_WORDS,
+                                      ws_tabR + (size_t)i * CV_TAB_WORDS, nw, r);
+    const bool acc = eq && ws_ok[i] && i0 < n;
+    const uint32_t bits = cv_quad_ballot_bits(__ballot(acc));
+    if ((threadIdx.x & 63u) == 0 && bits)
+        atomicOr(reinterpret_cast<unsigned long long *>(bitmap + (sig0 >> 6)), (unsigned long long)bits << (sig0 & 63u));
 }
 
 // Batches of at most this many signatures run the quad kernels (set by cvk_set_quad_max; 0 = never)
@@ -397,10 +434,24 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
         // ev (optional, single-chunk batches): phase boundaries for live per-kernel timing
         if (ev && c0 == 0) (void)hipEventRecord(ev[0], stream);
         const bool lat = n <= g_quad_max;   // small batch: latency forms of the single chains
+        if (lat && g_verify_mode == 1 && g_hs_quad) {
+            // half-size quad group: phases = fused prep | bitmap clear | hs_straus_quad
+            uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
+            hipLaunchKernelGGL(cv_hsfused_prep_kernel<true>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap,
+                               pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_dig, ws_tab,
+                               ws_tabR, ws_ok, status ? status + c0 : nullptr);
+            if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);
+            (void)hipMemsetAsync(bitmap + (size_t)c0 / 64, 0, (size_t)((m + 63) / 64) * 8, stream);
+            if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
+            hipLaunchKernelGGL(cv_hs_straus_quad_kernel, dim3((4 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
+                               stream, m, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
+            if (ev && c0 == 0) (void)hipEventRecord(ev[3], stream);
+            continue;
+        }
         if (!lat && g_verify_mode == 1 && g_hs_fused) {
             // fused half-size group: phases = fused prep | (empty) | hs_straus
             uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
-            hipLaunchKernelGGL(cv_hsfused_prep_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap,
+            hipLaunchKernelGGL(cv_hsfused_prep_kernel<false>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap,
                                pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_dig, ws_tab,
                                ws_tabR, ws_ok, status ? status + c0 : nullptr);
             if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);

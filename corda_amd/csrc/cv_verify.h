@@ -754,6 +754,7 @@ __host__ __device__ inline int cv_pmt_verify(uint32_t b, uint32_t e, const uint8
 // cv_verify_prep + cv_hs_prep in one pass: hash and scalars, lattice + packed digits, then the A and
 // R decodes interleaved (ge_decode2_0_1_0), then the two odd-multiple tables.  ok_out = key_ok AND
 // r_ok (the verdict mask); returns key_ok (the status byte).
+template <bool LAT = false>
 __host__ __device__ __forceinline__ bool cv_hs_prep_fused(const uint32_t aw[8], const uint32_t rw[8], const uint32_t sw[8],
                                                           const uint8_t *msg, uint32_t mlen, uint32_t *dig, size_t stride,
                                                           uint32_t *tabA, uint32_t *tabR, bool &ok_out) {
@@ -778,7 +779,7 @@ __host__ __device__ __forceinline__ bool cv_hs_prep_fused(const uint32_t aw[8], 
     }
     ge_p3 P[2];
     bool ok[2];
-    ge_decode2_0_1_0(P, ok, aw, rw);
+    ge_decode2_0_1_0<LAT>(P, ok, aw, rw);
     uint32_t enc[8], diff = 0;
     ge_abyte_from_key(enc, rw);                            // R canonical: its bytes re-encode to themselves
 #pragma unroll
@@ -795,6 +796,7 @@ __host__ __device__ __forceinline__ bool cv_hs_prep_fused(const uint32_t aw[8], 
 }
 
 // Single-signature convenience of the fused schedule (host harness).
+template <bool LAT = false>
 __host__ __device__ __forceinline__ bool cv_verify_one_hs_fused(const uint32_t *bcomb, const uint32_t aw[8],
                                                                 const uint32_t rw[8], const uint32_t sw[8],
                                                                 const uint8_t *msg, uint32_t mlen, bool *key_ok_out) {
@@ -802,7 +804,7 @@ __host__ __device__ __forceinline__ bool cv_verify_one_hs_fused(const uint32_t *
     alignas(16) uint32_t tabR[CV_TAB_WORDS];
     uint32_t dig[CV_HS_DIGWORDS];
     bool ok = false;
-    *key_ok_out = cv_hs_prep_fused(aw, rw, sw, msg, mlen, dig, 1, tab, tabR, ok);
+    *key_ok_out = cv_hs_prep_fused<LAT>(aw, rw, sw, msg, mlen, dig, 1, tab, tabR, ok);
     int nw = (int)dig[64];
     if (nw < 32) nw = 32;
     const bool eq = cv_hs_straus(bcomb, bcomb + 2 * CV_BTAB_ENTRIES * CV_BTAB_STRIDE, dig, 1, tab, tabR, nw);

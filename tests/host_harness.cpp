@@ -281,13 +281,14 @@ int cvh_pmt_verify(uint32_t b, uint32_t e, const uint8_t *kind, const uint32_t *
 }
 
 // Fused half-size prep (interleaved A/R decodes) + straus for one signature.
-int cvh_verify_hs_fused(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, uint32_t mlen, int *status) {
+int cvh_verify_hs_fused(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, uint32_t mlen, int *status, int lat) {
     uint32_t aw[8], rw[8], sw[8];
     words_from_bytes(aw, pk, 8);
     words_from_bytes(rw, sig, 8);
     words_from_bytes(sw, sig + 32, 8);
     bool key_ok = false;
-    const bool ok = cv_verify_one_hs_fused(CV_BCOMB_H, aw, rw, sw, msg, mlen, &key_ok);
+    const bool ok = lat ? cv_verify_one_hs_fused<true>(CV_BCOMB_H, aw, rw, sw, msg, mlen, &key_ok)
+                        : cv_verify_one_hs_fused<false>(CV_BCOMB_H, aw, rw, sw, msg, mlen, &key_ok);
     *status = key_ok ? 0 : 1;
     return ok ? 1 : 0;
 }

@@ -298,16 +298,17 @@ def test_halfsize_verify_logic_on_golden_corpus(host_harness, corpus, manifest):
     assert not bad, sorted(set(bad))
 
 
-def test_fused_halfsize_prep_logic_on_golden_corpus(host_harness, corpus, manifest):
-    """The fused prep (hash, lattice, A and R decoded as one interleaved pair, both tables) + the
-    half-size Straus reproduce every golden verdict and key status."""
+@pytest.mark.parametrize("lat", [0, 1])
+def test_fused_halfsize_prep_logic_on_golden_corpus(host_harness, corpus, manifest, lat):
+    """The fused prep (hash, lattice, A and R decoded as one interleaved pair, both tables; lat = the
+    latency field forms of small batches) + the half-size Straus reproduce every golden verdict."""
     H = host_harness
     bad = []
     for i in range(len(corpus["pk"])):
         m = corpus["arena"][corpus["off"][i]:corpus["off"][i] + corpus["len"][i]].tobytes()
         st = ctypes.c_int(0)
         v = H.cvh_verify_hs_fused(_b(corpus["pk"][i].tobytes()), _b(corpus["sig"][i].tobytes()), _b(m), len(m),
-                                  ctypes.byref(st))
+                                  ctypes.byref(st), lat)
         if v != corpus["verdict"][i] or st.value != corpus["status"][i]:
             bad.append(manifest["classes"][corpus["cls"][i]])
     assert not bad, sorted(set(bad))
