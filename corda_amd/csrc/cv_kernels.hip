@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "cv_verify.h"
 #include "cv_quad.h"
 #include "cv_hsquad.h"
@@ -135,7 +137,7 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsprep_kernel(uint32_t n, uint
 
 // fused half-size prep (cv_hs_prep_fused): hash, scalars, lattice + digits, A and R decoded as one
 // interleaved pair, both odd-multiple tables; ws_ok = key_ok AND r_ok, status = key status.
-template <bool LAT>
+template <bool LAT, bool SUB = false>
 __global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsfused_prep_kernel(
     uint32_t n, uint32_t cap, const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig,
     const uint8_t *__restrict__ arena, const uint64_t *__restrict__ off, const uint32_t *__restrict__ len,
@@ -157,7 +159,7 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsfused_prep_kernel(
 // hs_straus: E = [v]R + [u]A + [w]B per lane over the wave's largest window count, the identity
 // test, and the verdict word by wave ballot (bit i of word i/64 = signature i).  Lanes past n
 // replay signature n-1 so the whole wave takes part in the window-count reduction.
-template <int WAVES>
+template <int WAVES, bool SUB = false>
 __global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_hs_straus_kernel(uint32_t n, uint32_t cap,
                                                                        const uint32_t *__restrict__ ws_dig,
                                                                        const uint32_t *__restrict__ ws_tab,
@@ -193,6 +195,10 @@ template __global__ void cv_hs_straus_kernel<2>(uint32_t, uint32_t, const uint32
                                                 const uint32_t *, const uint8_t *, uint64_t *);
 template __global__ void cv_hs_straus_kernel<3>(uint32_t, uint32_t, const uint32_t *, const uint32_t *,
                                                 const uint32_t *, const uint8_t *, uint64_t *);
+template __global__ void cv_hs_straus_kernel<2, true>(uint32_t, uint32_t, const uint32_t *, const uint32_t *,
+                                                      const uint32_t *, const uint8_t *, uint64_t *);
+template __global__ void cv_hs_straus_kernel<3, true>(uint32_t, uint32_t, const uint32_t *, const uint32_t *,
+                                                      const uint32_t *, const uint8_t *, uint64_t *);
 
 // 1 = half-size verify for throughput batches (default), 0 = the full-width prep/straus/finish group
 static int g_verify_mode = 1;
@@ -278,6 +284,39 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_quad_kernel(uint32_t n,
 // Batches of at most this many signatures run the quad kernels (set by cvk_set_quad_max; 0 = never)
 static uint32_t g_quad_max = 32768;
 extern "C" void cvk_set_quad_max(uint32_t m) { g_quad_max = m; }
+
+// ---------------------------------------------------------------- two-stream sub-chunk overlap
+// A chunk of the half-size group is cut into a head and a tail sub-chunk; the tail runs on a helper
+// stream so its waves fill the partial last rounds (drain) of the head's kernels.  mode 0 = off,
+// 1 = both sub-chunks start together, 2 = the tail's prep waits for the head's prep, 3 = auto: mode 1
+// when the chunk's last round of hs_straus waves is at most 12 % full (a near-empty drain round: 1M
+// signatures = 5.09 rounds of 3072 resident waves on 256 CUs; measured 11.0-11.2 -> 10.7 ms), else off.
+static int g_split_mode = 3, g_split_pct = 25;
+extern "C" void cvk_set_split_mode(int m) { g_split_mode = (m >= 0 && m <= 3) ? m : 0; }
+extern "C" void cvk_set_split_pct(int p) { g_split_pct = (p >= 5 && p <= 50) ? p : 25; }
+struct SplitAux {
+    hipStream_t s2 = nullptr;
+    hipEvent_t start = nullptr, prep1 = nullptr, done2 = nullptr;
+    int cus = 0;
+    std::mutex mu;   // record/wait of the shared events is enqueued under it (callers on other threads)
+};
+static SplitAux g_split_aux[16];
+static hipError_t split_aux(SplitAux **out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 16) return hipErrorInvalidDevice;
+    SplitAux &a = g_split_aux[dev];
+    if (!a.s2) {
+        if ((e = hipStreamCreateWithFlags(&a.s2, hipStreamNonBlocking)) != hipSuccess) return e;
+        if ((e = hipEventCreateWithFlags(&a.start, hipEventDisableTiming)) != hipSuccess) return e;
+        if ((e = hipEventCreateWithFlags(&a.prep1, hipEventDisableTiming)) != hipSuccess) return e;
+        if ((e = hipEventCreateWithFlags(&a.done2, hipEventDisableTiming)) != hipSuccess) return e;
+        if ((e = hipDeviceGetAttribute(&a.cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+    }
+    *out = &a;
+    return hipSuccess;
+}
 
 // ---------------------------------------------------------------- keyed verify (per-key comb, f2)
 // key precompute: one lane per key (decode + 4 comb row tables of 8 cached multiples) into its slot
@@ -446,6 +485,49 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             hipLaunchKernelGGL(cv_hs_straus_quad_kernel, dim3((4 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
                                stream, m, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
             if (ev && c0 == 0) (void)hipEventRecord(ev[3], stream);
+            continue;
+        }
+        SplitAux *ax = nullptr;
+        bool split = false;
+        if (!lat && g_verify_mode == 1 && g_hs_fused && g_split_mode && !ev && m >= 131072) {
+            hipError_t e = split_aux(&ax);
+            if (e != hipSuccess) return e;
+            const uint32_t resident = (uint32_t)ax->cus * 4u * (uint32_t)g_hs_waves;   // waves in one round
+            const uint32_t last = ((m + 63) / 64) % resident;
+            split = g_split_mode != 3 || (resident && last && last * 100u <= resident * 12u);
+        }
+        if (split) {
+            // fused half-size group in two sub-chunks: head [0, m1) on `stream`, tail [m1, m) on the
+            // helper stream; `stream` waits for the tail before anything queued after this call.
+            // Sub-chunk launches use the <.., true> instances so traces tell them from whole-chunk ones.
+            uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
+            const uint32_t m1 = (uint32_t)(((uint64_t)m * (100 - g_split_pct) / 100) & ~(uint64_t)255);
+            const uint32_t m2 = m - m1;                 // the tail keeps the batch's ragged end
+            const uint32_t sub0[2] = {0, m1}, subn[2] = {m1, m2};
+            std::lock_guard<std::mutex> lk(ax->mu);
+            (void)hipEventRecord(ax->start, stream);
+            (void)hipStreamWaitEvent(ax->s2, ax->start, 0);
+            for (int h = 0; h < 2; h++) {
+                hipStream_t st = h ? ax->s2 : stream;
+                const uint32_t a = c0 + sub0[h], mm = subn[h], bl = (mm + CV_BLOCK - 1) / CV_BLOCK;
+                if (h == 1 && g_split_mode == 2) (void)hipStreamWaitEvent(st, ax->prep1, 0);
+                hipLaunchKernelGGL((cv_hsfused_prep_kernel<false, true>), dim3(bl), dim3(CV_BLOCK), 0, st, mm, ws_cap,
+                                   pk + (size_t)a * 32, sig + (size_t)a * 64, arena, off + a, len + a,
+                                   ws_dig + sub0[h], ws_tab + (size_t)sub0[h] * CV_TAB_WORDS,
+                                   ws_tabR + (size_t)sub0[h] * CV_TAB_WORDS, ws_ok + sub0[h],
+                                   status ? status + a : nullptr);
+                if (h == 0) (void)hipEventRecord(ax->prep1, st);
+                if (g_hs_waves == 2)
+                    hipLaunchKernelGGL((cv_hs_straus_kernel<2, true>), dim3(bl), dim3(CV_BLOCK), 0, st, mm, ws_cap,
+                                       ws_dig + sub0[h], ws_tab + (size_t)sub0[h] * CV_TAB_WORDS,
+                                       ws_tabR + (size_t)sub0[h] * CV_TAB_WORDS, ws_ok + sub0[h], bitmap + a / 64);
+                else
+                    hipLaunchKernelGGL((cv_hs_straus_kernel<3, true>), dim3(bl), dim3(CV_BLOCK), 0, st, mm, ws_cap,
+                                       ws_dig + sub0[h], ws_tab + (size_t)sub0[h] * CV_TAB_WORDS,
+                                       ws_tabR + (size_t)sub0[h] * CV_TAB_WORDS, ws_ok + sub0[h], bitmap + a / 64);
+            }
+            (void)hipEventRecord(ax->done2, ax->s2);
+            (void)hipStreamWaitEvent(stream, ax->done2, 0);
             continue;
         }
         if (!lat && g_verify_mode == 1 && g_hs_fused) {

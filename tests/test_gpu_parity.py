@@ -345,3 +345,38 @@ def test_full_width_and_half_size_schedules_agree(engine, corpus, oracle_c, mode
     finally:
         native.set_verify_mode(1)
         lib.cvk_set_quad_max(32768)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_split_launch_plans_agree(engine, corpus, mode):
+    """The two-stream sub-chunk plan (internal switch cvk_set_split_mode: 0 off, 1 concurrent, 2 tail
+    after head prep, 3 auto) over the golden corpus tiled to a ragged 200,003 signatures through the
+    device API: every verdict and key-status byte follows its record, bits past n stay clear."""
+    import ctypes
+    import torch
+    lib = native.load()
+    lib.cvk_set_split_mode.argtypes = [ctypes.c_int]
+    lib.cvk_set_split_pct.argtypes = [ctypes.c_int]
+    n = 200_003
+    rng = np.random.default_rng(7)
+    idx = rng.integers(0, len(corpus["pk"]), n)
+    dev = "cuda:0"
+    pk = torch.from_numpy(np.ascontiguousarray(corpus["pk"][idx])).to(dev)
+    sig = torch.from_numpy(np.ascontiguousarray(corpus["sig"][idx])).to(dev)
+    arena = torch.from_numpy(np.concatenate([corpus["arena"], np.zeros(64, np.uint8)])).to(dev)
+    off = torch.from_numpy(corpus["off"][idx].astype(np.uint64).view(np.int64)).to(dev)
+    ln = torch.from_numpy(corpus["len"][idx].astype(np.uint32).view(np.int32)).to(dev)
+    try:
+        lib.cvk_set_split_mode(mode)
+        lib.cvk_set_split_pct(25)
+        bm = torch.full(((n + 63) // 64,), -1, dtype=torch.int64, device=dev)
+        st = torch.full((n,), 7, dtype=torch.uint8, device=dev)
+        engine.verify_device(0, n, pk.data_ptr(), sig.data_ptr(), arena.data_ptr(), off.data_ptr(), ln.data_ptr(),
+                             bm.data_ptr(), st.data_ptr())
+        engine.synchronize(0)
+    finally:
+        lib.cvk_set_split_mode(3)
+    bits = bm.cpu().numpy().view(np.uint64)
+    assert np.array_equal(_bits(bits, n), corpus["verdict"][idx].astype(bool))
+    assert np.array_equal(st.cpu().numpy(), corpus["status"][idx])
+    assert int(bits[-1]) >> (n % 64) == 0
