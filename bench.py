@@ -19,6 +19,8 @@ Extra fields on the JSON line:
   cpu_baseline  oracle/ C restatement of eddsa-0.1.0 verify (rank 0, N=1 only, bounded sample)
   notary        p50/p99 end-to-end latency of a 4096-signature notary batch (host buffers in and
                 out, 1/16 adversarial), GPU vs the CPU restatement on the same batch
+  resolve_chain p50/p99 latency of a 5,000-tx dependency chain (2 signers/tx, 6 leaves/tx): one
+                Merkle call + one verify call + per-tx AND with the id check
 """
 from __future__ import annotations
 
@@ -125,6 +127,68 @@ def notary_latency(eng, device: int, reps: int, cpu: bool, key_pool=None):
             v, _ = cv_oracle.verify_batch(pk, sig, arena, off, ln, threads)
             cl.append(time.perf_counter() - t)
         assert np.array_equal(v.astype(bool), expect)
+        out["cpu_p50_ms"] = float(np.median(cl) * 1e3)
+        out["cpu_threads"] = threads
+    return out
+
+
+def resolve_chain_latency(eng, device: int, reps: int, cpu: bool, ntx: int = 5000, signers: int = 2):
+    """ResolveTransactionsFlow (core/src/main/kotlin/net/corda/flows/
+    ResolveTransactionsFlow.kt:105-111,119) checks a whole dependency chain; the reference loops
+    `stx.verifySignatures()` per transaction (id recompute + sequential EdDSAEngine verifies).  Here
+    the chain is ONE Merkle call (every WireTransaction.id) + ONE verify call (every signature over its
+    claimed id) + the per-tx AND with the id check, host buffers in and out; p50/p99 over reps.
+    Synthetic chain: C3-shaped leaves (6 per tx), `signers` signatures per tx, one in 16 txs with a
+    mutated signature and one in 64 with a mutated leaf (id mismatch)."""
+    tb = workload.make_tx_batch(eng, device, ntx, signers=signers, seed=5000)
+    arena = tb.leaf_arena.cpu().numpy().copy()
+    leaf_off = tb.leaf_off.cpu().numpy().astype(np.uint64)
+    leaf_len = tb.leaf_len.cpu().numpy().astype(np.uint32)
+    tx_begin = tb.tx_begin.cpu().numpy().astype(np.uint32)
+    claimed = tb.ids.cpu().numpy()
+    pk, sig, _, _, _ = tb.sigs.to_host()
+    sig = sig.copy()
+    bad_sig_tx = np.arange(0, ntx, 16)
+    sig[bad_sig_tx * signers, 40] ^= 1                         # S bit flip: reject
+    bad_leaf_tx = np.arange(3, ntx, 64)
+    arena[leaf_off[tx_begin[bad_leaf_tx]].astype(np.int64)] ^= 0x5a      # first leaf byte: id mismatch
+    msg_arena = np.concatenate([claimed.reshape(-1), np.zeros(16, np.uint8)])
+    msg_off = (np.arange(ntx * signers, dtype=np.uint64) // signers) * 32
+    msg_len = np.full(ntx * signers, 32, np.uint32)
+    sig_tx_begin = np.arange(0, ntx * signers + 1, signers, dtype=np.uint32)
+    expect = np.ones(ntx, bool)
+    expect[bad_sig_tx] = False
+    expect[bad_leaf_tx] = False
+
+    def chain_gpu():
+        ids, st = eng.merkle_tx_ids(arena, leaf_off, leaf_len, tx_begin)
+        bitmap, _ = eng.verify_batch(pk, sig, msg_arena, msg_off, msg_len, want_status=False)
+        return native.tx_verdicts(bitmap, sig_tx_begin).astype(bool) & (ids == claimed).all(axis=1) & (st == 0)
+
+    lat = []
+    for r in range(reps + 5):
+        t = time.perf_counter()
+        ok = chain_gpu()
+        dt = time.perf_counter() - t
+        if r >= 5:
+            lat.append(dt)
+    assert np.array_equal(ok, expect), "resolve chain verdicts wrong"
+    out = {"txs": ntx, "signers_per_tx": signers, "sigs": ntx * signers, "leaves_per_tx": 6,
+           "p50_ms": float(np.percentile(lat, 50) * 1e3), "p99_ms": float(np.percentile(lat, 99) * 1e3),
+           "reps": reps, "tx_ok": int(ok.sum())}
+    if cpu:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import cv_oracle  # noqa: E402
+        threads = int(os.environ.get("CV_CPU_THREADS", "16"))
+        cl = []
+        for r in range(3):
+            t = time.perf_counter()
+            ids_c = cv_oracle.merkle_tx_ids(arena, leaf_off, leaf_len, tx_begin)
+            v, _ = cv_oracle.verify_batch(pk, sig, msg_arena, msg_off, msg_len, threads)
+            cl.append(time.perf_counter() - t)
+        ids_c = ids_c[0] if isinstance(ids_c, tuple) else ids_c
+        okc = (v.astype(bool).reshape(ntx, signers).all(axis=1) & (ids_c == claimed).all(axis=1))
+        assert np.array_equal(okc, expect), "CPU restatement disagrees on the resolve chain"
         out["cpu_p50_ms"] = float(np.median(cl) * 1e3)
         out["cpu_threads"] = threads
     return out
@@ -347,6 +411,7 @@ def main():
         if not args.no_notary:
             result["notary"] = notary_latency(eng, local, 50, cpu=(world == 1 and not args.no_cpu))
             result["notary_keyed"] = notary_latency(eng, local, 50, cpu=False, key_pool=64)
+            result["resolve_chain"] = resolve_chain_latency(eng, local, 30, cpu=(world == 1 and not args.no_cpu))
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()
