@@ -347,17 +347,18 @@ def test_full_width_and_half_size_schedules_agree(engine, corpus, oracle_c, mode
         lib.cvk_set_quad_max(32768)
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2, 3])
-def test_split_launch_plans_agree(engine, corpus, mode):
+@pytest.mark.parametrize("mode,n", [(0, 200_003), (1, 200_003), (2, 200_003), (3, 200_003),
+                                    (3, (1 << 21) + 200_003), (1, (1 << 21) + 200_003)])
+def test_split_launch_plans_agree(engine, corpus, mode, n):
     """The two-stream sub-chunk plan (internal switch cvk_set_split_mode: 0 off, 1 concurrent, 2 tail
-    after head prep, 3 auto) over the golden corpus tiled to a ragged 200,003 signatures through the
-    device API: every verdict and key-status byte follows its record, bits past n stay clear."""
+    after head prep, 3 auto) over the golden corpus tiled to a ragged n through the device API — at
+    2^21 + 200,003 the batch is two workspace chunks and only the second one's last round is
+    near-empty: every verdict and key-status byte follows its record, bits past n stay clear."""
     import ctypes
     import torch
     lib = native.load()
     lib.cvk_set_split_mode.argtypes = [ctypes.c_int]
     lib.cvk_set_split_pct.argtypes = [ctypes.c_int]
-    n = 200_003
     rng = np.random.default_rng(7)
     idx = rng.integers(0, len(corpus["pk"]), n)
     dev = "cuda:0"
