@@ -180,3 +180,48 @@ def test_notary_batch(engine):
     r2 = notary.notarise([SignRequest(make_stx(engine, signer_idx=[94], inputs=(b"s-94",),
                                                extra_must=(notary.owning_key,)), caller="q")])
     assert r2[0].ok
+
+
+def test_c1_loadtest_self_issue_10k(engine, oracle_c):
+    """BASELINE config C1 (tools/loadtest self-issue): 10,000 single-signer cash-issue
+    transactions from a pool of 4 node keys, 2 leaves each (an output ~600 B, a command ~300 B), ids by
+    one Merkle call, signatures by the GPU signer over id.bytes (TransactionBuilder.signWith,
+    TransactionBuilder.kt:93-98).  verifySignatures() over the whole load in one batch: every honest
+    transaction passes, every 16th (one S bit flipped) raises SignatureException — the same verdicts as
+    the C restatement and as the sequential per-transaction reference shape on a sample."""
+    rng = np.random.default_rng(10_000)
+    ntx = 10_000
+    seeds = [seed(40 + k) for k in range(4)]
+    keys = [EdDSAPublicKey(E.public_key_of(s)) for s in seeds]
+    owner = rng.integers(0, 4, ntx)
+    wtxs = []
+    for t in range(ntx):
+        out = rng.integers(0, 256, int(rng.integers(450, 750)), dtype=np.uint8).tobytes()
+        cmd = rng.integers(0, 256, int(rng.integers(225, 375)), dtype=np.uint8).tobytes()
+        k = keys[owner[t]].composite
+        wtxs.append(WireTransaction(outputs=[out], commands=[cmd], must_sign=[k], command_descriptions={k: "Issue"}))
+    ids = compute_ids(wtxs, engine)
+    id_arena = np.frombuffer(b"".join(i.bytes for i in ids) + b"\0" * 16, np.uint8)
+    off = np.arange(ntx, dtype=np.uint64) * 32
+    ln = np.full(ntx, 32, np.uint32)
+    seed_arr = np.frombuffer(b"".join(seeds[o] for o in owner), np.uint8).reshape(ntx, 32)
+    pk, sig = engine.sign_batch(seed_arr, id_arena, off, ln)
+    assert all(pk[t].tobytes() == keys[owner[t]].encoded for t in range(0, ntx, 997))
+    bad = np.arange(5, ntx, 16)
+    sig[bad, 33] ^= 0x10
+    stxs = [SignedTransaction(w, [DigitalSignature.WithKey(keys[owner[t]], sig[t].tobytes())], w.id)
+            for t, w in enumerate(wtxs)]
+    errs = verify_signatures_batch(stxs, engine=engine)
+    got_ok = np.array([e is None for e in errs])
+    expect = np.ones(ntx, bool)
+    expect[bad] = False
+    assert np.array_equal(got_ok, expect)
+    assert all(isinstance(errs[t], SignatureException) for t in bad)
+    ref, _ = oracle_c.verify_batch(pk, sig, id_arena, off, ln, nthreads=8)
+    assert np.array_equal(ref.astype(bool), expect)
+    for t in list(range(0, 48)):                       # sequential reference shape on a sample
+        if expect[t]:
+            assert stxs[t].verify_signatures(engine=engine) is wtxs[t]
+        else:
+            with pytest.raises(SignatureException):
+                stxs[t].verify_signatures(engine=engine)
