@@ -140,6 +140,9 @@ int cv_tx_verdicts(size_t ntx, const uint64_t *verdict_bitmap, const uint32_t *t
  * All pointers are device pointers on HIP device `device` (which must be in the context); work is
  * enqueued on `stream` (a hipStream_t, NULL = the context's stream for that device) and the call
  * returns without synchronising.  These are the entry points bench.py times (inputs resident in HBM).
+ * A large batch may internally run part of its work on a per-device helper stream of the engine (the
+ * drain overlap, DESIGN.md "Schedules"); `stream` waits on that work before anything the caller
+ * enqueues after the call, so completion is still stream-ordered on `stream`.
  */
 int cv_ed25519_verify_device(cv_ctx *ctx, int device, size_t n, const void *d_pk, const void *d_sig,
                              const void *d_arena, const void *d_off, const void *d_len, void *d_bitmap,
