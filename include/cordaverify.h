@@ -149,9 +149,11 @@ int cv_ed25519_verify_device(cv_ctx *ctx, int device, size_t n, const void *d_pk
                              void *d_status, void *stream);
 
 /* Measurement entry point (bench.py): as cv_ed25519_verify_device (no status), but synchronous,
- * and fills phase_ms[0..2] with the summed durations of the three verify kernels measured with HIP
- * events on the launch stream: prep (key decode, challenge hash, -A table), Straus
- * double-scalar multiplication, finish (batched inversion, encode, compare, bitmap). */
+ * whole-chunk launches only (no drain overlap), and fills phase_ms[0..2] with the summed durations
+ * of the verify kernels measured with HIP events on the launch stream.  Half-size schedule (default):
+ * fused prep (decodes, challenge hash, lattice, digits, tables) | unused (0) | hs_straus (multi-scalar
+ * multiplication + verdict bits).  Full-width schedule: prep | Straus | finish (batched inversion,
+ * encode, compare, bitmap). */
 int cv_ed25519_verify_device_timed(cv_ctx *ctx, int device, size_t n, const void *d_pk, const void *d_sig,
                                    const void *d_arena, const void *d_off, const void *d_len, void *d_bitmap,
                                    void *stream, float *phase_ms);
