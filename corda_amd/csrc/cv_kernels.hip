@@ -291,9 +291,9 @@ extern "C" void cvk_set_quad_max(uint32_t m) { g_quad_max = m; }
 // 1 = both sub-chunks start together, 2 = the tail's prep waits for the head's prep, 3 = auto: mode 1
 // when the chunk's last round of hs_straus waves is at most 12 % full (a near-empty drain round: 1M
 // signatures = 5.09 rounds of 3072 resident waves on 256 CUs; measured 11.0-11.2 -> 10.7 ms), else off.
-static int g_split_mode = 3, g_split_pct = 25;
+static int g_split_mode = 3, g_split_pct = 10;
 extern "C" void cvk_set_split_mode(int m) { g_split_mode = (m >= 0 && m <= 3) ? m : 0; }
-extern "C" void cvk_set_split_pct(int p) { g_split_pct = (p >= 5 && p <= 50) ? p : 25; }
+extern "C" void cvk_set_split_pct(int p) { g_split_pct = (p >= 5 && p <= 50) ? p : 10; }
 struct SplitAux {
     hipStream_t s2 = nullptr;
     hipEvent_t start = nullptr, prep1 = nullptr, done2 = nullptr;

@@ -369,7 +369,7 @@ def test_split_launch_plans_agree(engine, corpus, mode, n):
     ln = torch.from_numpy(corpus["len"][idx].astype(np.uint32).view(np.int32)).to(dev)
     try:
         lib.cvk_set_split_mode(mode)
-        lib.cvk_set_split_pct(25)
+        lib.cvk_set_split_pct(10 if mode == 3 else 25)
         bm = torch.full(((n + 63) // 64,), -1, dtype=torch.int64, device=dev)
         st = torch.full((n,), 7, dtype=torch.uint8, device=dev)
         engine.verify_device(0, n, pk.data_ptr(), sig.data_ptr(), arena.data_ptr(), off.data_ptr(), ln.data_ptr(),
@@ -377,6 +377,7 @@ def test_split_launch_plans_agree(engine, corpus, mode, n):
         engine.synchronize(0)
     finally:
         lib.cvk_set_split_mode(3)
+        lib.cvk_set_split_pct(10)
     bits = bm.cpu().numpy().view(np.uint64)
     assert np.array_equal(_bits(bits, n), corpus["verdict"][idx].astype(bool))
     assert np.array_equal(st.cpu().numpy(), corpus["status"][idx])
