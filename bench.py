@@ -5,7 +5,8 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-A "step" = one verify pass over the whole per-GPU batch (inputs resident in HBM), plus — for N > 1 —
+A "step" = one verify pass over the whole per-GPU batch (inputs resident in HBM; the engine's
+production launch plan), plus — for N > 1 —
 the RCCL all-gather of the verdict bitmaps that feeds the notary commit step.  Weak scaling: every
 rank verifies its own N_PER_GPU signatures.  value = all signatures verified by all ranks / the max
 over ranks of the timed region.
@@ -14,8 +15,10 @@ Default workload (N=1): BASELINE config C2 — 1,000,000 single-signer Ed25519 s
 300-byte messages, distinct key per signature, generated on the GPU by the engine's signer.
 
 Extra fields on the JSON line:
-  roofline      VALU-issue roofline of the verify kernel (algorithmic 2.28e5 32x32->64 MACs per
-                verify) against the measured v_mad_u64_u32 peak of this GPU
+  roofline      VALU-issue roofline of the dominant kernel (cv_hs_straus_kernel: 141,660 32x32->64
+                MACs per verify, DESIGN.md "Half-size scalars") against the measured v_mad_u64_u32
+                peak of this GPU, kernel time from HIP events on whole-chunk launches of the same
+                batch; "group" = the whole launch group against its own MAC count
   cpu_baseline  oracle/ C restatement of eddsa-0.1.0 verify (rank 0, N=1 only, bounded sample)
   notary        p50/p99 end-to-end latency of a 4096-signature notary batch (host buffers in and
                 out, 1/16 adversarial), GPU vs the CPU restatement on the same batch
