@@ -382,3 +382,18 @@ def test_split_launch_plans_agree(engine, corpus, mode, n):
     assert np.array_equal(_bits(bits, n), corpus["verdict"][idx].astype(bool))
     assert np.array_equal(st.cpu().numpy(), corpus["status"][idx])
     assert int(bits[-1]) >> (n % 64) == 0
+
+
+def test_host_buffer_api_split_size_exact_pattern(engine):
+    """Host-buffer C-ABI (cv_ed25519_verify_batch: H2D, verify, D2H) at a size whose last Straus
+    round is near-empty (200,003 distinct-key signatures over 300-byte messages, so the drain-overlap
+    plan runs): honest signatures accepted, every 16th (one S bit flipped) rejected, key status clear."""
+    from corda_amd import workload
+    n = 200_003
+    b = workload.make_batch(engine, 0, n, 300, seed=123)
+    expect = workload.corrupt_fraction(b, 16).cpu().numpy()
+    pk, sig, arena, off, ln = b.to_host()
+    bitmap, status = engine.verify_batch(pk, sig, arena, off, ln)
+    assert np.array_equal(_bits(bitmap, n), expect)
+    assert int(status.sum()) == 0
+    assert int(bitmap[-1]) >> (n % 64) == 0
