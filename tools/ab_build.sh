@@ -8,6 +8,6 @@ rm -rf $D && mkdir -p $D/corda_amd/csrc $D/include
 cp corda_amd/csrc/*.h corda_amd/csrc/*.hip corda_amd/csrc/*.cpp $D/corda_amd/csrc/
 cp include/*.h $D/include/
 for o in "$@"; do cp "${o%%=*}" "$D/${o#*=}"; done
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -shared $D/corda_amd/csrc/cv_kernels.hip \
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -mllvm -amdgpu-sched-strategy=max-ilp -shared $D/corda_amd/csrc/cv_kernels.hip \
     -x hip $D/corda_amd/csrc/cv_api.cpp -o $D/libcv.so -lpthread
 echo $D/libcv.so
