@@ -615,12 +615,13 @@ __host__ __device__ __forceinline__ bool cv_hs_straus(const uint32_t *blo, const
         ge_p1p1 t;
         ge_p3 R3;
         if (win != nw - 1) {
-            ge_p2_dbl(t, R);
-            ge_p1p1_to_p2(R, t);
-            ge_p2_dbl(t, R);
-            ge_p1p1_to_p2(R, t);
-            ge_p2_dbl(t, R);
-            ge_p1p1_to_p2(R, t);
+            // the first three doublings as a rolled loop: one copy of the formula keeps the window
+            // loop's code at 91 KB instead of 115 KB (same-box A/B: hs_straus -1.5 %)
+#pragma unroll 1
+            for (int d = 0; d < 3; d++) {
+                ge_p2_dbl(t, R);
+                ge_p1p1_to_p2(R, t);
+            }
             ge_p2_dbl(t, R);
             ge_p1p1_to_p3(R3, t);
         } else {
