@@ -46,6 +46,9 @@ def build(verbose: bool = False, force: bool = False) -> str:
     gen = os.path.join(CSRC, "gen_tables.py")
     if force or _stale(tables, [gen]):
         subprocess.run([sys.executable, gen], check=True)
+    madc, gen_m = os.path.join(CSRC, "cv_madc.h"), os.path.join(CSRC, "gen_madc.py")
+    if force or _stale(madc, [gen_m]):
+        subprocess.run([sys.executable, gen_m], check=True)
     objs = []
     deps = _deps()
     for src in SOURCES:

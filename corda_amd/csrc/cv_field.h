@@ -20,6 +20,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "cv_madc.h"
 
 #define CV_HD __host__ __device__ __forceinline__
 
@@ -119,50 +120,23 @@ CV_HD void fe_check_mul_in(const fe &f, const fe &g) {
 // k-1, so a carry costs only its shift (the first v_mad_u64_u32 of the next column adds it for
 // free) instead of shift + 64-bit add.  CV_MADC(acc, a, b): acc = a*b + acc as ONE v_mad_u64_u32,
 // written in asm so the compiler cannot reassociate the carry to the end of the column sum.
-// An asm result read by the very next instruction costs a conservative s_nop, so independent
-// multiplications are interleaved N ways (fe_mul_n / fe_sq_n): product k of chain m is followed by
-// product k of chain m+1, and a chain's next product comes N instructions later.
+// The mad's carry-out goes to VCC, declared as a clobber (round 1 bound it to an "=s" output).  The
+// hardware needs no padding between dependent mads: distance 1, 2, 3 and 4 are exact
+// (tools/microbench/mad_hazard.hip: 0 mismatches in 10^7 chained mads on MI355X).  LLVM, however,
+// pads with "s_nop 0" any instruction that reads a VGPR written by the inline-asm statement
+// IMMEDIATELY before it (it cannot see whether the asm used dst_sel forwarding) — 1,414 such nops in
+// round 1's hs_straus.  So every mad is its own asm statement and the N independent chains of
+// fe_mul_n / fe_sq_n are issued round-robin: chain m's next product is N statements later and never
+// directly follows the statement that wrote its accumulator (N >= 2).
 #ifdef __HIP_DEVICE_COMPILE__
-#define CV_MADC(acc, a, b)                                                                   \
-    {                                                                                        \
-        uint64_t cc_;                                                                        \
-        asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc_) : "v"(a), "v"(b));     \
-    }
+#define CV_MADC(acc, a, b) asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b) : "vcc")
 #else
 #define CV_MADC(acc, a, b) ((acc) += (uint64_t)(a) * (uint64_t)(b))
 #endif
 
-// One product slot of N interleaved chains as ONE asm statement (N dependent-free mads back to back):
-// the compiler's conservative inline-asm hazard wait then costs one s_nop per N products.
 template <int N> CV_HD void cv_madc_n(uint64_t (&t)[N], const uint32_t (&a)[N], const uint32_t (&b)[N]) {
-#ifdef __HIP_DEVICE_COMPILE__
-    uint64_t cc;
-    if constexpr (N == 1) {
-        asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(t[0]), "=s"(cc) : "v"(a[0]), "v"(b[0]));
-    } else if constexpr (N == 2) {
-        asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\tv_mad_u64_u32 %1, %2, %5, %6, %1"
-            : "+v"(t[0]), "+v"(t[1]), "=s"(cc) : "v"(a[0]), "v"(b[0]), "v"(a[1]), "v"(b[1]));
-    } else {
-        // wider groups raise register pressure (all 2N operands live at once): issue pairs
-        static_assert(N == 3 || N == 4, "cv_madc_n: N in 1..4");
-        uint64_t t01[2] = {t[0], t[1]}, t23[2] = {t[2], N == 4 ? t[N - 1] : 0};
-        const uint32_t a01[2] = {a[0], a[1]}, b01[2] = {b[0], b[1]};
-        cv_madc_n<2>(t01, a01, b01);
-        if constexpr (N == 4) {
-            const uint32_t a23[2] = {a[2], a[N - 1]}, b23[2] = {b[2], b[N - 1]};
-            cv_madc_n<2>(t23, a23, b23);
-            t[N - 1] = t23[1];
-        } else {
-            uint64_t t2[1] = {t[2]};
-            const uint32_t a2[1] = {a[2]}, b2[1] = {b[2]};
-            cv_madc_n<1>(t2, a2, b2);
-            t23[0] = t2[0];
-        }
-        t[0] = t01[0]; t[1] = t01[1]; t[2] = t23[0];
-    }
-#else
-    for (int m = 0; m < N; m++) t[m] += (uint64_t)a[m] * (uint64_t)b[m];
-#endif
+#pragma unroll
+    for (int m = 0; m < N; m++) CV_MADC(t[m], a[m], b[m]);
 }
 
 // Closing the sequential chain: the carry out of limb 9 (< 2^40) wraps into limb 0 as 19*c, and one
@@ -195,19 +169,19 @@ template <int N> CV_HD void fe_mul_n(fe (&h)[N], const fe (&f)[N], const fe (&g)
     for (int m = 0; m < N; m++) t[m] = 0;
 #pragma unroll
     for (int k = 0; k < 10; k++) {
+        uint32_t a[10][N], b[10][N];
 #pragma unroll
         for (int i = 0; i < 10; i++) {
             const int j = (k - i + 10) % 10;
             const bool dbl = (i & 1) && (j & 1);
             const bool wrap = i + j >= 10;
-            uint32_t a[N], b[N];
 #pragma unroll
             for (int m = 0; m < N; m++) {
-                a[m] = dbl ? fd[m][i] : f[m].v[i];
-                b[m] = wrap ? g19[m][j] : g[m].v[j];
+                a[i][m] = dbl ? fd[m][i] : f[m].v[i];
+                b[i][m] = wrap ? g19[m][j] : g[m].v[j];
             }
-            cv_madc_n<N>(t, a, b);
         }
+        cv_madc_col<N, 10>(t, a, b);
 #pragma unroll
         for (int m = 0; m < N; m++) {
             r[m][k] = (uint32_t)t[m] & CV_MASK(k);
@@ -263,18 +237,25 @@ template <int N, unsigned DBL = 0> CV_HD void fe_sq_n(fe (&h)[N], const fe (&f)[
     for (int m = 0; m < N; m++) t[m] = 0;
 #pragma unroll
     for (int k = 0; k < 10; k++) {
+        constexpr int P0 = 6;
+        uint32_t a[P0][N], b[P0][N];
 #pragma unroll
-        for (int q = 0; q < 6; q++) {
+        for (int q = 0; q < P0; q++) {
             const int li = cv_sq_cols(k, q, 0), lm = cv_sq_cols(k, q, 1);
             const int ri = cv_sq_cols(k, q, 2), rm = cv_sq_cols(k, q, 3);
-            if (li < 0) continue;
-            uint32_t a[N], b[N];
 #pragma unroll
             for (int m = 0; m < N; m++) {
-                a[m] = lm == 2 ? l2[m][li] : l1[m][li];
-                b[m] = rm == 1 ? f[m].v[ri] : rm == 2 ? r2[m][ri] : rm == 19 ? r19[m][ri] : r38[m][ri];
+                a[q][m] = li < 0 ? 0u : lm == 2 ? l2[m][li] : l1[m][li];
+                b[q][m] = li < 0 ? 0u : rm == 1 ? f[m].v[ri] : rm == 2 ? r2[m][ri] : rm == 19 ? r19[m][ri] : r38[m][ri];
             }
-            cv_madc_n<N>(t, a, b);
+        }
+        // odd columns have 5 products (slot 5 unused), even columns 6
+        if (k & 1) {
+            const uint32_t(&a5)[5][N] = *reinterpret_cast<const uint32_t(*)[5][N]>(&a);
+            const uint32_t(&b5)[5][N] = *reinterpret_cast<const uint32_t(*)[5][N]>(&b);
+            cv_madc_col<N, 5>(t, a5, b5);
+        } else {
+            cv_madc_col<N, 6>(t, a, b);
         }
 #pragma unroll
         for (int m = 0; m < N; m++) {
