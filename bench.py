@@ -373,8 +373,8 @@ def main():
         achieved = n * w_straus / (straus_ms * 1e-3)
         group = n * w_group / (kern_ms * 1e-3)
         if hs:
-            phase_ms = {"prep": float(ph[0]), "hsprep": float(ph[1]), "hs_straus": float(ph[2])}
-            kname, gname = "cv_hs_straus_kernel", "prep + hsprep + hs_straus"
+            phase_ms = {"hash": float(ph[0]), "prep": float(ph[1]), "hs_straus": float(ph[2])}
+            kname, gname = "cv_hs_straus_kernel", "hash + prep + hs_straus"
             wdesc = (f"{w_straus} 32x32->64 MAC per verify in the half-size Straus phase at {HS_NW} windows "
                      f"(512 S + 1135 M)")
             gdesc = f"{w_group} MAC per verify (half-size schedule: Straus + 2 decodes + 2 tables)"

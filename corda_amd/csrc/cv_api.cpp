@@ -28,6 +28,10 @@ hipError_t cvk_merkle(uint32_t ntx, uint32_t nleaves, const uint8_t *arena, cons
                       const uint32_t *leaf_len, const uint32_t *tx_begin, uint32_t *leaf_digest, uint8_t *ids,
                       uint8_t *status, hipStream_t stream);
 hipError_t cvk_calibrate(uint32_t iters, int which, uint32_t blocks, void *scratch, hipStream_t stream);
+hipError_t cvk_prep_probe(uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off,
+                          const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t ws_cap, uint64_t *stamps,
+                          hipStream_t stream);
+hipError_t cvk_mad_clock(uint32_t iters, uint32_t blocks, uint64_t *out, hipStream_t stream);
 hipError_t cvk_keyprep(uint32_t nk, const uint8_t *keys, const uint32_t *slots, uint32_t *scratch, uint32_t *ktab_pool,
                        uint8_t *kok_pool, hipStream_t stream);
 hipError_t cvk_verify_keyed(uint32_t n, const uint8_t *keys, const uint32_t *key_index, const uint32_t *slot_of_key,
@@ -790,6 +794,86 @@ int cv_calibrate(cv_ctx *ctx, int device, double *mad_per_s, double *femul_per_s
     (void)hipFree(scratch);
     if (mad_per_s) *mad_per_s = rates[0];
     if (femul_per_s) *femul_per_s = rates[1];
+    return CV_OK;
+}
+
+// Roofline peak on a cycle basis (diagnostic): out[0] = chip-wide v_mad_u64_u32 rate (MAC/s),
+// out[1] = shader clock during the run (GHz, s_memtime over s_memrealtime in block 0),
+// out[2] = cycles per mad wave-instruction per SIMD at that clock, out[3] = SIMD count,
+// out[4] = the MAC ceiling at the 2.4 GHz peak clock for that cycle count (MAC/s).
+int cv_calibrate_cycles(cv_ctx *ctx, int device, double *out) {
+    if (!ctx || !out) return CV_E_ARGS;
+    Device *d = find_dev(ctx, device);
+    if (!d) return CV_E_ARGS;
+    CV_TRY(hipSetDevice(d->ordinal));
+    hipDeviceProp_t prop;
+    CV_TRY(hipGetDeviceProperties(&prop, d->ordinal));
+    const uint32_t blocks = (uint32_t)prop.multiProcessorCount * 8, iters = 20000;
+    uint64_t *buf = nullptr;
+    CV_TRY(hipMalloc(&buf, 64));
+    hipEvent_t e0, e1;
+    CV_TRY(hipEventCreate(&e0));
+    CV_TRY(hipEventCreate(&e1));
+    hipError_t e = cvk_mad_clock(iters / 10, blocks, buf, d->stream);
+    if (e == hipSuccess) e = hipEventRecord(e0, d->stream);
+    if (e == hipSuccess) e = cvk_mad_clock(iters, blocks, buf, d->stream);
+    if (e == hipSuccess) e = hipEventRecord(e1, d->stream);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    float ms = 0.f;
+    uint64_t clk[2] = {0, 0};
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    if (e == hipSuccess) e = hipMemcpy(clk, buf, 16, hipMemcpyDeviceToHost);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(buf);
+    if (e != hipSuccess) return hip_rc(e);
+    const double simds = 4.0 * prop.multiProcessorCount;
+    const double rate = 128.0 * iters * blocks * 256.0 / (ms * 1e-3);
+    const double ghz = clk[1] ? (double)clk[0] / ((double)clk[1] / 100e6) / 1e9 : 0.0;
+    const double wave_instr_per_s = rate / 64.0;
+    const double cyc = ghz > 0 ? simds * ghz * 1e9 / wave_instr_per_s : 0.0;
+    out[0] = rate;
+    out[1] = ghz;
+    out[2] = cyc;
+    out[3] = simds;
+    out[4] = cyc > 0 ? simds * 2.4e9 * 64.0 / cyc : 0.0;
+    return CV_OK;
+}
+
+// Per-phase shader cycles of the fused prep kernel (diagnostic build of the same code, one chunk):
+// out[k] = mean cycles per wave of phase k (hash, lattice, digits, decode A+R, tables), out[5] =
+// their sum, out[6] = waves measured, out[7] = the SHA-512 part of the hash phase.  The workspace is the device's verify workspace.
+int cv_diag_prep_phases(cv_ctx *ctx, int device, size_t n, const void *d_pk, const void *d_sig, const void *d_arena,
+                        const void *d_off, const void *d_len, double *out) {
+    if (!ctx || !out || n == 0) return CV_E_ARGS;
+    if (n > kVerifyChunk) return CV_E_TOO_LARGE;
+    Device *d = find_dev(ctx, device);
+    if (!d || !d_pk || !d_sig || !d_arena || !d_off || !d_len) return CV_E_ARGS;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    CV_TRY(hipSetDevice(d->ordinal));
+    CV_TRY(ensure_verify_ws(*d, n));
+    const size_t waves = (n + 63) / 64;
+    uint64_t *st = nullptr;
+    CV_TRY(hipMalloc(&st, waves * 64));
+    hipError_t e = cvk_prep_probe((uint32_t)n, static_cast<const uint8_t *>(d_pk), static_cast<const uint8_t *>(d_sig),
+                                  static_cast<const uint8_t *>(d_arena), static_cast<const uint64_t *>(d_off),
+                                  static_cast<const uint32_t *>(d_len), d->ws_dig.as<uint32_t>(), d->ws_tab.as<uint32_t>(),
+                                  d->ws_cap, st, d->stream);
+    std::vector<uint64_t> h(waves * 8);
+    if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
+    if (e == hipSuccess) e = hipMemcpy(h.data(), st, waves * 64, hipMemcpyDeviceToHost);
+    (void)hipFree(st);
+    if (e != hipSuccess) return hip_rc(e);
+    double sum[6] = {0, 0, 0, 0, 0, 0};
+    for (size_t w = 0; w < waves; w++)
+        for (int k = 0; k < 6; k++) sum[k] += (double)h[w * 8 + k];
+    out[5] = 0;
+    for (int k = 0; k < 5; k++) {
+        out[k] = sum[k] / (double)waves;
+        out[5] += out[k];
+    }
+    out[6] = (double)waves;
+    out[7] = sum[5] / (double)waves;
     return CV_OK;
 }
 

@@ -44,9 +44,11 @@ CV_HD void ge_p1p1_to_p2(ge_p2 &r, const ge_p1p1 &p) {
     fe_mul_n<3>(h, f, g);
     r.X = h[0]; r.Y = h[1]; r.Z = h[2];
 }
+// T3 = X*Y takes Y as f and X as g, so the four products need the 19*g operand of only two
+// elements (X and Z) — 9 fewer v_mul_lo_u32 per conversion than {.., X} x {.., Y}.
 CV_HD void ge_p1p1_to_p3(ge_p3 &r, const ge_p1p1 &p) {
     fe h[4];
-    const fe f[4] = {p.T, p.Y, p.T, p.X}, g[4] = {p.X, p.Z, p.Z, p.Y};
+    const fe f[4] = {p.T, p.Y, p.T, p.Y}, g[4] = {p.X, p.Z, p.Z, p.X};
     fe_mul_n<4>(h, f, g);
     r.X = h[0]; r.Y = h[1]; r.Z = h[2]; r.T = h[3];
 }

@@ -135,23 +135,50 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsprep_kernel(uint32_t n, uint
     if (!r_ok) ws_ok[i] = 0;
 }
 
-// fused half-size prep (cv_hs_prep_fused): hash, scalars, lattice + digits, A and R decoded as one
-// interleaved pair, both odd-multiple tables; ws_ok = key_ok AND r_ok, status = key status.
-template <bool LAT, bool SUB = false>
-__global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsfused_prep_kernel(
-    uint32_t n, uint32_t cap, const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig,
-    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ off, const uint32_t *__restrict__ len,
-    uint32_t *__restrict__ ws_dig, uint32_t *__restrict__ ws_tab, uint32_t *__restrict__ ws_tabR,
-    uint8_t *__restrict__ ws_ok, uint8_t *__restrict__ status) {
+// challenge hash of the half-size group: ws_hs = h || effective s per signature (64 B), with h =
+// SHA-512(R || Abyte || M) mod L.  Its own kernel so it runs at the occupancy its ~110 VGPRs allow
+// (4 waves per SIMD): inside the 256-VGPR fused prep (2 waves per SIMD) the hash was 32 % of the
+// prep's cycles (tools/prep_probe.py, profiles/r02_prep_probe.json) — a serial 64-bit chain per lane
+// that two waves per SIMD cannot cover.
+__global__ __launch_bounds__(CV_BLOCK, 4) void cv_hash_kernel(uint32_t n, const uint8_t *__restrict__ pk,
+                                                              const uint8_t *__restrict__ sig,
+                                                              const uint8_t *__restrict__ arena,
+                                                              const uint64_t *__restrict__ off,
+                                                              const uint32_t *__restrict__ len,
+                                                              uint32_t *__restrict__ ws_hs) {
     const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
     if (i >= n) return;
     uint32_t aw[8], rw[8], sw[8];
     load_words8(aw, pk + (size_t)i * 32);
     load_words8(rw, sig + (size_t)i * 64);
     load_words8(sw, sig + (size_t)i * 64 + 32);
+    uint32_t hs[CV_HS_WORDS];
+    cv_keyed_hs(aw, rw, sw, arena + off[i], len[i], hs);
+    store_words(ws_hs + (size_t)i * CV_HS_WORDS, hs, CV_HS_WORDS / 4);
+}
+
+// fused half-size prep (cv_hs_prep_fused_hs) after cv_hash_kernel: scalars from ws_hs, lattice +
+// digits, A and R decoded as one interleaved pair, both odd-multiple tables; ws_ok = key_ok AND
+// r_ok, status = key status.
+template <bool LAT, bool SUB = false>
+__global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsfused_prep_kernel(
+    uint32_t n, uint32_t cap, const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig,
+    const uint32_t *__restrict__ ws_hs, uint32_t *__restrict__ ws_dig, uint32_t *__restrict__ ws_tab,
+    uint32_t *__restrict__ ws_tabR, uint8_t *__restrict__ ws_ok, uint8_t *__restrict__ status) {
+    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    uint32_t aw[8], rw[8], hs[CV_HS_WORDS];
+    load_words8(aw, pk + (size_t)i * 32);
+    load_words8(rw, sig + (size_t)i * 64);
+    const uint4 *hp = reinterpret_cast<const uint4 *>(ws_hs + (size_t)i * CV_HS_WORDS);
+#pragma unroll
+    for (int q = 0; q < CV_HS_WORDS / 4; q++) {
+        const uint4 x = hp[q];
+        hs[4 * q] = x.x; hs[4 * q + 1] = x.y; hs[4 * q + 2] = x.z; hs[4 * q + 3] = x.w;
+    }
     bool ok = false;
-    const bool key_ok = cv_hs_prep_fused<LAT>(aw, rw, sw, arena + off[i], len[i], ws_dig + i, cap,
-                                         ws_tab + (size_t)i * CV_TAB_WORDS, ws_tabR + (size_t)i * CV_TAB_WORDS, ok);
+    const bool key_ok = cv_hs_prep_fused_hs<LAT>(aw, rw, hs, ws_dig + i, cap, ws_tab + (size_t)i * CV_TAB_WORDS,
+                                                 ws_tabR + (size_t)i * CV_TAB_WORDS, ok);
     ws_ok[i] = ok ? 1 : 0;
     if (status) status[i] = key_ok ? 0 : 1;
 }
@@ -476,9 +503,11 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
         if (lat && g_verify_mode == 1 && g_hs_quad) {
             // half-size quad group: phases = fused prep | bitmap clear | hs_straus_quad
             uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
+            hipLaunchKernelGGL(cv_hash_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, pk + (size_t)c0 * 32,
+                               sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_hs);
             hipLaunchKernelGGL(cv_hsfused_prep_kernel<true>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap,
-                               pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_dig, ws_tab,
-                               ws_tabR, ws_ok, status ? status + c0 : nullptr);
+                               pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, ws_hs, ws_dig, ws_tab, ws_tabR, ws_ok,
+                               status ? status + c0 : nullptr);
             if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);
             (void)hipMemsetAsync(bitmap + (size_t)c0 / 64, 0, (size_t)((m + 63) / 64) * 8, stream);
             if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
@@ -511,8 +540,10 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
                 hipStream_t st = h ? ax->s2 : stream;
                 const uint32_t a = c0 + sub0[h], mm = subn[h], bl = (mm + CV_BLOCK - 1) / CV_BLOCK;
                 if (h == 1 && g_split_mode == 2) (void)hipStreamWaitEvent(st, ax->prep1, 0);
+                hipLaunchKernelGGL(cv_hash_kernel, dim3(bl), dim3(CV_BLOCK), 0, st, mm, pk + (size_t)a * 32,
+                                   sig + (size_t)a * 64, arena, off + a, len + a, ws_hs + (size_t)sub0[h] * CV_HS_WORDS);
                 hipLaunchKernelGGL((cv_hsfused_prep_kernel<false, true>), dim3(bl), dim3(CV_BLOCK), 0, st, mm, ws_cap,
-                                   pk + (size_t)a * 32, sig + (size_t)a * 64, arena, off + a, len + a,
+                                   pk + (size_t)a * 32, sig + (size_t)a * 64, ws_hs + (size_t)sub0[h] * CV_HS_WORDS,
                                    ws_dig + sub0[h], ws_tab + (size_t)sub0[h] * CV_TAB_WORDS,
                                    ws_tabR + (size_t)sub0[h] * CV_TAB_WORDS, ws_ok + sub0[h],
                                    status ? status + a : nullptr);
@@ -531,12 +562,14 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             continue;
         }
         if (!lat && g_verify_mode == 1 && g_hs_fused) {
-            // fused half-size group: phases = fused prep | (empty) | hs_straus
+            // fused half-size group: phases = hash | fused prep | hs_straus
             uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
-            hipLaunchKernelGGL(cv_hsfused_prep_kernel<false>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap,
-                               pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_dig, ws_tab,
-                               ws_tabR, ws_ok, status ? status + c0 : nullptr);
+            hipLaunchKernelGGL(cv_hash_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, pk + (size_t)c0 * 32,
+                               sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_hs);
             if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);
+            hipLaunchKernelGGL(cv_hsfused_prep_kernel<false>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap,
+                               pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, ws_hs, ws_dig, ws_tab, ws_tabR, ws_ok,
+                               status ? status + c0 : nullptr);
             if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
             if (g_hs_waves == 2)
                 hipLaunchKernelGGL(cv_hs_straus_kernel<2>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, ws_dig,
@@ -727,6 +760,131 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_femul_bench_kernel(uint32_t it
 #pragma unroll
         for (int i = 0; i < 10; i++) s ^= x[k].v[i];
     if (s == 0x1234567) out[0] = s;
+}
+
+// ---------------------------------------------------------------- diagnostics: phase cycle probe
+// The fused prep (cv_hs_prep_fused) with s_memtime stamps at its phase boundaries: per wave, lane 0
+// stores the shader-clock cycles of hash | lattice | digit packing | A+R decode | tables into
+// stamps[wave * 8 + k] (vector stores).  Same code and launch shape as the product kernel; each
+// stamp is ordered after the phase's result by a data dependency.  Diagnostic build only.
+__device__ __forceinline__ uint64_t cv_stamp() {
+    uint64_t t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t));
+    return t;
+}
+#define CV_DEP(x) asm volatile("" ::"v"(x))
+
+__global__ __launch_bounds__(CV_BLOCK, 2) void cv_prep_probe_kernel(
+    uint32_t n, uint32_t cap, const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig,
+    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ off, const uint32_t *__restrict__ len,
+    uint32_t *__restrict__ ws_dig, uint32_t *__restrict__ ws_tab, uint32_t *__restrict__ ws_tabR,
+    uint64_t *__restrict__ stamps) {
+    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    uint32_t aw[8], rw[8], sw[8];
+    load_words8(aw, pk + (size_t)i * 32);
+    load_words8(rw, sig + (size_t)i * 64);
+    load_words8(sw, sig + (size_t)i * 64 + 32);
+    CV_DEP(aw[0]); CV_DEP(rw[0]); CV_DEP(sw[0]);
+    uint64_t t[8];
+    t[0] = cv_stamp();
+    uint32_t hs[CV_HS_WORDS];
+    {   // cv_keyed_hs, split: SHA-512 | the two mod-L scalars
+        uint32_t pre[16], dg[16], hh[8], abyte[8], ss[8];
+        ge_abyte_from_key(abyte, aw);
+#pragma unroll
+        for (int q = 0; q < 8; q++) { pre[q] = rw[q]; pre[8 + q] = abyte[q]; }
+        sha512_pre_msg(dg, pre, 64, arena + off[i], len[i]);
+        CV_DEP(dg[0]); CV_DEP(dg[15]);
+        t[6] = cv_stamp();
+        sc_reduce512(hh, dg);
+        sc_effective_s(ss, sw);
+#pragma unroll
+        for (int q = 0; q < 8; q++) { hs[q] = hh[q]; hs[8 + q] = ss[q]; }
+    }
+    CV_DEP(hs[0]); CV_DEP(hs[15]);
+    t[1] = cv_stamp();
+    uint32_t h[8], s8[8], u[8], v[8], w[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) { h[q] = hs[q]; s8[q] = hs[8 + q]; }
+    bool v_neg;
+    int nwin;
+    sc_halfsize(u, v, v_neg, nwin, w, h, s8);
+    CV_DEP(u[7]); CV_DEP(v[7]); CV_DEP(w[7]);
+    t[2] = cv_stamp();
+    uint32_t *dig = ws_dig + i;
+#pragma unroll 4
+    for (int win = 0; win < 64; win++) {
+        const int da = -digit16(u, win), dr = v_neg ? -digit16(v, win) : digit16(v, win);
+        const bool bw = (win & 1) == 0 && win < 32;
+        const int dlo = bw ? digit256(w, win >> 1) : 0, dhi = bw ? digit256(w, 16 + (win >> 1)) : 0;
+        dig[(size_t)win * cap] = ((uint32_t)da & 0x1fu) | (((uint32_t)dr & 0x1fu) << 5) |
+                                 (((uint32_t)dlo & 0x1ffu) << 10) | (((uint32_t)dhi & 0x1ffu) << 19);
+    }
+    dig[64 * (size_t)cap] = (uint32_t)nwin;
+    t[3] = cv_stamp();
+    ge_p3 P[2];
+    bool ok[2];
+    ge_decode2_0_1_0<false>(P, ok, aw, rw);
+    CV_DEP(P[0].T.v[0]); CV_DEP(P[1].T.v[0]);
+    t[4] = cv_stamp();
+    ge_p3 nA;
+    ge_p3_neg(nA, P[0]);
+    ge_cached_multiples8(ws_tab + (size_t)i * CV_TAB_WORDS, nA);
+    ge_cached_multiples8(ws_tabR + (size_t)i * CV_TAB_WORDS, P[1]);
+    t[5] = cv_stamp();
+    if ((threadIdx.x & 63u) == 0) {
+        uint64_t *o = stamps + (size_t)(i >> 6) * 8;
+#pragma unroll
+        for (int k = 0; k < 5; k++) o[k] = t[k + 1] - t[k];
+        o[5] = t[6] - t[0];                     // SHA-512 alone (part of phase 0)
+    }
+}
+
+// Cycle-basis calibration: the chip-wide v_mad_u64_u32 bench again, with block 0's lane 0 stamping
+// s_memtime (shader clock) and s_memrealtime (100 MHz) around its loop, so the rate converts to
+// cycles per wave-instruction per SIMD at the clock the chip actually ran.
+__global__ __launch_bounds__(CV_BLOCK) void cv_mad_clock_kernel(uint32_t iters, uint64_t *out) {
+    uint64_t acc[8];
+    uint32_t a[8], b[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        acc[k] = threadIdx.x + k;
+        a[k] = threadIdx.x * 2654435761u + k;
+        b[k] = blockIdx.x * 40503u + 7 * k + 1;
+    }
+    uint64_t c0, r0, c1, r1;
+    asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(c0), "=s"(r0));
+    for (uint32_t it = 0; it < iters; it++) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc[k]) : "v"(a[k]), "v"(b[(k + r) & 7]) : "vcc");
+        }
+    }
+    asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(c1), "=s"(r1));
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) s ^= acc[k];
+    if (s == 0x1234567) out[2] = s;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        out[0] = c1 - c0;
+        out[1] = r1 - r0;
+    }
+}
+
+extern "C" hipError_t cvk_prep_probe(uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
+                                     const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab,
+                                     uint32_t ws_cap, uint64_t *stamps, hipStream_t stream) {
+    if (n == 0 || n > ws_cap) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(cv_prep_probe_kernel, dim3((n + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, stream, n, ws_cap,
+                       pk, sig, arena, off, len, ws_dig, ws_tab, ws_tab + (size_t)ws_cap * CV_TAB_WORDS, stamps);
+    return hipGetLastError();
+}
+extern "C" hipError_t cvk_mad_clock(uint32_t iters, uint32_t blocks, uint64_t *out, hipStream_t stream) {
+    hipLaunchKernelGGL(cv_mad_clock_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, iters, out);
+    return hipGetLastError();
 }
 
 extern "C" hipError_t cvk_calibrate(uint32_t iters, int which, uint32_t blocks, void *scratch, hipStream_t stream) {

@@ -59,7 +59,33 @@ CV_HD uint32_t cv_k256(int i) {
 #endif
 }
 
+// 64-bit rotate right by a constant: two v_alignbit_b32 on the GPU (the generic shift/or form
+// compiles to two 64-bit shifts and two ors).
+template <int N> CV_HD uint64_t cv_rotr64(uint64_t x) {
+    static_assert(N > 0 && N < 64, "rotate count");
+#ifdef __HIP_DEVICE_COMPILE__
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    if constexpr (N < 32) {
+        return ((uint64_t)__builtin_amdgcn_alignbit(lo, hi, N) << 32) | __builtin_amdgcn_alignbit(hi, lo, N);
+    } else if constexpr (N == 32) {
+        return ((uint64_t)lo << 32) | hi;
+    } else {
+        return ((uint64_t)__builtin_amdgcn_alignbit(hi, lo, N - 32) << 32) | __builtin_amdgcn_alignbit(lo, hi, N - 32);
+    }
+#else
+    return (x >> N) | (x << (64 - N));
+#endif
+}
 CV_HD uint64_t cv_ror64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// low 32 bits of (hi:lo) >> sh, sh < 32 (v_alignbit_b32; a 64-bit shift of two array words would make
+// the compiler keep the array in scratch for an unaligned 8-byte load)
+CV_HD uint32_t cv_funnel32(uint32_t hi, uint32_t lo, uint32_t sh) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_alignbit(hi, lo, sh);
+#else
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh);
+#endif
+}
 CV_HD uint32_t cv_ror32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 CV_HD uint32_t cv_bswap32(uint32_t x) {
     return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
@@ -73,25 +99,47 @@ CV_HD void sha512_init(uint64_t st[8]) {
 }
 
 // One compression; w[16] = big-endian message words (clobbered: used as the schedule ring).
+// Written so every index is a compile-time constant: rounds 0-15 straight from w, then four passes
+// of 16 rounds that extend the schedule in place (w[j] for round 16 p + j), the eight working
+// variables rotated by renaming in the round macro rather than by moves.  (A single loop over i with
+// w[i & 15] compiled to indirect register indexing and a branch per round.)
+#define CV_S512_BSIG0(x) (cv_rotr64<28>(x) ^ cv_rotr64<34>(x) ^ cv_rotr64<39>(x))
+#define CV_S512_BSIG1(x) (cv_rotr64<14>(x) ^ cv_rotr64<18>(x) ^ cv_rotr64<41>(x))
+#define CV_S512_SSIG0(x) (cv_rotr64<1>(x) ^ cv_rotr64<8>(x) ^ ((x) >> 7))
+#define CV_S512_SSIG1(x) (cv_rotr64<19>(x) ^ cv_rotr64<61>(x) ^ ((x) >> 6))
+#define CV_S512_ROUND(a, b, c, d, e, f, g, h, kw)                                                     \
+    {                                                                                             \
+        const uint64_t t1_ = (h) + CV_S512_BSIG1(e) + (((e) & (f)) ^ (~(e) & (g))) + (kw);           \
+        const uint64_t t2_ = CV_S512_BSIG0(a) + (((a) & (b)) ^ ((a) & (c)) ^ ((b) & (c)));           \
+        (d) += t1_;                                                                               \
+        (h) = t1_ + t2_;                                                                          \
+    }
+#define CV_S512_8ROUNDS(base, W)                                                                  \
+    CV_S512_ROUND(a, b, c, d, e, f, g, h, cv_k512((base) + 0) + W(0))                             \
+    CV_S512_ROUND(h, a, b, c, d, e, f, g, cv_k512((base) + 1) + W(1))                             \
+    CV_S512_ROUND(g, h, a, b, c, d, e, f, cv_k512((base) + 2) + W(2))                             \
+    CV_S512_ROUND(f, g, h, a, b, c, d, e, cv_k512((base) + 3) + W(3))                             \
+    CV_S512_ROUND(e, f, g, h, a, b, c, d, cv_k512((base) + 4) + W(4))                             \
+    CV_S512_ROUND(d, e, f, g, h, a, b, c, cv_k512((base) + 5) + W(5))                             \
+    CV_S512_ROUND(c, d, e, f, g, h, a, b, cv_k512((base) + 6) + W(6))                             \
+    CV_S512_ROUND(b, c, d, e, f, g, h, a, cv_k512((base) + 7) + W(7))
+
 __host__ __device__ __forceinline__ void sha512_compress(uint64_t st[8], uint64_t w[16]) {
     uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-#pragma unroll 16
-    for (int i = 0; i < 80; i++) {
-        uint64_t wi;
-        if (i < 16) {
-            wi = w[i & 15];
-        } else {
-            const uint64_t x15 = w[(i - 15) & 15], x2 = w[(i - 2) & 15];
-            const uint64_t s0 = cv_ror64(x15, 1) ^ cv_ror64(x15, 8) ^ (x15 >> 7);
-            const uint64_t s1 = cv_ror64(x2, 19) ^ cv_ror64(x2, 61) ^ (x2 >> 6);
-            wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
-            w[i & 15] = wi;
-        }
-        const uint64_t t1 = h + (cv_ror64(e, 14) ^ cv_ror64(e, 18) ^ cv_ror64(e, 41)) + ((e & f) ^ (~e & g)) +
-                            cv_k512(i) + wi;
-        const uint64_t t2 = (cv_ror64(a, 28) ^ cv_ror64(a, 34) ^ cv_ror64(a, 39)) + ((a & b) ^ (a & c) ^ (b & c));
-        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+#define CV_W_LO(j) w[(j)]
+#define CV_W_HI(j) w[8 + (j)]
+    CV_S512_8ROUNDS(0, CV_W_LO)
+    CV_S512_8ROUNDS(8, CV_W_HI)
+#pragma unroll 1
+    for (int p = 1; p < 5; p++) {
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+            w[j] += CV_S512_SSIG0(w[(j + 1) & 15]) + w[(j + 9) & 15] + CV_S512_SSIG1(w[(j + 14) & 15]);
+        CV_S512_8ROUNDS(16 * p, CV_W_LO)
+        CV_S512_8ROUNDS(16 * p + 8, CV_W_HI)
     }
+#undef CV_W_LO
+#undef CV_W_HI
     st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
@@ -114,33 +162,87 @@ CV_HD uint32_t msg_dword_le(const uint8_t *msg, uint32_t mlen, uint32_t t) {
     return v;
 }
 
-// SHA-512(pre[0:npre] || msg[0:mlen]) with npre in {32, 64} (pre as LE words); out = 16 LE words
+// The message dwords one SHA-512 block needs: dw[k] = aligned dword at floor4(msg + tstart) + 4k,
+// k < 33 (any 128 message bytes lie in 33 aligned dwords).  Only dwords holding at least one message
+// byte are read — dwords past the last one repeat it (their value is discarded by the padding rule
+// of the caller) — and a lane with no message byte in the window reads nothing, so a message that
+// ends at the very end of an allocation is never read past (the same guarantee as msg_dword_le).
+// One branch per block instead of two conditional loads per dword.
+CV_HD void sha512_msg_window(uint32_t dw[33], const uint8_t *msg, uint32_t mlen, uint32_t tstart) {
+    const uint32_t sh = (uint32_t)((uintptr_t)msg & 3u);              // tstart is a multiple of 4
+    const uint32_t rem = mlen > tstart ? mlen - tstart + sh : 0u;     // message bytes from the window base
+    const uint32_t kmax = rem >= 132 ? 33u : (rem + 3) >> 2;          // dwords holding message bytes
+#pragma unroll
+    for (int k = 0; k < 33; k++) dw[k] = 0;
+    if (kmax > 0) {
+        const uint32_t *p = reinterpret_cast<const uint32_t *>(msg + tstart - sh);
+#pragma unroll
+        for (int k = 0; k < 33; k++) {
+            const uint32_t kk = (uint32_t)k < kmax ? (uint32_t)k : kmax - 1;
+            dw[k] = p[kk];
+        }
+    }
+}
+
+// The 16 schedule words of SHA-512 block `blk` of pre[0:NPRE] || msg[0:mlen] || padding || length.
+// Message dword at offset t (a multiple of 4) = bytes msg[t..t+4) little-endian, funnel-shifted out
+// of the block's aligned window (Q0 = first window dword of the block: NPRE/4 in block 0, else 0,
+// a compile-time constant so the window stays in registers); bytes past mlen are the SHA padding
+// (0x80, zeros) — msg_dword_le's rules, applied branch-free.
+template <int NPRE, bool FIRST>
+CV_HD void sha512_block_words(uint64_t w[16], const uint32_t pre[16], const uint8_t *msg, uint32_t mlen, uint32_t blk,
+                              uint32_t total, uint64_t bits) {
+    const uint32_t tstart = FIRST ? 0u : blk * 128 - NPRE;
+    uint32_t dw[33];
+    sha512_msg_window(dw, msg, mlen, tstart);
+    const uint32_t sh8 = 8u * (uint32_t)((uintptr_t)msg & 3u);
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        uint32_t d[2];
+#pragma unroll
+        for (int hl = 0; hl < 2; hl++) {
+            const int jj = 2 * j + hl;                              // dword of the block
+            const uint32_t u = blk * 128 + 4 * jj;                  // stream offset of this dword
+            uint32_t le;
+            if (FIRST && jj < NPRE / 4) {
+                le = pre[jj];
+            } else {
+                const int q = FIRST ? jj - NPRE / 4 : jj;           // window dword (constant)
+                const uint32_t t = u - NPRE;                        // message offset
+                le = cv_funnel32(dw[q + 1], dw[q], sh8);
+                const uint32_t valid = mlen - t;                    // message bytes left at t
+                const uint32_t keep = valid >= 4 ? 0xffffffffu : ((1u << (8 * (valid & 3u))) - 1u);
+                const uint32_t pad = valid >= 4 ? 0u : (0x80u << (8 * (valid & 3u)));
+                le = (le & keep) | pad;
+                if (t > mlen) le = 0;
+            }
+            d[hl] = cv_bswap32(le);
+            if (u >= total - 8) d[hl] = (uint32_t)(bits >> (hl ? 0 : 32));
+        }
+        w[j] = ((uint64_t)d[0] << 32) | d[1];
+    }
+}
+
+// SHA-512(pre[0:NPRE] || msg[0:mlen]) with NPRE in {32, 64} (pre as LE words); out = 16 LE words
 // of the 64-byte digest (byte order as produced by the hash, i.e. digest byte k = out[k/4] >> 8(k%4)).
-__host__ __device__ __forceinline__ void sha512_pre_msg(uint32_t out[16], const uint32_t pre[16], int npre, const uint8_t *msg,
-                                               uint32_t mlen) {
+template <int NPRE>
+__host__ __device__ __forceinline__ void sha512_pre_msg_t(uint32_t out[16], const uint32_t pre[16], const uint8_t *msg,
+                                                          uint32_t mlen) {
     uint64_t st[8];
     sha512_init(st);
-    const uint32_t data = npre + mlen;
+    const uint32_t data = NPRE + mlen;
     const uint32_t nblocks = (data + 1 + 16 + 127) / 128;
     const uint32_t total = nblocks * 128;
     const uint64_t bits = (uint64_t)data * 8;
-#pragma nounroll
-    for (uint32_t blk = 0; blk < nblocks; blk++) {
+    {
         uint64_t w[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            uint32_t d[2];
-#pragma unroll
-            for (int hl = 0; hl < 2; hl++) {
-                const uint32_t u = blk * 128 + 8 * j + 4 * hl;    // stream offset of this dword
-                uint32_t le;
-                if (u < (uint32_t)npre) le = pre[u >> 2];
-                else le = msg_dword_le(msg, mlen, u - npre);
-                d[hl] = cv_bswap32(le);
-                if (u >= total - 8) d[hl] = (uint32_t)(bits >> (hl ? 0 : 32));
-            }
-            w[j] = ((uint64_t)d[0] << 32) | d[1];
-        }
+        sha512_block_words<NPRE, true>(w, pre, msg, mlen, 0, total, bits);
+        sha512_compress(st, w);
+    }
+#pragma nounroll
+    for (uint32_t blk = 1; blk < nblocks; blk++) {
+        uint64_t w[16];
+        sha512_block_words<NPRE, false>(w, pre, msg, mlen, blk, total, bits);
         sha512_compress(st, w);
     }
 #pragma unroll
@@ -148,6 +250,11 @@ __host__ __device__ __forceinline__ void sha512_pre_msg(uint32_t out[16], const 
         out[2 * i] = cv_bswap32((uint32_t)(st[i] >> 32));
         out[2 * i + 1] = cv_bswap32((uint32_t)st[i]);
     }
+}
+__host__ __device__ __forceinline__ void sha512_pre_msg(uint32_t out[16], const uint32_t pre[16], int npre,
+                                                        const uint8_t *msg, uint32_t mlen) {
+    if (npre == 32) sha512_pre_msg_t<32>(out, pre, msg, mlen);
+    else sha512_pre_msg_t<64>(out, pre, msg, mlen);
 }
 
 // ---------------------------------------------------------------- SHA-256

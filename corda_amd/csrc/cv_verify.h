@@ -755,13 +755,14 @@ __host__ __device__ inline int cv_pmt_verify(uint32_t b, uint32_t e, const uint8
 // cv_verify_prep + cv_hs_prep in one pass: hash and scalars, lattice + packed digits, then the A and
 // R decodes interleaved (ge_decode2_0_1_0), then the two odd-multiple tables.  ok_out = key_ok AND
 // r_ok (the verdict mask); returns key_ok (the status byte).
+// The fused prep after the hash: hs = h || effective s (cv_keyed_hs, or the GPU kernel's wave-staged
+// hash of the same bytes).
 template <bool LAT = false>
-__host__ __device__ __forceinline__ bool cv_hs_prep_fused(const uint32_t aw[8], const uint32_t rw[8], const uint32_t sw[8],
-                                                          const uint8_t *msg, uint32_t mlen, uint32_t *dig, size_t stride,
-                                                          uint32_t *tabA, uint32_t *tabR, bool &ok_out) {
+__host__ __device__ __forceinline__ bool cv_hs_prep_fused_hs(const uint32_t aw[8], const uint32_t rw[8],
+                                                             const uint32_t hs[CV_HS_WORDS], uint32_t *dig,
+                                                             size_t stride, uint32_t *tabA, uint32_t *tabR,
+                                                             bool &ok_out) {
     {
-        uint32_t hs[CV_HS_WORDS];
-        cv_keyed_hs(aw, rw, sw, msg, mlen, hs);            // h = SHA-512(R || Abyte || M) mod L, effective s
         uint32_t h[8], s[8], u[8], v[8], w[8];
 #pragma unroll
         for (int q = 0; q < 8; q++) { h[q] = hs[q]; s[q] = hs[8 + q]; }
@@ -794,6 +795,14 @@ __host__ __device__ __forceinline__ bool cv_hs_prep_fused(const uint32_t aw[8], 
     ge_cached_multiples8(tabR, P[1]);
     ok_out = key_ok && r_ok;
     return key_ok;
+}
+template <bool LAT = false>
+__host__ __device__ __forceinline__ bool cv_hs_prep_fused(const uint32_t aw[8], const uint32_t rw[8], const uint32_t sw[8],
+                                                          const uint8_t *msg, uint32_t mlen, uint32_t *dig, size_t stride,
+                                                          uint32_t *tabA, uint32_t *tabR, bool &ok_out) {
+    uint32_t hs[CV_HS_WORDS];
+    cv_keyed_hs(aw, rw, sw, msg, mlen, hs);            // h = SHA-512(R || Abyte || M) mod L, effective s
+    return cv_hs_prep_fused_hs<LAT>(aw, rw, hs, dig, stride, tabA, tabR, ok_out);
 }
 
 // Single-signature convenience of the fused schedule (host harness).

@@ -28,7 +28,7 @@ EXPORTED = (
     "cv_ed25519_verify_batch", "cv_merkle_tx_ids", "cv_merkle_tx_ids_ex", "cv_ed25519_sign_batch",
     "cv_tx_verdicts", "cv_ed25519_verify_device", "cv_ed25519_verify_device_timed", "cv_ed25519_sign_device", "cv_merkle_tx_ids_device",
     "cv_synchronize", "cv_calibrate", "cv_ed25519_verify_batch_keyed", "cv_key_cache_reserve", "cv_key_cache_stats",
-    "cv_ed25519_verify_device_keyed", "cv_partial_merkle_verify",
+    "cv_ed25519_verify_device_keyed", "cv_partial_merkle_verify", "cv_calibrate_cycles", "cv_diag_prep_phases",
 )
 
 
@@ -120,6 +120,12 @@ def load():
             lib.cv_ed25519_verify_device_keyed.restype = ctypes.c_int
         lib.cv_calibrate.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         lib.cv_calibrate.restype = ctypes.c_int
+        if hasattr(lib, "cv_calibrate_cycles"):                 # absent only in pre-r02 A/B builds
+            lib.cv_calibrate_cycles.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+            lib.cv_calibrate_cycles.restype = ctypes.c_int
+            lib.cv_diag_prep_phases.argtypes = [_vp, ctypes.c_int, _sz, _vp, _vp, _vp, _vp, _vp,
+                                                ctypes.POINTER(ctypes.c_double)]
+            lib.cv_diag_prep_phases.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -327,6 +333,22 @@ class Engine:
         a, b = ctypes.c_double(0), ctypes.c_double(0)
         _check(self._lib.cv_calibrate(self._h, device, ctypes.byref(a), ctypes.byref(b)), "cv_calibrate")
         return a.value, b.value
+
+    def calibrate_cycles(self, device: int) -> dict:
+        """The v_mad_u64_u32 peak on a cycle basis (cv_calibrate_cycles)."""
+        o = (ctypes.c_double * 5)()
+        _check(self._lib.cv_calibrate_cycles(self._h, device, o), "cv_calibrate_cycles")
+        return {"mac_per_s": o[0], "clock_ghz": o[1], "cycles_per_wave_instr": o[2], "simds": int(o[3]),
+                "mac_per_s_at_2p4ghz": o[4]}
+
+    def diag_prep_phases(self, device: int, n: int, d_pk: int, d_sig: int, d_arena: int, d_off: int,
+                         d_len: int) -> dict:
+        """Mean shader cycles per wave of each fused-prep phase (cv_diag_prep_phases)."""
+        o = (ctypes.c_double * 8)()
+        _check(self._lib.cv_diag_prep_phases(self._h, device, n, d_pk, d_sig, d_arena, d_off, d_len, o),
+               "cv_diag_prep_phases")
+        return {"hash": o[0], "lattice": o[1], "digits": o[2], "decode": o[3], "tables": o[4], "total": o[5],
+                "waves": int(o[6]), "hash_sha512_part": o[7]}
 
     def synchronize(self, device: int):
         _check(self._lib.cv_synchronize(self._h, device), "cv_synchronize")

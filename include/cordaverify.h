@@ -186,6 +186,18 @@ int cv_synchronize(cv_ctx *ctx, int device);
  */
 int cv_calibrate(cv_ctx *ctx, int device, double *mad_per_s, double *femul_per_s);
 
+/* The same multiply-accumulate peak on a cycle basis: out[5] = {MAC/s, shader clock in GHz read
+ * in-kernel (s_memtime over s_memrealtime), cycles per v_mad_u64_u32 wave-instruction per SIMD,
+ * SIMD count, MAC/s ceiling at the 2.4 GHz peak clock for that cycle count}. */
+int cv_calibrate_cycles(cv_ctx *ctx, int device, double *out);
+
+/* Diagnostics (no reference counterpart): shader cycles per wave of each phase of the throughput
+ * prep kernel on a device-resident batch (n <= 2^21) — out[8] = {hash, lattice, digits, decode
+ * A+R, tables, total, waves, SHA-512 part of hash}.  Writes the device's verify workspace; not thread-safe with verifies
+ * on the same device. */
+int cv_diag_prep_phases(cv_ctx *ctx, int device, size_t n, const void *d_pk, const void *d_sig,
+                        const void *d_arena, const void *d_off, const void *d_len, double *out);
+
 #ifdef __cplusplus
 }
 #endif
