@@ -6,7 +6,9 @@
 #include <algorithm>
 #include <array>
 #include <cstring>
+#include <chrono>
 #include <mutex>
+#include <random>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -71,12 +73,37 @@ struct DevBuf {
 // Device-resident per-key comb tables (keyed verify), content-addressed by the
 // 32 key bytes.  A key's tables are computed once (cv_keyprep_kernel) and reused by every later
 // batch on that device; when the pool is full it is emptied (epoch reset) before new keys go in.
+// Key bytes come from untrusted submitters (and invalid keys are deduped before decoding), so the
+// host hash tables hash all 32 bytes with a per-process random seed: a batch of keys that share some
+// bytes cannot pile into one probe chain.  64-bit multiply-xorshift mixing of the four words, each
+// folded with its own seed (a keyed hash in the wyhash / murmur-finaliser family: not cryptographic,
+// only unpredictable to the submitter).
+static uint64_t key_seed(int k) {
+    static const std::array<uint64_t, 5> seeds = [] {
+        std::random_device rd;
+        std::array<uint64_t, 5> s{};
+        for (auto &x : s) x = ((uint64_t)rd() << 32) ^ rd() ^ (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+        return s;
+    }();
+    return seeds[k];
+}
+static inline uint64_t mix64(uint64_t x) {
+    x ^= x >> 32;
+    x *= 0xd6e8feb86659fd93ull;
+    x ^= x >> 32;
+    x *= 0xd6e8feb86659fd93ull;
+    x ^= x >> 32;
+    return x;
+}
+static inline uint64_t key_hash32(const uint8_t *k) {
+    uint64_t w[4];
+    std::memcpy(w, k, 32);
+    uint64_t h = key_seed(4);
+    for (int i = 0; i < 4; i++) h = mix64(h ^ (w[i] + key_seed(i)) * 0x9E3779B97F4A7C15ull) + (uint64_t)i;
+    return h;
+}
 struct KeyHash {
-    size_t operator()(const std::array<uint8_t, 32> &k) const {
-        size_t h;
-        std::memcpy(&h, k.data() + 8, sizeof h);   // key bytes are uniformly distributed curve points
-        return h;
-    }
+    size_t operator()(const std::array<uint8_t, 32> &k) const { return (size_t)key_hash32(k.data()); }
 };
 struct KeyCache {
     DevBuf ktab, kok, keys, slots, slot_of_key, key_index, scratch;
@@ -94,6 +121,9 @@ struct Device {
                                          // R record 128 B, ok 1 B, half-size digits 260 B
     uint32_t ws_cap = 0;
     KeyCache kc;
+    // the last stream that used the shared workspace / key pool, and an event after its use
+    hipStream_t ws_last = nullptr;
+    hipEvent_t ws_ev = nullptr;
 };
 
 // key-table pool capacity per device (keys); 4 KB of tables per key
@@ -119,13 +149,32 @@ hipError_t ensure_verify_ws(Device &d, size_t n) {
     return hipSuccess;
 }
 
+// Every use of a device's shared state (the verify workspace, the key pool) is ordered across
+// streams: a launch group enqueued on stream s first waits for the previous group when that ran on
+// another stream (ws_begin), and marks its own end (ws_end).  Device-pointer calls may therefore be
+// made on any streams; they serialise on the workspace instead of racing on it.  Callers hold
+// ctx->mu around ws_begin .. ws_end.
+hipError_t ws_begin(Device &d, hipStream_t s) {
+    hipError_t e = hipSuccess;
+    if (!d.ws_ev && (e = hipEventCreateWithFlags(&d.ws_ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if (d.ws_last && d.ws_last != s) e = hipStreamWaitEvent(s, d.ws_ev, 0);
+    return e;
+}
+hipError_t ws_end(Device &d, hipStream_t s) {
+    d.ws_last = s;
+    return hipEventRecord(d.ws_ev, s);
+}
+
 hipError_t launch_verify(Device &d, uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
                          const uint64_t *off, const uint32_t *len, uint64_t *bitmap, uint8_t *status, hipStream_t s,
                          hipEvent_t *ev = nullptr) {
     hipError_t e = ensure_verify_ws(d, n);
+    if (e == hipSuccess) e = ws_begin(d, s);
     if (e != hipSuccess) return e;
-    return cvk_verify(n, pk, sig, arena, off, len, bitmap, status, d.ws_hs.as<uint32_t>(), d.ws_tab.as<uint32_t>(),
-                      d.ws_R.as<uint32_t>(), d.ws_ok.as<uint8_t>(), d.ws_dig.as<uint32_t>(), d.ws_cap, s, ev);
+    e = cvk_verify(n, pk, sig, arena, off, len, bitmap, status, d.ws_hs.as<uint32_t>(), d.ws_tab.as<uint32_t>(),
+                   d.ws_R.as<uint32_t>(), d.ws_ok.as<uint8_t>(), d.ws_dig.as<uint32_t>(), d.ws_cap, s, ev);
+    const hipError_t e2 = ws_end(d, s);
+    return e != hipSuccess ? e : e2;
 }
 
 int hip_rc(hipError_t e) {
@@ -164,6 +213,13 @@ const char *cv_strerror(int code) {
     }
 }
 
+// Test knob (internal, not in the header): every device of the next cv_open appears k times in the
+// context — k independent Device slots (own stream, buffers, workspace, key pool) on one GPU — so the
+// multi-device host path (for_each_shard: one thread per slot, 64-aligned shard ranges, per-slot
+// dedupe and key pools) runs and is tested on a one-GPU box.  0 / 1 = off.
+static int g_virtual_devices = 1;
+void cvk_set_virtual_devices(int k) { g_virtual_devices = (k >= 1 && k <= 16) ? k : 1; }
+
 int cv_open(uint32_t device_mask, cv_ctx **out) {
     if (!out) return CV_E_ARGS;
     *out = nullptr;
@@ -173,13 +229,16 @@ int cv_open(uint32_t device_mask, cv_ctx **out) {
     if (!ctx) return CV_E_OOM;
     for (int d = 0; d < count && d < 32; d++) {
         if (device_mask && !(device_mask & (1u << d))) continue;
-        Device dev;
-        dev.ordinal = d;
-        if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&dev.stream, hipStreamNonBlocking) != hipSuccess) {
-            cv_close(ctx);
-            return CV_E_HIP;
+        for (int v = 0; v < g_virtual_devices; v++) {
+            Device dev;
+            dev.ordinal = d;
+            if (hipSetDevice(d) != hipSuccess ||
+                hipStreamCreateWithFlags(&dev.stream, hipStreamNonBlocking) != hipSuccess) {
+                cv_close(ctx);
+                return CV_E_HIP;
+            }
+            ctx->devs.push_back(dev);
         }
-        ctx->devs.push_back(dev);
     }
     if (ctx->devs.empty()) {
         delete ctx;
@@ -198,6 +257,7 @@ void cv_close(cv_ctx *ctx) {
                           &d.digest, &d.ids, &d.pmt, &d.ws_hs, &d.ws_tab, &d.ws_R, &d.ws_ok, &d.ws_dig, &d.kc.ktab, &d.kc.kok,
                           &d.kc.keys, &d.kc.slots, &d.kc.slot_of_key, &d.kc.key_index, &d.kc.scratch})
             b->release();
+        if (d.ws_ev) (void)hipEventDestroy(d.ws_ev);
         if (d.stream) (void)hipStreamDestroy(d.stream);
     }
     delete ctx;
@@ -345,6 +405,7 @@ static int verify_shard_keyed(uint32_t cap, Device &d, size_t b, size_t e, size_
     }
     if (hi < lo) hi = lo;
     hipStream_t s = d.stream;
+    CV_TRY(ws_begin(d, s));
     std::vector<uint32_t> sok;
     int rc = key_resolve(d, cap, nkeys, keys, used.data(), sok, s);
     if (rc != CV_OK) return rc;
@@ -372,6 +433,7 @@ static int verify_shard_keyed(uint32_t cap, Device &d, size_t b, size_t e, size_
                             d.arena.as<uint8_t>() - lo, d.off.as<uint64_t>(), d.len.as<uint32_t>(),
                             d.bitmap.as<uint64_t>(), status ? d.status.as<uint8_t>() : nullptr, d.ws_hs.as<uint32_t>(),
                             d.ws_R.as<uint32_t>(), d.ws_ok.as<uint8_t>(), d.ws_cap, s, nullptr));
+    CV_TRY(ws_end(d, s));
     CV_TRY(hipMemcpyAsync(bitmap + b / 64, d.bitmap.p, words * 8, hipMemcpyDeviceToHost, s));
     if (status) CV_TRY(hipMemcpyAsync(status + b, d.status.p, n, hipMemcpyDeviceToHost, s));
     CV_TRY(hipStreamSynchronize(s));
@@ -380,8 +442,8 @@ static int verify_shard_keyed(uint32_t cap, Device &d, size_t b, size_t e, size_
 
 // Host-side key dedupe for the plain entry point: keys[] = distinct key bytes, key_index[i] = its
 // index.  Returns false when the batch does not repeat keys enough for the keyed path to pay (it
-// gives up as soon as more than n/2 distinct keys have been seen).  Flat open addressing on the key
-// bytes (they are uniformly distributed curve-point encodings), no per-key allocation.
+// gives up as soon as more than n/2 distinct keys have been seen).  Flat open addressing on the
+// seeded hash of all 32 key bytes (key_hash32), no per-key allocation.
 static bool dedupe_keys(size_t n, const uint8_t *pk, std::vector<uint8_t> &keys, std::vector<uint32_t> &key_index) {
     if (n < 64 || n > kAutoKeyedMax) return false;
     size_t cap = 64;
@@ -394,9 +456,7 @@ static bool dedupe_keys(size_t n, const uint8_t *pk, std::vector<uint8_t> &keys,
     uniq_sig.reserve(n / 2 + 1);
     for (size_t i = 0; i < n; i++) {
         const uint8_t *k = pk + 32 * i;
-        uint64_t h;
-        std::memcpy(&h, k + 8, sizeof h);
-        size_t bkt = (size_t)(h * 0x9E3779B97F4A7C15ull >> 20) & (cap - 1);
+        size_t bkt = (size_t)key_hash32(k) & (cap - 1);
         for (;;) {
             const uint32_t f = first[bkt];
             if (f == UINT32_MAX) {
@@ -420,6 +480,20 @@ static bool dedupe_keys(size_t n, const uint8_t *pk, std::vector<uint8_t> &keys,
 }
 
 extern "C" {
+
+// Diagnostic: the host-side key dedupe of cv_ed25519_verify_batch on its own (no device needed).
+int cv_diag_dedupe_keys(size_t n, const uint8_t *pk, uint32_t *key_index, size_t *nkeys) {
+    if (!pk || !key_index || !nkeys) return CV_E_ARGS;
+    std::vector<uint8_t> keys;
+    std::vector<uint32_t> idx;
+    if (!dedupe_keys(n, pk, keys, idx)) {
+        *nkeys = 0;
+        return 0;
+    }
+    std::memcpy(key_index, idx.data(), n * sizeof(uint32_t));
+    *nkeys = keys.size() / 32;
+    return 1;
+}
 
 int cv_ed25519_verify_batch(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg_arena,
                             const uint64_t *msg_off, const uint32_t *msg_len, uint64_t *verdict_bitmap,
@@ -633,6 +707,7 @@ int cv_ed25519_verify_device(cv_ctx *ctx, int device, size_t n, const void *d_pk
     if (n > 0xffffffffull) return CV_E_TOO_LARGE;
     Device *d = find_dev(ctx, device);
     if (!d || !d_pk || !d_sig || !d_arena || !d_off || !d_len || !d_bitmap) return CV_E_ARGS;
+    std::lock_guard<std::mutex> g(ctx->mu);            // enqueue only; ordered on the workspace (ws_begin)
     CV_TRY(hipSetDevice(d->ordinal));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : d->stream;
     CV_TRY(launch_verify(*d, (uint32_t)n, static_cast<const uint8_t *>(d_pk), static_cast<const uint8_t *>(d_sig),
@@ -651,6 +726,7 @@ int cv_ed25519_verify_device_timed(cv_ctx *ctx, int device, size_t n, const void
     if (n > 0xffffffffull) return CV_E_TOO_LARGE;
     Device *d = find_dev(ctx, device);
     if (!d || !d_pk || !d_sig || !d_arena || !d_off || !d_len || !d_bitmap) return CV_E_ARGS;
+    std::lock_guard<std::mutex> g(ctx->mu);
     CV_TRY(hipSetDevice(d->ordinal));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : d->stream;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -696,6 +772,7 @@ int cv_ed25519_verify_device_keyed(cv_ctx *ctx, int device, size_t n, size_t nke
     if (phase_ms)
         for (int k = 0; k < 5 && e == hipSuccess; k++) e = hipEventCreate(&ev[k]);
     if (e == hipSuccess && phase_ms) e = hipEventRecord(ev[0], s);
+    if (e == hipSuccess) e = ws_begin(*d, s);
     std::vector<uint32_t> sok;
     int rc = e == hipSuccess ? key_resolve(*d, ctx->key_cap, nkeys, hkeys.data(), nullptr, sok, s) : hip_rc(e);
     KeyCache &kc = d->kc;
@@ -710,6 +787,10 @@ int cv_ed25519_verify_device_keyed(cv_ctx *ctx, int device, size_t n, size_t nke
                                      static_cast<const uint32_t *>(d_len), static_cast<uint64_t *>(d_bitmap),
                                      static_cast<uint8_t *>(d_status), d->ws_hs.as<uint32_t>(), d->ws_R.as<uint32_t>(),
                                      d->ws_ok.as<uint8_t>(), d->ws_cap, s, phase_ms ? ev + 1 : nullptr));
+    if (d->ws_ev) {
+        const hipError_t e2 = ws_end(*d, s);
+        if (rc == CV_OK) rc = hip_rc(e2);
+    }
     if (rc == CV_OK && phase_ms) {
         e = hipEventSynchronize(ev[4]);
         for (int k = 0; k < 4 && e == hipSuccess; k++) e = hipEventElapsedTime(&phase_ms[k], ev[k], ev[k + 1]);
@@ -855,10 +936,12 @@ int cv_diag_prep_phases(cv_ctx *ctx, int device, size_t n, const void *d_pk, con
     const size_t waves = (n + 63) / 64;
     uint64_t *st = nullptr;
     CV_TRY(hipMalloc(&st, waves * 64));
+    CV_TRY(ws_begin(*d, d->stream));
     hipError_t e = cvk_prep_probe((uint32_t)n, static_cast<const uint8_t *>(d_pk), static_cast<const uint8_t *>(d_sig),
                                   static_cast<const uint8_t *>(d_arena), static_cast<const uint64_t *>(d_off),
                                   static_cast<const uint32_t *>(d_len), d->ws_dig.as<uint32_t>(), d->ws_tab.as<uint32_t>(),
                                   d->ws_cap, st, d->stream);
+    if (e == hipSuccess) e = ws_end(*d, d->stream);
     std::vector<uint64_t> h(waves * 8);
     if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
     if (e == hipSuccess) e = hipMemcpy(h.data(), st, waves * 64, hipMemcpyDeviceToHost);

@@ -325,7 +325,8 @@ struct SplitAux {
     hipStream_t s2 = nullptr;
     hipEvent_t start = nullptr, prep1 = nullptr, done2 = nullptr;
     int cus = 0;
-    std::mutex mu;   // record/wait of the shared events is enqueued under it (callers on other threads)
+    bool ready = false;
+    std::mutex mu;   // creation, and record/wait of the shared events, happen under it
 };
 static SplitAux g_split_aux[16];
 static hipError_t split_aux(SplitAux **out) {
@@ -334,12 +335,15 @@ static hipError_t split_aux(SplitAux **out) {
     if (e != hipSuccess) return e;
     if (dev < 0 || dev >= 16) return hipErrorInvalidDevice;
     SplitAux &a = g_split_aux[dev];
-    if (!a.s2) {
-        if ((e = hipStreamCreateWithFlags(&a.s2, hipStreamNonBlocking)) != hipSuccess) return e;
-        if ((e = hipEventCreateWithFlags(&a.start, hipEventDisableTiming)) != hipSuccess) return e;
-        if ((e = hipEventCreateWithFlags(&a.prep1, hipEventDisableTiming)) != hipSuccess) return e;
-        if ((e = hipEventCreateWithFlags(&a.done2, hipEventDisableTiming)) != hipSuccess) return e;
+    // lazily created once per device; the lock makes two first callers (different threads) safe
+    std::lock_guard<std::mutex> lk(a.mu);
+    if (!a.ready) {
+        if (!a.s2 && (e = hipStreamCreateWithFlags(&a.s2, hipStreamNonBlocking)) != hipSuccess) return e;
+        if (!a.start && (e = hipEventCreateWithFlags(&a.start, hipEventDisableTiming)) != hipSuccess) return e;
+        if (!a.prep1 && (e = hipEventCreateWithFlags(&a.prep1, hipEventDisableTiming)) != hipSuccess) return e;
+        if (!a.done2 && (e = hipEventCreateWithFlags(&a.done2, hipEventDisableTiming)) != hipSuccess) return e;
         if ((e = hipDeviceGetAttribute(&a.cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+        a.ready = true;
     }
     *out = &a;
     return hipSuccess;

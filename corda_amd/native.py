@@ -29,6 +29,7 @@ EXPORTED = (
     "cv_tx_verdicts", "cv_ed25519_verify_device", "cv_ed25519_verify_device_timed", "cv_ed25519_sign_device", "cv_merkle_tx_ids_device",
     "cv_synchronize", "cv_calibrate", "cv_ed25519_verify_batch_keyed", "cv_key_cache_reserve", "cv_key_cache_stats",
     "cv_ed25519_verify_device_keyed", "cv_partial_merkle_verify", "cv_calibrate_cycles", "cv_diag_prep_phases",
+    "cv_diag_dedupe_keys",
 )
 
 
@@ -126,6 +127,8 @@ def load():
             lib.cv_diag_prep_phases.argtypes = [_vp, ctypes.c_int, _sz, _vp, _vp, _vp, _vp, _vp,
                                                 ctypes.POINTER(ctypes.c_double)]
             lib.cv_diag_prep_phases.restype = ctypes.c_int
+            lib.cv_diag_dedupe_keys.argtypes = [_sz, _vp, _vp, ctypes.POINTER(_sz)]
+            lib.cv_diag_dedupe_keys.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -352,6 +355,20 @@ class Engine:
 
     def synchronize(self, device: int):
         _check(self._lib.cv_synchronize(self._h, device), "cv_synchronize")
+
+
+def dedupe_keys(pk: np.ndarray):
+    """The engine's host-side key dedupe (cv_diag_dedupe_keys): (key_index, nkeys) or None when the
+    batch would not take the keyed path.  Runs on the host; no device needed."""
+    lib = load()
+    pk = _u8(pk, 32)
+    n = len(pk)
+    idx = np.zeros(n, np.uint32)
+    nk = ctypes.c_size_t(0)
+    rc = lib.cv_diag_dedupe_keys(n, _p(pk), _p(idx), ctypes.byref(nk))
+    if rc < 0:
+        raise CvError(rc, "cv_diag_dedupe_keys")
+    return (idx, int(nk.value)) if rc == 1 else None
 
 
 def tx_verdicts(bitmap: np.ndarray, tx_sig_begin) -> np.ndarray:

@@ -143,6 +143,9 @@ int cv_tx_verdicts(size_t ntx, const uint64_t *verdict_bitmap, const uint32_t *t
  * A large batch may internally run part of its work on a per-device helper stream of the engine (the
  * drain overlap, DESIGN.md "Schedules"); `stream` waits on that work before anything the caller
  * enqueues after the call, so completion is still stream-ordered on `stream`.
+ * Calls may use different streams, from any thread: the engine orders every use of a device's shared
+ * verify workspace and key pool (a call on a new stream first waits for the previous call's work on
+ * that workspace), so concurrent calls serialise on the device instead of racing.
  */
 int cv_ed25519_verify_device(cv_ctx *ctx, int device, size_t n, const void *d_pk, const void *d_sig,
                              const void *d_arena, const void *d_off, const void *d_len, void *d_bitmap,
@@ -151,7 +154,7 @@ int cv_ed25519_verify_device(cv_ctx *ctx, int device, size_t n, const void *d_pk
 /* Measurement entry point (bench.py): as cv_ed25519_verify_device (no status), but synchronous,
  * whole-chunk launches only (no drain overlap), and fills phase_ms[0..2] with the summed durations
  * of the verify kernels measured with HIP events on the launch stream.  Half-size schedule (default):
- * fused prep (decodes, challenge hash, lattice, digits, tables) | unused (0) | hs_straus (multi-scalar
+ * challenge hash | fused prep (decodes, lattice, digits, tables) | hs_straus (multi-scalar
  * multiplication + verdict bits).  Full-width schedule: prep | Straus | finish (batched inversion,
  * encode, compare, bitmap). */
 int cv_ed25519_verify_device_timed(cv_ctx *ctx, int device, size_t n, const void *d_pk, const void *d_sig,
@@ -197,6 +200,12 @@ int cv_calibrate_cycles(cv_ctx *ctx, int device, double *out);
  * on the same device. */
 int cv_diag_prep_phases(cv_ctx *ctx, int device, size_t n, const void *d_pk, const void *d_sig,
                         const void *d_arena, const void *d_off, const void *d_len, double *out);
+
+/* Diagnostics: the host-side key dedupe cv_ed25519_verify_batch runs before choosing the keyed path
+ * (seeded hash of all 32 key bytes).  Returns 1 and fills key_index[n] / *nkeys when the batch
+ * repeats keys enough for the keyed path (64 <= n <= 2^18, at least two signatures per distinct
+ * key), else 0.  Host only: needs no device and no context. */
+int cv_diag_dedupe_keys(size_t n, const uint8_t *pk, uint32_t *key_index, size_t *nkeys);
 
 #ifdef __cplusplus
 }

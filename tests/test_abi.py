@@ -62,3 +62,34 @@ def test_bitmap_to_bools():
     bm = np.array([1 | (1 << 63), 2], np.uint64)
     b = native.bitmap_to_bools(bm, 66)
     assert b[0] and b[63] and b[65] and not b[64] and b.sum() == 3
+
+
+def test_dedupe_maps_repeated_keys():
+    """Host key dedupe (the auto-keyed decision of cv_ed25519_verify_batch): every signature maps to
+    the distinct key with its bytes, first-seen order."""
+    rng = np.random.default_rng(7)
+    keys = rng.integers(0, 256, (100, 32), dtype=np.uint8)
+    order = rng.integers(0, 100, 1000)
+    order[:100] = np.arange(100)                           # every key appears, first in index order
+    pk = keys[order]
+    idx, nk = native.dedupe_keys(pk)
+    assert nk == 100
+    assert np.array_equal(idx, order)
+    assert native.dedupe_keys(rng.integers(0, 256, (1000, 32), dtype=np.uint8)) is None   # all distinct
+
+
+def test_dedupe_resists_shared_key_bytes():
+    """keys are untrusted, so a batch whose keys agree on bytes 8..15 (the old hash input)
+    must not collapse into one probe chain.  2^17 distinct keys x 2 signatures, all sharing bytes
+    0..23 and differing only in the last 8: the seeded all-bytes hash keeps the dedupe linear."""
+    import time
+    n_keys = 1 << 17
+    base = np.full(32, 0xA5, np.uint8)
+    keys = np.tile(base, (n_keys, 1))
+    keys[:, 24:32] = np.arange(n_keys, dtype=np.uint64).view(np.uint8).reshape(n_keys, 8)
+    pk = np.concatenate([keys, keys])
+    t = time.perf_counter()
+    idx, nk = native.dedupe_keys(pk)
+    dt = time.perf_counter() - t
+    assert nk == n_keys and np.array_equal(idx[:n_keys], np.arange(n_keys)) and np.array_equal(idx[n_keys:], idx[:n_keys])
+    assert dt < 2.0, f"dedupe of 2^18 adversarial keys took {dt:.2f} s"

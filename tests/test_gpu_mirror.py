@@ -225,3 +225,82 @@ def test_c1_loadtest_self_issue_10k(engine, oracle_c):
         else:
             with pytest.raises(SignatureException):
                 stxs[t].verify_signatures(engine=engine)
+
+
+def _jvm_shim_verify_all(engine, items):
+    """Line-by-line restatement of INTEGRATION.md's Kotlin GpuVerify.verifyAll: prefilter failures
+    recorded per item, one native call over the rest, per-item exceptions in input order."""
+    n = len(items)
+    out = [None] * n
+    live = []
+    for i, (key, _content, bits) in enumerate(items):
+        if not isinstance(key, EdDSAPublicKey):
+            out[i] = InvalidKeyException(f"cannot identify EdDSA public key: {type(key).__name__}")
+        elif len(bits) != 64:
+            out[i] = SignatureException("signature length is wrong")
+        else:
+            live.append(i)
+    if not live:
+        return out
+    m = len(live)
+    pk = np.stack([np.frombuffer(items[i][0].encoded, np.uint8) for i in live])
+    sig = np.stack([np.frombuffer(items[i][2], np.uint8) for i in live])
+    lens = np.array([len(items[i][1]) for i in live], np.uint32)
+    offs = np.zeros(m, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    arena = np.frombuffer(b"".join(items[i][1] for i in live) + b"\0" * 16, np.uint8)
+    bitmap, status = engine.verify_batch(pk, sig, arena, offs, lens)
+    valid = native.bitmap_to_bools(bitmap, m)
+    for j, i in enumerate(live):
+        if status[j] == native.CV_SIG_BAD_KEY:
+            out[i] = InvalidKeyException("not a valid GroupElement")
+        elif not valid[j]:
+            out[i] = SignatureException("Signature did not match")
+    return out
+
+
+def _shim_check_signatures(engine, sigs, content):
+    """INTEGRATION.md checkSignaturesAreValid: throw the first failure in input order."""
+    for e in _jvm_shim_verify_all(engine, [(s.by, content, s.bytes) for s in sigs]):
+        if e is not None:
+            raise e
+
+
+def _reference_check_signatures(sigs, content):
+    """SignedTransaction.kt:84-86: `for (sig in sigs) sig.verifyWithECDSA(id.bytes)`, one verify
+    (CryptoUtilities.kt:90-96) per signature in list order."""
+    for s in sigs:
+        s.verify_with_ecdsa(content)
+
+
+def test_jvm_shim_first_failure_order(engine):
+    """the JVM shim must throw the reference's first failure in list order,
+    whatever its kind.  Every ordering of {good, bad bits, NullPublicKey, 63-byte signature} (and with
+    a repeated failure) through the Kotlin logic restated above vs the sequential reference loop:
+    same exception type and message, or both pass."""
+    import itertools
+    s, pk = keypair(40)
+    content = bytes(range(32))
+    good = DigitalSignature.WithKey(pk, sign(s, content))
+    bad = DigitalSignature.WithKey(pk, sign(s, content[::-1]))
+    null = DigitalSignature.WithKey(NullPublicKey, b"\x01" * 64)
+    short = DigitalSignature.WithKey(pk, sign(s, content)[:63])
+    pool = {"good": good, "bad": bad, "null": null, "short": short}
+    cases = list(itertools.permutations(pool, 4)) + list(itertools.permutations(["good", "bad", "bad", "null"], 4))
+    cases += [("good",), ("good", "good"), ("short", "good"), ("null",)]
+    for names in cases:
+        sigs = [pool[k] for k in names]
+        ref = shim = None
+        try:
+            _reference_check_signatures(sigs, content)
+        except Exception as e:          # noqa: BLE001 - comparing exact exception kinds
+            ref = e
+        try:
+            _shim_check_signatures(engine, sigs, content)
+        except Exception as e:          # noqa: BLE001
+            shim = e
+        assert type(ref) is type(shim), f"{names}: reference {ref!r}, shim {shim!r}"
+        assert str(ref) == str(shim), f"{names}: reference {ref!r}, shim {shim!r}"
+    # the round-1 shim's failure case, spelled out
+    with pytest.raises(SignatureException, match="did not match"):
+        _shim_check_signatures(engine, [bad, null], content)
