@@ -135,18 +135,21 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsprep_kernel(uint32_t n, uint
     if (!r_ok) ws_ok[i] = 0;
 }
 
-// challenge hash of the half-size group: ws_hs = h || effective s per signature (64 B), with h =
-// SHA-512(R || Abyte || M) mod L.  Its own kernel so it runs at the occupancy its ~110 VGPRs allow
-// (4 waves per SIMD): inside the 256-VGPR fused prep (2 waves per SIMD) the hash was 32 % of the
-// prep's cycles (tools/prep_probe.py, profiles/r02_prep_probe.json) — a serial 64-bit chain per lane
-// that two waves per SIMD cannot cover.
-__global__ __launch_bounds__(CV_BLOCK, 4) void cv_hash_kernel(uint32_t n, const uint8_t *__restrict__ pk,
-                                                              const uint8_t *__restrict__ sig,
-                                                              const uint8_t *__restrict__ arena,
-                                                              const uint64_t *__restrict__ off,
-                                                              const uint32_t *__restrict__ len,
-                                                              uint32_t *__restrict__ ws_hs) {
-    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
+// scalars of the half-size group, one lane per signature: h = SHA-512(R || Abyte || M) mod L, the
+// effective S, the lattice (u, v, w) and the packed window digits -> ws_dig (cv_hs_scalars).  Its own
+// kernel, at the occupancy its registers allow (3 waves per SIMD), because inside the 256-VGPR point
+// kernel (2 waves per SIMD) the hash's serial 64-bit chains were 32 % of the prep's cycles
+// (tools/prep_probe.py).  Any block size (small latency batches launch 64-thread blocks so the few
+// waves spread over CUs).
+template <bool LAT>
+__global__ __launch_bounds__(CV_BLOCK, 3) void cv_scalars_kernel(uint32_t n, uint32_t cap,
+                                                                 const uint8_t *__restrict__ pk,
+                                                                 const uint8_t *__restrict__ sig,
+                                                                 const uint8_t *__restrict__ arena,
+                                                                 const uint64_t *__restrict__ off,
+                                                                 const uint32_t *__restrict__ len,
+                                                                 uint32_t *__restrict__ ws_dig) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t aw[8], rw[8], sw[8];
     load_words8(aw, pk + (size_t)i * 32);
@@ -154,33 +157,52 @@ __global__ __launch_bounds__(CV_BLOCK, 4) void cv_hash_kernel(uint32_t n, const 
     load_words8(sw, sig + (size_t)i * 64 + 32);
     uint32_t hs[CV_HS_WORDS];
     cv_keyed_hs(aw, rw, sw, arena + off[i], len[i], hs);
-    store_words(ws_hs + (size_t)i * CV_HS_WORDS, hs, CV_HS_WORDS / 4);
+    cv_hs_scalars(hs, ws_dig + i, cap);
 }
 
-// fused half-size prep (cv_hs_prep_fused_hs) after cv_hash_kernel: scalars from ws_hs, lattice +
-// digits, A and R decoded as one interleaved pair, both odd-multiple tables; ws_ok = key_ok AND
-// r_ok, status = key status.
-template <bool LAT, bool SUB = false>
-__global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsfused_prep_kernel(
-    uint32_t n, uint32_t cap, const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig,
-    const uint32_t *__restrict__ ws_hs, uint32_t *__restrict__ ws_dig, uint32_t *__restrict__ ws_tab,
-    uint32_t *__restrict__ ws_tabR, uint8_t *__restrict__ ws_ok, uint8_t *__restrict__ status) {
+// points of the half-size group (throughput form): A and R decoded as one interleaved pair per lane,
+// both odd-multiple tables (cv_hs_points); ws_ok = key_ok AND r_ok, status = key status.
+template <bool SUB = false>
+__global__ __launch_bounds__(CV_BLOCK, 2) void cv_points_kernel(uint32_t n, const uint8_t *__restrict__ pk,
+                                                                const uint8_t *__restrict__ sig,
+                                                                uint32_t *__restrict__ ws_tab,
+                                                                uint32_t *__restrict__ ws_tabR,
+                                                                uint8_t *__restrict__ ws_ok,
+                                                                uint8_t *__restrict__ status) {
     const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
     if (i >= n) return;
-    uint32_t aw[8], rw[8], hs[CV_HS_WORDS];
+    uint32_t aw[8], rw[8];
     load_words8(aw, pk + (size_t)i * 32);
     load_words8(rw, sig + (size_t)i * 64);
-    const uint4 *hp = reinterpret_cast<const uint4 *>(ws_hs + (size_t)i * CV_HS_WORDS);
-#pragma unroll
-    for (int q = 0; q < CV_HS_WORDS / 4; q++) {
-        const uint4 x = hp[q];
-        hs[4 * q] = x.x; hs[4 * q + 1] = x.y; hs[4 * q + 2] = x.z; hs[4 * q + 3] = x.w;
-    }
     bool ok = false;
-    const bool key_ok = cv_hs_prep_fused_hs<LAT>(aw, rw, hs, ws_dig + i, cap, ws_tab + (size_t)i * CV_TAB_WORDS,
-                                                 ws_tabR + (size_t)i * CV_TAB_WORDS, ok);
+    const bool key_ok = cv_hs_points<false>(aw, rw, ws_tab + (size_t)i * CV_TAB_WORDS, ws_tabR + (size_t)i * CV_TAB_WORDS,
+                                            ok);
     ws_ok[i] = ok ? 1 : 0;
     if (status) status[i] = key_ok ? 0 : 1;
+}
+
+// points of the half-size group (latency form, small batches): a lane PAIR per signature, the even
+// lane decoding the key A into k*(-A), the odd lane R into k*R, side by side (the same instructions
+// on both lanes: cv_hs_point_one) with the latency (ILP) field forms — half the serial chain of the
+// throughput form, whose single lane runs both decodes.  The even lane writes ok = key_ok AND r_ok.
+__global__ __launch_bounds__(64) void cv_points_pair_kernel(uint32_t n, const uint8_t *__restrict__ pk,
+                                                            const uint8_t *__restrict__ sig,
+                                                            uint32_t *__restrict__ ws_tab,
+                                                            uint32_t *__restrict__ ws_tabR,
+                                                            uint8_t *__restrict__ ws_ok,
+                                                            uint8_t *__restrict__ status) {
+    const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+    const uint32_t i = g >> 1;
+    if (i >= n) return;                       // both lanes of a pair leave together
+    const bool is_r = (g & 1u) != 0;
+    uint32_t w[8];
+    load_words8(w, is_r ? sig + (size_t)i * 64 : pk + (size_t)i * 32);
+    const bool ok = cv_hs_point_one<true>(w, is_r, (is_r ? ws_tabR : ws_tab) + (size_t)i * CV_TAB_WORDS);
+    const bool r_ok = __shfl_xor((int)ok, 1) != 0;
+    if (!is_r) {
+        ws_ok[i] = (ok && r_ok) ? 1 : 0;
+        if (status) status[i] = ok ? 0 : 1;
+    }
 }
 
 // hs_straus: E = [v]R + [u]A + [w]B per lane over the wave's largest window count, the identity
@@ -505,12 +527,13 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
         if (ev && c0 == 0) (void)hipEventRecord(ev[0], stream);
         const bool lat = n <= g_quad_max;   // small batch: latency forms of the single chains
         if (lat && g_verify_mode == 1 && g_hs_quad) {
-            // half-size quad group: phases = fused prep | bitmap clear | hs_straus_quad
+            // half-size quad group: phases = scalars + point pairs | bitmap clear | hs_straus_quad
             uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
-            hipLaunchKernelGGL(cv_hash_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, pk + (size_t)c0 * 32,
-                               sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_hs);
-            hipLaunchKernelGGL(cv_hsfused_prep_kernel<true>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap,
-                               pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, ws_hs, ws_dig, ws_tab, ws_tabR, ws_ok,
+            // 64-thread blocks: the few waves of a small batch spread over CUs (one per SIMD)
+            hipLaunchKernelGGL(cv_scalars_kernel<true>, dim3((m + 63) / 64), dim3(64), 0, stream, m, ws_cap,
+                               pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_dig);
+            hipLaunchKernelGGL(cv_points_pair_kernel, dim3((2 * m + 63) / 64), dim3(64), 0, stream, m,
+                               pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, ws_tab, ws_tabR, ws_ok,
                                status ? status + c0 : nullptr);
             if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);
             (void)hipMemsetAsync(bitmap + (size_t)c0 / 64, 0, (size_t)((m + 63) / 64) * 8, stream);
@@ -544,11 +567,11 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
                 hipStream_t st = h ? ax->s2 : stream;
                 const uint32_t a = c0 + sub0[h], mm = subn[h], bl = (mm + CV_BLOCK - 1) / CV_BLOCK;
                 if (h == 1 && g_split_mode == 2) (void)hipStreamWaitEvent(st, ax->prep1, 0);
-                hipLaunchKernelGGL(cv_hash_kernel, dim3(bl), dim3(CV_BLOCK), 0, st, mm, pk + (size_t)a * 32,
-                                   sig + (size_t)a * 64, arena, off + a, len + a, ws_hs + (size_t)sub0[h] * CV_HS_WORDS);
-                hipLaunchKernelGGL((cv_hsfused_prep_kernel<false, true>), dim3(bl), dim3(CV_BLOCK), 0, st, mm, ws_cap,
-                                   pk + (size_t)a * 32, sig + (size_t)a * 64, ws_hs + (size_t)sub0[h] * CV_HS_WORDS,
-                                   ws_dig + sub0[h], ws_tab + (size_t)sub0[h] * CV_TAB_WORDS,
+                hipLaunchKernelGGL(cv_scalars_kernel<false>, dim3(bl), dim3(CV_BLOCK), 0, st, mm, ws_cap,
+                                   pk + (size_t)a * 32, sig + (size_t)a * 64, arena, off + a, len + a,
+                                   ws_dig + sub0[h]);
+                hipLaunchKernelGGL(cv_points_kernel<true>, dim3(bl), dim3(CV_BLOCK), 0, st, mm, pk + (size_t)a * 32,
+                                   sig + (size_t)a * 64, ws_tab + (size_t)sub0[h] * CV_TAB_WORDS,
                                    ws_tabR + (size_t)sub0[h] * CV_TAB_WORDS, ws_ok + sub0[h],
                                    status ? status + a : nullptr);
                 if (h == 0) (void)hipEventRecord(ax->prep1, st);
@@ -566,14 +589,13 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             continue;
         }
         if (!lat && g_verify_mode == 1 && g_hs_fused) {
-            // fused half-size group: phases = hash | fused prep | hs_straus
+            // half-size group: phases = scalars (hash, lattice, digits) | points (decodes, tables) | hs_straus
             uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
-            hipLaunchKernelGGL(cv_hash_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, pk + (size_t)c0 * 32,
-                               sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_hs);
+            hipLaunchKernelGGL(cv_scalars_kernel<false>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap,
+                               pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_dig);
             if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);
-            hipLaunchKernelGGL(cv_hsfused_prep_kernel<false>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap,
-                               pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, ws_hs, ws_dig, ws_tab, ws_tabR, ws_ok,
-                               status ? status + c0 : nullptr);
+            hipLaunchKernelGGL(cv_points_kernel<false>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, pk + (size_t)c0 * 32,
+                               sig + (size_t)c0 * 64, ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr);
             if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
             if (g_hs_waves == 2)
                 hipLaunchKernelGGL(cv_hs_straus_kernel<2>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, ws_dig,

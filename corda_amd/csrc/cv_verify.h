@@ -751,42 +751,50 @@ __host__ __device__ inline int cv_pmt_verify(uint32_t b, uint32_t e, const uint8
     return 0;
 }
 
-// ---------------------------------------------------------------- fused half-size prep
-// cv_verify_prep + cv_hs_prep in one pass: hash and scalars, lattice + packed digits, then the A and
-// R decodes interleaved (ge_decode2_0_1_0), then the two odd-multiple tables.  ok_out = key_ok AND
-// r_ok (the verdict mask); returns key_ok (the status byte).
-// The fused prep after the hash: hs = h || effective s (cv_keyed_hs, or the GPU kernel's wave-staged
-// hash of the same bytes).
-template <bool LAT = false>
-__host__ __device__ __forceinline__ bool cv_hs_prep_fused_hs(const uint32_t aw[8], const uint32_t rw[8],
-                                                             const uint32_t hs[CV_HS_WORDS], uint32_t *dig,
-                                                             size_t stride, uint32_t *tabA, uint32_t *tabR,
-                                                             bool &ok_out) {
-    {
-        uint32_t h[8], s[8], u[8], v[8], w[8];
+// ---------------------------------------------------------------- half-size prep, in two parts
+// scalars : h = SHA-512(R || Abyte || M) mod L (cv_keyed_hs), the lattice (u, v, w) and the packed
+//           window digits -> dig (window-major, stride `stride`), dig[64 * stride] = window count
+// points  : A and R decoded (eddsa-0.1.0 rules; R must also be canonical) and the odd-multiple tables
+//           k*(-A), k*R; key_ok = A decodes (the status byte), verdict mask = key_ok AND r_ok
+// The GPU runs them as separate kernels (cv_kernels.hip: cv_scalars_kernel at 4 waves per SIMD;
+// cv_points_kernel with both decodes interleaved per lane for throughput, or cv_points_pair_kernel
+// with one decode per lane of a lane pair for small latency-bound batches).
+__host__ __device__ __forceinline__ void cv_hs_scalars(const uint32_t hs[CV_HS_WORDS], uint32_t *dig, size_t stride) {
+    uint32_t h[8], s[8], u[8], v[8], w[8];
 #pragma unroll
-        for (int q = 0; q < 8; q++) { h[q] = hs[q]; s[q] = hs[8 + q]; }
-        bool v_neg;
-        int nwin;
-        sc_halfsize(u, v, v_neg, nwin, w, h, s);
+    for (int q = 0; q < 8; q++) { h[q] = hs[q]; s[q] = hs[8 + q]; }
+    bool v_neg;
+    int nwin;
+    sc_halfsize(u, v, v_neg, nwin, w, h, s);
 #pragma unroll 4
-        for (int win = 0; win < 64; win++) {
-            const int da = -digit16(u, win), dr = v_neg ? -digit16(v, win) : digit16(v, win);
-            const bool bw = (win & 1) == 0 && win < 32;
-            const int dlo = bw ? digit256(w, win >> 1) : 0, dhi = bw ? digit256(w, 16 + (win >> 1)) : 0;
-            dig[(size_t)win * stride] = ((uint32_t)da & 0x1fu) | (((uint32_t)dr & 0x1fu) << 5) |
-                                        (((uint32_t)dlo & 0x1ffu) << 10) | (((uint32_t)dhi & 0x1ffu) << 19);
-        }
-        dig[64 * stride] = (uint32_t)nwin;
+    for (int win = 0; win < 64; win++) {
+        const int da = -digit16(u, win), dr = v_neg ? -digit16(v, win) : digit16(v, win);
+        const bool bw = (win & 1) == 0 && win < 32;
+        const int dlo = bw ? digit256(w, win >> 1) : 0, dhi = bw ? digit256(w, 16 + (win >> 1)) : 0;
+        dig[(size_t)win * stride] = ((uint32_t)da & 0x1fu) | (((uint32_t)dr & 0x1fu) << 5) |
+                                    (((uint32_t)dlo & 0x1ffu) << 10) | (((uint32_t)dhi & 0x1ffu) << 19);
     }
+    dig[64 * stride] = (uint32_t)nwin;
+}
+
+// R's canonical-encoding check: its bytes re-encode to themselves (y < p; x = 0 only with sign 0)
+CV_HD bool cv_r_canonical(const uint32_t rw[8]) {
+    uint32_t enc[8], diff = 0;
+    ge_abyte_from_key(enc, rw);
+#pragma unroll
+    for (int q = 0; q < 8; q++) diff |= enc[q] ^ rw[q];
+    return diff == 0;
+}
+
+// points, both decodes interleaved in one lane (throughput form).  Returns key_ok; ok_out = key_ok
+// AND r_ok.
+template <bool LAT = false>
+__host__ __device__ __forceinline__ bool cv_hs_points(const uint32_t aw[8], const uint32_t rw[8], uint32_t *tabA,
+                                                      uint32_t *tabR, bool &ok_out) {
     ge_p3 P[2];
     bool ok[2];
     ge_decode2_0_1_0<LAT>(P, ok, aw, rw);
-    uint32_t enc[8], diff = 0;
-    ge_abyte_from_key(enc, rw);                            // R canonical: its bytes re-encode to themselves
-#pragma unroll
-    for (int q = 0; q < 8; q++) diff |= enc[q] ^ rw[q];
-    const bool key_ok = ok[0], r_ok = ok[1] && diff == 0;
+    const bool key_ok = ok[0], r_ok = ok[1] && cv_r_canonical(rw);
     if (!key_ok) ge_p3_identity(P[0]);
     if (!r_ok) ge_p3_identity(P[1]);
     ge_p3 nA;
@@ -795,6 +803,31 @@ __host__ __device__ __forceinline__ bool cv_hs_prep_fused_hs(const uint32_t aw[8
     ge_cached_multiples8(tabR, P[1]);
     ok_out = key_ok && r_ok;
     return key_ok;
+}
+
+// points, one encoding per lane (latency form: a lane pair per signature runs the two decodes side by
+// side): is_r = false decodes the key A into k*(-A), true decodes R (canonical) into k*R.  Both lanes
+// run the same instructions.  Returns the lane's decode verdict (key_ok or r_ok).
+template <bool LAT = true>
+__host__ __device__ __forceinline__ bool cv_hs_point_one(const uint32_t w[8], bool is_r, uint32_t *tab) {
+    ge_p3 P, nP;
+    bool ok = ge_decode_0_1_0<LAT>(P, w);
+    ok = ok && (!is_r || cv_r_canonical(w));
+    if (!ok) ge_p3_identity(P);
+    ge_p3_neg(nP, P);
+    if (!is_r) P = nP;
+    ge_cached_multiples8(tab, P);
+    return ok;
+}
+
+// hash + scalars + points in one pass (host harness, and the reference order of the GPU kernels)
+template <bool LAT = false>
+__host__ __device__ __forceinline__ bool cv_hs_prep_fused_hs(const uint32_t aw[8], const uint32_t rw[8],
+                                                             const uint32_t hs[CV_HS_WORDS], uint32_t *dig,
+                                                             size_t stride, uint32_t *tabA, uint32_t *tabR,
+                                                             bool &ok_out) {
+    cv_hs_scalars(hs, dig, stride);
+    return cv_hs_points<LAT>(aw, rw, tabA, tabR, ok_out);
 }
 template <bool LAT = false>
 __host__ __device__ __forceinline__ bool cv_hs_prep_fused(const uint32_t aw[8], const uint32_t rw[8], const uint32_t sw[8],

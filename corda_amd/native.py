@@ -127,6 +127,7 @@ def load():
             lib.cv_diag_prep_phases.argtypes = [_vp, ctypes.c_int, _sz, _vp, _vp, _vp, _vp, _vp,
                                                 ctypes.POINTER(ctypes.c_double)]
             lib.cv_diag_prep_phases.restype = ctypes.c_int
+        if hasattr(lib, "cv_diag_dedupe_keys"):                 # absent only in older A/B builds
             lib.cv_diag_dedupe_keys.argtypes = [_sz, _vp, _vp, ctypes.POINTER(_sz)]
             lib.cv_diag_dedupe_keys.restype = ctypes.c_int
         _lib = lib
