@@ -20,8 +20,16 @@ Extra fields on the JSON line:
                 peak of this GPU, kernel time from HIP events on whole-chunk launches of the same
                 batch; "group" = the whole launch group against its own MAC count
   cpu_baseline  oracle/ C restatement of eddsa-0.1.0 verify (rank 0, N=1 only, bounded sample)
-  notary        p50/p99 end-to-end latency of a 4096-signature notary batch (host buffers in and
-                out, 1/16 adversarial), GPU vs the CPU restatement on the same batch
+  roofline.cycle_basis  the same peak priced per shader cycle (SIMDs x 64 / cycles per wave-level
+                v_mad_u64_u32 x the clock measured over the calibration launch), and against 2.4 GHz
+  cpu_baseline  oracle/ C restatement of eddsa-0.1.0 verify (rank 0, N=1 only, bounded sample) on the
+                host cores this process may use (capped by the box's OMP_NUM_THREADS share)
+  c3, c5_shard  BASELINE configs C3 (1M txs x 8 signers: Merkle tx-id recompute + 8M verifies) and
+                C5 (8M-signature shard) on the same GPU: value, tx_ids_per_s, phases, roofline
+  notary        C4: p50/p99 end-to-end latency of a 4096-signature notary batch (host buffers in and
+                out, 1/16 adversarial records from the golden corpus's rejected classes), with the
+                p50 breakdown (transfers + host, launch + sync, per kernel) and the CPU restatement on
+                the same batch; notary_sweep = the same at 256 and 65536; notary_keyed = 64 signers
   resolve_chain p50/p99 latency of a 5,000-tx dependency chain (2 signers/tx, 6 leaves/tx): one
                 Merkle call + one verify call + per-tx AND with the id check
 """
@@ -76,12 +84,45 @@ def pmc_traffic(n: int, hs: bool):
     return d["hbm_bytes_per_launch"] * n / d["n"]
 
 
+def affinity_cores() -> int:
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def host_threads() -> int:
+    """Host cores the CPU baseline uses, read on the box at run time: the cores this process may run
+    on (sched_getaffinity), capped by the box's declared CPU share when it sets one (OMP_NUM_THREADS:
+    a shared box's affinity mask can list every core of the machine).  CV_CPU_THREADS overrides."""
+    if os.environ.get("CV_CPU_THREADS"):
+        return int(os.environ["CV_CPU_THREADS"])
+    n = affinity_cores()
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    return min(n, int(share)) if share.isdigit() and int(share) > 0 else n
+
+
+def jvm_probe() -> str:
+    """the reference's own verify path (JVM + eddsa-0.1.0) is timed when a JDK and
+    the jar exist on the box; report what the probe found."""
+    import shutil
+    import subprocess
+    java = shutil.which("java")
+    if not java:
+        return "java absent (no JDK on the box): the C restatement of eddsa-0.1.0 stands in"
+    try:
+        r = subprocess.run([java, "-version"], capture_output=True, text=True, timeout=10)
+        return "java present (" + (r.stderr or r.stdout).strip().splitlines()[0] + "), eddsa-0.1.0 jar absent"
+    except Exception as e:  # noqa: BLE001
+        return f"java probe failed: {e}"
+
+
 def cpu_baseline(batch, rank_device: int, seconds: float):
     """Times the C restatement (oracle/, test infrastructure) on a bounded sample of the same batch."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import cv_oracle  # noqa: E402
 
-    threads = int(os.environ.get("CV_CPU_THREADS", "16"))
+    threads = host_threads()
     # 1-thread probe sizes the sample so the multi-thread leg runs ~`seconds`
     n1 = 1024
     pk, sig, arena, off, ln = batch.to_host(0, n1)
@@ -94,20 +135,23 @@ def cpu_baseline(batch, rank_device: int, seconds: float):
     vm, _ = cv_oracle.verify_batch(pk, sig, arena, off, ln, threads)
     ratem = ns / (time.perf_counter() - t)
     return {"value": ratem, "unit": "verifies/s", "cores": threads, "kind": "port",
-            "single_thread_value": rate1,
+            "single_thread_value": rate1, "jvm_probe": jvm_probe(), "affinity_cores": affinity_cores(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
             "sample": f"first {ns} signatures of the same batch ({batch.msg_len}-byte msgs) on {threads} host "
                       f"threads; single-thread rate from the first {n1}",
             "accepted_fraction": float(vm.mean())}
 
 
-def notary_latency(eng, device: int, reps: int, cpu: bool, key_pool=None):
-    """C4 at 4096: host-buffer verify (H2D + kernel + D2H) + per-tx AND, p50/p99 over reps.  With
-    key_pool, the batch's signers come from that many parties (the engine's host dedupe then takes the
-    keyed path; the key pool is warm after the first repetition, as on a running notary)."""
-    b = workload.make_batch(eng, device, 4096, 32, seed=4096, key_pool=key_pool)
-    expect = workload.corrupt_fraction(b, 16).cpu().numpy()
-    pk, sig, arena, off, ln = b.to_host()
-    tx_begin = np.arange(0, 4097, 8, dtype=np.uint32)            # 8 signers per tx (512 txs)
+def notary_latency(eng, device: int, n: int, reps: int, cpu: bool, key_pool=None, adv=None):
+    """C4 (BASELINE.json configs[3]): one notary batch of n signatures over 32-byte tx ids, 8 signers
+    per transaction, 1/16 adversarial records cycling through the golden corpus's rejected classes.
+    p50/p99 of the notary's end-to-end step through the host-buffer C-ABI (H2D + kernels + D2H + the
+    per-tx AND), and where it goes: the same batch through the device API on resident inputs
+    (kernels + launch overhead) and the per-kernel HIP-event phases.  With key_pool the signers come
+    from that many parties (the engine's host dedupe takes the keyed path; the key pool is warm after
+    the first repetition, as on a running notary)."""
+    pk, sig, arena, off, ln, expect = workload.notary_batch(eng, device, n, adv, key_pool=key_pool)
+    tx_begin = np.arange(0, n + 1, 8, dtype=np.uint32)
     lat = []
     for r in range(reps + 5):
         t = time.perf_counter()
@@ -116,14 +160,36 @@ def notary_latency(eng, device: int, reps: int, cpu: bool, key_pool=None):
         dt = time.perf_counter() - t
         if r >= 5:
             lat.append(dt)
-    got = native.bitmap_to_bools(bitmap, 4096)
-    assert np.array_equal(got, expect), "notary batch verdicts wrong"
-    out = {"batch": 4096, "p50_ms": float(np.percentile(lat, 50) * 1e3), "p99_ms": float(np.percentile(lat, 99) * 1e3),
-           "reps": reps, "txs": 512, "tx_ok": int(txok.sum()), "signer_keys": key_pool or "distinct"}
+    assert np.array_equal(native.bitmap_to_bools(bitmap, n), expect), "notary batch verdicts wrong"
+    out = {"batch": n, "p50_ms": float(np.percentile(lat, 50) * 1e3), "p99_ms": float(np.percentile(lat, 99) * 1e3),
+           "reps": reps, "txs": n // 8, "tx_ok": int(txok.sum()), "signer_keys": key_pool or "distinct",
+           "adversarial": "1/16, golden corpus rejected classes"}
+    if key_pool is None:
+        dev = torch.device("cuda", device)
+        d = [torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in
+             (pk, sig, arena, off.view(np.int64), ln.view(np.int32))]
+        bm = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+        s = torch.cuda.Stream(dev)
+        dl = []
+        for r in range(reps + 5):
+            t = time.perf_counter()
+            eng.verify_device(device, n, *[x.data_ptr() for x in d], bm.data_ptr(), 0, s.cuda_stream)
+            s.synchronize()
+            if r >= 5:
+                dl.append(time.perf_counter() - t)
+        ph = np.median(np.array([eng.verify_device_timed(device, n, *[x.data_ptr() for x in d], bm.data_ptr(),
+                                                         s.cuda_stream) for _ in range(10)]), axis=0)
+        dev_p50 = float(np.percentile(dl, 50) * 1e3)
+        names = (("scalars_and_point_pairs", "bitmap_clear", "hs_straus_quad") if n <= 32768
+                 else ("scalars", "points", "hs_straus"))
+        out["breakdown_p50_ms"] = {"host_api_total": out["p50_ms"], "device_api_total": dev_p50,
+                                   "transfers_and_host": out["p50_ms"] - dev_p50,
+                                   "kernels": {k: float(v) for k, v in zip(names, ph)},
+                                   "launch_and_sync": dev_p50 - float(ph.sum())}
     if cpu:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import cv_oracle  # noqa: E402
-        threads = int(os.environ.get("CV_CPU_THREADS", "16"))
+        threads = host_threads()
         cl = []
         for r in range(3):
             t = time.perf_counter()
@@ -182,7 +248,7 @@ def resolve_chain_latency(eng, device: int, reps: int, cpu: bool, ntx: int = 500
     if cpu:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import cv_oracle  # noqa: E402
-        threads = int(os.environ.get("CV_CPU_THREADS", "16"))
+        threads = host_threads()
         cl = []
         for r in range(3):
             t = time.perf_counter()
@@ -218,10 +284,19 @@ def keyed_rate(eng, device: int, n: int, msg_len: int, steps: int, sh: int, pool
             "cold_key_tables_ms": float(cold[0]), "comb_work_per_unit": "240 S + 915 M per verify (60 doublings)"}
 
 
-def run_c3(args, eng, local, rank, world, stream, sh, dev):
-    """C3 step: recompute every tx id (leaf SHA-256 + Merkle tree), verify all signatures over the
-    claimed ids, then per transaction: id matches AND all its signature bits set."""
-    ntx = args.n or 1_000_000
+def straus_roofline(eng, local: int, n: int, straus_ms: float, kern_ms: float, mad_rate: float):
+    """Roofline fields of the dominant kernel from its HIP-event time (half-size schedule counts)."""
+    achieved = n * W_MAC_HS_STRAUS / (straus_ms * 1e-3)
+    group = n * W_MAC_HS_GROUP / (kern_ms * 1e-3)
+    return {"bound": "valu", "achieved": achieved / 1e12, "peak": mad_rate / 1e12, "unit": "Tmac/s",
+            "frac": achieved / mad_rate, "kernel": "cv_hs_straus_kernel", "kernel_ms": straus_ms,
+            "group": {"kernel_ms": kern_ms, "achieved": group / 1e12, "frac": group / mad_rate}}
+
+
+def run_c3(eng, local, rank, world, sh, dev, ntx: int, steps: int, warmup: int):
+    """C3 step (BASELINE.json configs[2]): recompute every tx id (leaf SHA-256 + Merkle tree), verify
+    all signatures over the claimed ids, then per transaction: id matches AND all its signature bits
+    set.  Returns the timing dict (rank 0's view after the max over ranks)."""
     t0 = time.perf_counter()
     tb = workload.make_tx_batch(eng, local, ntx, 8, seed=20261015 + 7919 * rank, stream=sh)
     log(f"[rank {rank}] generated {ntx} txs / {tb.sigs.n} signatures on GPU in {time.perf_counter() - t0:.2f}s")
@@ -230,44 +305,85 @@ def run_c3(args, eng, local, rank, world, stream, sh, dev):
     ids = torch.empty_like(tb.ids)
     ws = torch.empty(nleaves * 32, dtype=torch.uint8, device=dev)
     bitmap = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+    sig_args = (tb.sigs.pk.data_ptr(), tb.sigs.sig.data_ptr(), tb.sigs.arena.data_ptr(), tb.sigs.off.data_ptr(),
+                tb.sigs.len.data_ptr(), bitmap.data_ptr())
 
-    def step():
+    def merkle():
         eng.merkle_device(local, ntx, nleaves, tb.leaf_arena.data_ptr(), tb.leaf_off.data_ptr(),
                           tb.leaf_len.data_ptr(), tb.tx_begin.data_ptr(), ws.data_ptr(), ids.data_ptr(), 0, sh)
-        eng.verify_device(local, n, tb.sigs.pk.data_ptr(), tb.sigs.sig.data_ptr(), tb.sigs.arena.data_ptr(),
-                          tb.sigs.off.data_ptr(), tb.sigs.len.data_ptr(), bitmap.data_ptr(), 0, sh)
-        ok = D.tx_verdicts_torch(bitmap, tb.sig_tx_begin) & (ids == tb.ids).all(dim=1)
-        return ok
 
-    for _ in range(args.warmup):
+    def step():
+        merkle()
+        eng.verify_device(local, n, *sig_args[:5], sig_args[5], 0, sh)
+        return D.tx_verdicts_torch(bitmap, tb.sig_tx_begin) & (ids == tb.ids).all(dim=1)
+
+    for _ in range(warmup):
         step()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         ok = step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     assert bool(ok.all()), "an honest transaction was rejected"
+    # phases: the Merkle call (torch events on the same stream) and the verify kernels (HIP events)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    mk = []
+    for _ in range(max(2, steps)):
+        e0.record()
+        merkle()
+        e1.record()
+        e1.synchronize()
+        mk.append(e0.elapsed_time(e1))
+    ph = np.mean(np.array([eng.verify_device_timed(local, n, *sig_args, sh) for _ in range(max(2, steps))]), axis=0)
+    merkle_ms = float(np.mean(mk))
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt[0])
-    if rank == 0:
-        result = {
-            "metric": "Ed25519 verifies/sec (node)", "value": world * n * args.steps / elapsed, "unit": "verifies/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "uint32/uint64 (GF(2^255-19) radix 2^25.5 limbs), SHA-256",
-            "data": "synthetic (leaf blobs, keys, signatures generated on-GPU from seeded RNG)",
-            "config": {"workload": CONFIG_NAME["c3"], "txs_per_gpu": ntx, "signers_per_tx": 8,
-                       "leaves_per_tx": 6, "sigs_per_gpu": n, "parallelism": f"shard-by-transaction x{world}"},
-            "tx_ids_per_s": world * ntx * args.steps / elapsed,
-        }
-        print(json.dumps(result), flush=True)
+    tb = None
+    return {"n": n, "ntx": ntx, "elapsed": elapsed, "merkle_ms": merkle_ms, "phases": ph,
+            "leaves": nleaves}
+
+
+def c3_line(eng, local, rank, world, sh, dev, ntx, steps, warmup, mad_rate):
+    r = run_c3(eng, local, rank, world, sh, dev, ntx, steps, warmup)
+    ph = r["phases"]
+    return {"workload": CONFIG_NAME["c3"], "value": world * r["n"] * steps / r["elapsed"], "unit": "verifies/s",
+            "tx_ids_per_s": world * ntx * steps / r["elapsed"], "ms_per_step": r["elapsed"] / steps * 1e3,
+            "steps": steps, "txs_per_gpu": ntx, "sigs_per_gpu": r["n"], "leaves_per_gpu": r["leaves"],
+            "phase_ms": {"merkle": r["merkle_ms"], "scalars": float(ph[0]), "points": float(ph[1]),
+                         "hs_straus": float(ph[2])},
+            "roofline": straus_roofline(eng, local, r["n"], float(ph[2]), float(ph.sum()), mad_rate)}
+
+
+def c5_line(eng, local, rank, sh, dev, n, steps, mad_rate):
+    """C5 (BASELINE.json configs[4]) single-GPU shard: n single-signer signatures over 32-byte tx ids,
+    verified in the engine's 2M-signature workspace chunks."""
+    t0 = time.perf_counter()
+    b = workload.make_batch(eng, local, n, 32, seed=5 + 7919 * rank, stream=sh)
+    log(f"[rank {rank}] generated {n} C5 signatures in {time.perf_counter() - t0:.2f}s")
+    bm = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+    a = (b.pk.data_ptr(), b.sig.data_ptr(), b.arena.data_ptr(), b.off.data_ptr(), b.len.data_ptr(), bm.data_ptr())
+    eng.verify_device(local, n, *a, 0, sh)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.verify_device(local, n, *a, 0, sh)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    assert bool((bm == -1).all()) or n % 64, "C5: verify rejected an honest signature"
+    ph = np.mean(np.array([eng.verify_device_timed(local, n, *a, sh) for _ in range(2)]), axis=0)
+    del b
+    return {"workload": CONFIG_NAME["c5"], "value": n * steps / el, "unit": "verifies/s",
+            "ms_per_step": el / steps * 1e3, "steps": steps, "sigs_per_gpu": n,
+            "tx_ids_per_s": n * steps / el, "tx_ids_note": "single-signer: one tx id per signature",
+            "phase_ms": {"scalars": float(ph[0]), "points": float(ph[1]), "hs_straus": float(ph[2])},
+            "roofline": straus_roofline(eng, local, n, float(ph[2]), float(ph.sum()), mad_rate)}
 
 
 def main():
@@ -282,6 +398,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-notary", action="store_true")
     ap.add_argument("--no-keyed", action="store_true")
+    ap.add_argument("--no-sub", action="store_true", help="skip the C3 / C5-shard sub-lines")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -302,7 +419,23 @@ def main():
     sh = stream.cuda_stream
     assert sh != 0
     if args.config == "c3":
-        run_c3(args, eng, local, rank, world, stream, sh, dev)
+        ntx = args.n or 1_000_000
+        r = run_c3(eng, local, rank, world, sh, dev, ntx, args.steps, args.warmup)
+        if rank == 0:
+            mad_rate, _ = eng.calibrate(local)
+            ph = r["phases"]
+            print(json.dumps({
+                "metric": "Ed25519 verifies/sec (node)", "value": world * r["n"] * args.steps / r["elapsed"],
+                "unit": "verifies/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": r["elapsed"] / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None, "dtype": "uint32/uint64 (GF(2^255-19) radix 2^25.5 limbs), SHA-256",
+                "data": "synthetic (leaf blobs, keys, signatures generated on-GPU from seeded RNG)",
+                "config": {"workload": CONFIG_NAME["c3"], "txs_per_gpu": ntx, "signers_per_tx": 8,
+                           "leaves_per_tx": 6, "sigs_per_gpu": r["n"], "parallelism": f"shard-by-transaction x{world}"},
+                "tx_ids_per_s": world * ntx * args.steps / r["elapsed"],
+                "phase_ms": {"merkle": r["merkle_ms"], "scalars": float(ph[0]), "points": float(ph[1]),
+                             "hs_straus": float(ph[2])},
+                "roofline": straus_roofline(eng, local, r["n"], float(ph[2]), float(ph.sum()), mad_rate)}), flush=True)
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
@@ -373,8 +506,8 @@ def main():
         achieved = n * w_straus / (straus_ms * 1e-3)
         group = n * w_group / (kern_ms * 1e-3)
         if hs:
-            phase_ms = {"hash": float(ph[0]), "prep": float(ph[1]), "hs_straus": float(ph[2])}
-            kname, gname = "cv_hs_straus_kernel", "hash + prep + hs_straus"
+            phase_ms = {"scalars": float(ph[0]), "points": float(ph[1]), "hs_straus": float(ph[2])}
+            kname, gname = "cv_hs_straus_kernel", "scalars + points + hs_straus"
             wdesc = (f"{w_straus} 32x32->64 MAC per verify in the half-size Straus phase at {HS_NW} windows "
                      f"(512 S + 1135 M)")
             gdesc = f"{w_group} MAC per verify (half-size schedule: Straus + 2 decodes + 2 tables)"
@@ -407,13 +540,28 @@ def main():
                                    "achieved": group / 1e12, "frac": group / mad_rate, "work_per_unit": gdesc},
                          "fe_mul_per_s": femul_rate},
         }
+        cyc = eng.calibrate_cycles(local)
+        result["roofline"]["cycle_basis"] = {
+            "clock_ghz": cyc["clock_ghz"], "cycles_per_wave_mad": cyc["cycles_per_wave_instr"],
+            "peak_at_measured_clock": cyc["mac_per_s"] / 1e12, "peak_at_2p4ghz": cyc["mac_per_s_at_2p4ghz"] / 1e12,
+            "frac_vs_measured_clock": achieved / cyc["mac_per_s"], "frac_vs_2p4ghz": achieved / cyc["mac_per_s_at_2p4ghz"],
+            "note": "peak = SIMDs x 64 lanes / cycles-per-wave-mad x clock; clock from s_memtime/s_memrealtime "
+                    "over the same calibration launch"}
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(batch, local, args.cpu_seconds)
+        if world == 1 and not args.no_sub:
+            del batch
+            result["c3"] = c3_line(eng, local, rank, world, sh, dev, 1_000_000, 3, 1, mad_rate)
+            result["c5_shard"] = c5_line(eng, local, rank, sh, dev, 8_000_000, 3, mad_rate)
         if not args.no_keyed and world == 1:
             result["keyed"] = keyed_rate(eng, local, n, msg_len, max(3, args.steps // 2), sh)
         if not args.no_notary:
-            result["notary"] = notary_latency(eng, local, 50, cpu=(world == 1 and not args.no_cpu))
-            result["notary_keyed"] = notary_latency(eng, local, 50, cpu=False, key_pool=64)
+            adv = workload.adversarial_records(os.path.join(REPO, "tests", "golden", "ed25519_corpus.npz"))
+            cpu4 = world == 1 and not args.no_cpu
+            result["notary"] = notary_latency(eng, local, 4096, 60, cpu=cpu4, adv=adv)
+            result["notary_sweep"] = [notary_latency(eng, local, k, r, cpu=False, adv=adv)
+                                      for k, r in ((256, 60), (65536, 20))]
+            result["notary_keyed"] = notary_latency(eng, local, 4096, 60, cpu=False, key_pool=64, adv=adv)
             result["resolve_chain"] = resolve_chain_latency(eng, local, 30, cpu=(world == 1 and not args.no_cpu))
         print(json.dumps(result), flush=True)
     if world > 1:

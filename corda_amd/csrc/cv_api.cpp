@@ -70,6 +70,34 @@ struct DevBuf {
     }
 };
 
+// Pinned (page-locked) host staging buffer: the host-buffer API packs a call's inputs into it so one
+// DMA moves them (pageable hipMemcpyAsync stages every copy through the runtime's own buffers — five
+// input copies cost ~0.1 ms of a 0.4-0.7 ms notary batch, tools/notary_probe.py).
+struct PinBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 16);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return e;
+        }
+        cap = want;
+        return hipSuccess;
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
 // Device-resident per-key comb tables (keyed verify), content-addressed by the
 // 32 key bytes.  A key's tables are computed once (cv_keyprep_kernel) and reused by every later
 // batch on that device; when the pool is full it is emptied (epoch reset) before new keys go in.
@@ -116,6 +144,8 @@ struct Device {
     int ordinal = 0;
     hipStream_t stream = nullptr;
     DevBuf pk, sig, arena, off, len, bitmap, status, seed, tx_begin, digest, ids;
+    DevBuf packed;                       // host-buffer verify: pk | sig | off | len | arena in one block
+    PinBuf pin_in, pin_out;              // its pinned host staging (inputs; bitmap | status)
     DevBuf pmt;                          // partial Merkle trees: inputs, outputs and workspace, packed
     DevBuf ws_hs, ws_tab, ws_R, ws_ok, ws_dig;   // verify workspace per signature: hs 64 B, 2 tables 2560 B,
                                          // R record 128 B, ok 1 B, half-size digits 260 B
@@ -257,6 +287,9 @@ void cv_close(cv_ctx *ctx) {
                           &d.digest, &d.ids, &d.pmt, &d.ws_hs, &d.ws_tab, &d.ws_R, &d.ws_ok, &d.ws_dig, &d.kc.ktab, &d.kc.kok,
                           &d.kc.keys, &d.kc.slots, &d.kc.slot_of_key, &d.kc.key_index, &d.kc.scratch})
             b->release();
+        d.packed.release();
+        d.pin_in.release();
+        d.pin_out.release();
         if (d.ws_ev) (void)hipEventDestroy(d.ws_ev);
         if (d.stream) (void)hipStreamDestroy(d.stream);
     }
@@ -273,14 +306,17 @@ static Device *find_dev(cv_ctx *ctx, int device) {
 
 // ---------------------------------------------------------------- verify (host buffers)
 // One shard [b, e) of a batch on one device.  b is a multiple of 64, so the shard's bitmap words
-// are whole words of the caller's bitmap.
+// are whole words of the caller's bitmap.  The inputs are packed into the device's pinned staging
+// buffer (pk | sig | off rebased to the shard's arena range | len | arena bytes, 16-B aligned parts),
+// moved by ONE DMA into one device block, verified, and the bitmap (+ status) come back by one DMA.
+static inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 static int verify_shard(Device &d, size_t b, size_t e, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
                         const uint64_t *off, const uint32_t *len, uint64_t *bitmap, uint8_t *status) {
     const size_t n = e - b;
     if (n == 0) return CV_OK;
     if (n > 0xffffffffull) return CV_E_TOO_LARGE;
     CV_TRY(hipSetDevice(d.ordinal));
-    // arena sub-range used by this shard; offsets are rebased by passing (d_arena - lo)
+    // arena sub-range used by this shard; offsets are rebased to it
     uint64_t lo = UINT64_MAX, hi = 0;
     for (size_t i = b; i < e; i++) {
         lo = std::min<uint64_t>(lo, off[i]);
@@ -288,25 +324,33 @@ static int verify_shard(Device &d, size_t b, size_t e, const uint8_t *pk, const 
     }
     if (hi < lo) hi = lo;
     const size_t words = (n + 63) / 64;
-    CV_TRY(d.pk.ensure(n * 32));
-    CV_TRY(d.sig.ensure(n * 64));
-    CV_TRY(d.arena.ensure(hi - lo + 16));
-    CV_TRY(d.off.ensure(n * 8));
-    CV_TRY(d.len.ensure(n * 4));
-    CV_TRY(d.bitmap.ensure(words * 8));
-    CV_TRY(d.status.ensure(n));
+    const size_t o_pk = 0, o_sig = al16(n * 32), o_off = o_sig + al16(n * 64), o_len = o_off + al16(n * 8);
+    const size_t o_ar = o_len + al16(n * 4), total = o_ar + al16(hi - lo + 16);
+    const size_t o_bm = 0, o_st = al16(words * 8), total_out = o_st + al16(n);
+    CV_TRY(d.pin_in.ensure(total));
+    CV_TRY(d.pin_out.ensure(total_out));
+    CV_TRY(d.packed.ensure(total));
+    CV_TRY(d.bitmap.ensure(total_out));
     hipStream_t s = d.stream;
-    CV_TRY(hipMemcpyAsync(d.pk.p, pk + b * 32, n * 32, hipMemcpyHostToDevice, s));
-    CV_TRY(hipMemcpyAsync(d.sig.p, sig + b * 64, n * 64, hipMemcpyHostToDevice, s));
-    if (hi > lo) CV_TRY(hipMemcpyAsync(d.arena.p, arena + lo, hi - lo, hipMemcpyHostToDevice, s));
-    CV_TRY(hipMemcpyAsync(d.off.p, off + b, n * 8, hipMemcpyHostToDevice, s));
-    CV_TRY(hipMemcpyAsync(d.len.p, len + b, n * 4, hipMemcpyHostToDevice, s));
-    CV_TRY(launch_verify(d, (uint32_t)n, d.pk.as<uint8_t>(), d.sig.as<uint8_t>(), d.arena.as<uint8_t>() - lo,
-                         d.off.as<uint64_t>(), d.len.as<uint32_t>(), d.bitmap.as<uint64_t>(),
-                         status ? d.status.as<uint8_t>() : nullptr, s));
-    CV_TRY(hipMemcpyAsync(bitmap + b / 64, d.bitmap.p, words * 8, hipMemcpyDeviceToHost, s));
-    if (status) CV_TRY(hipMemcpyAsync(status + b, d.status.p, n, hipMemcpyDeviceToHost, s));
+    // the staging buffers are reused by the next call: the previous call synchronised at its end
+    uint8_t *h = d.pin_in.as<uint8_t>();
+    std::memcpy(h + o_pk, pk + b * 32, n * 32);
+    std::memcpy(h + o_sig, sig + b * 64, n * 64);
+    uint64_t *hoff = reinterpret_cast<uint64_t *>(h + o_off);
+    for (size_t i = 0; i < n; i++) hoff[i] = off[b + i] - lo;
+    std::memcpy(h + o_len, len + b, n * 4);
+    if (hi > lo) std::memcpy(h + o_ar, arena + lo, hi - lo);
+    std::memset(h + o_ar + (hi - lo), 0, 16);
+    uint8_t *dv = d.packed.as<uint8_t>();
+    CV_TRY(hipMemcpyAsync(dv, h, total, hipMemcpyHostToDevice, s));
+    uint8_t *dout = d.bitmap.as<uint8_t>();
+    CV_TRY(launch_verify(d, (uint32_t)n, dv + o_pk, dv + o_sig, dv + o_ar, reinterpret_cast<const uint64_t *>(dv + o_off),
+                         reinterpret_cast<const uint32_t *>(dv + o_len), reinterpret_cast<uint64_t *>(dout + o_bm),
+                         status ? dout + o_st : nullptr, s));
+    CV_TRY(hipMemcpyAsync(d.pin_out.p, dout, status ? o_st + n : words * 8, hipMemcpyDeviceToHost, s));
     CV_TRY(hipStreamSynchronize(s));
+    std::memcpy(bitmap + b / 64, d.pin_out.as<uint8_t>() + o_bm, words * 8);
+    if (status) std::memcpy(status + b, d.pin_out.as<uint8_t>() + o_st, n);
     return CV_OK;
 }
 

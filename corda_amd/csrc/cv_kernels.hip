@@ -141,16 +141,9 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsprep_kernel(uint32_t n, uint
 // kernel (2 waves per SIMD) the hash's serial 64-bit chains were 32 % of the prep's cycles
 // (tools/prep_probe.py).  Any block size (small latency batches launch 64-thread blocks so the few
 // waves spread over CUs).
-template <bool LAT>
-__global__ __launch_bounds__(CV_BLOCK, 3) void cv_scalars_kernel(uint32_t n, uint32_t cap,
-                                                                 const uint8_t *__restrict__ pk,
-                                                                 const uint8_t *__restrict__ sig,
-                                                                 const uint8_t *__restrict__ arena,
-                                                                 const uint64_t *__restrict__ off,
-                                                                 const uint32_t *__restrict__ len,
-                                                                 uint32_t *__restrict__ ws_dig) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+__device__ __forceinline__ void cv_scalars_lane(uint32_t i, uint32_t cap, const uint8_t *pk, const uint8_t *sig,
+                                                const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                                                uint32_t *ws_dig) {
     uint32_t aw[8], rw[8], sw[8];
     load_words8(aw, pk + (size_t)i * 32);
     load_words8(rw, sig + (size_t)i * 64);
@@ -158,6 +151,27 @@ __global__ __launch_bounds__(CV_BLOCK, 3) void cv_scalars_kernel(uint32_t n, uin
     uint32_t hs[CV_HS_WORDS];
     cv_keyed_hs(aw, rw, sw, arena + off[i], len[i], hs);
     cv_hs_scalars(hs, ws_dig + i, cap);
+}
+__global__ __launch_bounds__(CV_BLOCK, 3) void cv_scalars_kernel(uint32_t n, uint32_t cap, const uint8_t *__restrict__ pk,
+                                                                 const uint8_t *__restrict__ sig,
+                                                                 const uint8_t *__restrict__ arena,
+                                                                 const uint64_t *__restrict__ off,
+                                                                 const uint32_t *__restrict__ len,
+                                                                 uint32_t *__restrict__ ws_dig) {
+    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (i < n) cv_scalars_lane(i, cap, pk, sig, arena, off, len, ws_dig);
+}
+// Small (latency) batches: 64-thread blocks (one wave each, spread over CUs) and the whole register
+// file for the lone wave — no spills.  A spilling version took 62 us at 256 signatures but 208 us at
+// 4,096 (rocprofv3, profiles/r02_notary_kernels.txt): waves that need scratch queue for scratch slots.
+__global__ __launch_bounds__(64, 1) void cv_scalars_lat_kernel(uint32_t n, uint32_t cap, const uint8_t *__restrict__ pk,
+                                                               const uint8_t *__restrict__ sig,
+                                                               const uint8_t *__restrict__ arena,
+                                                               const uint64_t *__restrict__ off,
+                                                               const uint32_t *__restrict__ len,
+                                                               uint32_t *__restrict__ ws_dig) {
+    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+    if (i < n) cv_scalars_lane(i, cap, pk, sig, arena, off, len, ws_dig);
 }
 
 // points of the half-size group (throughput form): A and R decoded as one interleaved pair per lane,
@@ -530,7 +544,7 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             // half-size quad group: phases = scalars + point pairs | bitmap clear | hs_straus_quad
             uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
             // 64-thread blocks: the few waves of a small batch spread over CUs (one per SIMD)
-            hipLaunchKernelGGL(cv_scalars_kernel<true>, dim3((m + 63) / 64), dim3(64), 0, stream, m, ws_cap,
+            hipLaunchKernelGGL(cv_scalars_lat_kernel, dim3((m + 63) / 64), dim3(64), 0, stream, m, ws_cap,
                                pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_dig);
             hipLaunchKernelGGL(cv_points_pair_kernel, dim3((2 * m + 63) / 64), dim3(64), 0, stream, m,
                                pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, ws_tab, ws_tabR, ws_ok,
@@ -567,7 +581,7 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
                 hipStream_t st = h ? ax->s2 : stream;
                 const uint32_t a = c0 + sub0[h], mm = subn[h], bl = (mm + CV_BLOCK - 1) / CV_BLOCK;
                 if (h == 1 && g_split_mode == 2) (void)hipStreamWaitEvent(st, ax->prep1, 0);
-                hipLaunchKernelGGL(cv_scalars_kernel<false>, dim3(bl), dim3(CV_BLOCK), 0, st, mm, ws_cap,
+                hipLaunchKernelGGL(cv_scalars_kernel, dim3(bl), dim3(CV_BLOCK), 0, st, mm, ws_cap,
                                    pk + (size_t)a * 32, sig + (size_t)a * 64, arena, off + a, len + a,
                                    ws_dig + sub0[h]);
                 hipLaunchKernelGGL(cv_points_kernel<true>, dim3(bl), dim3(CV_BLOCK), 0, st, mm, pk + (size_t)a * 32,
@@ -591,7 +605,7 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
         if (!lat && g_verify_mode == 1 && g_hs_fused) {
             // half-size group: phases = scalars (hash, lattice, digits) | points (decodes, tables) | hs_straus
             uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
-            hipLaunchKernelGGL(cv_scalars_kernel<false>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap,
+            hipLaunchKernelGGL(cv_scalars_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap,
                                pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_dig);
             if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);
             hipLaunchKernelGGL(cv_points_kernel<false>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, pk + (size_t)c0 * 32,

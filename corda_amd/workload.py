@@ -68,6 +68,35 @@ def make_batch(engine: native.Engine, device: int, n: int, msg_len: int, seed: i
     return SigBatch(n, pk, sig, arena, off, ln, msg_len)
 
 
+def adversarial_records(corpus_path: str):
+    """The golden corpus's REJECTED records with 32-byte (tx-id-shaped) messages: (pk, sig, msgs) —
+    the §8(a) adversarial classes (non-canonical / off-curve / small-order R and A, S >= L, the slide
+    carry loss, cofactored-only, wrong message or key) with verdicts pinned by the oracle."""
+    z = np.load(corpus_path)
+    rej = np.nonzero(z["verdict"] == 0)[0]
+    keep = [i for i in rej if int(z["len"][i]) == 32]
+    msgs = np.stack([z["arena"][int(z["off"][i]):int(z["off"][i]) + 32] for i in keep])
+    return z["pk"][keep], z["sig"][keep], msgs
+
+
+def notary_batch(engine: native.Engine, device: int, n: int, adversarial, key_pool: Optional[int] = None,
+                 seed: int = 4096):
+    """C4 notary batch on the host (as the notary's JVM shim hands it over): n signatures over 32-byte
+    tx ids, 8 signers per transaction, every 16th record replaced by the next adversarial record
+    (cycling through adversarial_records).  Returns (pk, sig, arena, off, len, expected verdicts)."""
+    b = make_batch(engine, device, n, 32, seed=seed + n, key_pool=key_pool)
+    pk, sig, arena, off, ln = b.to_host()
+    pk, sig, arena = pk.copy(), sig.copy(), arena.copy()
+    expect = np.ones(n, bool)
+    apk, asig, amsg = adversarial
+    for j, i in enumerate(range(0, n, 16)):
+        a = j % len(apk)
+        pk[i], sig[i] = apk[a], asig[a]
+        arena[i * 32:(i + 1) * 32] = amsg[a]
+        expect[i] = False
+    return pk, sig, np.concatenate([arena, np.zeros(16, np.uint8)]), off, ln, expect
+
+
 def corrupt_fraction(batch: SigBatch, every: int = 16) -> torch.Tensor:
     """Flip one bit of S in every `every`-th signature (the C4 "1/16 adversarial" mix); returns the
     expected verdicts (bool tensor on the device)."""

@@ -312,3 +312,24 @@ def test_fused_halfsize_prep_logic_on_golden_corpus(host_harness, corpus, manife
         if v != corpus["verdict"][i] or st.value != corpus["status"][i]:
             bad.append(manifest["classes"][corpus["cls"][i]])
     assert not bad, sorted(set(bad))
+
+
+def test_slide_replay_structured(host_harness):
+    """The word-skipping slide() replay (cv_scalar.h) against the literal oracle on structured
+    scalars: all-ones with one hole at every position, a top bit over low runs of every length,
+    sparse words with the top bit set, and alternating patterns."""
+    H = host_harness
+    full = (1 << 256) - 1
+    cases = [full ^ (1 << k) for k in range(256)]
+    cases += [(1 << 255) | ((1 << k) - 1) for k in range(256)]
+    cases += [(1 << 255) | (((1 << 20) - 1) << k) for k in range(0, 235, 7)]
+    cases += [(1 << 255) | (1 << k) | (1 << (k + 7)) for k in range(0, 240, 5)]
+    cases += [int("10" * 128, 2), int("01" * 128, 2) | (1 << 255), int("1110" * 64, 2), int("1000001" * 36, 2) | (1 << 255)]
+    rng = random.Random(11)
+    for _ in range(300):
+        s = (1 << 255) | rng.getrandbits(255)
+        s &= ~(rng.getrandbits(256) & rng.getrandbits(256))      # sparse holes
+        cases.append(s | (1 << 255))
+    for s in cases:
+        sb = (s & full).to_bytes(32, "little")
+        assert H.cvh_slide_drops(_b(sb)) == int(E.slide_drops_carry(sb)), hex(s)
