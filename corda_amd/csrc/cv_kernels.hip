@@ -199,13 +199,9 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_points_kernel(uint32_t n, cons
 // lane decoding the key A into k*(-A), the odd lane R into k*R, side by side (the same instructions
 // on both lanes: cv_hs_point_one) with the latency (ILP) field forms — half the serial chain of the
 // throughput form, whose single lane runs both decodes.  The even lane writes ok = key_ok AND r_ok.
-__global__ __launch_bounds__(64) void cv_points_pair_kernel(uint32_t n, const uint8_t *__restrict__ pk,
-                                                            const uint8_t *__restrict__ sig,
-                                                            uint32_t *__restrict__ ws_tab,
-                                                            uint32_t *__restrict__ ws_tabR,
-                                                            uint8_t *__restrict__ ws_ok,
-                                                            uint8_t *__restrict__ status) {
-    const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+__device__ __forceinline__ void cv_points_pair_lane(uint32_t g, uint32_t n, const uint8_t *pk, const uint8_t *sig,
+                                                    uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok,
+                                                    uint8_t *status) {
     const uint32_t i = g >> 1;
     if (i >= n) return;                       // both lanes of a pair leave together
     const bool is_r = (g & 1u) != 0;
@@ -216,6 +212,38 @@ __global__ __launch_bounds__(64) void cv_points_pair_kernel(uint32_t n, const ui
     if (!is_r) {
         ws_ok[i] = (ok && r_ok) ? 1 : 0;
         if (status) status[i] = ok ? 0 : 1;
+    }
+}
+__global__ __launch_bounds__(64) void cv_points_pair_kernel(uint32_t n, const uint8_t *__restrict__ pk,
+                                                            const uint8_t *__restrict__ sig,
+                                                            uint32_t *__restrict__ ws_tab,
+                                                            uint32_t *__restrict__ ws_tabR,
+                                                            uint8_t *__restrict__ ws_ok,
+                                                            uint8_t *__restrict__ status) {
+    cv_points_pair_lane(blockIdx.x * 64 + threadIdx.x, n, pk, sig, ws_tab, ws_tabR, ws_ok, status);
+}
+
+// Small (latency) batches: the scalars and the point pairs of a signature are independent (both
+// read only the inputs), so one launch runs them side by side on otherwise idle SIMDs — blocks
+// [0, nbp) decode point pairs, blocks [nbp, grid) derive the scalars — and the batch pays
+// max(scalars, points) instead of their sum.  One wave per 64-thread block, the whole register
+// file for it (no spills in either role).
+__global__ __launch_bounds__(64, 1) void cv_prep_lat_kernel(uint32_t n, uint32_t cap, uint32_t nbp,
+                                                            const uint8_t *__restrict__ pk,
+                                                            const uint8_t *__restrict__ sig,
+                                                            const uint8_t *__restrict__ arena,
+                                                            const uint64_t *__restrict__ off,
+                                                            const uint32_t *__restrict__ len,
+                                                            uint32_t *__restrict__ ws_dig,
+                                                            uint32_t *__restrict__ ws_tab,
+                                                            uint32_t *__restrict__ ws_tabR,
+                                                            uint8_t *__restrict__ ws_ok,
+                                                            uint8_t *__restrict__ status) {
+    if (blockIdx.x < nbp) {
+        cv_points_pair_lane(blockIdx.x * 64 + threadIdx.x, n, pk, sig, ws_tab, ws_tabR, ws_ok, status);
+    } else {
+        const uint32_t i = (blockIdx.x - nbp) * 64 + threadIdx.x;
+        if (i < n) cv_scalars_lane(i, cap, pk, sig, arena, off, len, ws_dig);
     }
 }
 
@@ -343,6 +371,10 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_quad_kernel(uint32_t n,
     if ((threadIdx.x & 63u) == 0 && bits)
         atomicOr(reinterpret_cast<unsigned long long *>(bitmap + (sig0 >> 6)), (unsigned long long)bits << (sig0 & 63u));
 }
+
+// 1 = small batches run scalars and point pairs in one launch (cv_prep_lat_kernel), 0 = two launches
+static int g_prep_lat_fused = 1;
+extern "C" void cvk_set_prep_lat_fused(int v) { g_prep_lat_fused = v ? 1 : 0; }
 
 // Batches of at most this many signatures run the quad kernels (set by cvk_set_quad_max; 0 = never)
 static uint32_t g_quad_max = 32768;
@@ -544,11 +576,18 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             // half-size quad group: phases = scalars + point pairs | bitmap clear | hs_straus_quad
             uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
             // 64-thread blocks: the few waves of a small batch spread over CUs (one per SIMD)
-            hipLaunchKernelGGL(cv_scalars_lat_kernel, dim3((m + 63) / 64), dim3(64), 0, stream, m, ws_cap,
-                               pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_dig);
-            hipLaunchKernelGGL(cv_points_pair_kernel, dim3((2 * m + 63) / 64), dim3(64), 0, stream, m,
-                               pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, ws_tab, ws_tabR, ws_ok,
-                               status ? status + c0 : nullptr);
+            if (g_prep_lat_fused) {
+                const uint32_t nbp = (2 * m + 63) / 64, nbs = (m + 63) / 64;
+                hipLaunchKernelGGL(cv_prep_lat_kernel, dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp,
+                                   pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_dig,
+                                   ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr);
+            } else {
+                hipLaunchKernelGGL(cv_scalars_lat_kernel, dim3((m + 63) / 64), dim3(64), 0, stream, m, ws_cap,
+                                   pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_dig);
+                hipLaunchKernelGGL(cv_points_pair_kernel, dim3((2 * m + 63) / 64), dim3(64), 0, stream, m,
+                                   pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, ws_tab, ws_tabR, ws_ok,
+                                   status ? status + c0 : nullptr);
+            }
             if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);
             (void)hipMemsetAsync(bitmap + (size_t)c0 / 64, 0, (size_t)((m + 63) / 64) * 8, stream);
             if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);

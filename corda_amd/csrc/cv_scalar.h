@@ -153,66 +153,51 @@ __host__ __device__ __forceinline__ void sc_muladd(uint32_t out[8], const uint32
 
 // ---------------------------------------------------------------- slide() carry loss
 
-// Exact replay of GroupElement.slide(S) tracking only what decides the dropped carry: the scan
-// keeps the not-yet-absorbed bits as a 256-bit integer U; a "subtract" step adds 2^(i+b) to U
-// (the Java loop that zeroes a run of ones and sets the next zero); a carry out of bit 255 is the
-// drop.  Fast path: with bit 255 clear no carry can leave the top (checked exhaustively on the top
-// bits and on 10^5 random scalars by tests/test_oracle.py::test_slide_drop_needs_bit255).
-// U lives in four 64-bit registers (word selects, never a dynamically indexed array, which the GPU
-// would keep in scratch memory) and runs of zero bits are skipped with count-trailing-zeros, so the
-// scan visits only the ~45 window starts instead of all 256 positions: a lane with bit 255 set no
-// longer holds its wave for the whole bit-by-bit replay (it cost a 4,096-signature notary batch with
-// 1/16 adversarial items +0.15 ms, tools/lat_scaling.py).
+// Exact replay of GroupElement.slide(S) reduced to what decides the dropped carry.  Facts about the
+// Java loop (window start i = a set bit, r[i] = 1, then b = 1..6 over r[i+b]):
+//   b <= 3: r[i] + 2^b <= 1 + 2 + 4 + 8 = 15, so a set bit is always ADDED (no carry);
+//   b == 4: r[i] + 16 > 15 and r[i] - 16 >= -15, so a set bit is always SUBTRACTED: r[i+4] cleared
+//           and +2^(i+5) carried into the bits above (the loop that zeroes a run of ones and sets
+//           the next zero);  b = 5, 6: neither fits (|r[i]| <= 15 < 17), a set bit only breaks.
+// So the scan is a two-state machine over the ORIGINAL bits: with no carry pending the next window
+// starts at the next set bit; with a carry pending the run of ones above is cleared and the window
+// starts at the first zero (which the carry turns into a one).  A window at j leaves a carry iff
+// j + 4 < 256 and bit j+4 is set, and the next scan resumes at j + 5.  A carry reaching bit 256 is
+// the drop.  Runs are skipped with count-trailing-zeros on 64-bit windows of S, so a scalar costs
+// its ~45 windows, not its 256 bits (the bit-by-bit replay held a 4,096-signature notary batch with
+// 1/16 adversarial items for +0.1 ms, tools/lat_scaling.py).  Fast path: with bit 255 clear no
+// carry can leave the top (checked by tests/test_oracle.py::test_slide_drop_needs_bit255); the
+// replay is pinned against the literal oracle by tests/test_device_logic.py::test_slide_replay_*.
+// The 256-bit value lives in four 64-bit registers read through select trees (never a dynamically
+// indexed array, which the GPU would keep in scratch memory).
 CV_HD uint64_t cv_sel4(const uint64_t u[4], int q) { return (q & 2) ? ((q & 1) ? u[3] : u[2]) : ((q & 1) ? u[1] : u[0]); }
-// bit j of U (j < 256)
-CV_HD uint32_t cv_u_bit(const uint64_t u[4], int j) { return (uint32_t)(cv_sel4(u, j >> 6) >> (j & 63)) & 1u; }
-CV_HD void cv_u_clear(uint64_t u[4], int j) {
-    const uint64_t m = ~(1ull << (j & 63));
-#pragma unroll
-    for (int k = 0; k < 4; k++)
-        if (k == (j >> 6)) u[k] &= m;
-}
-// U += 2^j; true when the carry runs out of bit 255
-CV_HD bool cv_u_add_pow2(uint64_t u[4], int j) {
-    uint64_t c = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint64_t a = (k == (j >> 6)) ? (1ull << (j & 63)) : 0ull;
-        const uint64_t t = u[k] + a, t2 = t + c;
-        c = (uint64_t)((t < a) | (t2 < t));
-        u[k] = t2;
-    }
-    return c != 0;
+// bits [j, j + 64) of U, zeros past bit 255 (0 <= j < 256)
+CV_HD uint64_t cv_u_window(const uint64_t u[4], int j) {
+    const int q = j >> 6, b = j & 63;
+    const uint64_t lo = cv_sel4(u, q), hi = q < 3 ? cv_sel4(u, q + 1) : 0ull;
+    return b ? (lo >> b) | (hi << (64 - b)) : lo;
 }
 __host__ __device__ __forceinline__ bool slide_drops_carry(const uint32_t s[8]) {
     if (!(s[7] >> 31)) return false;
     uint64_t u[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) u[k] = s[2 * k] | ((uint64_t)s[2 * k + 1] << 32);
-    int i = 0;
-    while (i < 256) {
-        const uint64_t w = cv_sel4(u, i >> 6) >> (i & 63);
-        if (w == 0) {                                  // no set bit left in this word: next word
-            i = ((i >> 6) + 1) << 6;
+    int j = 0;
+    bool carry = false;
+    while (j < 256) {
+        const uint64_t w = cv_u_window(u, j);
+        // carry pending: first zero bit (the carry's landing place); none: first set bit
+        const uint64_t look = carry ? ~w : w;
+        if (look == 0) {                               // not in this 64-bit window (runs of ones
+            j += 64;                                   // end at bit 256 at the latest: zero padding)
             continue;
         }
-        i += __builtin_ctzll(w);                       // next window start (a set bit)
-        int d = 1;
-        for (int b = 1; b <= 6 && i + b < 256; b++) {
-            if (!cv_u_bit(u, i + b)) continue;
-            if (d + (1 << b) <= 15) {
-                d += 1 << b;
-                cv_u_clear(u, i + b);
-            } else if (d - (1 << b) >= -15) {
-                d -= 1 << b;
-                if (cv_u_add_pow2(u, i + b)) return true;
-            } else {
-                break;
-            }
-        }
-        i++;
+        j += __builtin_ctzll(look);                    // the window start
+        if (j >= 256) return carry;                    // a carry ran past bit 255: dropped
+        carry = j + 4 < 256 && ((cv_u_window(u, j) >> 4) & 1u);
+        j += 5;
     }
-    return false;
+    return carry;
 }
 
 // Effective [S]B scalar of eddsa-0.1.0, reduced mod L: (S - 2^256 * drop) mod L.

@@ -330,6 +330,7 @@ def test_slide_replay_structured(host_harness):
         s = (1 << 255) | rng.getrandbits(255)
         s &= ~(rng.getrandbits(256) & rng.getrandbits(256))      # sparse holes
         cases.append(s | (1 << 255))
+    cases += [(1 << 255) | rng.getrandbits(255) for _ in range(3000)]      # dense random
     for s in cases:
         sb = (s & full).to_bytes(32, "little")
         assert H.cvh_slide_drops(_b(sb)) == int(E.slide_drops_carry(sb)), hex(s)

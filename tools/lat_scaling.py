@@ -15,10 +15,19 @@ from corda_amd import native, workload  # noqa: E402
 from notary_sweep import adversarial_pool, build  # noqa: E402
 
 eng = native.Engine(1)
+lib = native.load()
+import ctypes  # noqa: E402
+for kv in filter(None, os.environ.get("CV_KNOBS", "").split(",")):   # e.g. cvk_set_prep_lat_fused=0
+    k, v = kv.split("=")
+    getattr(lib, k).argtypes = [ctypes.c_int]
+    getattr(lib, k)(int(v))
 adv = adversarial_pool()
 dev = torch.device("cuda", 0)
-for n in (256, 1024, 4096, 16384):
-    for mix in (False, True):
+# python tools/lat_scaling.py [SIZES [MIXES]]   e.g. 4096 1  (one size, adversarial only)
+sizes = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else (256, 1024, 4096, 16384)
+mixes = [bool(int(x)) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else (False, True)
+for n in sizes:
+    for mix in mixes:
         if mix:
             pk, sig, arena, off, ln, _ = build(eng, n, None, adv)
         else:
