@@ -141,6 +141,7 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsprep_kernel(uint32_t n, uint
 // kernel (2 waves per SIMD) the hash's serial 64-bit chains were 32 % of the prep's cycles
 // (tools/prep_probe.py).  Any block size (small latency batches launch 64-thread blocks so the few
 // waves spread over CUs).
+template <bool B16 = false>
 __device__ __forceinline__ void cv_scalars_lane(uint32_t i, uint32_t cap, const uint8_t *pk, const uint8_t *sig,
                                                 const uint8_t *arena, const uint64_t *off, const uint32_t *len,
                                                 uint32_t *ws_dig) {
@@ -150,7 +151,7 @@ __device__ __forceinline__ void cv_scalars_lane(uint32_t i, uint32_t cap, const 
     load_words8(sw, sig + (size_t)i * 64 + 32);
     uint32_t hs[CV_HS_WORDS];
     cv_keyed_hs(aw, rw, sw, arena + off[i], len[i], hs);
-    cv_hs_scalars(hs, ws_dig + i, cap);
+    cv_hs_scalars<B16>(hs, ws_dig + i, cap);
 }
 __global__ __launch_bounds__(CV_BLOCK, 3) void cv_scalars_kernel(uint32_t n, uint32_t cap, const uint8_t *__restrict__ pk,
                                                                  const uint8_t *__restrict__ sig,
@@ -228,6 +229,7 @@ __global__ __launch_bounds__(64) void cv_points_pair_kernel(uint32_t n, const ui
 // [0, nbp) decode point pairs, blocks [nbp, grid) derive the scalars — and the batch pays
 // max(scalars, points) instead of their sum.  One wave per 64-thread block, the whole register
 // file for it (no spills in either role).
+template <bool B16>
 __global__ __launch_bounds__(64, 1) void cv_prep_lat_kernel(uint32_t n, uint32_t cap, uint32_t nbp,
                                                             const uint8_t *__restrict__ pk,
                                                             const uint8_t *__restrict__ sig,
@@ -243,7 +245,7 @@ __global__ __launch_bounds__(64, 1) void cv_prep_lat_kernel(uint32_t n, uint32_t
         cv_points_pair_lane(blockIdx.x * 64 + threadIdx.x, n, pk, sig, ws_tab, ws_tabR, ws_ok, status);
     } else {
         const uint32_t i = (blockIdx.x - nbp) * 64 + threadIdx.x;
-        if (i < n) cv_scalars_lane(i, cap, pk, sig, arena, off, len, ws_dig);
+        if (i < n) cv_scalars_lane<B16>(i, cap, pk, sig, arena, off, len, ws_dig);
     }
 }
 
@@ -371,6 +373,46 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_quad_kernel(uint32_t n,
     if ((threadIdx.x & 63u) == 0 && bits)
         atomicOr(reinterpret_cast<unsigned long long *>(bitmap + (sig0 >> 6)), (unsigned long long)bits << (sig0 & 63u));
 }
+
+// Tri-chain kernel (cv_hsquad.h): grid 16n lanes, 4 signatures per wave; digits from
+// cv_hs_scalars<true>.  Bitmap words zero on entry, as for the quad kernel.
+__global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_tri_kernel(uint32_t n, uint32_t cap,
+                                                                    const uint32_t *__restrict__ ws_dig,
+                                                                    const uint32_t *__restrict__ ws_tab,
+                                                                    const uint32_t *__restrict__ ws_tabR,
+                                                                    const uint8_t *__restrict__ ws_ok,
+                                                                    uint64_t *__restrict__ bitmap) {
+    constexpr int ROW = CV_BTAB_ENTRIES * CV_BTAB_STRIDE;
+    const uint32_t lane0 = blockIdx.x * CV_BLOCK + (threadIdx.x & ~63u);
+    const uint32_t sig0 = lane0 >> 4;                        // first signature of this wave
+    if (sig0 >= n) return;                                   // whole waves leave together
+    const uint32_t i0 = (blockIdx.x * CV_BLOCK + threadIdx.x) >> 4;
+    const int r = threadIdx.x & 3, c = (threadIdx.x >> 2) & 3;
+    const uint32_t i = i0 < n ? i0 : n - 1;
+    int nw = (int)ws_dig[(size_t)64 * cap + i];
+    nw = nw < 32 ? 32 : nw;                                  // the B halves need 32 windows
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const int x = __shfl_xor(nw, o);
+        nw = x > nw ? x : nw;
+    }
+    nw = __builtin_amdgcn_readfirstlane(nw);
+    // quad 0: v digits over k*R, 1: -u digits over k*(-A), 2: w_lo over k*B, 3: w_hi over k*2^128*B
+    const uint32_t *tab = c == 0 ? ws_tabR + (size_t)i * CV_TAB_WORDS
+                        : c == 1 ? ws_tab + (size_t)i * CV_TAB_WORDS
+                                 : CV_BCOMB + (c == 2 ? 0 : 2 * ROW);
+    const int field = c == 0 ? 5 : c == 1 ? 0 : c == 2 ? 10 : 15;
+    const bool eq = cv_tri_hs_straus(ws_dig + i, cap, tab, c >= 2, field, nw, r);
+    const bool acc = eq && ws_ok[i] && i0 < n && (threadIdx.x & 15u) == 0;
+    uint64_t b = __ballot(acc) & 0x0001000100010001ull;      // lanes 0, 16, 32, 48
+    b = (b | (b >> 15)) & 0x0000000300000003ull;
+    b = (b | (b >> 30)) & 0xfull;
+    if ((threadIdx.x & 63u) == 0 && b) atomicOr((unsigned long long *)(bitmap + sig0 / 64), (unsigned long long)b << (sig0 & 63));
+}
+
+// Batches of at most this many signatures run the tri-chain kernel (cvk_set_tri_max; 0 = never)
+static uint32_t g_tri_max = 4096;
+extern "C" void cvk_set_tri_max(int m) { g_tri_max = (uint32_t)(m < 0 ? 0 : m); }
 
 // 1 = small batches run scalars and point pairs in one launch (cv_prep_lat_kernel), 0 = two launches
 static int g_prep_lat_fused = 1;
@@ -576,11 +618,17 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             // half-size quad group: phases = scalars + point pairs | bitmap clear | hs_straus_quad
             uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
             // 64-thread blocks: the few waves of a small batch spread over CUs (one per SIMD)
-            if (g_prep_lat_fused) {
+            const bool tri = m <= g_tri_max;
+            if (g_prep_lat_fused || tri) {
                 const uint32_t nbp = (2 * m + 63) / 64, nbs = (m + 63) / 64;
-                hipLaunchKernelGGL(cv_prep_lat_kernel, dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp,
-                                   pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_dig,
-                                   ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr);
+                if (tri)
+                    hipLaunchKernelGGL(cv_prep_lat_kernel<true>, dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp,
+                                       pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0,
+                                       ws_dig, ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr);
+                else
+                    hipLaunchKernelGGL(cv_prep_lat_kernel<false>, dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp,
+                                       pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0,
+                                       ws_dig, ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr);
             } else {
                 hipLaunchKernelGGL(cv_scalars_lat_kernel, dim3((m + 63) / 64), dim3(64), 0, stream, m, ws_cap,
                                    pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_dig);
@@ -591,8 +639,12 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);
             (void)hipMemsetAsync(bitmap + (size_t)c0 / 64, 0, (size_t)((m + 63) / 64) * 8, stream);
             if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
-            hipLaunchKernelGGL(cv_hs_straus_quad_kernel, dim3((4 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
-                               stream, m, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
+            if (tri)
+                hipLaunchKernelGGL(cv_hs_straus_tri_kernel, dim3((16 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
+                                   stream, m, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
+            else
+                hipLaunchKernelGGL(cv_hs_straus_quad_kernel, dim3((4 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK),
+                                   0, stream, m, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
             if (ev && c0 == 0) (void)hipEventRecord(ev[3], stream);
             continue;
         }

@@ -759,6 +759,11 @@ __host__ __device__ inline int cv_pmt_verify(uint32_t b, uint32_t e, const uint8
 // The GPU runs them as separate kernels (cv_kernels.hip: cv_scalars_kernel at 4 waves per SIMD;
 // cv_points_kernel with both decodes interleaved per lane for throughput, or cv_points_pair_kernel
 // with one decode per lane of a lane pair for small latency-bound batches).
+// B16 = false: w as signed radix-256 digits at the even windows (dlo, dhi: 9 bits at 10 and 19, the
+// k*B / k*2^128*B rows of the single-chain forms); B16 = true: w as 64 signed radix-16 digits split in
+// two 32-window halves (bits 10 and 15, 5 bits each: window t holds digit t and digit 32 + t), for the
+// tri-chain form (cv_hsquad.h) whose two B quads each add one digit per window like the R / A quads.
+template <bool B16 = false>
 __host__ __device__ __forceinline__ void cv_hs_scalars(const uint32_t hs[CV_HS_WORDS], uint32_t *dig, size_t stride) {
     uint32_t h[8], s[8], u[8], v[8], w[8];
 #pragma unroll
@@ -769,10 +774,16 @@ __host__ __device__ __forceinline__ void cv_hs_scalars(const uint32_t hs[CV_HS_W
 #pragma unroll 4
     for (int win = 0; win < 64; win++) {
         const int da = -digit16(u, win), dr = v_neg ? -digit16(v, win) : digit16(v, win);
-        const bool bw = (win & 1) == 0 && win < 32;
-        const int dlo = bw ? digit256(w, win >> 1) : 0, dhi = bw ? digit256(w, 16 + (win >> 1)) : 0;
-        dig[(size_t)win * stride] = ((uint32_t)da & 0x1fu) | (((uint32_t)dr & 0x1fu) << 5) |
-                                    (((uint32_t)dlo & 0x1ffu) << 10) | (((uint32_t)dhi & 0x1ffu) << 19);
+        uint32_t bf;
+        if (B16) {
+            const int dlo = win < 32 ? digit16(w, win) : 0, dhi = win < 32 ? digit16(w, 32 + win) : 0;
+            bf = (((uint32_t)dlo & 0x1fu) << 10) | (((uint32_t)dhi & 0x1fu) << 15);
+        } else {
+            const bool bw = (win & 1) == 0 && win < 32;
+            const int dlo = bw ? digit256(w, win >> 1) : 0, dhi = bw ? digit256(w, 16 + (win >> 1)) : 0;
+            bf = (((uint32_t)dlo & 0x1ffu) << 10) | (((uint32_t)dhi & 0x1ffu) << 19);
+        }
+        dig[(size_t)win * stride] = ((uint32_t)da & 0x1fu) | (((uint32_t)dr & 0x1fu) << 5) | bf;
     }
     dig[64 * stride] = (uint32_t)nwin;
 }

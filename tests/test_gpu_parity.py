@@ -271,14 +271,17 @@ def test_keyed_device_baseline_size(engine):
 
 
 # ---------------------------------------------------------------- both Straus forms at every size
-@pytest.mark.parametrize("quad_max", [0, 1 << 30])
-def test_lane_and_quad_forms_agree(engine, corpus, oracle_c, quad_max):
-    """Small batches normally run the 4-lanes-per-signature (quad) Straus; force each form in turn
-    (internal switch cvk_set_quad_max) over the golden corpus, keyed and plain, and a random batch."""
+@pytest.mark.parametrize("quad_max,tri_max", [(0, 0), (1 << 30, 0), (1 << 30, 1 << 30)])
+def test_lane_quad_and_tri_forms_agree(engine, corpus, oracle_c, quad_max, tri_max):
+    """Small batches normally run the 16-lanes-per-signature (tri-chain) or 4-lanes-per-signature
+    (quad) Straus; force each form in turn (internal switches cvk_set_quad_max / cvk_set_tri_max)
+    over the golden corpus, keyed and plain, and a random batch."""
     import ctypes
     lib = native.load()
     lib.cvk_set_quad_max.argtypes = [ctypes.c_uint32]
     lib.cvk_set_quad_max(quad_max)
+    lib.cvk_set_tri_max.argtypes = [ctypes.c_int]
+    lib.cvk_set_tri_max(tri_max)
     try:
         bitmap, status = engine.verify_batch(corpus["pk"], corpus["sig"], corpus["arena"], corpus["off"], corpus["len"])
         assert np.array_equal(_bits(bitmap, len(corpus["pk"])), corpus["verdict"].astype(bool))
@@ -301,6 +304,7 @@ def test_lane_and_quad_forms_agree(engine, corpus, oracle_c, quad_max):
         assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
     finally:
         lib.cvk_set_quad_max(32768)
+        lib.cvk_set_tri_max(4096)
 
 
 # ---------------------------------------------------------------- both throughput schedules
