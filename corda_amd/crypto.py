@@ -145,7 +145,8 @@ class DigitalSignature(OpaqueBytes):
             self.by = by
 
         def verify_with_ecdsa(self, content) -> None:
-            content = content.bytes if isinstance(content, OpaqueBytes) else bytes(content)
+            # verifyWithECDSA(content: OpaqueBytes): SecureHash is OpaqueBytes in the reference
+            content = content.bytes if hasattr(content, "bytes") and not isinstance(content, bytes) else bytes(content)
             verify_with_ecdsa(self.by, content, self)
 
 

@@ -42,6 +42,19 @@ def gather_bitmap(local_words: torch.Tensor, n: int, group=None) -> torch.Tensor
     return out[: (n + 63) // 64]
 
 
+def gather_bitmaps(local: torch.Tensor, n: int, group=None) -> torch.Tensor:
+    """gather_bitmap for k bitmaps at once (local: (k, shard_words) int64 — e.g. verdict bits and
+    key-status bits): ONE all-gather, returns (k, ceil(n/64)) global bitmaps on every rank."""
+    world = dist.get_world_size(group)
+    per = shard_words(n, world)
+    k = local.shape[0]
+    if local.shape != (k, per):
+        raise ValueError(f"local bitmaps have shape {tuple(local.shape)}, expected ({k}, {per})")
+    out = torch.empty(world * k * per, dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, local.contiguous().view(-1), group=group)
+    return out.view(world, k, per).permute(1, 0, 2).reshape(k, world * per)[:, : (n + 63) // 64]
+
+
 def tx_verdicts_torch(bitmap: torch.Tensor, tx_sig_begin: torch.Tensor) -> torch.Tensor:
     """Per-transaction AND of signature bits on whatever device the bitmap lives on (the commit step):
     tx t is ok iff it has at least one signature and all of [begin_t, begin_{t+1}) are set."""

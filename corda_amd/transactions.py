@@ -75,11 +75,17 @@ class WireTransaction:
     def id(self) -> SecureHash:
         if self._id is None:
             compute_ids([self])
+            if self._id is None:
+                raise MerkleTreeException("Cannot calculate Merkle root on empty hash list.")
         return self._id
 
 
-def compute_ids(txs: Sequence[WireTransaction], engine: Optional[native.Engine] = None) -> List[SecureHash]:
-    """WireTransaction.id for many transactions in one GPU call (leaf SHA-256 + Merkle tree)."""
+def compute_ids(txs: Sequence[WireTransaction], engine: Optional[native.Engine] = None
+                ) -> List[Optional[SecureHash]]:
+    """WireTransaction.id for many transactions in one GPU call (leaf SHA-256 + Merkle tree).  Per
+    transaction: its id, or None for a transaction with no leaves — whose `.id` then raises
+    MerkleTreeException on its own (MerkleTree.getMerkleTree(emptyList), MerkleTransaction.kt), so
+    one empty transaction does not fail the others in the batch."""
     leaves: List[bytes] = []
     begin = [0]
     for t in txs:
@@ -95,7 +101,8 @@ def compute_ids(txs: Sequence[WireTransaction], engine: Optional[native.Engine] 
     out = []
     for k, t in enumerate(txs):
         if st[k] == native.CV_TX_EMPTY:
-            raise MerkleTreeException("Cannot calculate Merkle root on empty hash list.")
+            out.append(None)
+            continue
         t._id = SecureHash(ids[k].tobytes())
         out.append(t._id)
     return out

@@ -7,9 +7,10 @@ import ed25519_ref as E
 from corda_amd import native
 from corda_amd.crypto import (CompositeKey, DigitalSignature, DummyPublicKey, EdDSAPublicKey, IllegalArgumentException,
                               InvalidKeyException, NullPublicKey, NullSignature, SignatureException, verify_with_ecdsa)
-from corda_amd.notary import (BatchingNotary, Conflict, SignaturesMissing, SignRequest, TransactionInvalid)
-from corda_amd.transactions import (IllegalStateException, SecureHash, SignaturesMissingException, SignedTransaction,
-                                    WireTransaction, compute_ids, verify_signatures_batch)
+from corda_amd.notary import (BatchingNotary, Conflict, ConsumingTx, NotaryException, SignaturesMissing, SignRequest,
+                              TimestampChecker, TimestampInvalid, Timestamp, TransactionInvalid)
+from corda_amd.transactions import (IllegalStateException, MerkleTreeException, SecureHash, SignaturesMissingException,
+                                    SignedTransaction, WireTransaction, compute_ids, verify_signatures_batch)
 
 pytestmark = pytest.mark.gpu
 
@@ -180,6 +181,133 @@ def test_notary_batch(engine):
     r2 = notary.notarise([SignRequest(make_stx(engine, signer_idx=[94], inputs=(b"s-94",),
                                                extra_must=(notary.owning_key,)), caller="q")])
     assert r2[0].ok
+
+
+# ---------------------------------------------------------------- NotaryServiceTests.kt:46-106 restated
+NOTARY_SEED = E.entropy_to_seed(21)
+
+
+def _notary(engine, validating=False, clock=None):
+    return BatchingNotary(NOTARY_SEED, validating=validating, engine=engine,
+                          timestamp_checker=TimestampChecker(clock=clock) if clock else None)
+
+
+def test_notary_signs_unique_tx_with_valid_timestamp(engine):
+    """NotaryServiceTests.kt:46-58: setTime(now, 30 s) -> a notary signature over stx.id."""
+    now = 1_700_000_000.0
+    notary = _notary(engine, clock=lambda: now)
+    stx = make_stx(engine, signer_idx=[110], inputs=(b"issued-110",))
+    r = notary.notarise([SignRequest(stx, "MiniCorp", timestamp=Timestamp.around(now, 30.0))])[0]
+    sig = r.get_or_throw()
+    sig.verify_with_ecdsa(stx.id)
+    assert sig.by == notary.public_key
+
+
+def test_notary_signs_unique_tx_without_timestamp(engine):
+    """NotaryServiceTests.kt:60-71."""
+    notary = _notary(engine)
+    stx = make_stx(engine, signer_idx=[111], inputs=(b"issued-111",))
+    notary.notarise([SignRequest(stx, "MiniCorp")])[0].get_or_throw().verify_with_ecdsa(stx.id)
+
+
+def test_notary_reports_invalid_timestamp(engine):
+    """NotaryServiceTests.kt:73-86: setTime(now + 3600 s, 30 s) -> NotaryError.TimestampInvalid."""
+    now = 1_700_000_000.0
+    notary = _notary(engine, clock=lambda: now)
+    stx = make_stx(engine, signer_idx=[112], inputs=(b"issued-112",))
+    r = notary.notarise([SignRequest(stx, "MiniCorp", timestamp=Timestamp.around(now + 3600, 30.0))])[0]
+    with pytest.raises(NotaryException) as ei:
+        r.get_or_throw()
+    assert isinstance(ei.value.error, TimestampInvalid)
+    # TimestampChecker.kt:19-24 bounds: a window ending 31 s ago or starting 31 s ahead is invalid
+    tc = TimestampChecker(clock=lambda: now)
+    assert tc.is_valid(Timestamp(now - 30, None)) and not tc.is_valid(Timestamp(None, now - 31))
+    assert tc.is_valid(Timestamp(None, now + 5)) and not tc.is_valid(Timestamp(now + 31, None))
+
+
+def test_notary_reports_conflict_for_duplicate(engine):
+    """NotaryServiceTests.kt:88-106: the same stx notarised twice -> the second gets
+    NotaryError.Conflict whose tx is stx.tx and whose signed conflict report verifies against the
+    notary key (conflict.verified()); in one batch and across batches alike."""
+    notary = _notary(engine)
+    stx = make_stx(engine, signer_idx=[113], inputs=(b"issued-113",))
+    first, second = notary.notarise([SignRequest(stx, "MiniCorp"), SignRequest(stx, "MiniCorp")])
+    first.get_or_throw().verify_with_ecdsa(stx.id)
+    with pytest.raises(NotaryException) as ei:
+        second.get_or_throw()
+    err = ei.value.error
+    assert isinstance(err, Conflict) and err.tx is stx.tx and err.tx.id == stx.id
+    report = err.conflict.verified(engine)
+    assert report.state_history == {b"issued-113": ConsumingTx(stx.id, 0, "MiniCorp")}
+    assert err.conflict.sig.by == notary.public_key
+    third = notary.notarise([SignRequest(stx, "Other")])[0]       # a later batch sees the same commit
+    assert isinstance(third.error, Conflict)
+    assert third.error.conflict.verified(engine).state_history[b"issued-113"].requesting_party == "MiniCorp"
+    forged = type(err.conflict)(err.conflict.raw.replace(b"MiniCorp", b"MegaCorp"), err.conflict.sig)
+    with pytest.raises(SignatureException):
+        forged.verified(engine)
+
+
+def test_validating_notary_errors(engine):
+    """ValidatingNotaryServiceTests.kt:44-82 + ValidatingNotaryFlow.kt:24-45: missing signatures ->
+    SignaturesMissing(exact set); a bad signature -> TransactionInvalid; a signature by a non-EdDSA
+    key (InvalidKeyException: not a SignatureException) is re-thrown, failing the flow."""
+    notary = _notary(engine, validating=True)
+    missing = make_stx(engine, signer_idx=[114], must_idx=[114, 115], inputs=(b"s-114",))
+    bad = make_stx(engine, signer_idx=[116], inputs=(b"s-116",))
+    bad = SignedTransaction(bad._wtx, [DigitalSignature.WithKey(bad.sigs[0].by, b"\x07" * 64)], bad.id)
+    nonkey = make_stx(engine, signer_idx=[117], inputs=(b"s-117",))
+    nonkey = SignedTransaction(nonkey._wtx, [DigitalSignature.WithKey(NullPublicKey, b"\x00" * 64)] + nonkey.sigs,
+                               nonkey.id)
+    good = make_stx(engine, signer_idx=[118], inputs=(b"s-118",))
+    res = notary.notarise([SignRequest(x, "p") for x in (missing, bad, nonkey, good)])
+    assert isinstance(res[0].error, SignaturesMissing)
+    assert res[0].error.missing_signers == {keypair(115)[1].composite}
+    assert isinstance(res[1].error, TransactionInvalid)
+    assert res[2].error is None and isinstance(res[2].failure, InvalidKeyException)
+    with pytest.raises(InvalidKeyException):
+        res[2].get_or_throw()
+    res[3].get_or_throw().verify_with_ecdsa(good.id)
+    # neither failed request consumed its inputs
+    assert notary.notarise([SignRequest(make_stx(engine, signer_idx=[116], inputs=(b"s-116",), outputs=(b"o2",)),
+                                        "p")])[0].ok
+
+
+def test_notary_id_mismatch_fails_the_flow(engine):
+    """NotaryFlow.kt:99: `val wtx = stx.tx` sits outside the try, so a claimed id that does not match
+    the contents is an IllegalStateException that fails the flow (no NotaryError, no signature); the
+    rest of the batch is unaffected."""
+    notary = _notary(engine, validating=True)
+    stx = make_stx(engine, signer_idx=[119], inputs=(b"s-119",))
+    other = WireTransaction(inputs=[b"s-119"], outputs=[b"changed"], must_sign=stx._wtx.must_sign)
+    tampered = SignedTransaction(other, stx.sigs, stx.id)
+    good = make_stx(engine, signer_idx=[120], inputs=(b"s-120",))
+    res = notary.notarise([SignRequest(tampered, "p"), SignRequest(good, "q")])
+    assert not res[0].ok and res[0].error is None and isinstance(res[0].failure, IllegalStateException)
+    with pytest.raises(IllegalStateException):
+        res[0].get_or_throw()
+    res[1].get_or_throw().verify_with_ecdsa(good.id)
+    # the tampered request committed nothing: its input is still free
+    assert notary.notarise([SignRequest(make_stx(engine, signer_idx=[119], inputs=(b"s-119",), outputs=(b"o3",)),
+                                        "p")])[0].ok
+
+
+def test_empty_transaction_fails_only_its_request(engine):
+    """an empty WireTransaction (MerkleTree.getMerkleTree(emptyList) -> MerkleTreeException)
+    fails its own request; compute_ids reports it per item and the others still succeed."""
+    empty = WireTransaction()
+    ids = compute_ids([WireTransaction(outputs=[b"a"]), empty, WireTransaction(outputs=[b"b"])], engine)
+    assert ids[0] is not None and ids[1] is None and ids[2] is not None
+    with pytest.raises(MerkleTreeException):
+        empty.id
+    notary = _notary(engine, validating=True)
+    good = make_stx(engine, signer_idx=[121], inputs=(b"s-121",))
+    bogus = SignedTransaction(WireTransaction(), good.sigs, good.id)
+    res = notary.notarise([SignRequest(bogus, "p"), SignRequest(good, "q")])
+    assert isinstance(res[0].failure, MerkleTreeException)
+    res[1].get_or_throw().verify_with_ecdsa(good.id)
+    out = verify_signatures_batch([bogus, good], engine=engine)
+    assert isinstance(out[0], MerkleTreeException) and out[1] is None
 
 
 def test_c1_loadtest_self_issue_10k(engine, oracle_c):
