@@ -153,10 +153,12 @@ int cv_ed25519_verify_device(cv_ctx *ctx, int device, size_t n, const void *d_pk
 
 /* Measurement entry point (bench.py): as cv_ed25519_verify_device (no status), but synchronous,
  * whole-chunk launches only (no drain overlap), and fills phase_ms[0..2] with the summed durations
- * of the verify kernels measured with HIP events on the launch stream.  Half-size schedule (default):
- * challenge hash | fused prep (decodes, lattice, digits, tables) | hs_straus (multi-scalar
- * multiplication + verdict bits).  Full-width schedule: prep | Straus | finish (batched inversion,
- * encode, compare, bitmap). */
+ * of the verify kernels measured with HIP events on the launch stream.  Half-size schedule (default),
+ * batches above 32,768: scalars (challenge hash, effective S, lattice, window digits) | points
+ * (decode A and R, both odd-multiple tables) | hs_straus (multi-scalar multiplication + verdict
+ * bits).  Batches up to 32,768 (latency forms): scalars and point pairs in one launch | bitmap clear |
+ * tri-chain (<= 4,096) or quad Straus.  Full-width schedule: prep | Straus | finish (batched
+ * inversion, encode, compare, bitmap). */
 int cv_ed25519_verify_device_timed(cv_ctx *ctx, int device, size_t n, const void *d_pk, const void *d_sig,
                                    const void *d_arena, const void *d_off, const void *d_len, void *d_bitmap,
                                    void *stream, float *phase_ms);
@@ -204,7 +206,8 @@ int cv_diag_prep_phases(cv_ctx *ctx, int device, size_t n, const void *d_pk, con
 /* Diagnostics: the host-side key dedupe cv_ed25519_verify_batch runs before choosing the keyed path
  * (seeded hash of all 32 key bytes).  Returns 1 and fills key_index[n] / *nkeys when the batch
  * repeats keys enough for the keyed path (64 <= n <= 2^18, at least two signatures per distinct
- * key), else 0.  Host only: needs no device and no context. */
+ * key; above 1,024 signatures a first 256 carrying more than 192 distinct keys is taken as
+ * distinct-keyed without hashing the rest), else 0.  Host only: needs no device and no context. */
 int cv_diag_dedupe_keys(size_t n, const uint8_t *pk, uint32_t *key_index, size_t *nkeys);
 
 #ifdef __cplusplus
