@@ -180,8 +180,8 @@ def notary_latency(eng, device: int, n: int, reps: int, cpu: bool, key_pool=None
         ph = np.median(np.array([eng.verify_device_timed(device, n, *[x.data_ptr() for x in d], bm.data_ptr(),
                                                          s.cuda_stream) for _ in range(10)]), axis=0)
         dev_p50 = float(np.percentile(dl, 50) * 1e3)
-        names = (("scalars_and_point_pairs", "bitmap_clear", "hs_straus_quad") if n <= 32768
-                 else ("scalars", "points", "hs_straus"))
+        names = (("scalars_and_point_pairs", "bitmap_clear", "hs_straus_tri" if n <= 4096 else "hs_straus_quad")
+                 if n <= 32768 else ("scalars", "points", "hs_straus"))
         out["breakdown_p50_ms"] = {"host_api_total": out["p50_ms"], "device_api_total": dev_p50,
                                    "transfers_and_host": out["p50_ms"] - dev_p50,
                                    "kernels": {k: float(v) for k, v in zip(names, ph)},

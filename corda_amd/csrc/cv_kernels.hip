@@ -413,6 +413,7 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_tri_kernel(uint32_t n, 
 // Batches of at most this many signatures run the tri-chain kernel (cvk_set_tri_max; 0 = never)
 static uint32_t g_tri_max = 4096;
 extern "C" void cvk_set_tri_max(int m) { g_tri_max = (uint32_t)(m < 0 ? 0 : m); }
+extern "C" uint32_t cvk_get_tri_max(void) { return g_tri_max; }
 
 // 1 = small batches run scalars and point pairs in one launch (cv_prep_lat_kernel), 0 = two launches
 static int g_prep_lat_fused = 1;

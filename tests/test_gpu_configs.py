@@ -164,7 +164,7 @@ def test_multi_device_host_path_virtual_shards(engine, corpus, oracle_c, k):
         assert np.array_equal(bm_v, bm_1) and np.array_equal(st_v, st_1)
         assert np.array_equal(native.bitmap_to_bools(bm_v, n), expect)
         # auto-keyed: golden corpus tiled to a ragged size (keys repeat)
-        m = 2 * len(corpus["pk"]) + 64 * k + 5
+        m = 6 * len(corpus["pk"]) + 64 * k + 5             # above 4,096: the dedupe runs
         idx = np.arange(m) % len(corpus["pk"])
         args = (corpus["pk"][idx], corpus["sig"][idx], corpus["arena"], corpus["off"][idx], corpus["len"][idx])
         bm_v, st_v = ve.verify_batch(*args)

@@ -202,8 +202,16 @@ def test_keyed_golden_corpus(engine, corpus, manifest):
 
 
 def test_auto_keyed_path_matches_plain(engine, corpus):
-    """cv_ed25519_verify_batch dedupes keys itself when they repeat (>= 2 signatures per key)."""
-    idx = np.tile(np.arange(len(corpus["pk"])), 4)
+    """cv_ed25519_verify_batch dedupes keys itself when they repeat (>= 2 signatures per key) in
+    batches above the tri-chain size (4,096); smaller batches stay on the plain latency path."""
+    small = np.tile(np.arange(len(corpus["pk"])), 4)[:4096]
+    before = engine.key_cache_stats(0)
+    bitmap, status = engine.verify_batch(corpus["pk"][small], corpus["sig"][small], corpus["arena"],
+                                         corpus["off"][small], corpus["len"][small])
+    assert np.array_equal(_bits(bitmap, small.size), corpus["verdict"][small].astype(bool))
+    after = engine.key_cache_stats(0)
+    assert after["hits"] + after["misses"] == before["hits"] + before["misses"], "keyed path taken at 4,096"
+    idx = np.tile(np.arange(len(corpus["pk"])), 8)
     before = engine.key_cache_stats(0)
     bitmap, status = engine.verify_batch(corpus["pk"][idx], corpus["sig"][idx], corpus["arena"], corpus["off"][idx],
                                          corpus["len"][idx])
