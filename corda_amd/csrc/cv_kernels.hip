@@ -196,6 +196,48 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_points_kernel(uint32_t n, cons
     if (status) status[i] = key_ok ? 0 : 1;
 }
 
+// points of the half-size group, lane-pair throughput form: the even lane decodes A into k*(-A), the
+// odd lane R into k*R (cv_hs_point_one with the sequential-carry field forms), so a lane holds one
+// decode's state instead of two and the kernel fits WAVES waves per SIMD.  Grid 2n lanes.
+template <int WAVES, bool SUB = false>
+__global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_points_one_kernel(uint32_t n, const uint8_t *__restrict__ pk,
+                                                                        const uint8_t *__restrict__ sig,
+                                                                        uint32_t *__restrict__ ws_tab,
+                                                                        uint32_t *__restrict__ ws_tabR,
+                                                                        uint8_t *__restrict__ ws_ok,
+                                                                        uint8_t *__restrict__ status) {
+    const uint32_t g = blockIdx.x * CV_BLOCK + threadIdx.x;
+    const uint32_t i = g >> 1;
+    if (i >= n) return;                       // both lanes of a pair leave together
+    const bool is_r = (g & 1u) != 0;
+    uint32_t w[8];
+    load_words8(w, is_r ? sig + (size_t)i * 64 : pk + (size_t)i * 32);
+    const bool ok = cv_hs_point_one<false>(w, is_r, (is_r ? ws_tabR : ws_tab) + (size_t)i * CV_TAB_WORDS);
+    const bool r_ok = __shfl_xor((int)ok, 1) != 0;
+    if (!is_r) {
+        ws_ok[i] = (ok && r_ok) ? 1 : 0;
+        if (status) status[i] = ok ? 0 : 1;
+    }
+}
+// 0 = one lane decodes both points (cv_points_kernel: 256 VGPRs, 23 spilled, 2 waves/SIMD), 2 / 3 =
+// lane pairs at that many waves per SIMD.  Default 3: points 2.46 -> 2.37 ms per 1M, C2 -0.8 % per step
+// (same-box A/B, 3 alternating rounds, profiles/r02_ab_points_modes.log)
+static int g_points_mode = 3;
+extern "C" void cvk_set_points_mode(int v) { g_points_mode = (v == 2 || v == 3) ? v : 0; }
+template <bool SUB>
+static void launch_points(uint32_t m, const uint8_t *pk, const uint8_t *sig, uint32_t *tabA, uint32_t *tabR, uint8_t *ok,
+                          uint8_t *status, hipStream_t st) {
+    if (g_points_mode == 3)
+        hipLaunchKernelGGL((cv_points_one_kernel<3, SUB>), dim3((2 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, st,
+                           m, pk, sig, tabA, tabR, ok, status);
+    else if (g_points_mode == 2)
+        hipLaunchKernelGGL((cv_points_one_kernel<2, SUB>), dim3((2 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, st,
+                           m, pk, sig, tabA, tabR, ok, status);
+    else
+        hipLaunchKernelGGL(cv_points_kernel<SUB>, dim3((m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, st, m, pk, sig,
+                           tabA, tabR, ok, status);
+}
+
 // points of the half-size group (latency form, small batches): a lane PAIR per signature, the even
 // lane decoding the key A into k*(-A), the odd lane R into k*R, side by side (the same instructions
 // on both lanes: cv_hs_point_one) with the latency (ILP) field forms — half the serial chain of the
@@ -676,10 +718,9 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
                 hipLaunchKernelGGL(cv_scalars_kernel, dim3(bl), dim3(CV_BLOCK), 0, st, mm, ws_cap,
                                    pk + (size_t)a * 32, sig + (size_t)a * 64, arena, off + a, len + a,
                                    ws_dig + sub0[h]);
-                hipLaunchKernelGGL(cv_points_kernel<true>, dim3(bl), dim3(CV_BLOCK), 0, st, mm, pk + (size_t)a * 32,
-                                   sig + (size_t)a * 64, ws_tab + (size_t)sub0[h] * CV_TAB_WORDS,
-                                   ws_tabR + (size_t)sub0[h] * CV_TAB_WORDS, ws_ok + sub0[h],
-                                   status ? status + a : nullptr);
+                launch_points<true>(mm, pk + (size_t)a * 32, sig + (size_t)a * 64, ws_tab + (size_t)sub0[h] * CV_TAB_WORDS,
+                                    ws_tabR + (size_t)sub0[h] * CV_TAB_WORDS, ws_ok + sub0[h],
+                                    status ? status + a : nullptr, st);
                 if (h == 0) (void)hipEventRecord(ax->prep1, st);
                 if (g_hs_waves == 2)
                     hipLaunchKernelGGL((cv_hs_straus_kernel<2, true>), dim3(bl), dim3(CV_BLOCK), 0, st, mm, ws_cap,
@@ -700,8 +741,8 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             hipLaunchKernelGGL(cv_scalars_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap,
                                pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_dig);
             if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);
-            hipLaunchKernelGGL(cv_points_kernel<false>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, pk + (size_t)c0 * 32,
-                               sig + (size_t)c0 * 64, ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr);
+            launch_points<false>(m, pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, ws_tab, ws_tabR, ws_ok,
+                                 status ? status + c0 : nullptr, stream);
             if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
             if (g_hs_waves == 2)
                 hipLaunchKernelGGL(cv_hs_straus_kernel<2>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, ws_dig,

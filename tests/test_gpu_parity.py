@@ -409,3 +409,40 @@ def test_host_buffer_api_split_size_exact_pattern(engine):
     assert np.array_equal(_bits(bitmap, n), expect)
     assert int(status.sum()) == 0
     assert int(bitmap[-1]) >> (n % 64) == 0
+
+
+# ---------------------------------------------------------------- the points kernel forms
+@pytest.mark.parametrize("points_mode", [0, 2, 3])
+def test_points_kernel_forms_agree(engine, corpus, oracle_c, points_mode):
+    """The throughput points phase in each form (internal switch cvk_set_points_mode: 0 = one lane
+    decodes A and R interleaved, 2 / 3 = a lane pair per signature at 2 / 3 waves per SIMD) over the
+    golden corpus (every key / R class, statuses) and a corrupted random batch vs the C oracle."""
+    import ctypes
+    lib = native.load()
+    lib.cvk_set_quad_max.argtypes = [ctypes.c_uint32]
+    lib.cvk_set_points_mode.argtypes = [ctypes.c_int]
+    lib.cvk_set_quad_max(0)
+    lib.cvk_set_points_mode(points_mode)
+    try:
+        for n in (len(corpus["pk"]), 1001):
+            sel = np.arange(n) % len(corpus["pk"])
+            bitmap, status = engine.verify_batch(corpus["pk"][sel], corpus["sig"][sel], corpus["arena"],
+                                                 corpus["off"][sel], corpus["len"][sel])
+            assert np.array_equal(_bits(bitmap, n), corpus["verdict"][sel].astype(bool))
+            assert np.array_equal(status, corpus["status"][sel])
+        rng = np.random.default_rng(43 + points_mode)
+        n = 5000
+        seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+        arena = rng.integers(0, 256, n * 32 + 16, dtype=np.uint8)
+        off = np.arange(n, dtype=np.uint64) * 32
+        ln = np.full(n, 32, np.uint32)
+        pk, sig = engine.sign_batch(seeds, arena, off, ln)
+        sig[1::7, rng.integers(0, 32)] ^= 0x08          # R corrupted
+        pk[2::9, 5] ^= 0x10                             # key corrupted (often not a point)
+        bitmap, status = engine.verify_batch(pk, sig, arena, off, ln)
+        ref, rst = oracle_c.verify_batch(pk, sig, arena, off, ln, nthreads=8)
+        assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
+        assert np.array_equal(status, rst)
+    finally:
+        lib.cvk_set_points_mode(3)
+        lib.cvk_set_quad_max(32768)
