@@ -11,6 +11,7 @@ import glob
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
@@ -20,7 +21,8 @@ OBJDIR = os.path.join(HERE, "_obj")
 ARCH = os.environ.get("CV_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES = ["cv_kernels.hip", "cv_api.cpp"]
+# kernel translation units (cv_kcommon.h) compile in parallel; cv_kernels.hip holds the launchers
+SOURCES = ["cv_k_hs.hip", "cv_k_lat.hip", "cv_k_full.hip", "cv_k_misc.hip", "cv_kernels.hip", "cv_api.cpp"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
           "-Wno-unused-variable"]
 # kernels: LLVM's max-ILP machine scheduler (A/B on one MI355X, 3 alternating rounds: C2 1M verify
@@ -49,7 +51,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
     madc, gen_m = os.path.join(CSRC, "cv_madc.h"), os.path.join(CSRC, "gen_madc.py")
     if force or _stale(madc, [gen_m]):
         subprocess.run([sys.executable, gen_m], check=True)
-    objs = []
+    objs, cmds = [], []
     deps = _deps()
     for src in SOURCES:
         sp = os.path.join(CSRC, src)
@@ -59,9 +61,18 @@ def build(verbose: bool = False, force: bool = False) -> str:
             cmd = [HIPCC] + CFLAGS + KERNEL_FLAGS + ["-c", sp, "-o", op]
             if src.endswith(".cpp"):
                 cmd = [HIPCC, "-x", "hip"] + CFLAGS + ["-c", sp, "-o", op]
-            if verbose:
-                print(" ".join(cmd), flush=True)
-            subprocess.run(cmd, check=True)
+            cmds.append(cmd)
+    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+    if verbose:
+        for cmd in cmds:
+            print(" ".join(cmd), flush=True)
+    with ThreadPoolExecutor(jobs) as pool:
+        for r in pool.map(lambda c: subprocess.run(c, capture_output=True, text=True), cmds):
+            if r.returncode:
+                sys.stderr.write(r.stderr)
+                raise subprocess.CalledProcessError(r.returncode, r.args)
+            if verbose and r.stderr.strip():
+                sys.stderr.write(r.stderr)
     if force or _stale(LIB, objs):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + ["-lpthread"]
         if verbose:

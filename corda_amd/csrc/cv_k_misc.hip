@@ -1,0 +1,232 @@
+// cv_k_misc.hip — signing (synthetic inputs), Merkle tx ids, partial Merkle trees, calibration and probe kernels.
+// Shared helpers and every kernel declaration: cv_kcommon.h; launchers: cv_kernels.hip.
+#include "cv_kcommon.h"
+
+// ---------------------------------------------------------------- sign (synthetic inputs)
+__global__ __launch_bounds__(CV_BLOCK, 2) void cv_sign_kernel(
+    uint32_t n, const uint8_t *__restrict__ seed, const uint8_t *__restrict__ arena,
+    const uint64_t *__restrict__ off, const uint32_t *__restrict__ len, uint8_t *__restrict__ pk_out,
+    uint8_t *__restrict__ sig_out) {
+    __shared__ __attribute__((aligned(16))) uint32_t btab[CV_BTAB_ENTRIES * CV_BTAB_STRIDE];
+    stage_btab(btab);
+    const uint32_t gid = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (gid >= n) return;
+    uint32_t sd[8], pkw[8], sgw[16];
+    load_words8(sd, seed + (size_t)gid * 32);
+    cv_sign_one(btab, sd, arena + off[gid], len[gid], pkw, sgw);
+    uint4 *po = reinterpret_cast<uint4 *>(pk_out + (size_t)gid * 32);
+    uint4 *so = reinterpret_cast<uint4 *>(sig_out + (size_t)gid * 64);
+    po[0] = make_uint4(pkw[0], pkw[1], pkw[2], pkw[3]);
+    po[1] = make_uint4(pkw[4], pkw[5], pkw[6], pkw[7]);
+#pragma unroll
+    for (int q = 0; q < 4; q++) so[q] = make_uint4(sgw[4 * q], sgw[4 * q + 1], sgw[4 * q + 2], sgw[4 * q + 3]);
+}
+
+// ---------------------------------------------------------------- Merkle tx ids
+__global__ __launch_bounds__(CV_BLOCK) void cv_leaf_hash_kernel(uint32_t nleaves, const uint8_t *__restrict__ arena,
+                                                                const uint64_t *__restrict__ off,
+                                                                const uint32_t *__restrict__ len,
+                                                                uint32_t *__restrict__ leaf_digest) {
+    const uint32_t gid = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (gid >= nleaves) return;
+    uint32_t d[8];
+    sha256_bytes(d, arena + off[gid], len[gid]);
+    uint4 *o = reinterpret_cast<uint4 *>(leaf_digest + (size_t)gid * 8);
+    o[0] = make_uint4(d[0], d[1], d[2], d[3]);
+    o[1] = make_uint4(d[4], d[5], d[6], d[7]);
+}
+
+// one lane per transaction, in place over its leaf digests; ids are written as digest bytes
+__global__ __launch_bounds__(CV_BLOCK) void cv_merkle_tree_kernel(uint32_t ntx, const uint32_t *__restrict__ tx_begin,
+                                                                  uint32_t *__restrict__ leaf_digest,
+                                                                  uint8_t *__restrict__ ids,
+                                                                  uint8_t *__restrict__ status) {
+    const uint32_t gid = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (gid >= ntx) return;
+    const uint32_t b = tx_begin[gid], e = tx_begin[gid + 1];
+    uint32_t root[8];
+    const bool ok = cv_merkle_root_inplace(leaf_digest + (size_t)b * 8, e - b, root);
+    uint4 *o = reinterpret_cast<uint4 *>(ids + (size_t)gid * 32);
+    o[0] = make_uint4(cv_bswap32(root[0]), cv_bswap32(root[1]), cv_bswap32(root[2]), cv_bswap32(root[3]));
+    o[1] = make_uint4(cv_bswap32(root[4]), cv_bswap32(root[5]), cv_bswap32(root[6]), cv_bswap32(root[7]));
+    if (status) status[gid] = ok ? 0 : 1;
+}
+
+// ---------------------------------------------------------------- partial Merkle trees (f3)
+// one lane per tree (FilteredTransaction.verify / PartialMerkleTree.verify, cv_verify.h)
+__global__ __launch_bounds__(CV_BLOCK) void cv_pmt_verify_kernel(uint32_t ntrees, const uint8_t *__restrict__ kind,
+                                                                 const uint32_t *__restrict__ left,
+                                                                 const uint32_t *__restrict__ right,
+                                                                 const uint8_t *__restrict__ leaf_hash,
+                                                                 const uint32_t *__restrict__ tree_begin,
+                                                                 const uint8_t *__restrict__ root,
+                                                                 const uint8_t *__restrict__ check,
+                                                                 const uint32_t *__restrict__ check_begin,
+                                                                 uint32_t *__restrict__ dig, uint8_t *__restrict__ flag,
+                                                                 uint8_t *__restrict__ verdict, uint8_t *__restrict__ status) {
+    const uint32_t t = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (t >= ntrees) return;
+    bool v = false;
+    const int st = cv_pmt_verify(tree_begin[t], tree_begin[t + 1], kind, left, right, leaf_hash, root + 32 * (size_t)t,
+                                 check, check_begin[t], check_begin[t + 1], dig, flag, v);
+    verdict[t] = v ? 1 : 0;
+    status[t] = (uint8_t)st;
+}
+
+// ---------------------------------------------------------------- calibration microbenchmarks
+// Peak rate of the multiply-accumulate instruction the field arithmetic is built on (roofline
+// denominator): 8 independent accumulators x 16 unrolled v_mad_u64_u32 per iteration, no other VALU.
+// (cv_field.h accumulates every limb product with v_mad_u64_u32.)
+__global__ __launch_bounds__(CV_BLOCK) void cv_mad_bench_kernel(uint32_t iters, uint64_t *out) {
+    uint64_t acc[8];
+    uint32_t a[8], b[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        acc[k] = threadIdx.x + k;
+        a[k] = threadIdx.x * 2654435761u + k;
+        b[k] = blockIdx.x * 40503u + 7 * k + 1;
+    }
+    for (uint32_t it = 0; it < iters; it++) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc[k]) : "v"(a[k]), "v"(b[(k + r) & 7]) : "vcc");
+        }
+    }
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) s ^= acc[k];
+    if (s == 0x1234567) out[0] = s;   // keep the chains alive
+}
+
+// Practical field-multiply rate: 4 independent fe_mul chains per lane.
+__global__ __launch_bounds__(CV_BLOCK, 2) void cv_femul_bench_kernel(uint32_t iters, int32_t *out) {
+    fe x[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int i = 0; i < 10; i++) x[k].v[i] = (threadIdx.x * 977u + k * 131u + i * 7919u) & 0xffffff;
+    for (uint32_t it = 0; it < iters; it++) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) fe_mul(x[k], x[k], x[(k + 1) & 3]);
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int i = 0; i < 10; i++) s ^= x[k].v[i];
+    if (s == 0x1234567) out[0] = s;
+}
+
+// ---------------------------------------------------------------- diagnostics: phase cycle probe
+// The fused prep (cv_hs_prep_fused) with s_memtime stamps at its phase boundaries: per wave, lane 0
+// stores the shader-clock cycles of hash | lattice | digit packing | A+R decode | tables into
+// stamps[wave * 8 + k] (vector stores).  Same code and launch shape as the product kernel; each
+// stamp is ordered after the phase's result by a data dependency.  Diagnostic build only.
+__device__ __forceinline__ uint64_t cv_stamp() {
+    uint64_t t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t));
+    return t;
+}
+#define CV_DEP(x) asm volatile("" ::"v"(x))
+
+__global__ __launch_bounds__(CV_BLOCK, 2) void cv_prep_probe_kernel(
+    uint32_t n, uint32_t cap, const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig,
+    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ off, const uint32_t *__restrict__ len,
+    uint32_t *__restrict__ ws_dig, uint32_t *__restrict__ ws_tab, uint32_t *__restrict__ ws_tabR,
+    uint64_t *__restrict__ stamps) {
+    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    uint32_t aw[8], rw[8], sw[8];
+    load_words8(aw, pk + (size_t)i * 32);
+    load_words8(rw, sig + (size_t)i * 64);
+    load_words8(sw, sig + (size_t)i * 64 + 32);
+    CV_DEP(aw[0]); CV_DEP(rw[0]); CV_DEP(sw[0]);
+    uint64_t t[8];
+    t[0] = cv_stamp();
+    uint32_t hs[CV_HS_WORDS];
+    {   // cv_keyed_hs, split: SHA-512 | the two mod-L scalars
+        uint32_t pre[16], dg[16], hh[8], abyte[8], ss[8];
+        ge_abyte_from_key(abyte, aw);
+#pragma unroll
+        for (int q = 0; q < 8; q++) { pre[q] = rw[q]; pre[8 + q] = abyte[q]; }
+        sha512_pre_msg(dg, pre, 64, arena + off[i], len[i]);
+        CV_DEP(dg[0]); CV_DEP(dg[15]);
+        t[6] = cv_stamp();
+        sc_reduce512(hh, dg);
+        sc_effective_s(ss, sw);
+#pragma unroll
+        for (int q = 0; q < 8; q++) { hs[q] = hh[q]; hs[8 + q] = ss[q]; }
+    }
+    CV_DEP(hs[0]); CV_DEP(hs[15]);
+    t[1] = cv_stamp();
+    uint32_t h[8], s8[8], u[8], v[8], w[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) { h[q] = hs[q]; s8[q] = hs[8 + q]; }
+    bool v_neg;
+    int nwin;
+    sc_halfsize(u, v, v_neg, nwin, w, h, s8);
+    CV_DEP(u[7]); CV_DEP(v[7]); CV_DEP(w[7]);
+    t[2] = cv_stamp();
+    uint32_t *dig = ws_dig + i;
+#pragma unroll 4
+    for (int win = 0; win < 64; win++) {
+        const int da = -digit16(u, win), dr = v_neg ? -digit16(v, win) : digit16(v, win);
+        const bool bw = (win & 1) == 0 && win < 32;
+        const int dlo = bw ? digit256(w, win >> 1) : 0, dhi = bw ? digit256(w, 16 + (win >> 1)) : 0;
+        dig[(size_t)win * cap] = ((uint32_t)da & 0x1fu) | (((uint32_t)dr & 0x1fu) << 5) |
+                                 (((uint32_t)dlo & 0x1ffu) << 10) | (((uint32_t)dhi & 0x1ffu) << 19);
+    }
+    dig[64 * (size_t)cap] = (uint32_t)nwin;
+    t[3] = cv_stamp();
+    ge_p3 P[2];
+    bool ok[2];
+    ge_decode2_0_1_0<false>(P, ok, aw, rw);
+    CV_DEP(P[0].T.v[0]); CV_DEP(P[1].T.v[0]);
+    t[4] = cv_stamp();
+    ge_p3 nA;
+    ge_p3_neg(nA, P[0]);
+    ge_cached_multiples8(ws_tab + (size_t)i * CV_TAB_WORDS, nA);
+    ge_cached_multiples8(ws_tabR + (size_t)i * CV_TAB_WORDS, P[1]);
+    t[5] = cv_stamp();
+    if ((threadIdx.x & 63u) == 0) {
+        uint64_t *o = stamps + (size_t)(i >> 6) * 8;
+#pragma unroll
+        for (int k = 0; k < 5; k++) o[k] = t[k + 1] - t[k];
+        o[5] = t[6] - t[0];                     // SHA-512 alone (part of phase 0)
+    }
+}
+
+// Cycle-basis calibration: the chip-wide v_mad_u64_u32 bench again, with block 0's lane 0 stamping
+// s_memtime (shader clock) and s_memrealtime (100 MHz) around its loop, so the rate converts to
+// cycles per wave-instruction per SIMD at the clock the chip actually ran.
+__global__ __launch_bounds__(CV_BLOCK) void cv_mad_clock_kernel(uint32_t iters, uint64_t *out) {
+    uint64_t acc[8];
+    uint32_t a[8], b[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        acc[k] = threadIdx.x + k;
+        a[k] = threadIdx.x * 2654435761u + k;
+        b[k] = blockIdx.x * 40503u + 7 * k + 1;
+    }
+    uint64_t c0, r0, c1, r1;
+    asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(c0), "=s"(r0));
+    for (uint32_t it = 0; it < iters; it++) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc[k]) : "v"(a[k]), "v"(b[(k + r) & 7]) : "vcc");
+        }
+    }
+    asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(c1), "=s"(r1));
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) s ^= acc[k];
+    if (s == 0x1234567) out[2] = s;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        out[0] = c1 - c0;
+        out[1] = r1 - r0;
+    }
+}

@@ -3,19 +3,20 @@
 
     python tools/isa_stats.py [kernel-substring ...]
 
-Compiles corda_amd/csrc/cv_kernels.hip to assembly (device only) and prints, per kernel, the
+Compiles the kernel translation units corda_amd/csrc/cv_k_*.hip to assembly (device only) and prints, per kernel, the
 instruction counts by opcode, the scratch (spill) instructions, and the weighted issue cost using
 the per-wave-instruction cycle costs measured on the box (tools/microbench/instr_rates.hip).
 Static counts: loop bodies count once — use it to compare variants of the same kernel.
 """
 import collections
+import glob
 import os
 import re
 import subprocess
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(REPO, "corda_amd", "csrc", "cv_kernels.hip")
+SRCS = sorted(glob.glob(os.path.join(REPO, "corda_amd", "csrc", "cv_k_*.hip")))
 
 # measured clk per wave64 instruction on MI355X (DESIGN.md "Instruction rates"), default 2.4
 COST = {"v_mad_u64_u32": 5.0, "v_mad_i64_i32": 5.7, "v_lshrrev_b64": 4.2, "v_lshlrev_b64": 4.2,
@@ -26,10 +27,14 @@ COST = {"v_mad_u64_u32": 5.0, "v_mad_i64_i32": 5.7, "v_lshrrev_b64": 4.2, "v_lsh
 
 
 def asm(flags=()):
-    out = "/tmp/cv_kernels_isa.s"
-    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "--offload-device-only",
-                    "-S", SRC, "-o", out, *flags], check=True, stderr=subprocess.DEVNULL)
-    return open(out).read()
+    text = []
+    for src in SRCS:
+        out = "/tmp/" + os.path.basename(src) + ".s"
+        subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "--offload-device-only",
+                        "-mllvm", "-amdgpu-sched-strategy=max-ilp", "-S", src, "-o", out, *flags], check=True,
+                       stderr=subprocess.DEVNULL)
+        text.append(open(out).read())
+    return "\n".join(text)
 
 
 def kernels(s):
