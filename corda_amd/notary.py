@@ -29,7 +29,6 @@ the flow end with it, never a notary signature.
 """
 from __future__ import annotations
 
-import struct
 import time
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Sequence
@@ -77,88 +76,9 @@ class TimestampChecker:
         return True
 
 
-# ---------------------------------------------------------------- uniqueness (UniquenessProvider.kt:13-32)
-@dataclass(frozen=True)
-class ConsumingTx:
-    id: SecureHash
-    input_index: int
-    requesting_party: str
-
-
-def _enc(x) -> bytes:
-    """Canonical tagged encoding of the state references and parties a conflict report carries
-    (the reference's Kryo serialization is out of scope; this is the bytes the notary signs)."""
-    if isinstance(x, SecureHash):
-        return b"H" + x.bytes
-    if isinstance(x, (bytes, bytearray)):
-        return b"B" + struct.pack("<I", len(x)) + bytes(x)
-    if isinstance(x, str):
-        b = x.encode()
-        return b"S" + struct.pack("<I", len(b)) + b
-    if isinstance(x, bool) or not isinstance(x, (int, tuple, list)):
-        raise IllegalArgumentException(f"cannot serialize {type(x).__name__}")
-    if isinstance(x, int):
-        return b"I" + struct.pack("<q", x)
-    return b"T" + struct.pack("<I", len(x)) + b"".join(_enc(v) for v in x)
-
-
-def _dec(b: bytes, p: int):
-    t = b[p:p + 1]
-    p += 1
-    if t == b"H":
-        return SecureHash(b[p:p + 32]), p + 32
-    if t in (b"B", b"S"):
-        (m,) = struct.unpack_from("<I", b, p)
-        v = b[p + 4:p + 4 + m]
-        return (bytes(v) if t == b"B" else v.decode()), p + 4 + m
-    if t == b"I":
-        return struct.unpack_from("<q", b, p)[0], p + 8
-    if t == b"T":
-        (m,) = struct.unpack_from("<I", b, p)
-        p += 4
-        out = []
-        for _ in range(m):
-            v, p = _dec(b, p)
-            out.append(v)
-        return tuple(out), p
-    raise IllegalArgumentException("malformed conflict encoding")
-
-
-@dataclass
-class UniquenessConflict:
-    """UniquenessProvider.Conflict(stateHistory): the consuming transaction of every conflicting state."""
-    state_history: Dict[object, ConsumingTx]
-
-    def serialize(self) -> bytes:
-        rows = sorted((_enc(s), c) for s, c in self.state_history.items())
-        return b"CONFLICT" + _enc(tuple((s_enc, c.id, c.input_index, c.requesting_party) for s_enc, c in rows))
-
-    @staticmethod
-    def deserialize(raw: bytes) -> "UniquenessConflict":
-        if not raw.startswith(b"CONFLICT"):
-            raise IllegalArgumentException("not a conflict report")
-        rows, _ = _dec(raw, 8)
-        return UniquenessConflict({_dec(s_enc, 0)[0]: ConsumingTx(h, i, party) for s_enc, h, i, party in rows})
-
-
-class UniquenessException(Exception):
-    def __init__(self, conflict: UniquenessConflict):
-        super().__init__("conflict")
-        self.error = conflict
-
-
-class InMemoryUniquenessProvider:
-    """node/.../services/transactions/InMemoryUniquenessProvider.kt semantics: all-or-nothing commit."""
-
-    def __init__(self):
-        self.committed: Dict[object, ConsumingTx] = {}
-
-    def commit(self, states: Sequence[object], tx_id: SecureHash, caller: str) -> None:
-        conflict = {s: self.committed[s] for s in states if s in self.committed}
-        if conflict:
-            raise UniquenessException(UniquenessConflict(conflict))
-        for i, s in enumerate(states):
-            self.committed[s] = ConsumingTx(tx_id, i, caller)
+# ---------------------------------------------------------------- uniqueness (corda_amd/uniqueness.py)
+from .uniqueness import (ConsumingTx, InMemoryUniquenessProvider, PersistentUniquenessProvider,  # noqa: E402,F401
+                         UniquenessConflict, UniquenessException)
 
 
 @dataclass
@@ -274,7 +194,7 @@ def verify_many_sharded(items: Sequence[VerifyItem], engine, group=None) -> List
 # ---------------------------------------------------------------- the notary
 class BatchingNotary:
     def __init__(self, notary_seed: bytes, validating: bool = True, engine: Optional[native.Engine] = None,
-                 uniqueness: Optional[InMemoryUniquenessProvider] = None,
+                 uniqueness=None,
                  timestamp_checker: Optional[TimestampChecker] = None, group=None):
         self.engine = engine or native.default_engine()
         self.seed = np.frombuffer(bytes(notary_seed), np.uint8).reshape(1, 32)
@@ -283,7 +203,7 @@ class BatchingNotary:
         self.public_key = EdDSAPublicKey(pk[0].tobytes())
         self.owning_key: CompositeKey = self.public_key.composite
         self.validating = validating
-        self.uniqueness = uniqueness or InMemoryUniquenessProvider()
+        self.uniqueness = uniqueness if uniqueness is not None else InMemoryUniquenessProvider()
         self.timestamp_checker = timestamp_checker or TimestampChecker()
         self.group = group
 
@@ -329,6 +249,7 @@ class BatchingNotary:
                 first_bad[k] = next((e for e in errs[begin[k]:begin[k + 1]] if e is not None), None)
         accepted: List[int] = []
         conflicts: List[tuple] = []
+        to_commit: List[tuple] = []
         for k, r in enumerate(requests):
             if failed[k] is not None:
                 results[k] = Result(False, failure=failed[k])
@@ -353,12 +274,24 @@ class BatchingNotary:
                         results[k] = Result(False, failure=e)
                     continue
             refs = r.input_refs if r.input_refs is not None else list(r.stx._wtx.inputs)
-            try:
-                self.uniqueness.commit(refs, r.stx.id, r.caller)
-            except UniquenessException as ex:
-                conflicts.append((k, ex.error.serialize()))
-                continue
-            accepted.append(k)
+            to_commit.append((k, refs))
+        # commitInputStates for the whole batch, decided in request order (uniqueness.py)
+        reqs = [(refs, requests[k].stx.id, requests[k].caller) for k, refs in to_commit]
+        if hasattr(self.uniqueness, "commit_batch"):
+            decided = self.uniqueness.commit_batch(reqs)
+        else:
+            decided = []
+            for states, tx_id, caller in reqs:
+                try:
+                    self.uniqueness.commit(states, tx_id, caller)
+                    decided.append(None)
+                except UniquenessException as ex:
+                    decided.append(ex.error)
+        for (k, _), c in zip(to_commit, decided):
+            if c is None:
+                accepted.append(k)
+            else:
+                conflicts.append((k, c.serialize()))
         msgs = [requests[k].stx.id.bytes for k in accepted] + [raw for _, raw in conflicts]
         sigs = self._sign(msgs) if msgs else []
         for j, k in enumerate(accepted):

@@ -248,6 +248,29 @@ def test_notary_reports_conflict_for_duplicate(engine):
         forged.verified(engine)
 
 
+def test_notary_with_persistent_uniqueness_survives_restart(engine, tmp_path):
+    """f4: the batched notary on PersistentUniquenessProvider (PersistentUniquenessProvider.kt:19-81,
+    one SQLite transaction per batch): the decisions equal the in-memory provider's for the same
+    requests, and a notary restarted on the same store still reports the earlier consumer."""
+    from corda_amd.uniqueness import PersistentUniquenessProvider
+    stxs = [make_stx(engine, signer_idx=[120 + i], inputs=(b"pstate-%d" % (i % 5),)) for i in range(8)]
+    reqs = [SignRequest(s, f"party{i}") for i, s in enumerate(stxs)]
+    path = str(tmp_path / "notary_commit_log.db")
+    durable = BatchingNotary(NOTARY_SEED, engine=engine, uniqueness=PersistentUniquenessProvider(path))
+    got = durable.notarise(reqs)
+    want = _notary(engine).notarise(reqs)
+    assert [r.ok for r in got] == [r.ok for r in want] == [True] * 5 + [False] * 3
+    for g, w in zip(got, want):
+        if not g.ok:
+            assert g.error.conflict.verified(engine).state_history == w.error.conflict.verified(engine).state_history
+    durable.uniqueness.close()
+    restarted = BatchingNotary(NOTARY_SEED, engine=engine, uniqueness=PersistentUniquenessProvider(path))
+    again = restarted.notarise([SignRequest(stxs[0], "late")])[0]
+    assert isinstance(again.error, Conflict)
+    assert again.error.conflict.verified(engine).state_history[b"pstate-0"] == ConsumingTx(stxs[0].id, 0, "party0")
+    restarted.uniqueness.close()
+
+
 def test_validating_notary_errors(engine):
     """ValidatingNotaryServiceTests.kt:44-82 + ValidatingNotaryFlow.kt:24-45: missing signatures ->
     SignaturesMissing(exact set); a bad signature -> TransactionInvalid; a signature by a non-EdDSA
