@@ -148,7 +148,7 @@ struct Device {
     DevBuf packed;                       // host-buffer verify: pk | sig | off | len | arena in one block
     PinBuf pin_in, pin_out;              // its pinned host staging (inputs; bitmap | status)
     DevBuf pmt;                          // partial Merkle trees: inputs, outputs and workspace, packed
-    DevBuf ws_hs, ws_tab, ws_R, ws_ok, ws_dig;   // verify workspace per signature: hs 64 B, 2 tables 2560 B,
+    DevBuf ws_hs, ws_tab, ws_R, ws_ok, ws_dig;   // verify workspace per signature: hs 64 B, 2 tables 2 x 1440 B,
                                          // R record 128 B, ok 1 B, half-size digits 260 B
     uint32_t ws_cap = 0;
     KeyCache kc;
@@ -160,6 +160,7 @@ struct Device {
 // key-table pool capacity per device (keys); 4 KB of tables per key
 constexpr uint32_t kDefaultKeyCap = 1u << 16;
 constexpr size_t kKtabBytes = 1024 * 4;   // CV_KTAB_WORDS
+constexpr size_t kTabBytes = 9 * 40 * 4;  // CV_TAB_WORDS: k*P, k = 0..8, cached form (cv_verify.h)
 // cv_ed25519_verify_batch dedupes keys on the host up to this batch size, and takes the keyed
 // (per-key comb) path when the batch has at least two signatures per distinct key on average
 constexpr size_t kAutoKeyedMax = 1u << 18;
@@ -172,7 +173,7 @@ hipError_t ensure_verify_ws(Device &d, size_t n) {
     if (want <= d.ws_cap) return hipSuccess;
     hipError_t e;
     if ((e = d.ws_hs.ensure((size_t)want * 64)) != hipSuccess) return e;
-    if ((e = d.ws_tab.ensure((size_t)want * 2560)) != hipSuccess) return e;   // k*(-A) and k*R tables
+    if ((e = d.ws_tab.ensure((size_t)want * 2 * kTabBytes)) != hipSuccess) return e;   // k*(-A), k*R
     if ((e = d.ws_R.ensure((size_t)want * 128)) != hipSuccess) return e;
     if ((e = d.ws_ok.ensure((size_t)want)) != hipSuccess) return e;
     if ((e = d.ws_dig.ensure((size_t)want * 65 * 4)) != hipSuccess) return e;   // CV_HS_DIGWORDS

@@ -55,7 +55,7 @@ __device__ __forceinline__ bool cv_quad_hs_straus(const uint32_t *blo, const uin
 // form, for 4x its lanes (4 signatures per wave).  Only for batches whose waves leave SIMDs idle.
 
 // this lane's coordinate of d * P, cached form, from either table format: the per-signature cached
-// tables (precomp = false: 40 words per entry, entry k-1 = k P) or the CV_BCOMB affine rows
+// tables (precomp = false: 40 words per entry, entry k = k P, entry 0 = identity) or the CV_BCOMB affine rows
 // (precomp = true: stride CV_BTAB_STRIDE, row k = k P, row 0 = identity; Z = 1).  Same instructions
 // on every lane (only addresses and selects differ), so the four quads never diverge.
 __device__ __forceinline__ void quad_any_coord(fe &q, const uint32_t *tab, bool precomp, int a, int r) {
@@ -63,7 +63,7 @@ __device__ __forceinline__ void quad_any_coord(fe &q, const uint32_t *tab, bool 
     const bool neg = a < 0;
     const int c = (r < 2 && neg) ? 1 - r : r;            // -(Y+X, Y-X, Z, T2d) = (Y-X, Y+X, Z, -T2d)
     const int stride = precomp ? CV_BTAB_STRIDE : 40;
-    const int row = precomp ? m : (m ? m - 1 : 0);
+    const int row = m;                                   // row 0 = identity in both formats
     const int offc = (precomp && r == 3) ? 20 : 10 * c;  // affine rows: 2dxy at word 20
     const uint2 *p2 = reinterpret_cast<const uint2 *>(tab + stride * row + offc);
 #pragma unroll
@@ -72,13 +72,11 @@ __device__ __forceinline__ void quad_any_coord(fe &q, const uint32_t *tab, bool 
         q.v[2 * j] = v.x;
         q.v[2 * j + 1] = v.y;
     }
-    fe nq, one, zero;
+    fe nq, one;
     fe_neg(nq, q);
     fe_sel(q, q, nq, neg && r == 3);
     fe_one(one);
     fe_sel(q, q, one, precomp && r == 2);
-    fe_zero(zero);
-    fe_sel(q, q, r == 3 ? zero : one, m == 0);           // identity (1, 1, 1, 0)
 }
 
 // this lane's coordinate of a full extended point in cached form (Y+X, Y-X, Z, 2dT), from each

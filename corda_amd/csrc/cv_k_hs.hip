@@ -67,11 +67,15 @@ __global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_hs_straus_kernel(uint32_t 
                                                                        const uint32_t *__restrict__ ws_tabR,
                                                                        const uint8_t *__restrict__ ws_ok,
                                                                        uint64_t *__restrict__ bitmap) {
-    __shared__ __attribute__((aligned(16))) uint32_t btab[2 * CV_BTAB_ENTRIES * CV_BTAB_STRIDE];
-    constexpr int ROW = CV_BTAB_ENTRIES * CV_BTAB_STRIDE;
+    // LDS rows padded to CV_BTAB_LDS_STRIDE words: the 64 lanes of a wave gather data-dependent rows,
+    // and with 128-B rows every row started in one of two 4-bank groups (32-way conflicts); with
+    // 144-B rows consecutive row indices start 36 words apart and spread over 16 groups
+    __shared__ __attribute__((aligned(16))) uint32_t btab[2 * CV_BTAB_ENTRIES * CV_BTAB_LDS_STRIDE];
+    constexpr int ROW = CV_BTAB_ENTRIES * CV_BTAB_STRIDE, LROW = CV_BTAB_ENTRIES * CV_BTAB_LDS_STRIDE;
     for (int k = threadIdx.x; k < ROW; k += blockDim.x) {
-        btab[k] = CV_BCOMB[k];                 // k * B
-        btab[ROW + k] = CV_BCOMB[2 * ROW + k]; // k * 2^128 * B
+        const int at = (k / CV_BTAB_STRIDE) * CV_BTAB_LDS_STRIDE + k % CV_BTAB_STRIDE;
+        btab[at] = CV_BCOMB[k];                  // k * B
+        btab[LROW + at] = CV_BCOMB[2 * ROW + k]; // k * 2^128 * B
     }
     __syncthreads();
     const uint32_t wave0 = blockIdx.x * CV_BLOCK + (threadIdx.x & ~63u);
@@ -86,7 +90,7 @@ __global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_hs_straus_kernel(uint32_t 
         nw = x > nw ? x : nw;
     }
     nw = __builtin_amdgcn_readfirstlane(nw);
-    const bool eq = cv_hs_straus(btab, btab + ROW, ws_dig + i, cap, ws_tab + (size_t)i * CV_TAB_WORDS,
+    const bool eq = cv_hs_straus<CV_BTAB_LDS_STRIDE>(btab, btab + LROW, ws_dig + i, cap, ws_tab + (size_t)i * CV_TAB_WORDS,
                                  ws_tabR + (size_t)i * CV_TAB_WORDS, nw);
     const bool acc = eq && ws_ok[i] && i0 < n;
     const uint64_t bits = __ballot(acc);

@@ -74,12 +74,12 @@ __device__ __forceinline__ void quad_add(fe &P, const fe &q, int r) {
     quad_finish_products(P, R1);
 }
 
-// this lane's coordinate of +-k*(-A) from a per-signature cached table (40 words per entry)
+// this lane's coordinate of +-k*(-A) from a per-signature cached table (40 words per entry, entry k = kP)
 __device__ __forceinline__ void quad_cached_coord(fe &q, const uint32_t *tab, int a, int r) {
     const int m = a < 0 ? -a : a;
     const bool neg = a < 0;
     const int c = (r < 2 && neg) ? 1 - r : r;        // -(Y+X, Y-X, Z, T2d) = (Y-X, Y+X, Z, -T2d)
-    const uint32_t *p = tab + 40 * (m ? m - 1 : 0) + 10 * c;
+    const uint32_t *p = tab + 40 * m + 10 * c;           // entry 0 = identity (1, 1, 1, 0)
     const uint2 *p2 = reinterpret_cast<const uint2 *>(p);
 #pragma unroll
     for (int j = 0; j < 5; j++) {
@@ -90,11 +90,6 @@ __device__ __forceinline__ void quad_cached_coord(fe &q, const uint32_t *tab, in
     fe nq;
     fe_neg(nq, q);
     fe_sel(q, q, nq, neg && r == 3);
-    fe one;
-    fe_one(one);
-    fe zero;
-    fe_zero(zero);
-    fe_sel(q, q, r == 3 ? zero : one, m == 0);     // identity (1, 1, 1, 0)
 }
 
 // this lane's coordinate of +-|d| * P from an affine table (entries `stride` words apart: y+x at 0,

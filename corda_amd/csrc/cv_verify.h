@@ -9,10 +9,12 @@
 #include "cv_sha.h"
 #include "cv_tables.h"
 
-// k*B for a signed digit k in [-128, 128] from the precomp table (LDS on the GPU)
+// k*B for a signed digit k in [-128, 128] from the precomp table (LDS on the GPU), rows STRIDE words
+// apart (a multiple of 4: each row is eight 16-B reads)
+template <int STRIDE = CV_BTAB_STRIDE>
 CV_HD void btab_select(ge_precomp &r, const uint32_t *btab, int k) {
     const int m = k < 0 ? -k : k;
-    const uint4 *row = reinterpret_cast<const uint4 *>(btab + m * CV_BTAB_STRIDE);
+    const uint4 *row = reinterpret_cast<const uint4 *>(btab + m * STRIDE);
     uint32_t t[32];
 #pragma unroll
     for (int q = 0; q < 8; q++) {
@@ -67,7 +69,7 @@ CV_HD void ge_p3_encode(uint32_t w[8], const ge_p3 &p) {
 // Invalid keys are replaced by the identity in phase 1 (verdict forced false) so that every Z
 // entering the batch inversion is a non-zero coordinate of a genuine curve point.
 
-#define CV_TAB_ENTRIES 8            // k*(-A), k = 1..8
+#define CV_TAB_ENTRIES 9            // k*P, k = 0..8 (entry 0 = the identity: a digit 0 is a plain lookup)
 #define CV_TAB_WORDS (CV_TAB_ENTRIES * 40)
 #define CV_HS_WORDS 16              // h (8 words) || s (8 words)
 #define CV_R_WORDS 32               // X, Y, Z (10 limbs each) + 2 pad (16-B aligned records)
@@ -111,23 +113,26 @@ CV_HD void ge_p3_neg(ge_p3 &r, const ge_p3 &a) {
     fe_carry(r.T, r.T);
 }
 
-// tab[k-1] = k * P (k = 1..8) in cached form, 40 words per entry (16-B aligned)
+// tab[k] = k * P (k = 0..8) in cached form, 40 words per entry (16-B aligned); entry 0 is the
+// identity (1, 1, 1, 0), so a window digit of 0 is the same lookup as any other (no identity select)
 __host__ __device__ __forceinline__ void ge_cached_multiples8(uint32_t *tab, const ge_p3 &P1) {
     ge_cached c1, c;
     ge_p3 P;
+    ge_cached_identity(c);
+    ge_cached_store(tab, c);
     ge_p3_to_cached(c1, P1);
-    ge_cached_store(tab, c1);
+    ge_cached_store(tab + 40, c1);
     ge_p1p1 t;
     ge_p3_dbl(t, P1);
     ge_p1p1_to_p3(P, t);
     ge_p3_to_cached(c, P);
-    ge_cached_store(tab + 40, c);
+    ge_cached_store(tab + 80, c);
 #pragma unroll 1
     for (int k = 3; k <= 8; k++) {
         ge_add(t, P, c1);
         ge_p1p1_to_p3(P, t);
         ge_p3_to_cached(c, P);
-        ge_cached_store(tab + 40 * (k - 1), c);
+        ge_cached_store(tab + 40 * k, c);
     }
 }
 
@@ -188,13 +193,8 @@ __host__ __device__ __forceinline__ void cv_verify_straus(const uint32_t *btab, 
         {
             const int a = digit16(h, w);
             const int m = a < 0 ? -a : a;
-            ge_cached e, id;
-            ge_cached_load(e, tab + 40 * (m ? m - 1 : 0));   // branch-free: always one lookup
-            ge_cached_identity(id);
-            fe_sel(e.YplusX, e.YplusX, id.YplusX, m == 0);
-            fe_sel(e.YminusX, e.YminusX, id.YminusX, m == 0);
-            fe_sel(e.Z, e.Z, id.Z, m == 0);
-            fe_sel(e.T2d, e.T2d, id.T2d, m == 0);
+            ge_cached e;
+            ge_cached_load(e, tab + 40 * m);                 // entry 0 = identity: always one lookup
             ge_cached_cneg(e, a < 0);
             ge_add(t, R3, e);
         }
@@ -590,21 +590,17 @@ template <bool LAT = false> __host__ __device__ __forceinline__ bool cv_hs_prep(
     return r_ok;
 }
 
-// entry |d| of a cached k*P table (identity for d = 0), negated for d < 0
+// entry |d| of a cached k*P table (entry 0 = identity), negated for d < 0
 CV_HD void tab_cached_select(ge_cached &e, const uint32_t *tab, int d) {
     const int m = d < 0 ? -d : d;
-    ge_cached id;
-    ge_cached_load(e, tab + 40 * (m ? m - 1 : 0));
-    ge_cached_identity(id);
-    fe_sel(e.YplusX, e.YplusX, id.YplusX, m == 0);
-    fe_sel(e.YminusX, e.YminusX, id.YminusX, m == 0);
-    fe_sel(e.Z, e.Z, id.Z, m == 0);
-    fe_sel(e.T2d, e.T2d, id.T2d, m == 0);
+    ge_cached_load(e, tab + 40 * m);
     ge_cached_cneg(e, d < 0);
 }
 
 // E = [v]R + [u]A + [w]B from the packed digits (tabA = k*(-A), tabR = k*R); nw (>= 32, uniform
-// over the wave on the GPU) windows.  Returns E == O.
+// over the wave on the GPU) windows; the basepoint rows blo / bhi are BSTRIDE words apart.
+// Returns E == O.
+template <int BSTRIDE = CV_BTAB_STRIDE>
 __host__ __device__ __forceinline__ bool cv_hs_straus(const uint32_t *blo, const uint32_t *bhi, const uint32_t *dig,
                                                       size_t stride, const uint32_t *tabA, const uint32_t *tabR, int nw) {
     ge_p2 R;
@@ -641,10 +637,10 @@ __host__ __device__ __forceinline__ bool cv_hs_straus(const uint32_t *blo, const
         if ((win & 1) == 0 && win < 32) {
             ge_precomp e;
             ge_p1p1_to_p3(R3, t);
-            btab_select(e, blo, cv_sfield(dw, 10, 9));
+            btab_select<BSTRIDE>(e, blo, cv_sfield(dw, 10, 9));
             ge_madd(t, R3, e);
             ge_p1p1_to_p3(R3, t);
-            btab_select(e, bhi, cv_sfield(dw, 19, 9));
+            btab_select<BSTRIDE>(e, bhi, cv_sfield(dw, 19, 9));
             ge_madd(t, R3, e);
         }
         ge_p1p1_to_p2(R, t);
