@@ -43,17 +43,31 @@ __global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_points_one_kernel(uint32_t
                                                                         uint32_t *__restrict__ ws_tabR,
                                                                         uint8_t *__restrict__ ws_ok,
                                                                         uint8_t *__restrict__ status) {
-    const uint32_t g = blockIdx.x * CV_BLOCK + threadIdx.x;
-    const uint32_t i = g >> 1;
-    if (i >= n) return;                       // both lanes of a pair leave together
-    const bool is_r = (g & 1u) != 0;
-    uint32_t w[8];
-    load_words8(w, is_r ? sig + (size_t)i * 64 : pk + (size_t)i * 32);
-    const bool ok = cv_hs_point_one<false>(w, is_r, (is_r ? ws_tabR : ws_tab) + (size_t)i * CV_TAB_WORDS);
-    const bool r_ok = __shfl_xor((int)ok, 1) != 0;
-    if (!is_r) {
-        ws_ok[i] = (ok && r_ok) ? 1 : 0;
-        if (status) status[i] = ok ? 0 : 1;
+    cv_points_one_lane(blockIdx.x * CV_BLOCK + threadIdx.x, n, pk, sig, ws_tab, ws_tabR, ws_ok, status);
+}
+
+// scalars and points of the half-size group in ONE launch (throughput form): blocks [0, nbp) run the
+// point lane pairs, blocks [nbp, grid) the scalars.  The two roles are independent (both read only
+// the inputs), so the short scalar waves, dispatched last, fill the partial last round of the point
+// waves instead of paying a kernel boundary (drain + launch) of their own.  Both roles fit 3 waves
+// per SIMD; every wave is one role (blocks are role-uniform), so the lane-pair shuffle stays valid.
+template <bool SUB>
+__global__ __launch_bounds__(CV_BLOCK, 3) void cv_prep_tp_kernel(uint32_t n, uint32_t cap, uint32_t nbp,
+                                                                 const uint8_t *__restrict__ pk,
+                                                                 const uint8_t *__restrict__ sig,
+                                                                 const uint8_t *__restrict__ arena,
+                                                                 const uint64_t *__restrict__ off,
+                                                                 const uint32_t *__restrict__ len,
+                                                                 uint32_t *__restrict__ ws_dig,
+                                                                 uint32_t *__restrict__ ws_tab,
+                                                                 uint32_t *__restrict__ ws_tabR,
+                                                                 uint8_t *__restrict__ ws_ok,
+                                                                 uint8_t *__restrict__ status) {
+    if (blockIdx.x < nbp) {
+        cv_points_one_lane(blockIdx.x * CV_BLOCK + threadIdx.x, n, pk, sig, ws_tab, ws_tabR, ws_ok, status);
+    } else {
+        const uint32_t i = (blockIdx.x - nbp) * CV_BLOCK + threadIdx.x;
+        if (i < n) cv_scalars_lane(i, cap, pk, sig, arena, off, len, ws_dig);
     }
 }
 
@@ -111,3 +125,5 @@ template __global__ void cv_points_one_kernel<2, false>(uint32_t n, const uint8_
 template __global__ void cv_points_one_kernel<2, true>(uint32_t n, const uint8_t *pk, const uint8_t *sig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
 template __global__ void cv_points_one_kernel<3, false>(uint32_t n, const uint8_t *pk, const uint8_t *sig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
 template __global__ void cv_points_one_kernel<3, true>(uint32_t n, const uint8_t *pk, const uint8_t *sig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
+template __global__ void cv_prep_tp_kernel<false>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
+template __global__ void cv_prep_tp_kernel<true>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);

@@ -77,6 +77,24 @@ __device__ __forceinline__ void cv_points_pair_lane(uint32_t g, uint32_t n, cons
     }
 }
 
+// points of the half-size group, lane-pair throughput form: lane g of the grid handles signature
+// g/2, the even lane decoding A into k*(-A), the odd lane R into k*R (sequential-carry field forms)
+__device__ __forceinline__ void cv_points_one_lane(uint32_t g, uint32_t n, const uint8_t *pk, const uint8_t *sig,
+                                                   uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok,
+                                                   uint8_t *status) {
+    const uint32_t i = g >> 1;
+    if (i >= n) return;                       // both lanes of a pair leave together
+    const bool is_r = (g & 1u) != 0;
+    uint32_t w[8];
+    load_words8(w, is_r ? sig + (size_t)i * 64 : pk + (size_t)i * 32);
+    const bool ok = cv_hs_point_one<false>(w, is_r, (is_r ? ws_tabR : ws_tab) + (size_t)i * CV_TAB_WORDS);
+    const bool r_ok = __shfl_xor((int)ok, 1) != 0;
+    if (!is_r) {
+        ws_ok[i] = (ok && r_ok) ? 1 : 0;
+        if (status) status[i] = ok ? 0 : 1;
+    }
+}
+
 // ---------------------------------------------------------------- kernel declarations
 template <bool LAT> __global__ void cv_prep_kernel( uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_hs, uint32_t *ws_tab, uint8_t *ws_ok, uint8_t *status);
 template <int WAVES> __global__ void cv_straus_kernel(uint32_t n, const uint32_t *ws_hs, const uint32_t *ws_tab, uint32_t *ws_R);
@@ -104,3 +122,4 @@ __global__ void cv_mad_bench_kernel(uint32_t iters, uint64_t *out);
 __global__ void cv_femul_bench_kernel(uint32_t iters, int32_t *out);
 __global__ void cv_prep_probe_kernel( uint32_t n, uint32_t cap, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint64_t *stamps);
 __global__ void cv_mad_clock_kernel(uint32_t iters, uint64_t *out);
+template <bool SUB> __global__ void cv_prep_tp_kernel(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
