@@ -3,7 +3,7 @@
 import json
 import sys
 
-d = json.loads(open(sys.argv[1]).read().strip().split("\n")[-1])
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
 r = d["roofline"]
 print(f"C2 {d['value'] / 1e6:.1f} M/s  {d['ms_per_step']:.3f} ms/step  hs frac {r['frac']:.3f}  phases {r['phase_ms']}")
 print(f"group frac {r['group']['frac']:.3f}  cycle basis {r.get('cycle_basis', {}).get('frac_vs_measured_clock')}")
