@@ -40,11 +40,15 @@ __global__ __launch_bounds__(64, 1) void cv_prep_lat_kernel(uint32_t n, uint32_t
                                                             uint32_t *__restrict__ ws_tab,
                                                             uint32_t *__restrict__ ws_tabR,
                                                             uint8_t *__restrict__ ws_ok,
-                                                            uint8_t *__restrict__ status) {
+                                                            uint8_t *__restrict__ status,
+                                                            uint64_t *__restrict__ bitmap) {
     if (blockIdx.x < nbp) {
         cv_points_pair_lane(blockIdx.x * 64 + threadIdx.x, n, pk, sig, ws_tab, ws_tabR, ws_ok, status);
     } else {
         const uint32_t i = (blockIdx.x - nbp) * 64 + threadIdx.x;
+        // the chunk's verdict words start at zero for the Straus kernel's atomicOr (it runs after this
+        // launch on the same stream): one lane per word, instead of a separate memset launch
+        if (i < n && (i & 63u) == 0) bitmap[i >> 6] = 0;
         if (i < n) cv_scalars_lane<B16>(i, cap, pk, sig, arena, off, len, ws_dig);
     }
 }
@@ -117,5 +121,5 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_tri_kernel(uint32_t n, 
     if ((threadIdx.x & 63u) == 0 && b) atomicOr((unsigned long long *)(bitmap + sig0 / 64), (unsigned long long)b << (sig0 & 63));
 }
 
-template __global__ void cv_prep_lat_kernel<true>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
-template __global__ void cv_prep_lat_kernel<false>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
+template __global__ void cv_prep_lat_kernel<true>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
+template __global__ void cv_prep_lat_kernel<false>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);

@@ -175,11 +175,13 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
                 if (tri)
                     hipLaunchKernelGGL(cv_prep_lat_kernel<true>, dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp,
                                        pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0,
-                                       ws_dig, ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr);
+                                       ws_dig, ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr,
+                                       bitmap + (size_t)c0 / 64);
                 else
                     hipLaunchKernelGGL(cv_prep_lat_kernel<false>, dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp,
                                        pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0,
-                                       ws_dig, ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr);
+                                       ws_dig, ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr,
+                                       bitmap + (size_t)c0 / 64);
             } else {
                 hipLaunchKernelGGL(cv_scalars_lat_kernel, dim3((m + 63) / 64), dim3(64), 0, stream, m, ws_cap,
                                    pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_dig);
@@ -188,7 +190,9 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
                                    status ? status + c0 : nullptr);
             }
             if (ev && c0 == 0) (void)hipEventRecord(ev[1], stream);
-            (void)hipMemsetAsync(bitmap + (size_t)c0 / 64, 0, (size_t)((m + 63) / 64) * 8, stream);
+            // the fused prep zeroes the chunk's verdict words itself (no memset launch: -9 us)
+            if (!(g_prep_lat_fused || tri))
+                (void)hipMemsetAsync(bitmap + (size_t)c0 / 64, 0, (size_t)((m + 63) / 64) * 8, stream);
             if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
             if (tri)
                 hipLaunchKernelGGL(cv_hs_straus_tri_kernel, dim3((16 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,

@@ -13,4 +13,5 @@ for k in ("c3", "c5_shard", "keyed"):
 n = d.get("notary", {})
 print(f"notary 4096 p50 {n.get('p50_ms')} p99 {n.get('p99_ms')}  sweep " +
       " ".join(f"{s['batch']}:{s['p50_ms']:.3f}" for s in d.get("notary_sweep", [])))
-print(f"cpu_baseline {d['cpu_baseline']['value']:.0f} {d['cpu_baseline']['unit']} cores {d['cpu_baseline']['cores']}")
+if "cpu_baseline" in d:
+    print(f"cpu_baseline {d['cpu_baseline']['value']:.0f} {d['cpu_baseline']['unit']} cores {d['cpu_baseline']['cores']}")
