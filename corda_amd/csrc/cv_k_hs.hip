@@ -2,7 +2,9 @@
 // Shared helpers and every kernel declaration: cv_kcommon.h; launchers: cv_kernels.hip.
 #include "cv_kcommon.h"
 
-__global__ __launch_bounds__(CV_BLOCK, 3) void cv_scalars_kernel(uint32_t n, uint32_t cap, const uint8_t *__restrict__ pk,
+// (WAVES: the waves per SIMD its register budget is built for; 3 spills ~64 VGPRs of the SHA-512 state)
+template <int WAVES>
+__global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_scalars_kernel(uint32_t n, uint32_t cap, const uint8_t *__restrict__ pk,
                                                                  const uint8_t *__restrict__ sig,
                                                                  const uint8_t *__restrict__ arena,
                                                                  const uint64_t *__restrict__ off,
@@ -127,3 +129,5 @@ template __global__ void cv_points_one_kernel<3, false>(uint32_t n, const uint8_
 template __global__ void cv_points_one_kernel<3, true>(uint32_t n, const uint8_t *pk, const uint8_t *sig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
 template __global__ void cv_prep_tp_kernel<false>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
 template __global__ void cv_prep_tp_kernel<true>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
+template __global__ void cv_scalars_kernel<2>(uint32_t n, uint32_t cap, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig);
+template __global__ void cv_scalars_kernel<3>(uint32_t n, uint32_t cap, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig);

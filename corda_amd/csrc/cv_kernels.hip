@@ -38,6 +38,9 @@ extern "C" void cvk_set_points_mode(int v) { g_points_mode = (v == 2 || v == 3) 
 // 1 = scalars and point pairs of a throughput chunk in one launch (cv_prep_tp_kernel), 0 = two launches
 static int g_prep_tp = 0;   // neutral in the same-box A/B (3.25 ms fused vs 0.89 + 2.39 ms), kept as a knob
 extern "C" void cvk_set_prep_tp(int v) { g_prep_tp = v ? 1 : 0; }
+// waves per SIMD of the throughput scalars kernel (2 = no VGPR spills, 3 = more latency hiding)
+static int g_scalars_waves = 3;
+extern "C" void cvk_set_scalars_waves(int v) { g_scalars_waves = (v == 2) ? 2 : 3; }
 // the prep of a throughput (sub-)chunk [a, a + m): scalars -> ws_dig, decodes + tables -> tabA / tabR;
 // mid (optional) is recorded between the two launches of the unfused form
 template <bool SUB>
@@ -54,8 +57,12 @@ static void launch_prep_tp(uint32_t m, uint32_t cap, const uint8_t *pk, const ui
         if (mid) (void)hipEventRecord(mid, st);
         return;
     }
-    hipLaunchKernelGGL(cv_scalars_kernel, dim3((m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, st, m, cap, pk, sig,
-                       arena, off, len, dig);
+    if (g_scalars_waves == 2)
+        hipLaunchKernelGGL(cv_scalars_kernel<2>, dim3((m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, st, m, cap, pk,
+                           sig, arena, off, len, dig);
+    else
+        hipLaunchKernelGGL(cv_scalars_kernel<3>, dim3((m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, st, m, cap, pk,
+                           sig, arena, off, len, dig);
     if (mid) (void)hipEventRecord(mid, st);
     launch_points<SUB>(m, pk, sig, tabA, tabR, ok, status, st);
 }
