@@ -135,6 +135,11 @@ def test_id_mismatch_is_illegal_state(engine):
         tampered.tx
 
 
+def stx_missing(stx) -> bool:
+    """SignedTransaction.getMissingSignatures non-empty (SignedTransaction.kt:89-93), from the keys."""
+    return bool(stx._missing_signatures())
+
+
 def test_batch_verify_matches_sequential(engine):
     stxs = [make_stx(engine, signer_idx=[i, i + 1], must_idx=[i, i + 1, i + 2] if i % 5 == 0 else None,
                      outputs=(bytes([i]) * 40,)) for i in range(20, 60)]
@@ -147,6 +152,14 @@ def test_batch_verify_matches_sequential(engine):
         except Exception as e:  # noqa: BLE001
             exp = e
         assert type(got) is type(exp)
+        # independent check: the literal eddsa-0.1.0 restatement over each signature, in order
+        first_bad = next((i for i, s in enumerate(stx.sigs) if not E.verify(s.by.encoded, stx.id.bytes, s.bits)), None)
+        if first_bad is not None:
+            assert isinstance(got, SignatureException) and not isinstance(got, SignaturesMissingException)
+        elif stx_missing(stx):
+            assert isinstance(got, SignaturesMissingException)
+        else:
+            assert got is None
 
 
 def test_compute_ids_golden():

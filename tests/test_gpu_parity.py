@@ -127,14 +127,25 @@ def test_baseline_size_all_honest_and_exact_pattern(engine):
 
 
 def test_key_pool_batch(engine, oracle_c):
-    """1,024-key pool variant: repeated keys across lanes."""
+    """1,024-key pool variant (repeated keys across lanes; above 4,096 signatures the host dedupe
+    sends it down the keyed comb path) with S, R, message and key corruptions vs the C oracle."""
     from corda_amd import workload
-    n = 4096
-    b = workload.make_batch(engine, 0, n, 32, seed=5, key_pool=1024)
-    pk, sig, arena, off, ln = b.to_host()
-    assert len({bytes(r) for r in pk}) == 1024
-    bitmap, _ = engine.verify_batch(pk, sig, arena, off, ln)
-    assert _bits(bitmap, n).all()
+    for n in (4096, 9000):
+        b = workload.make_batch(engine, 0, n, 32, seed=5, key_pool=1024)
+        pk, sig, arena, off, ln = b.to_host()
+        assert len({bytes(r) for r in pk}) == 1024
+        bitmap, _ = engine.verify_batch(pk, sig, arena, off, ln)
+        assert _bits(bitmap, n).all()
+        sig, arena, pk = sig.copy(), arena.copy(), pk.copy()
+        sig[1::17, 50] ^= 0x04                          # S
+        sig[2::19, 7] ^= 0x80                           # R
+        arena[off[3::23].astype(np.int64) + 5] ^= 0x01  # message
+        pk[5::29, 31] ^= 0x40                           # key (sign bit or y bit 254)
+        bitmap, status = engine.verify_batch(pk, sig, arena, off, ln)
+        ref, rst = oracle_c.verify_batch(pk, sig, arena, off, ln, nthreads=8)
+        assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
+        assert np.array_equal(status, rst)
+        assert 0 < int(ref.sum()) < n
 
 
 def test_merkle_golden(engine, merkle_cases):
@@ -445,4 +456,40 @@ def test_points_kernel_forms_agree(engine, corpus, oracle_c, points_mode):
         assert np.array_equal(status, rst)
     finally:
         lib.cvk_set_points_mode(3)
+        lib.cvk_set_quad_max(32768)
+
+
+# ---------------------------------------------------------------- prep launch variants (knobs)
+@pytest.mark.parametrize("knob,value", [("cvk_set_prep_tp", 1), ("cvk_set_scalars_waves", 2)])
+def test_prep_variants_agree(engine, corpus, oracle_c, knob, value):
+    """The non-default throughput prep launches — scalars and point pairs fused into one launch
+    (cv_prep_tp_kernel), the scalars kernel at 2 waves/SIMD — give the default's verdicts: golden
+    corpus (every class, statuses) and a corrupted random batch vs the C oracle."""
+    import ctypes
+    lib = native.load()
+    lib.cvk_set_quad_max.argtypes = [ctypes.c_uint32]
+    getattr(lib, knob).argtypes = [ctypes.c_int]
+    lib.cvk_set_quad_max(0)
+    getattr(lib, knob)(value)
+    try:
+        sel = np.arange(2 * len(corpus["pk"]) + 37) % len(corpus["pk"])
+        bitmap, status = engine.verify_batch(corpus["pk"][sel], corpus["sig"][sel], corpus["arena"],
+                                             corpus["off"][sel], corpus["len"][sel])
+        assert np.array_equal(_bits(bitmap, len(sel)), corpus["verdict"][sel].astype(bool))
+        assert np.array_equal(status, corpus["status"][sel])
+        rng = np.random.default_rng(47)
+        n = 3000
+        seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+        arena = rng.integers(0, 256, n * 32 + 16, dtype=np.uint8)
+        off = np.arange(n, dtype=np.uint64) * 32
+        ln = np.full(n, 32, np.uint32)
+        pk, sig = engine.sign_batch(seeds, arena, off, ln)
+        sig[3::11, 40] ^= 0x02                           # S corrupted
+        pk[4::13, 9] ^= 0x20                             # key corrupted
+        bitmap, status = engine.verify_batch(pk, sig, arena, off, ln)
+        ref, rst = oracle_c.verify_batch(pk, sig, arena, off, ln, nthreads=8)
+        assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
+        assert np.array_equal(status, rst)
+    finally:
+        getattr(lib, knob)(0 if knob == "cvk_set_prep_tp" else 3)
         lib.cvk_set_quad_max(32768)
