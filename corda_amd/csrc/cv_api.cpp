@@ -176,7 +176,7 @@ hipError_t ensure_verify_ws(Device &d, size_t n) {
     if ((e = d.ws_tab.ensure((size_t)want * 2 * kTabBytes)) != hipSuccess) return e;   // k*(-A), k*R
     if ((e = d.ws_R.ensure((size_t)want * 128)) != hipSuccess) return e;
     if ((e = d.ws_ok.ensure((size_t)want)) != hipSuccess) return e;
-    if ((e = d.ws_dig.ensure((size_t)want * 65 * 4)) != hipSuccess) return e;   // CV_HS_DIGWORDS
+    if ((e = d.ws_dig.ensure((size_t)want * 73 * 4)) != hipSuccess) return e;   // CV_HS_DIGWORDS
     d.ws_cap = want;
     return hipSuccess;
 }

@@ -80,7 +80,7 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsprep_kernel(uint32_t n, uint
         const uint4 x = hp[q];
         hs[4 * q] = x.x; hs[4 * q + 1] = x.y; hs[4 * q + 2] = x.z; hs[4 * q + 3] = x.w;
     }
-    const bool r_ok = cv_hs_prep<LAT>(rw, hs, ws_dig + i, cap, ws_tabR + (size_t)i * CV_TAB_WORDS, reduce != 0);
+    const bool r_ok = cv_hs_prep<LAT, true>(rw, hs, ws_dig + i, cap, ws_tabR + (size_t)i * CV_TAB_WORDS, reduce != 0);
     if (!r_ok) ws_ok[i] = 0;
 }
 

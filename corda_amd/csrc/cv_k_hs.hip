@@ -11,7 +11,7 @@ __global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_scalars_kernel(uint32_t n,
                                                                  const uint32_t *__restrict__ len,
                                                                  uint32_t *__restrict__ ws_dig) {
     const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
-    if (i < n) cv_scalars_lane(i, cap, pk, sig, arena, off, len, ws_dig);
+    if (i < n) cv_scalars_lane<false, true>(i, cap, pk, sig, arena, off, len, ws_dig);
 }
 
 // points of the half-size group (throughput form): A and R decoded as one interleaved pair per lane,
@@ -69,31 +69,24 @@ __global__ __launch_bounds__(CV_BLOCK, 3) void cv_prep_tp_kernel(uint32_t n, uin
         cv_points_one_lane(blockIdx.x * CV_BLOCK + threadIdx.x, n, pk, sig, ws_tab, ws_tabR, ws_ok, status);
     } else {
         const uint32_t i = (blockIdx.x - nbp) * CV_BLOCK + threadIdx.x;
-        if (i < n) cv_scalars_lane(i, cap, pk, sig, arena, off, len, ws_dig);
+        if (i < n) cv_scalars_lane<false, true>(i, cap, pk, sig, arena, off, len, ws_dig);
     }
 }
 
 // hs_straus: E = [v]R + [u]A + [w]B per lane over the wave's largest window count, the identity
 // test, and the verdict word by wave ballot (bit i of word i/64 = signature i).  Lanes past n
-// replay signature n-1 so the whole wave takes part in the window-count reduction.
+// replay signature n-1 so the whole wave takes part in the window-count reduction.  The basepoint
+// digits are the W16 pairs (radix 2^16, one pair every fourth window) against the CV_BW16 rows in
+// global memory (bw16: 2 x 32,769 entries, 8.4 MB, L2 / Infinity-Cache resident; the lanes' gathers
+// are data-dependent, as they were from LDS).
 template <int WAVES, bool SUB>
 __global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_hs_straus_kernel(uint32_t n, uint32_t cap,
                                                                        const uint32_t *__restrict__ ws_dig,
                                                                        const uint32_t *__restrict__ ws_tab,
                                                                        const uint32_t *__restrict__ ws_tabR,
                                                                        const uint8_t *__restrict__ ws_ok,
-                                                                       uint64_t *__restrict__ bitmap) {
-    // LDS rows padded to CV_BTAB_LDS_STRIDE words: the 64 lanes of a wave gather data-dependent rows,
-    // and with 128-B rows every row started in one of two 4-bank groups (32-way conflicts); with
-    // 144-B rows consecutive row indices start 36 words apart and spread over 16 groups
-    __shared__ __attribute__((aligned(16))) uint32_t btab[2 * CV_BTAB_ENTRIES * CV_BTAB_LDS_STRIDE];
-    constexpr int ROW = CV_BTAB_ENTRIES * CV_BTAB_STRIDE, LROW = CV_BTAB_ENTRIES * CV_BTAB_LDS_STRIDE;
-    for (int k = threadIdx.x; k < ROW; k += blockDim.x) {
-        const int at = (k / CV_BTAB_STRIDE) * CV_BTAB_LDS_STRIDE + k % CV_BTAB_STRIDE;
-        btab[at] = CV_BCOMB[k];                  // k * B
-        btab[LROW + at] = CV_BCOMB[2 * ROW + k]; // k * 2^128 * B
-    }
-    __syncthreads();
+                                                                       uint64_t *__restrict__ bitmap,
+                                                                       const uint32_t *__restrict__ bw16) {
     const uint32_t wave0 = blockIdx.x * CV_BLOCK + (threadIdx.x & ~63u);
     if (wave0 >= n) return;                    // whole waves past the end leave together
     const uint32_t i0 = wave0 + (threadIdx.x & 63u);
@@ -106,20 +99,56 @@ __global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_hs_straus_kernel(uint32_t 
         nw = x > nw ? x : nw;
     }
     nw = __builtin_amdgcn_readfirstlane(nw);
-    const bool eq = cv_hs_straus<CV_BTAB_LDS_STRIDE>(btab, btab + LROW, ws_dig + i, cap, ws_tab + (size_t)i * CV_TAB_WORDS,
-                                 ws_tabR + (size_t)i * CV_TAB_WORDS, nw);
+    const bool eq = cv_hs_straus<CV_BTAB_STRIDE, true>(bw16, bw16 + CV_BW16_ROW, ws_dig + i, cap,
+                                                       ws_tab + (size_t)i * CV_TAB_WORDS,
+                                                       ws_tabR + (size_t)i * CV_TAB_WORDS, nw);
     const bool acc = eq && ws_ok[i] && i0 < n;
     const uint64_t bits = __ballot(acc);
     if ((threadIdx.x & 63u) == 0) bitmap[wave0 >> 6] = bits;
 }
+
+// The CV_BW16 table: row r (0, 1), entry k (0 .. 2^15) = k * 2^(128 r) * B as an affine precomp
+// (y+x, y-x, 2dxy), canonical limbs, CV_BTAB_STRIDE words per entry (30 used).  Built once per device
+// (cv_kernels.hip: bw16_table) by one lane per entry: [k 2^(128 r)]B from the radix-256 basepoint
+// table in LDS, then Z^-1.
+__global__ __launch_bounds__(CV_BLOCK) void cv_bw16_init_kernel(uint32_t *__restrict__ tab) {
+    __shared__ __attribute__((aligned(16))) uint32_t btab[CV_BTAB_ENTRIES * CV_BTAB_STRIDE];
+    stage_btab(btab);
+    const uint32_t t = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (t >= 2 * CV_BW16_ENTRIES) return;
+    const uint32_t row = t / CV_BW16_ENTRIES, k = t % CV_BW16_ENTRIES;
+    uint32_t sc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    sc[row ? 4 : 0] = k;                       // k * 2^(128 row)
+    ge_p3 P;
+    ge_scalarmult_base(P, sc, btab);
+    fe zi, x, y, xy, d2, f[3];
+    fe_invert(zi, P.Z);
+    fe_mul(x, P.X, zi);
+    fe_mul(y, P.Y, zi);
+    fe_add(f[0], y, x);
+    fe_sub<2>(f[1], y, x);
+    fe_mul(xy, x, y);
+    fe_const_d2(d2);
+    fe_mul(f[2], xy, d2);
+    uint32_t *o = tab + (size_t)t * CV_BTAB_STRIDE;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        uint32_t w[8];
+        fe_to_words(w, f[c]);                  // canonical (< p): limbs < M_i after the re-split
+        fe canon;
+        fe_from_words(canon, w);
+        fe_store(o + 10 * c, canon);
+    }
+    o[30] = o[31] = 0;
+}
 template __global__ void cv_hs_straus_kernel<2>(uint32_t, uint32_t, const uint32_t *, const uint32_t *,
-                                                const uint32_t *, const uint8_t *, uint64_t *);
+                                                const uint32_t *, const uint8_t *, uint64_t *, const uint32_t *);
 template __global__ void cv_hs_straus_kernel<3>(uint32_t, uint32_t, const uint32_t *, const uint32_t *,
-                                                const uint32_t *, const uint8_t *, uint64_t *);
+                                                const uint32_t *, const uint8_t *, uint64_t *, const uint32_t *);
 template __global__ void cv_hs_straus_kernel<2, true>(uint32_t, uint32_t, const uint32_t *, const uint32_t *,
-                                                      const uint32_t *, const uint8_t *, uint64_t *);
+                                                const uint32_t *, const uint8_t *, uint64_t *, const uint32_t *);
 template __global__ void cv_hs_straus_kernel<3, true>(uint32_t, uint32_t, const uint32_t *, const uint32_t *,
-                                                      const uint32_t *, const uint8_t *, uint64_t *);
+                                                const uint32_t *, const uint8_t *, uint64_t *, const uint32_t *);
 
 template __global__ void cv_points_kernel<false>(uint32_t n, const uint8_t *pk, const uint8_t *sig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
 template __global__ void cv_points_kernel<true>(uint32_t n, const uint8_t *pk, const uint8_t *sig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);

@@ -44,7 +44,7 @@ __device__ __forceinline__ void store_words(uint32_t *dst, const uint32_t *src, 
 // kernel (2 waves per SIMD) the hash's serial 64-bit chains were 32 % of the prep's cycles
 // (tools/prep_probe.py).  Any block size (small latency batches launch 64-thread blocks so the few
 // waves spread over CUs).
-template <bool B16 = false>
+template <bool B16 = false, bool W16 = false>
 __device__ __forceinline__ void cv_scalars_lane(uint32_t i, uint32_t cap, const uint8_t *pk, const uint8_t *sig,
                                                 const uint8_t *arena, const uint64_t *off, const uint32_t *len,
                                                 uint32_t *ws_dig) {
@@ -54,7 +54,7 @@ __device__ __forceinline__ void cv_scalars_lane(uint32_t i, uint32_t cap, const 
     load_words8(sw, sig + (size_t)i * 64 + 32);
     uint32_t hs[CV_HS_WORDS];
     cv_keyed_hs(aw, rw, sw, arena + off[i], len[i], hs);
-    cv_hs_scalars<B16>(hs, ws_dig + i, cap);
+    cv_hs_scalars<B16, W16>(hs, ws_dig + i, cap);
 }
 
 // points of the half-size group (latency form, small batches): a lane PAIR per signature, the even
@@ -108,7 +108,8 @@ template <int WAVES> __global__ void cv_comb_kernel(uint32_t n, const uint32_t *
 template <int WAVES> __global__ void cv_scalars_kernel(uint32_t n, uint32_t cap, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig);
 template <bool SUB = false> __global__ void cv_points_kernel(uint32_t n, const uint8_t *pk, const uint8_t *sig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
 template <int WAVES, bool SUB = false> __global__ void cv_points_one_kernel(uint32_t n, const uint8_t *pk, const uint8_t *sig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
-template <int WAVES, bool SUB = false> __global__ void cv_hs_straus_kernel(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap);
+template <int WAVES, bool SUB = false> __global__ void cv_hs_straus_kernel(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);
+__global__ void cv_bw16_init_kernel(uint32_t *tab);
 __global__ void cv_scalars_lat_kernel(uint32_t n, uint32_t cap, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig);
 __global__ void cv_points_pair_kernel(uint32_t n, const uint8_t *pk, const uint8_t *sig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
 template <bool B16> __global__ void cv_prep_lat_kernel(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);

@@ -154,6 +154,32 @@ static int g_comb_waves = 3;
 extern "C" void cvk_set_comb_waves(int w) { g_comb_waves = (w == 2) ? 2 : 3; }
 
 // ---------------------------------------------------------------- launchers (internal ABI)
+// The CV_BW16 basepoint rows of the throughput group (cv_bw16_init_kernel), built once per device on
+// first use: 2 x 32,769 entries x 128 B = 8.4 MB of device memory for the process's lifetime.
+static uint32_t *g_bw16[16];
+static std::mutex g_bw16_mu;
+static hipError_t bw16_table(const uint32_t **out, hipStream_t st) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 16) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> lk(g_bw16_mu);
+    if (!g_bw16[dev]) {
+        uint32_t *p = nullptr;
+        if ((e = hipMalloc(&p, (size_t)2 * CV_BW16_ROW * 4)) != hipSuccess) return e;
+        hipLaunchKernelGGL(cv_bw16_init_kernel, dim3((2 * CV_BW16_ENTRIES + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK),
+                           0, st, p);
+        if ((e = hipGetLastError()) == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) {
+            (void)hipFree(p);
+            return e;
+        }
+        g_bw16[dev] = p;
+    }
+    *out = g_bw16[dev];
+    return hipSuccess;
+}
+
 extern "C" {
 
 // Verify n signatures with the workspace ws (capacity ws_cap signatures, a multiple of 512); the
@@ -166,6 +192,11 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
                       hipEvent_t *ev) {
     if (n == 0) return hipSuccess;
     if (ws_cap == 0 || ws_cap % 512) return hipErrorInvalidValue;
+    const uint32_t *bw16 = nullptr;            // the throughput group's basepoint rows
+    if (n > g_quad_max && g_verify_mode == 1) {
+        const hipError_t e = bw16_table(&bw16, stream);
+        if (e != hipSuccess) return e;
+    }
     for (uint32_t c0 = 0; c0 < n; c0 += ws_cap) {
         const uint32_t m = (n - c0 < ws_cap) ? n - c0 : ws_cap;
         const uint32_t blocks = (m + CV_BLOCK - 1) / CV_BLOCK;
@@ -242,11 +273,11 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
                 if (g_hs_waves == 2)
                     hipLaunchKernelGGL((cv_hs_straus_kernel<2, true>), dim3(bl), dim3(CV_BLOCK), 0, st, mm, ws_cap,
                                        ws_dig + sub0[h], ws_tab + (size_t)sub0[h] * CV_TAB_WORDS,
-                                       ws_tabR + (size_t)sub0[h] * CV_TAB_WORDS, ws_ok + sub0[h], bitmap + a / 64);
+                                       ws_tabR + (size_t)sub0[h] * CV_TAB_WORDS, ws_ok + sub0[h], bitmap + a / 64, bw16);
                 else
                     hipLaunchKernelGGL((cv_hs_straus_kernel<3, true>), dim3(bl), dim3(CV_BLOCK), 0, st, mm, ws_cap,
                                        ws_dig + sub0[h], ws_tab + (size_t)sub0[h] * CV_TAB_WORDS,
-                                       ws_tabR + (size_t)sub0[h] * CV_TAB_WORDS, ws_ok + sub0[h], bitmap + a / 64);
+                                       ws_tabR + (size_t)sub0[h] * CV_TAB_WORDS, ws_ok + sub0[h], bitmap + a / 64, bw16);
             }
             (void)hipEventRecord(ax->done2, ax->s2);
             (void)hipStreamWaitEvent(stream, ax->done2, 0);
@@ -262,10 +293,10 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
             if (g_hs_waves == 2)
                 hipLaunchKernelGGL(cv_hs_straus_kernel<2>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, ws_dig,
-                                   ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
+                                   ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64, bw16);
             else
                 hipLaunchKernelGGL(cv_hs_straus_kernel<3>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, ws_dig,
-                                   ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
+                                   ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64, bw16);
             if (ev && c0 == 0) (void)hipEventRecord(ev[3], stream);
             continue;
         }
@@ -290,10 +321,10 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
             if (g_hs_waves == 2)
                 hipLaunchKernelGGL(cv_hs_straus_kernel<2>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, ws_dig,
-                                   ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
+                                   ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64, bw16);
             else
                 hipLaunchKernelGGL(cv_hs_straus_kernel<3>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, ws_dig,
-                                   ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
+                                   ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64, bw16);
             if (ev && c0 == 0) (void)hipEventRecord(ev[3], stream);
             continue;
         }

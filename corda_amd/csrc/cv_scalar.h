@@ -246,6 +246,23 @@ CV_HD int digit256(const uint32_t n[8], int k) {
     return (int)byte - 256 * top + prev;
 }
 
+// Signed radix-2^16 digits of a scalar n < 2^253 with the carry propagated (x = raw_k + carry;
+// x >= 2^15 -> d_k = x - 2^16, carry 1), d_k in [-2^15, 2^15), sum d_k 2^(16k) = n; packed two per
+// word as 16-bit two's complement: out[j] = d_j | d_(j+8) << 16 (j = 0..7), i.e. the digit of the
+// k*B row and the digit of the k*2^128*B row that the Straus loop adds at the same window.
+CV_HD void digits65536_pairs(uint32_t out[8], const uint32_t n[8]) {
+    int d[16];
+    uint32_t carry = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const uint32_t x = ((n[k >> 1] >> (16 * (k & 1))) & 0xffffu) + carry;
+        carry = x >= 0x8000u ? 1u : 0u;
+        d[k] = (int)x - (int)(carry << 16);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) out[j] = ((uint32_t)d[j] & 0xffffu) | ((uint32_t)d[j + 8] << 16);
+}
+
 // ---------------------------------------------------------------- half-size scalars
 // For the verify equation R = [s]B - [h]A (eddsa-0.1.0, cofactorless) find u, v with
 //     u = v * h  (mod 8L),   v odd,   |u|, |v| ~ 2^128

@@ -551,7 +551,14 @@ __host__ __device__ __forceinline__ bool cv_merkle_root_inplace(uint32_t *lvl, u
 // 19-27 = radix-256 digits in [-128, 128] of w for k*B and k*2^128*B (even windows < 32 only).
 // dig[64 * stride + i] = the lane's window count.
 CV_HD int cv_sfield(uint32_t w, int off, int width) { return (int)(w << (32 - off - width)) >> (32 - width); }
-#define CV_HS_DIGWORDS 65
+// W16 digit format (the throughput group): the window words carry only the A and R digits; w's 16
+// signed radix-2^16 digits live in 8 more words (digits65536_pairs), word j at dig[(CV_HS_BWORD + j) *
+// stride], added at window 4j from the CV_BW16 rows k*B and k*2^128*B (16 basepoint madds per verify
+// instead of 32 with the radix-256 rows).
+#define CV_HS_BWORD 65
+#define CV_HS_DIGWORDS 73
+#define CV_BW16_ENTRIES 32769          // |d| = 0..2^15
+#define CV_BW16_ROW (CV_BW16_ENTRIES * CV_BTAB_STRIDE)
 
 // Canonical decode of R: true iff the 8 words are exactly GroupElement.toByteArray() of a point.
 template <bool LAT = false> __host__ __device__ __forceinline__ bool ge_decode_canonical(ge_p3 &P, const uint32_t w[8]) {
@@ -563,9 +570,9 @@ template <bool LAT = false> __host__ __device__ __forceinline__ bool ge_decode_c
     return ok && diff == 0;
 }
 
-template <bool LAT = false> __host__ __device__ __forceinline__ bool cv_hs_prep(const uint32_t rw[8], const uint32_t *hs,
-                                                                               uint32_t *dig, size_t stride,
-                                                                               uint32_t *tabR, bool reduce = true) {
+template <bool LAT = false, bool W16 = false>
+__host__ __device__ __forceinline__ bool cv_hs_prep(const uint32_t rw[8], const uint32_t *hs, uint32_t *dig, size_t stride,
+                                                    uint32_t *tabR, bool reduce = true) {
     {
         uint32_t h[8], s[8], u[8], v[8], w[8];
 #pragma unroll
@@ -576,12 +583,18 @@ template <bool LAT = false> __host__ __device__ __forceinline__ bool cv_hs_prep(
 #pragma unroll 4
         for (int win = 0; win < 64; win++) {
             const int da = -digit16(u, win), dr = v_neg ? -digit16(v, win) : digit16(v, win);
-            const bool bw = (win & 1) == 0 && win < 32;
+            const bool bw = !W16 && (win & 1) == 0 && win < 32;
             const int dlo = bw ? digit256(w, win >> 1) : 0, dhi = bw ? digit256(w, 16 + (win >> 1)) : 0;
             dig[(size_t)win * stride] = ((uint32_t)da & 0x1fu) | (((uint32_t)dr & 0x1fu) << 5) |
                                         (((uint32_t)dlo & 0x1ffu) << 10) | (((uint32_t)dhi & 0x1ffu) << 19);
         }
         dig[64 * stride] = (uint32_t)nwin;
+        if (W16) {
+            uint32_t bw16[8];
+            digits65536_pairs(bw16, w);
+#pragma unroll
+            for (int j = 0; j < 8; j++) dig[(size_t)(CV_HS_BWORD + j) * stride] = bw16[j];
+        }
     }
     ge_p3 R;
     const bool r_ok = ge_decode_canonical<LAT>(R, rw);
@@ -599,8 +612,10 @@ CV_HD void tab_cached_select(ge_cached &e, const uint32_t *tab, int d) {
 
 // E = [v]R + [u]A + [w]B from the packed digits (tabA = k*(-A), tabR = k*R); nw (>= 32, uniform
 // over the wave on the GPU) windows; the basepoint rows blo / bhi are BSTRIDE words apart.
-// Returns E == O.
-template <int BSTRIDE = CV_BTAB_STRIDE>
+// W16 = false: radix-256 digits of w in the even window words, rows k*B / k*2^128*B for k = 0..128
+// (CV_BCOMB); W16 = true: radix-2^16 digit pairs in their own words, added every fourth window from
+// the CV_BW16 rows (k = 0..2^15).  Returns E == O.
+template <int BSTRIDE = CV_BTAB_STRIDE, bool W16 = false>
 __host__ __device__ __forceinline__ bool cv_hs_straus(const uint32_t *blo, const uint32_t *bhi, const uint32_t *dig,
                                                       size_t stride, const uint32_t *tabA, const uint32_t *tabR, int nw) {
     ge_p2 R;
@@ -634,13 +649,22 @@ __host__ __device__ __forceinline__ bool cv_hs_straus(const uint32_t *blo, const
             tab_cached_select(e, tabA, cv_sfield(dw, 0, 5));
             ge_add(t, R3, e);
         }
-        if ((win & 1) == 0 && win < 32) {
+        if (W16 ? ((win & 3) == 0 && win < 32) : ((win & 1) == 0 && win < 32)) {
+            int dlo, dhi;
+            if (W16) {
+                const uint32_t bw = dig[(size_t)(CV_HS_BWORD + (win >> 2)) * stride];
+                dlo = (int)(int16_t)(bw & 0xffffu);
+                dhi = (int)bw >> 16;
+            } else {
+                dlo = cv_sfield(dw, 10, 9);
+                dhi = cv_sfield(dw, 19, 9);
+            }
             ge_precomp e;
             ge_p1p1_to_p3(R3, t);
-            btab_select<BSTRIDE>(e, blo, cv_sfield(dw, 10, 9));
+            btab_select<BSTRIDE>(e, blo, dlo);
             ge_madd(t, R3, e);
             ge_p1p1_to_p3(R3, t);
-            btab_select<BSTRIDE>(e, bhi, cv_sfield(dw, 19, 9));
+            btab_select<BSTRIDE>(e, bhi, dhi);
             ge_madd(t, R3, e);
         }
         ge_p1p1_to_p2(R, t);
@@ -759,7 +783,9 @@ __host__ __device__ inline int cv_pmt_verify(uint32_t b, uint32_t e, const uint8
 // k*B / k*2^128*B rows of the single-chain forms); B16 = true: w as 64 signed radix-16 digits split in
 // two 32-window halves (bits 10 and 15, 5 bits each: window t holds digit t and digit 32 + t), for the
 // tri-chain form (cv_hsquad.h) whose two B quads each add one digit per window like the R / A quads.
-template <bool B16 = false>
+// W16 = true (the throughput group): the window words carry only the A / R digits and w goes to
+// the 8 radix-2^16 pair words (CV_HS_BWORD).
+template <bool B16 = false, bool W16 = false>
 __host__ __device__ __forceinline__ void cv_hs_scalars(const uint32_t hs[CV_HS_WORDS], uint32_t *dig, size_t stride) {
     uint32_t h[8], s[8], u[8], v[8], w[8];
 #pragma unroll
@@ -774,6 +800,8 @@ __host__ __device__ __forceinline__ void cv_hs_scalars(const uint32_t hs[CV_HS_W
         if (B16) {
             const int dlo = win < 32 ? digit16(w, win) : 0, dhi = win < 32 ? digit16(w, 32 + win) : 0;
             bf = (((uint32_t)dlo & 0x1fu) << 10) | (((uint32_t)dhi & 0x1fu) << 15);
+        } else if (W16) {
+            bf = 0;
         } else {
             const bool bw = (win & 1) == 0 && win < 32;
             const int dlo = bw ? digit256(w, win >> 1) : 0, dhi = bw ? digit256(w, 16 + (win >> 1)) : 0;
@@ -782,6 +810,12 @@ __host__ __device__ __forceinline__ void cv_hs_scalars(const uint32_t hs[CV_HS_W
         dig[(size_t)win * stride] = ((uint32_t)da & 0x1fu) | (((uint32_t)dr & 0x1fu) << 5) | bf;
     }
     dig[64 * stride] = (uint32_t)nwin;
+    if (W16) {
+        uint32_t bw16[8];
+        digits65536_pairs(bw16, w);
+#pragma unroll
+        for (int j = 0; j < 8; j++) dig[(size_t)(CV_HS_BWORD + j) * stride] = bw16[j];
+    }
 }
 
 // R's canonical-encoding check: its bytes re-encode to themselves (y < p; x = 0 only with sign 0)

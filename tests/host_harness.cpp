@@ -204,6 +204,11 @@ int cvh_digit16(const uint8_t *s, int k) {
     words_from_bytes(w, s, 8);
     return digit16(w, k);
 }
+void cvh_digits65536(const uint8_t *s, uint32_t *out8) {
+    uint32_t w[8];
+    std::memcpy(w, s, 32);
+    digits65536_pairs(out8, w);
+}
 int cvh_digit256(const uint8_t *s, int k) {
     uint32_t w[8];
     words_from_bytes(w, s, 8);

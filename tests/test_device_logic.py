@@ -152,6 +152,31 @@ def test_signed_digits(host_harness):
         assert all(-128 <= H.cvh_digit256(_b(s), k) <= 128 for k in range(32))
 
 
+def test_radix65536_digit_pairs(host_harness):
+    """The throughput group's basepoint digits (cv_scalar.h digits65536_pairs): 16 signed radix-2^16
+    digits of w < L with the carry propagated, in [-2^15, 2^15), packed (d_j, d_(j+8)) as 16-bit
+    two's complement; sum d_k 2^(16k) = w exactly, on random w and on every carry boundary."""
+    import ctypes
+    H = host_harness
+    L = 2**252 + 27742317777372353535851937790883648493
+    rng = random.Random(16)
+    cases = [0, 1, L - 1, 2**252, 2**253 - 1]
+    cases += [(0x7fff << (16 * k)) | (1 << (16 * k - 1) if k else 0) for k in range(15)]      # x = 2^15 - 1 + carry
+    cases += [0x8000 << (16 * k) for k in range(15)] + [(2**(16 * k) - 1) for k in range(1, 16)]
+    cases += [rng.randrange(L) for _ in range(3000)]
+    out = (ctypes.c_uint32 * 8)()
+    for w in cases:
+        w %= 2**253
+        H.cvh_digits65536(_b(w.to_bytes(32, "little")), out)
+        d = []
+        for half in (0, 1):
+            for j in range(8):
+                x = (out[j] >> (16 * half)) & 0xffff
+                d.append(x - 0x10000 if x >= 0x8000 else x)
+        assert all(-2**15 <= x < 2**15 for x in d)
+        assert sum(x * 2**(16 * k) for k, x in enumerate(d)) == w, hex(w)
+
+
 def test_sha512_and_sha256(host_harness):
     import hashlib
     H = host_harness
