@@ -158,12 +158,14 @@ __global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_comb_kernel(uint32_t n, co
                                                                   const uint32_t *__restrict__ key_index,
                                                                   const uint32_t *__restrict__ slot_of_key,
                                                                   const uint32_t *__restrict__ ktab_pool,
-                                                                  uint32_t *__restrict__ ws_R) {
+                                                                  uint32_t *__restrict__ ws_R,
+                                                                  const uint32_t *__restrict__ bw16) {
     const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint32_t slot = slot_of_key[key_index[i]];
     ge_p2 R;
-    cv_comb_straus(CV_BCOMB, ws_hs + (size_t)i * CV_HS_WORDS, ktab_pool + (size_t)slot * CV_KTAB_WORDS, R);
+    // s * B from the radix-2^16 rows (16 madds instead of 32)
+    cv_comb_straus<true>(bw16, ws_hs + (size_t)i * CV_HS_WORDS, ktab_pool + (size_t)slot * CV_KTAB_WORDS, R);
     uint32_t rec[CV_R_WORDS];
     fe_store(rec, R.X);
     fe_store(rec + 10, R.Y);
@@ -172,9 +174,9 @@ __global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_comb_kernel(uint32_t n, co
     store_words(ws_R + (size_t)i * CV_R_WORDS, rec, CV_R_WORDS / 4);
 }
 template __global__ void cv_comb_kernel<2>(uint32_t, const uint32_t *, const uint32_t *, const uint32_t *,
-                                           const uint32_t *, uint32_t *);
+                                           const uint32_t *, uint32_t *, const uint32_t *);
 template __global__ void cv_comb_kernel<3>(uint32_t, const uint32_t *, const uint32_t *, const uint32_t *,
-                                           const uint32_t *, uint32_t *);
+                                           const uint32_t *, uint32_t *, const uint32_t *);
 
 template __global__ void cv_prep_kernel<true>( uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_hs, uint32_t *ws_tab, uint8_t *ws_ok, uint8_t *status);
 template __global__ void cv_prep_kernel<false>( uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_hs, uint32_t *ws_tab, uint8_t *ws_ok, uint8_t *status);

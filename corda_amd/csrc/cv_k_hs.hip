@@ -77,7 +77,7 @@ __global__ __launch_bounds__(CV_BLOCK, 3) void cv_prep_tp_kernel(uint32_t n, uin
 // test, and the verdict word by wave ballot (bit i of word i/64 = signature i).  Lanes past n
 // replay signature n-1 so the whole wave takes part in the window-count reduction.  The basepoint
 // digits are the W16 pairs (radix 2^16, one pair every fourth window) against the CV_BW16 rows in
-// global memory (bw16: 2 x 32,769 entries, 8.4 MB, L2 / Infinity-Cache resident; the lanes' gathers
+// global memory (bw16: rows 0 and 2 of 4 x 32,769 entries, 16.8 MB, L2 / Infinity-Cache resident; the lanes' gathers
 // are data-dependent, as they were from LDS).
 template <int WAVES, bool SUB>
 __global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_hs_straus_kernel(uint32_t n, uint32_t cap,
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_hs_straus_kernel(uint32_t 
         nw = x > nw ? x : nw;
     }
     nw = __builtin_amdgcn_readfirstlane(nw);
-    const bool eq = cv_hs_straus<CV_BTAB_STRIDE, true>(bw16, bw16 + CV_BW16_ROW, ws_dig + i, cap,
+    const bool eq = cv_hs_straus<CV_BTAB_STRIDE, true>(bw16, bw16 + 2 * CV_BW16_ROW, ws_dig + i, cap,
                                                        ws_tab + (size_t)i * CV_TAB_WORDS,
                                                        ws_tabR + (size_t)i * CV_TAB_WORDS, nw);
     const bool acc = eq && ws_ok[i] && i0 < n;
@@ -107,7 +107,7 @@ __global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_hs_straus_kernel(uint32_t 
     if ((threadIdx.x & 63u) == 0) bitmap[wave0 >> 6] = bits;
 }
 
-// The CV_BW16 table: row r (0, 1), entry k (0 .. 2^15) = k * 2^(128 r) * B as an affine precomp
+// The CV_BW16 table: row r (0..3), entry k (0 .. 2^15) = k * 2^(64 r) * B as an affine precomp
 // (y+x, y-x, 2dxy), canonical limbs, CV_BTAB_STRIDE words per entry (30 used).  Built once per device
 // (cv_kernels.hip: bw16_table) by one lane per entry: [k 2^(128 r)]B from the radix-256 basepoint
 // table in LDS, then Z^-1.
@@ -115,10 +115,11 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_bw16_init_kernel(uint32_t *__rest
     __shared__ __attribute__((aligned(16))) uint32_t btab[CV_BTAB_ENTRIES * CV_BTAB_STRIDE];
     stage_btab(btab);
     const uint32_t t = blockIdx.x * CV_BLOCK + threadIdx.x;
-    if (t >= 2 * CV_BW16_ENTRIES) return;
+    if (t >= CV_BW16_ROWS * CV_BW16_ENTRIES) return;
     const uint32_t row = t / CV_BW16_ENTRIES, k = t % CV_BW16_ENTRIES;
     uint32_t sc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    sc[row ? 4 : 0] = k;                       // k * 2^(128 row)
+#pragma unroll
+    for (int q = 0; q < 4; q++) sc[2 * q] = (uint32_t)q == row ? k : 0u;   // k * 2^(64 row)
     ge_p3 P;
     ge_scalarmult_base(P, sc, btab);
     fe zi, x, y, xy, d2, f[3];

@@ -155,7 +155,7 @@ extern "C" void cvk_set_comb_waves(int w) { g_comb_waves = (w == 2) ? 2 : 3; }
 
 // ---------------------------------------------------------------- launchers (internal ABI)
 // The CV_BW16 basepoint rows of the throughput group (cv_bw16_init_kernel), built once per device on
-// first use: 2 x 32,769 entries x 128 B = 8.4 MB of device memory for the process's lifetime.
+// first use: 4 x 32,769 entries x 128 B = 16.8 MB of device memory for the process's lifetime.
 static uint32_t *g_bw16[16];
 static std::mutex g_bw16_mu;
 static hipError_t bw16_table(const uint32_t **out, hipStream_t st) {
@@ -166,8 +166,8 @@ static hipError_t bw16_table(const uint32_t **out, hipStream_t st) {
     std::lock_guard<std::mutex> lk(g_bw16_mu);
     if (!g_bw16[dev]) {
         uint32_t *p = nullptr;
-        if ((e = hipMalloc(&p, (size_t)2 * CV_BW16_ROW * 4)) != hipSuccess) return e;
-        hipLaunchKernelGGL(cv_bw16_init_kernel, dim3((2 * CV_BW16_ENTRIES + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK),
+        if ((e = hipMalloc(&p, (size_t)CV_BW16_ROWS * CV_BW16_ROW * 4)) != hipSuccess) return e;
+        hipLaunchKernelGGL(cv_bw16_init_kernel, dim3((CV_BW16_ROWS * CV_BW16_ENTRIES + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK),
                            0, st, p);
         if ((e = hipGetLastError()) == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) {
@@ -370,6 +370,11 @@ hipError_t cvk_verify_keyed(uint32_t n, const uint8_t *keys, const uint32_t *key
                             hipStream_t stream, hipEvent_t *ev) {
     if (n == 0) return hipSuccess;
     if (ws_cap == 0 || ws_cap % 512) return hipErrorInvalidValue;
+    const uint32_t *bw16 = nullptr;            // the comb kernel's radix-2^16 basepoint rows
+    if (n > g_quad_max) {
+        const hipError_t e = bw16_table(&bw16, stream);
+        if (e != hipSuccess) return e;
+    }
     for (uint32_t c0 = 0; c0 < n; c0 += ws_cap) {
         const uint32_t m = (n - c0 < ws_cap) ? n - c0 : ws_cap;
         const uint32_t blocks = (m + CV_BLOCK - 1) / CV_BLOCK;
@@ -383,10 +388,10 @@ hipError_t cvk_verify_keyed(uint32_t n, const uint8_t *keys, const uint32_t *key
                                m, ws_hs, key_index + c0, slot_of_key, ktab_pool, ws_R);
         else if (g_comb_waves == 2)
             hipLaunchKernelGGL(cv_comb_kernel<2>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, key_index + c0,
-                               slot_of_key, ktab_pool, ws_R);
+                               slot_of_key, ktab_pool, ws_R, bw16);
         else
             hipLaunchKernelGGL(cv_comb_kernel<3>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_hs, key_index + c0,
-                               slot_of_key, ktab_pool, ws_R);
+                               slot_of_key, ktab_pool, ws_R, bw16);
         if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
         const uint32_t nbytes = ((m + 63) / 64) * 8;
         if (n <= g_quad_max)

@@ -74,6 +74,10 @@ CV_HD void ge_p3_encode(uint32_t w[8], const ge_p3 &p) {
 #define CV_HS_WORDS 16              // h (8 words) || s (8 words)
 #define CV_R_WORDS 32               // X, Y, Z (10 limbs each) + 2 pad (16-B aligned records)
 #define CV_FIN_CHUNK 8              // signatures per lane in the finish phase
+// radix-2^16 basepoint rows k * 2^(64 r) * B (r = 0..3, k = 0..2^15; see CV_HS_BWORD below)
+#define CV_BW16_ENTRIES 32769
+#define CV_BW16_ROWS 4
+#define CV_BW16_ROW (CV_BW16_ENTRIES * CV_BTAB_STRIDE)
 
 CV_HD void fe_store(uint32_t *p, const fe &f) {
 #pragma unroll
@@ -426,12 +430,16 @@ CV_HD void krow_select(ge_precomp &e, const uint32_t *row, int d) {
     ge_precomp_cneg(e, d < 0);
 }
 
-// Keyed phase 2: R' = [h](-A) + [s]B by the 4-row comb.  bcomb = CV_BCOMB (global or LDS copy).
+// Keyed phase 2: R' = [h](-A) + [s]B by the 4-row comb.  W16 = false: bcomb = CV_BCOMB (radix-256
+// rows, 4 madds every other window: 32); W16 = true: bcomb = the CV_BW16 table (rows k * 2^(64 r) * B,
+// k <= 2^15): s's 16 carry-propagated radix-2^16 digits, 4 madds every fourth window (16).
+template <bool W16 = false>
 __host__ __device__ __forceinline__ void cv_comb_straus(const uint32_t *bcomb, const uint32_t *hs, const uint32_t *ktab,
                                                         ge_p2 &out) {
-    uint32_t h[8], s[8];
+    uint32_t h[8], s[8], sd[8];
 #pragma unroll
     for (int q = 0; q < 8; q++) { h[q] = hs[q]; s[q] = hs[8 + q]; }
+    if (W16) digits65536_pairs(sd, s);      // sd[j] = d_j | d_(j+8) << 16
     ge_p2 R;
     ge_p2_identity(R);
 #pragma unroll 1
@@ -450,7 +458,7 @@ __host__ __device__ __forceinline__ void cv_comb_straus(const uint32_t *bcomb, c
         } else {
             ge_p3_identity(R3);
         }
-        const bool with_b = (u & 1) == 0;
+        const bool with_b = W16 ? (u & 3) == 0 : (u & 1) == 0;
 #pragma unroll
         for (int j = 0; j < CV_COMB_ROWS; j++) {
             ge_precomp e;
@@ -462,7 +470,15 @@ __host__ __device__ __forceinline__ void cv_comb_straus(const uint32_t *bcomb, c
 #pragma unroll
             for (int j = 0; j < CV_COMB_ROWS; j++) {
                 ge_precomp e;
-                btab_select(e, bcomb + j * CV_BTAB_ENTRIES * CV_BTAB_STRIDE, digit256(s, 8 * j + (u >> 1)));
+                if (W16) {
+                    // digit k = 4j + u/4 of s: the low half of sd[k] (k < 8) or the high half of sd[k - 8]
+                    const int k = 4 * j + (u >> 2);
+                    const uint32_t word = sel8(sd, k & 7);
+                    const int d = k < 8 ? (int)(int16_t)(word & 0xffffu) : (int)word >> 16;
+                    btab_select(e, bcomb + j * CV_BW16_ROW, d);
+                } else {
+                    btab_select(e, bcomb + j * CV_BTAB_ENTRIES * CV_BTAB_STRIDE, digit256(s, 8 * j + (u >> 1)));
+                }
                 ge_madd(t, R3, e);
                 if (j + 1 < CV_COMB_ROWS) ge_p1p1_to_p3(R3, t);
             }
@@ -554,11 +570,10 @@ CV_HD int cv_sfield(uint32_t w, int off, int width) { return (int)(w << (32 - of
 // W16 digit format (the throughput group): the window words carry only the A and R digits; w's 16
 // signed radix-2^16 digits live in 8 more words (digits65536_pairs), word j at dig[(CV_HS_BWORD + j) *
 // stride], added at window 4j from the CV_BW16 rows k*B and k*2^128*B (16 basepoint madds per verify
-// instead of 32 with the radix-256 rows).
+// instead of 32 with the radix-256 rows).  The table has four rows, k * 2^(64 r) * B (r = 0..3): the
+// half-size Straus uses rows 0 and 2, the keyed comb all four.
 #define CV_HS_BWORD 65
 #define CV_HS_DIGWORDS 73
-#define CV_BW16_ENTRIES 32769          // |d| = 0..2^15
-#define CV_BW16_ROW (CV_BW16_ENTRIES * CV_BTAB_STRIDE)
 
 // Canonical decode of R: true iff the 8 words are exactly GroupElement.toByteArray() of a point.
 template <bool LAT = false> __host__ __device__ __forceinline__ bool ge_decode_canonical(ge_p3 &P, const uint32_t w[8]) {
