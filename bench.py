@@ -55,9 +55,11 @@ W_MAC_PER_VERIFY = 2.28e5       # algorithmic 32x32->64 MACs p
 # + 32 B madds x 7 M = 1008 S + 1491 M, at S = 55 and M = 100 limb products (DESIGN.md "Roofline")
 W_MAC_STRAUS = 1008 * 55 + 1491 * 100
 # Half-size schedule (DESIGN.md "Half-size scalars"), cv_hs_straus_kernel at the typical 33 windows:
-# 32 x 4 doublings (16 S + 13 M) + 33 x (R add + A add: 15 M) + 16 x 2 B madds (14 M) = 512 S + 1135 M
+# 32 x 4 doublings (16 S + 13 M) + 33 x (R add + A add: 15 M) + 8 x 2 B madds from the radix-2^16
+# rows (14 M per B window) = 512 S + 1023 M  (round 2 start: 16 B windows from radix-256 rows, 1135 M)
 HS_NW = 33
-W_MAC_HS_STRAUS = (HS_NW - 1) * (16 * 55 + 13 * 100) + HS_NW * 15 * 100 + 16 * 14 * 100
+HS_BWIN = 8
+W_MAC_HS_STRAUS = (HS_NW - 1) * (16 * 55 + 13 * 100) + HS_NW * 15 * 100 + HS_BWIN * 14 * 100
 # whole half-size group: + 2 point decodes (254 S + 19 M each) + 2 odd-multiple tables (4 S + 59 M each)
 W_MAC_HS_GROUP = W_MAC_HS_STRAUS + 2 * (258 * 55 + 78 * 100)
 MSG_BYTES = {"c2": 300, "c5": 32, "c3": 32}
@@ -281,7 +283,7 @@ def keyed_rate(eng, device: int, n: int, msg_len: int, steps: int, sh: int, pool
     return {"workload": f"C2 shape, {pool}-key pool, keyed device path", "value": n * steps / dt,
             "unit": "verifies/s", "ms_per_step": dt / steps * 1e3,
             "phase_ms": {"key_tables": float(m[0]), "hash": float(m[1]), "comb": float(m[2]), "finish": float(m[3])},
-            "cold_key_tables_ms": float(cold[0]), "comb_work_per_unit": "240 S + 915 M per verify (60 doublings)"}
+            "cold_key_tables_ms": float(cold[0]), "comb_work_per_unit": "240 S + 803 M per verify (60 doublings, 64 key-row + 16 radix-2^16 basepoint madds)"}
 
 
 def straus_roofline(eng, local: int, n: int, straus_ms: float, kern_ms: float, mad_rate: float):
@@ -509,7 +511,7 @@ def main():
             phase_ms = {"scalars": float(ph[0]), "points": float(ph[1]), "hs_straus": float(ph[2])}
             kname, gname = "cv_hs_straus_kernel", "scalars + points + hs_straus"
             wdesc = (f"{w_straus} 32x32->64 MAC per verify in the half-size Straus phase at {HS_NW} windows "
-                     f"(512 S + 1135 M)")
+                     f"(512 S + 1023 M: 16 basepoint madds from the radix-2^16 rows)")
             gdesc = f"{w_group} MAC per verify (half-size schedule: Straus + 2 decodes + 2 tables)"
         else:
             phase_ms = {"prep": float(ph[0]), "straus": float(ph[1]), "finish": float(ph[2])}
