@@ -283,7 +283,7 @@ def keyed_rate(eng, device: int, n: int, msg_len: int, steps: int, sh: int, pool
     return {"workload": f"C2 shape, {pool}-key pool, keyed device path", "value": n * steps / dt,
             "unit": "verifies/s", "ms_per_step": dt / steps * 1e3,
             "phase_ms": {"key_tables": float(m[0]), "hash": float(m[1]), "comb": float(m[2]), "finish": float(m[3])},
-            "cold_key_tables_ms": float(cold[0]), "comb_work_per_unit": "240 S + 803 M per verify (60 doublings, 64 key-row + 16 radix-2^16 basepoint madds)"}
+            "cold_key_tables_ms": float(cold[0]), "comb_work_per_unit": "224 S + 535 M per verify (56 doublings, 32 radix-256 key-row + 16 radix-2^16 basepoint madds)"}
 
 
 def straus_roofline(eng, local: int, n: int, straus_ms: float, kern_ms: float, mad_rate: float):

@@ -157,12 +157,14 @@ struct Device {
     hipEvent_t ws_ev = nullptr;
 };
 
-// key-table pool capacity per device (keys); 4 KB of tables per key
-constexpr uint32_t kDefaultKeyCap = 1u << 16;
-constexpr size_t kKtabBytes = 1024 * 4;   // CV_KTAB_WORDS
+// key-table pool capacity per device (keys); 66 KB of tables per key (1.1 GB at the default; the pool
+// grows to a call's distinct keys when they exceed it)
+constexpr uint32_t kDefaultKeyCap = 1u << 14;
+constexpr size_t kKtabBytes = 16512 * 4;  // CV_KTAB_WORDS: 4 comb rows x 129 affine entries x 128 B
 constexpr size_t kTabBytes = 9 * 40 * 4;  // CV_TAB_WORDS: k*P, k = 0..8, cached form (cv_verify.h)
 // cv_ed25519_verify_batch dedupes keys on the host up to this batch size, and takes the keyed
-// (per-key comb) path when the batch has at least two signatures per distinct key on average
+// (per-key comb) path when the batch has at least eight signatures per distinct key on average (a key's
+// 66 KB of tables cost about as much as 7 plain verifies to build; cached keys cost nothing)
 constexpr size_t kAutoKeyedMax = 1u << 18;
 
 // Verify workspace capacity: batches above it run in chunks of this many signatures.
@@ -527,7 +529,7 @@ static int verify_shard_keyed(uint32_t cap, Device &d, size_t b, size_t e, size_
 
 // Host-side key dedupe for the plain entry point: keys[] = distinct key bytes, key_index[i] = its
 // index.  Returns false when the batch does not repeat keys enough for the keyed path to pay (it
-// gives up as soon as more than n/2 distinct keys have been seen).  Flat open addressing on the
+// gives up as soon as more than n/8 distinct keys have been seen).  Flat open addressing on the
 // seeded hash of all 32 key bytes (key_hash32), no per-key allocation.
 static bool dedupe_keys(size_t n, const uint8_t *pk, std::vector<uint8_t> &keys, std::vector<uint32_t> &key_index) {
     if (n < 64 || n > kAutoKeyedMax) return false;
@@ -572,7 +574,7 @@ static bool dedupe_keys(size_t n, const uint8_t *pk, std::vector<uint8_t> &keys,
                 uid[bkt] = nuniq;
                 key_index[i] = nuniq++;
                 uniq_sig.push_back((uint32_t)i);
-                if (2 * (size_t)nuniq > n) return false;   // fewer than two signatures per key
+                if (8 * (size_t)nuniq > n) return false;   // fewer than eight signatures per key
                 break;
             }
             if (std::memcmp(pk + 32 * (size_t)f, k, 32) == 0) {

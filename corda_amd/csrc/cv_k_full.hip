@@ -120,13 +120,16 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_keyprep_kernel(uint32_t nk, const
                                                               uint32_t *__restrict__ scratch,
                                                               uint32_t *__restrict__ ktab_pool,
                                                               uint8_t *__restrict__ kok_pool) {
-    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
+    // CV_COMB_ROWS consecutive lanes per key, one comb row each (129 entries)
+    const uint32_t g = blockIdx.x * CV_BLOCK + threadIdx.x;
+    const uint32_t i = g / CV_COMB_ROWS;
     if (i >= nk) return;
+    const int j = (int)(g % CV_COMB_ROWS);
     uint32_t aw[8];
     load_words8(aw, keys + (size_t)i * 32);
     const uint32_t slot = slots[i];
-    const bool ok = cv_key_prep(aw, scratch + (size_t)i * CV_KTAB_WORDS, ktab_pool + (size_t)slot * CV_KTAB_WORDS);
-    kok_pool[slot] = ok ? 1 : 0;
+    const bool ok = cv_key_prep_row(aw, j, scratch + (size_t)i * CV_KTAB_WORDS, ktab_pool + (size_t)slot * CV_KTAB_WORDS);
+    if (j == 0) kok_pool[slot] = ok ? 1 : 0;
 }
 
 // keyed phase 1: hash + scalar per signature; key validity from the key's slot

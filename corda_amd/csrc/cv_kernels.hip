@@ -356,7 +356,7 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
 hipError_t cvk_keyprep(uint32_t nk, const uint8_t *keys, const uint32_t *slots, uint32_t *scratch, uint32_t *ktab_pool,
                        uint8_t *kok_pool, hipStream_t stream) {
     if (nk == 0) return hipSuccess;
-    hipLaunchKernelGGL(cv_keyprep_kernel, dim3((nk + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, stream, nk, keys,
+    hipLaunchKernelGGL(cv_keyprep_kernel, dim3((CV_COMB_ROWS * nk + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, stream, nk, keys,
                        slots, scratch, ktab_pool, kok_pool);
     return hipGetLastError();
 }

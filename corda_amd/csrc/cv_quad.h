@@ -147,7 +147,8 @@ __device__ __forceinline__ void cv_quad_straus(const uint32_t *btab, const uint3
     }
 }
 
-// Quad version of cv_comb_straus (keyed path): affine key rows (entry k-1 = k * 2^(64 j)(-A)).
+// Quad version of cv_comb_straus (keyed path, reference schedule): affine key rows (entry k =
+// k * 2^(64 j)(-A), entry 0 the identity), radix-16 digits of h, radix-256 CV_BCOMB rows for s.
 __device__ __forceinline__ void cv_quad_comb(const uint32_t *bcomb, const uint32_t *hs, const uint32_t *ktab, int r,
                                              fe &P) {
     uint32_t h[8], s[8];
@@ -166,7 +167,7 @@ __device__ __forceinline__ void cv_quad_comb(const uint32_t *bcomb, const uint32
 #pragma unroll
         for (int j = 0; j < CV_COMB_ROWS; j++) {
             fe q;
-            quad_precomp_coord(q, ktab + j * CV_KROW_WORDS, CV_KENT_WORDS, digit16(h, 16 * j + u), r, false);
+            quad_precomp_coord(q, ktab + j * CV_KROW_WORDS, CV_KENT_WORDS, digit16(h, 16 * j + u), r, true);
             quad_add(P, q, r);
         }
         if ((u & 1) == 0) {

@@ -290,97 +290,105 @@ __host__ __device__ __forceinline__ bool cv_verify_one(const uint32_t *btab, con
 // ---------------------------------------------------------------- keyed verify (per-key comb)
 // For keys that repeat across a batch (notary / party keys) the key work is
 // done once per key: decode A (eddsa-0.1.0 rules) and the comb tables
-//     T_j[k-1] = k * 2^(64 j) * (-A),   j = 0..3, k = 1..8     (affine, CV_KTAB_WORDS words per key)
-// Then [h](-A) = sum_j [h_j] 2^(64 j)(-A) over the four 64-bit rows of h's signed radix-16 digits
-// (digit w = 16 j + u uses row table j at row position u), and [s]B likewise from CV_BCOMB
-// (digit k = 8 j + u/2 of s at even row positions u): 15 x 4 = 60 doublings instead of 252, the
-// same 64 + 32 additions, all mixed (affine tables).  The sums are exact integer scalar multiples, so torsion components of
-// A come out exactly as in the single-key schedule (and eddsa-0.1.0's slide-based one).
+//     T_j[k] = k * 2^(64 j) * (-A),   j = 0..3, k = 0..128 (entry 0 the identity)
+// (affine precomp, CV_KTAB_WORDS words = 66 KB per key).  Then [h](-A) = sum_j [h_j] 2^(64 j)(-A) over
+// the four 64-bit rows of h's signed radix-256 digits (digit 8 j + u uses row table j at window u of
+// 8 bits), and [s]B from the radix-2^16 CV_BW16 rows k * 2^(64 j) * B (digit 4 j + u/2 of s at even
+// windows u): 7 x 8 = 56 doublings instead of 252, 32 + 16 additions, all mixed (affine tables).  The
+// sums are exact integer scalar multiples, so torsion components of A come out exactly as in the
+// single-key schedule (and eddsa-0.1.0's slide-based one).  The W16 = false form of the comb (host
+// harness, reference schedule) reads the same key rows with radix-16 digits (entries 0..8) and the
+// radix-256 CV_BCOMB rows for B.
 
 #define CV_COMB_ROWS 4
 #define CV_KENT_WORDS 32                                      // one affine entry: 30 words + pad (128 B)
-#define CV_KROW_WORDS (8 * CV_KENT_WORDS)                     // 8 multiples per row table
-#define CV_KTAB_WORDS (CV_COMB_ROWS * CV_KROW_WORDS)          // 1024 words = 4 KB per key
+#define CV_KENT_ENTRIES 129                                   // k = 0..128 per row
+#define CV_KROW_WORDS (CV_KENT_ENTRIES * CV_KENT_WORDS)
+#define CV_KTAB_WORDS (CV_COMB_ROWS * CV_KROW_WORDS)          // 16,512 words = 66 KB per key
 
-// (X, Y, Z) of k * P, k = 1..8, into ext[(k-1) * CV_KENT_WORDS ..] (X 0..9, Y 10..19, Z 20..29)
-__host__ __device__ __forceinline__ void ge_p3_multiples8(uint32_t *ext, const ge_p3 &P1) {
-    ge_cached c1;
-    ge_p3 P;
-    ge_p1p1 t;
-    ge_p3_to_cached(c1, P1);
-    P = P1;
-#pragma unroll 1
-    for (int k = 1; k <= 8; k++) {
-        if (k == 2) {
-            ge_p3_dbl(t, P1);
-            ge_p1p1_to_p3(P, t);
-        } else if (k > 2) {
-            ge_add(t, P, c1);
-            ge_p1p1_to_p3(P, t);
-        }
-        fe_store(ext + (k - 1) * CV_KENT_WORDS, P.X);
-        fe_store(ext + (k - 1) * CV_KENT_WORDS + 10, P.Y);
-        fe_store(ext + (k - 1) * CV_KENT_WORDS + 20, P.Z);
-    }
+CV_HD void ge_p3_sel(ge_p3 &r, const ge_p3 &f, const ge_p3 &g, bool b) {
+    fe_sel(r.X, f.X, g.X, b);
+    fe_sel(r.Y, f.Y, g.Y, b);
+    fe_sel(r.Z, f.Z, g.Z, b);
+    fe_sel(r.T, f.T, g.T, b);
 }
 
-// Key precompute: decode A (eddsa-0.1.0 rules) and the comb tables of -A in affine "precomp" form
-//     ktab[j][k-1] = (y+x, y-x, 2dxy) of k * 2^(64 j) * (-A),   j = 0..3, k = 1..8
-// The 32 multiples are computed in extended coordinates into `ext` (CV_KTAB_WORDS words of scratch)
-// and normalised with one inversion (Montgomery's trick), so every table addition of the verify is a
-// mixed addition (3 products instead of 4).  Returns key_ok; invalid keys get identity tables.
-__host__ __device__ __forceinline__ bool cv_key_prep(const uint32_t aw[8], uint32_t *ext, uint32_t *ktab) {
-    ge_p3 A, P;
+// Key precompute, ONE comb row j of one key (the GPU runs a key's four rows on four lanes):
+//     ktab[j][k] = (y+x, y-x, 2dxy) of k * 2^(64 j) * (-A),   k = 0..128
+// The 128 multiples go to `ext` (scratch, same layout) in extended coordinates and are normalised
+// with one inversion per row (Montgomery's trick; the prefix products are parked in the not yet
+// written xy2d words of ktab's entries).  Every lane runs the same 3 x 64 doublings and keeps its
+// row's base point, so the four lanes never diverge.  Returns key_ok; invalid keys get identity
+// tables (-A = identity).
+__host__ __device__ __forceinline__ bool cv_key_prep_row(const uint32_t aw[8], int j, uint32_t *ext, uint32_t *ktab) {
+    ge_p3 A, P, Pj;
     const bool key_ok = ge_decode_0_1_0<true>(A, aw);
     if (!key_ok) ge_p3_identity(A);
     ge_p3_neg(P, A);
+    Pj = P;
 #pragma unroll 1
-    for (int j = 0; j < CV_COMB_ROWS; j++) {
-        ge_p3_multiples8(ext + j * CV_KROW_WORDS, P);
-        if (j + 1 < CV_COMB_ROWS) {   // P <- 2^64 P
-            ge_p2 q;
-            ge_p1p1 t;
-            ge_p3_to_p2(q, P);
+    for (int r = 1; r < CV_COMB_ROWS; r++) {   // P <- 2^64 P
+        ge_p2 q;
+        ge_p1p1 t;
+        ge_p3_to_p2(q, P);
 #pragma unroll 1
-            for (int d = 0; d < 63; d++) {
-                ge_p2_dbl(t, q);
-                ge_p1p1_to_p2(q, t);
-            }
+        for (int d = 0; d < 63; d++) {
             ge_p2_dbl(t, q);
-            ge_p1p1_to_p3(P, t);
+            ge_p1p1_to_p2(q, t);
+        }
+        ge_p2_dbl(t, q);
+        ge_p1p1_to_p3(P, t);
+        ge_p3_sel(Pj, Pj, P, r == j);
+    }
+    uint32_t *xrow = ext + (size_t)j * CV_KROW_WORDS, *trow = ktab + (size_t)j * CV_KROW_WORDS;
+    {
+        ge_cached c1;
+        ge_p3 Q = Pj;
+        ge_p1p1 t;
+        ge_p3_to_cached(c1, Pj);
+#pragma unroll 1
+        for (int k = 1; k < CV_KENT_ENTRIES; k++) {
+            if (k == 2) {
+                ge_p3_dbl(t, Pj);
+                ge_p1p1_to_p3(Q, t);
+            } else if (k > 2) {
+                ge_add(t, Q, c1);
+                ge_p1p1_to_p3(Q, t);
+            }
+            fe_store(xrow + k * CV_KENT_WORDS, Q.X);
+            fe_store(xrow + k * CV_KENT_WORDS + 10, Q.Y);
+            fe_store(xrow + k * CV_KENT_WORDS + 20, Q.Z);
         }
     }
-    // prefix products of the Z's, parked in the (not yet written) xy2d words of ktab's entries
-    const int NE = CV_COMB_ROWS * 8;
     fe acc, z;
-    fe_load(acc, ext + 20);
-    fe_store(ktab + 20, acc);
+    fe_load(acc, xrow + CV_KENT_WORDS + 20);
+    fe_store(trow + CV_KENT_WORDS + 20, acc);
 #pragma unroll 1
-    for (int k = 1; k < NE; k++) {
-        fe_load(z, ext + k * CV_KENT_WORDS + 20);
+    for (int k = 2; k < CV_KENT_ENTRIES; k++) {
+        fe_load(z, xrow + k * CV_KENT_WORDS + 20);
         fe_mul_m<true>(acc, acc, z);
-        fe_store(ktab + k * CV_KENT_WORDS + 20, acc);
+        fe_store(trow + k * CV_KENT_WORDS + 20, acc);
     }
     fe inv, d2;
     fe_invert<true>(inv, acc);
     fe_const_d2(d2);
 #pragma unroll 1
-    for (int k = NE - 1; k >= 0; k--) {
+    for (int k = CV_KENT_ENTRIES - 1; k >= 1; k--) {
         fe zi, x, y, t;
-        if (k > 0) {
+        if (k > 1) {
             fe pre;
-            fe_load(pre, ktab + (k - 1) * CV_KENT_WORDS + 20);
+            fe_load(pre, trow + (k - 1) * CV_KENT_WORDS + 20);
             fe_mul_m<true>(zi, inv, pre);
-            fe_load(z, ext + k * CV_KENT_WORDS + 20);
+            fe_load(z, xrow + k * CV_KENT_WORDS + 20);
             fe_mul_m<true>(inv, inv, z);
         } else {
             zi = inv;
         }
-        fe_load(x, ext + k * CV_KENT_WORDS);
-        fe_load(y, ext + k * CV_KENT_WORDS + 10);
+        fe_load(x, xrow + k * CV_KENT_WORDS);
+        fe_load(y, xrow + k * CV_KENT_WORDS + 10);
         fe_mul_m<true>(x, x, zi);
         fe_mul_m<true>(y, y, zi);
-        uint32_t *e = ktab + k * CV_KENT_WORDS;
+        uint32_t *e = trow + k * CV_KENT_WORDS;
         fe_add(t, y, x);
         fe_carry(t, t);
         fe_store(e, t);                      // y + x
@@ -392,7 +400,22 @@ __host__ __device__ __forceinline__ bool cv_key_prep(const uint32_t aw[8], uint3
         fe_store(e + 20, t);                 // 2 d x y
         e[30] = e[31] = 0;
     }
+    {   // entry 0: the identity (1, 1, 0)
+        ge_precomp id;
+        ge_precomp_identity(id);
+        fe_store(trow, id.yplusx);
+        fe_store(trow + 10, id.yminusx);
+        fe_store(trow + 20, id.xy2d);
+        trow[30] = trow[31] = 0;
+    }
     return key_ok;
+}
+
+// The whole key's four rows (host harness).
+__host__ __device__ __forceinline__ bool cv_key_prep(const uint32_t aw[8], uint32_t *ext, uint32_t *ktab) {
+    bool ok = true;
+    for (int j = 0; j < CV_COMB_ROWS; j++) ok = cv_key_prep_row(aw, j, ext, ktab);
+    return ok;
 }
 
 // Keyed phase 1 for one signature: only the hash and scalar (the key work is in the table).
@@ -409,10 +432,10 @@ __host__ __device__ __forceinline__ void cv_keyed_hs(const uint32_t aw[8], const
     for (int q = 0; q < 8; q++) { hs[q] = h[q]; hs[8 + q] = s[q]; }
 }
 
-// affine entry |d| of one key row table (identity for d = 0), negated for d < 0
+// affine entry |d| of one key row table (entry 0 = identity), negated for d < 0
 CV_HD void krow_select(ge_precomp &e, const uint32_t *row, int d) {
     const int m = d < 0 ? -d : d;
-    const uint4 *q = reinterpret_cast<const uint4 *>(row + (m ? m - 1 : 0) * CV_KENT_WORDS);
+    const uint4 *q = reinterpret_cast<const uint4 *>(row + m * CV_KENT_WORDS);
     uint32_t t[32];
 #pragma unroll
     for (int j = 0; j < 8; j++) {
@@ -422,17 +445,15 @@ CV_HD void krow_select(ge_precomp &e, const uint32_t *row, int d) {
     fe_load(e.yplusx, t);
     fe_load(e.yminusx, t + 10);
     fe_load(e.xy2d, t + 20);
-    ge_precomp id;
-    ge_precomp_identity(id);
-    fe_sel(e.yplusx, e.yplusx, id.yplusx, m == 0);
-    fe_sel(e.yminusx, e.yminusx, id.yminusx, m == 0);
-    fe_sel(e.xy2d, e.xy2d, id.xy2d, m == 0);
     ge_precomp_cneg(e, d < 0);
 }
 
-// Keyed phase 2: R' = [h](-A) + [s]B by the 4-row comb.  W16 = false: bcomb = CV_BCOMB (radix-256
-// rows, 4 madds every other window: 32); W16 = true: bcomb = the CV_BW16 table (rows k * 2^(64 r) * B,
-// k <= 2^15): s's 16 carry-propagated radix-2^16 digits, 4 madds every fourth window (16).
+// Keyed phase 2: R' = [h](-A) + [s]B by the 4-row comb.
+//   W16 = true (the GPU): h as signed radix-256 digits (row j, 8-bit window u: digit 8 j + u, key
+//     entries 0..128), s as its 16 carry-propagated radix-2^16 digits from the CV_BW16 rows
+//     k * 2^(64 j) * B (bcomb; digit 4 j + u/2 at even windows): 7 x 8 = 56 doublings, 32 + 16 madds.
+//   W16 = false (the host harness's reference schedule): h as radix-16 digits (key entries 0..8), s
+//     as radix-256 digits from CV_BCOMB (bcomb): 15 x 4 = 60 doublings, 64 + 32 madds.
 template <bool W16 = false>
 __host__ __device__ __forceinline__ void cv_comb_straus(const uint32_t *bcomb, const uint32_t *hs, const uint32_t *ktab,
                                                         ge_p2 &out) {
@@ -440,29 +461,29 @@ __host__ __device__ __forceinline__ void cv_comb_straus(const uint32_t *bcomb, c
 #pragma unroll
     for (int q = 0; q < 8; q++) { h[q] = hs[q]; s[q] = hs[8 + q]; }
     if (W16) digits65536_pairs(sd, s);      // sd[j] = d_j | d_(j+8) << 16
+    constexpr int NWIN = W16 ? 8 : 16, WBITS = W16 ? 8 : 4;
     ge_p2 R;
     ge_p2_identity(R);
 #pragma unroll 1
-    for (int u = 15; u >= 0; u--) {
+    for (int u = NWIN - 1; u >= 0; u--) {
         ge_p1p1 t;
         ge_p3 R3;
-        if (u != 15) {
-            ge_p2_dbl(t, R);
-            ge_p1p1_to_p2(R, t);
-            ge_p2_dbl(t, R);
-            ge_p1p1_to_p2(R, t);
-            ge_p2_dbl(t, R);
-            ge_p1p1_to_p2(R, t);
+        if (u != NWIN - 1) {
+#pragma unroll 1
+            for (int d = 0; d < WBITS - 1; d++) {
+                ge_p2_dbl(t, R);
+                ge_p1p1_to_p2(R, t);
+            }
             ge_p2_dbl(t, R);
             ge_p1p1_to_p3(R3, t);
         } else {
             ge_p3_identity(R3);
         }
-        const bool with_b = W16 ? (u & 3) == 0 : (u & 1) == 0;
+        const bool with_b = (u & 1) == 0;
 #pragma unroll
         for (int j = 0; j < CV_COMB_ROWS; j++) {
             ge_precomp e;
-            krow_select(e, ktab + j * CV_KROW_WORDS, digit16(h, 16 * j + u));
+            krow_select(e, ktab + j * CV_KROW_WORDS, W16 ? digit256(h, 8 * j + u) : digit16(h, 16 * j + u));
             ge_madd(t, R3, e);
             if (j + 1 < CV_COMB_ROWS || with_b) ge_p1p1_to_p3(R3, t);
         }
@@ -471,8 +492,8 @@ __host__ __device__ __forceinline__ void cv_comb_straus(const uint32_t *bcomb, c
             for (int j = 0; j < CV_COMB_ROWS; j++) {
                 ge_precomp e;
                 if (W16) {
-                    // digit k = 4j + u/4 of s: the low half of sd[k] (k < 8) or the high half of sd[k - 8]
-                    const int k = 4 * j + (u >> 2);
+                    // digit k = 4j + u/2 of s: the low half of sd[k] (k < 8) or the high half of sd[k - 8]
+                    const int k = 4 * j + (u >> 1);
                     const uint32_t word = sel8(sd, k & 7);
                     const int d = k < 8 ? (int)(int16_t)(word & 0xffffu) : (int)word >> 16;
                     btab_select(e, bcomb + j * CV_BW16_ROW, d);

@@ -85,10 +85,11 @@ int cv_ed25519_verify_batch(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint
  * key_index[n] into them.  Replaces the same N x PublicKey.verifyWithECDSA as
  * cv_ed25519_verify_batch — identical verdicts and status — for batches whose keys repeat (a notary
  * batch, a ResolveTransactionsFlow chain, a party's transactions): the engine keeps per-key tables
- * (decoded A and comb multiples k * 2^(64j) * (-A), 4 KB per key, affine) resident on each device, keyed by
- * the 32 key bytes, so a key is decoded once and each verify needs 60 doublings instead of 252.
+ * (decoded A and comb multiples k * 2^(64j) * (-A), k = 0..128, 66 KB per key, affine) resident on each
+ * device, keyed by the 32 key bytes, so a key is decoded once and each verify needs 56 doublings
+ * instead of 252.
  * cv_ed25519_verify_batch takes this path by itself (host-side dedupe) for batches of up to 2^18
- * signatures with at least two signatures per distinct key. */
+ * signatures with at least eight signatures per distinct key. */
 int cv_ed25519_verify_batch_keyed(cv_ctx *ctx, size_t n, size_t nkeys, const uint8_t *keys, const uint32_t *key_index,
                                   const uint8_t *sig, const uint8_t *msg_arena, const uint64_t *msg_off,
                                   const uint32_t *msg_len, uint64_t *verdict_bitmap, uint8_t *status);
@@ -205,7 +206,7 @@ int cv_diag_prep_phases(cv_ctx *ctx, int device, size_t n, const void *d_pk, con
 
 /* Diagnostics: the host-side key dedupe cv_ed25519_verify_batch runs before choosing the keyed path
  * (seeded hash of all 32 key bytes).  Returns 1 and fills key_index[n] / *nkeys when the batch
- * repeats keys enough for the keyed path (64 <= n <= 2^18, at least two signatures per distinct
+ * repeats keys enough for the keyed path (64 <= n <= 2^18, at least eight signatures per distinct
  * key; above 1,024 signatures a first 256 carrying more than 192 distinct keys is taken as
  * distinct-keyed without hashing the rest), else 0.  Host only: needs no device and no context. */
 int cv_diag_dedupe_keys(size_t n, const uint8_t *pk, uint32_t *key_index, size_t *nkeys);

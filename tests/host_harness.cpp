@@ -3,6 +3,7 @@
 // the oracle without a GPU.  Built by tests/conftest.py into tests/_build/libcvhost.so.
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "../corda_amd/csrc/cv_verify.h"
 
@@ -33,8 +34,11 @@ int cvh_verify_keyed(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, 
     words_from_bytes(aw, pk, 8);
     words_from_bytes(rw, sig, 8);
     words_from_bytes(sw, sig + 32, 8);
-    static thread_local uint32_t ktab[CV_KTAB_WORDS] __attribute__((aligned(16)));
-    static thread_local uint32_t ext[CV_KTAB_WORDS] __attribute__((aligned(16)));
+    // 2 x 66 KB of key tables: heap, not thread_local TLS (large TLS blocks in a dlopen'ed library
+    // crashed the multi-process tests that share the pytest process)
+    std::vector<uint32_t> ktab_v(CV_KTAB_WORDS + 4), ext_v(CV_KTAB_WORDS + 4);
+    uint32_t *ktab = reinterpret_cast<uint32_t *>((reinterpret_cast<uintptr_t>(ktab_v.data()) + 15) & ~(uintptr_t)15);
+    uint32_t *ext = reinterpret_cast<uint32_t *>((reinterpret_cast<uintptr_t>(ext_v.data()) + 15) & ~(uintptr_t)15);
     uint32_t hs[CV_HS_WORDS];
     uint32_t Rrec[CV_R_WORDS] __attribute__((aligned(16)));
     const bool key_ok = cv_key_prep(aw, ext, ktab);
@@ -246,7 +250,8 @@ int cvh_merkle_root(const uint8_t *leaves, uint32_t cnt, uint8_t *out) {
     return ok ? 1 : 0;
 }
 
-// Half-size-scalar verify of one signature (prep + hsprep + straus, identity test).  sc_out: 65 words.
+// Half-size-scalar verify of one signature (prep + hsprep + straus, identity test).  sc_out:
+// CV_HS_DIGWORDS (73) words.
 int cvh_verify_hs(const uint8_t *pk, const uint8_t *sig, const uint8_t *msg, uint32_t mlen, int *status,
                   uint32_t *sc_out) {
     uint32_t aw[8], rw[8], sw[8];

@@ -80,29 +80,32 @@ def test_dedupe_maps_repeated_keys():
 
 def test_dedupe_resists_shared_key_bytes():
     """keys are untrusted, so a batch whose keys agree on bytes 8..15 (the old hash input)
-    must not collapse into one probe chain.  2^17 distinct keys x 2 signatures, all sharing bytes
-    0..23 and differing only in the last 8: the seeded all-bytes hash keeps the dedupe linear."""
+    must not collapse into one probe chain.  2^15 distinct keys x 8 signatures (the keyed path's
+    threshold), all sharing bytes 0..23 and differing only in the last 8: the seeded all-bytes hash
+    keeps the dedupe of the 2^18 signatures linear."""
     import time
-    n_keys = 1 << 17
+    n_keys = 1 << 15
     base = np.full(32, 0xA5, np.uint8)
     keys = np.tile(base, (n_keys, 1))
     keys[:, 24:32] = np.arange(n_keys, dtype=np.uint64).view(np.uint8).reshape(n_keys, 8)
-    pk = np.repeat(keys, 2, axis=0)                       # each key signs twice, back to back
+    pk = np.repeat(keys, 8, axis=0)                       # each key signs 8 times, back to back
     t = time.perf_counter()
     idx, nk = native.dedupe_keys(pk)
     dt = time.perf_counter() - t
-    assert nk == n_keys and np.array_equal(idx[0::2], np.arange(n_keys)) and np.array_equal(idx[1::2], idx[0::2])
+    assert nk == n_keys and np.array_equal(idx, np.repeat(np.arange(n_keys), 8))
     assert dt < 2.0, f"dedupe of 2^18 adversarial keys took {dt:.2f} s"
 
 
 def test_dedupe_prefix_early_out():
     """Batches above 1024 signatures whose first 256 carry more than 192 distinct keys skip the
     dedupe (taken as distinct-keyed: a performance guess, the verdicts are the same either way);
-    a batch whose prefix repeats keys is deduped in full."""
+    a batch whose prefix repeats keys is deduped in full; fewer than 8 signatures per distinct key
+    on average is not worth the key tables."""
     rng = np.random.default_rng(9)
-    keys = rng.integers(0, 256, (600, 32), dtype=np.uint8)
-    pk = np.concatenate([keys, keys, keys, keys])          # 2400 sigs, 4 per key, prefix distinct
+    keys = rng.integers(0, 256, (300, 32), dtype=np.uint8)
+    pk = np.concatenate([keys] * 8)                          # 2400 sigs, 8 per key, prefix distinct
     assert native.dedupe_keys(pk) is None
-    pk2 = np.repeat(keys, 4, axis=0)                        # same multiset, prefix repeats
+    pk2 = np.repeat(keys, 8, axis=0)                        # same multiset, prefix repeats
     idx, nk = native.dedupe_keys(pk2)
-    assert nk == 600 and np.array_equal(idx, np.repeat(np.arange(600), 4))
+    assert nk == 300 and np.array_equal(idx, np.repeat(np.arange(300), 8))
+    assert native.dedupe_keys(np.repeat(keys, 7, axis=0)) is None   # 7 per key: plain path

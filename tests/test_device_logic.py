@@ -312,7 +312,7 @@ def test_halfsize_verify_logic_on_golden_corpus(host_harness, corpus, manifest):
     golden verdict: non-canonical / off-curve / small-order R, torsion keys, S >= L, carry loss."""
     H = host_harness
     bad = []
-    sc = (ctypes.c_uint32 * 65)()
+    sc = (ctypes.c_uint32 * 73)()          # CV_HS_DIGWORDS
     for i in range(len(corpus["pk"])):
         m = corpus["arena"][corpus["off"][i]:corpus["off"][i] + corpus["len"][i]].tobytes()
         st = ctypes.c_int(0)
