@@ -10,7 +10,9 @@
 
 // E = [v]R + [u]A + [w]B from the packed window digits (cv_verify.h), nw windows (uniform over the
 // wave); blo / bhi = k*B and k*2^128*B rows (row 0 = identity), tabA = k*(-A), tabR = k*R (cached).
-// Returns E == O on every lane of the quad.
+// W16: w's radix-2^16 digit pairs every fourth window from the CV_BW16 rows (as cv_hs_straus<.., true>),
+// else radix-256 digits every other window from CV_BCOMB.  Returns E == O on every lane of the quad.
+template <bool W16 = false>
 __device__ __forceinline__ bool cv_quad_hs_straus(const uint32_t *blo, const uint32_t *bhi, const uint32_t *dig,
                                                   size_t stride, const uint32_t *tabA, const uint32_t *tabR, int nw,
                                                   int r) {
@@ -31,10 +33,19 @@ __device__ __forceinline__ bool cv_quad_hs_straus(const uint32_t *blo, const uin
         quad_add(P, q, r);
         quad_cached_coord(q, tabA, cv_sfield(dw, 0, 5), r);
         quad_add(P, q, r);
-        if ((win & 1) == 0 && win < 32) {
-            quad_precomp_coord(q, blo, CV_BTAB_STRIDE, cv_sfield(dw, 10, 9), r, true);
+        if (W16 ? ((win & 3) == 0 && win < 32) : ((win & 1) == 0 && win < 32)) {
+            int dlo, dhi;
+            if (W16) {
+                const uint32_t bw = dig[(size_t)(CV_HS_BWORD + (win >> 2)) * stride];
+                dlo = (int)(int16_t)(bw & 0xffffu);
+                dhi = (int)bw >> 16;
+            } else {
+                dlo = cv_sfield(dw, 10, 9);
+                dhi = cv_sfield(dw, 19, 9);
+            }
+            quad_precomp_coord(q, blo, CV_BTAB_STRIDE, dlo, r, true);
             quad_add(P, q, r);
-            quad_precomp_coord(q, bhi, CV_BTAB_STRIDE, cv_sfield(dw, 19, 9), r, true);
+            quad_precomp_coord(q, bhi, CV_BTAB_STRIDE, dhi, r, true);
             quad_add(P, q, r);
         }
     }

@@ -12,7 +12,7 @@ __global__ __launch_bounds__(64, 1) void cv_scalars_lat_kernel(uint32_t n, uint3
                                                                const uint32_t *__restrict__ len,
                                                                uint32_t *__restrict__ ws_dig) {
     const uint32_t i = blockIdx.x * 64 + threadIdx.x;
-    if (i < n) cv_scalars_lane(i, cap, pk, sig, arena, off, len, ws_dig);
+    if (i < n) cv_scalars_lane<false, true>(i, cap, pk, sig, arena, off, len, ws_dig);
 }
 
 __global__ __launch_bounds__(64) void cv_points_pair_kernel(uint32_t n, const uint8_t *__restrict__ pk,
@@ -49,7 +49,8 @@ __global__ __launch_bounds__(64, 1) void cv_prep_lat_kernel(uint32_t n, uint32_t
         // the chunk's verdict words start at zero for the Straus kernel's atomicOr (it runs after this
         // launch on the same stream): one lane per word, instead of a separate memset launch
         if (i < n && (i & 63u) == 0) bitmap[i >> 6] = 0;
-        if (i < n) cv_scalars_lane<B16>(i, cap, pk, sig, arena, off, len, ws_dig);
+        // tri (B16): radix-16 halves of w; quad: the radix-2^16 pairs of the throughput group
+        if (i < n) cv_scalars_lane<B16, !B16>(i, cap, pk, sig, arena, off, len, ws_dig);
     }
 }
 
@@ -61,8 +62,8 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_quad_kernel(uint32_t n,
                                                                      const uint32_t *__restrict__ ws_tab,
                                                                      const uint32_t *__restrict__ ws_tabR,
                                                                      const uint8_t *__restrict__ ws_ok,
-                                                                     uint64_t *__restrict__ bitmap) {
-    constexpr int ROW = CV_BTAB_ENTRIES * CV_BTAB_STRIDE;
+                                                                     uint64_t *__restrict__ bitmap,
+                                                                     const uint32_t *__restrict__ bw16) {
     const uint32_t lane0 = blockIdx.x * CV_BLOCK + (threadIdx.x & ~63u);
     const uint32_t sig0 = lane0 >> 2;                        // first signature of this wave
     if (sig0 >= n) return;                                   // whole waves leave together
@@ -77,8 +78,9 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_quad_kernel(uint32_t n,
         nw = x > nw ? x : nw;
     }
     nw = __builtin_amdgcn_readfirstlane(nw);
-    const bool eq = cv_quad_hs_straus(CV_BCOMB, CV_BCOMB + 2 * ROW, ws_dig + i, cap, ws_tab + (size_t)i * CV_TAB_WORDS,
-                                      ws_tabR + (size_t)i * CV_TAB_WORDS, nw, r);
+    // w's radix-2^16 pairs against the CV_BW16 rows k*B (row 0) and k*2^128*B (row 2)
+    const bool eq = cv_quad_hs_straus<true>(bw16, bw16 + 2 * CV_BW16_ROW, ws_dig + i, cap,
+                                            ws_tab + (size_t)i * CV_TAB_WORDS, ws_tabR + (size_t)i * CV_TAB_WORDS, nw, r);
     const bool acc = eq && ws_ok[i] && i0 < n;
     const uint32_t bits = cv_quad_ballot_bits(__ballot(acc));
     if ((threadIdx.x & 63u) == 0 && bits)

@@ -192,8 +192,9 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
                       hipEvent_t *ev) {
     if (n == 0) return hipSuccess;
     if (ws_cap == 0 || ws_cap % 512) return hipErrorInvalidValue;
-    const uint32_t *bw16 = nullptr;            // the throughput group's basepoint rows
-    if (n > g_quad_max && g_verify_mode == 1) {
+    // the radix-2^16 basepoint rows, for the throughput (n > quad max) and quad (n > tri max) forms
+    const uint32_t *bw16 = nullptr;
+    if (g_verify_mode == 1 && (n > g_quad_max || n > g_tri_max)) {
         const hipError_t e = bw16_table(&bw16, stream);
         if (e != hipSuccess) return e;
     }
@@ -208,6 +209,7 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
             // 64-thread blocks: the few waves of a small batch spread over CUs (one per SIMD)
             const bool tri = m <= g_tri_max;
+            if (!tri && !bw16) return hipErrorInvalidValue;   // (cannot happen: fetched above)
             if (g_prep_lat_fused || tri) {
                 const uint32_t nbp = (2 * m + 63) / 64, nbs = (m + 63) / 64;
                 if (tri)
@@ -237,10 +239,11 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
                                    stream, m, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
             else
                 hipLaunchKernelGGL(cv_hs_straus_quad_kernel, dim3((4 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK),
-                                   0, stream, m, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
+                                   0, stream, m, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64, bw16);
             if (ev && c0 == 0) (void)hipEventRecord(ev[3], stream);
             continue;
         }
+        if (g_verify_mode == 1 && !bw16) return hipErrorInvalidValue;   // (cannot happen: fetched above)
         SplitAux *ax = nullptr;
         bool split = false;
         if (!lat && g_verify_mode == 1 && g_hs_fused && g_split_mode && !ev && m >= 131072) {
