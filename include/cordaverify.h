@@ -94,8 +94,9 @@ int cv_ed25519_verify_batch_keyed(cv_ctx *ctx, size_t n, size_t nkeys, const uin
                                   const uint8_t *sig, const uint8_t *msg_arena, const uint64_t *msg_off,
                                   const uint32_t *msg_len, uint64_t *verdict_bitmap, uint8_t *status);
 
-/* Per-device key-table pool capacity in keys (default 65536 = 256 MB of HBM per device); takes
- * effect at the next keyed call.  A pool that fills up is emptied before new keys go in. */
+/* Per-device key-table pool capacity in keys (default 16384 = 1.1 GB of HBM per device: 66 KB of
+ * comb tables per key); takes effect at the next keyed call.  A pool that fills up is emptied before
+ * new keys go in; a call with more distinct keys than the capacity grows the pool to fit them. */
 int cv_key_cache_reserve(cv_ctx *ctx, size_t max_keys);
 
 /* out4 = {resident keys, capacity, lookups that hit, lookups that missed} for `device`. */
