@@ -35,6 +35,7 @@ hipError_t cvk_prep_probe(uint32_t n, const uint8_t *pk, const uint8_t *sig, con
                           hipStream_t stream);
 hipError_t cvk_mad_clock(uint32_t iters, uint32_t blocks, uint64_t *out, hipStream_t stream);
 uint32_t cvk_get_tri_max(void);
+hipError_t cvk_prepare(hipStream_t stream);
 hipError_t cvk_keyprep(uint32_t nk, const uint8_t *keys, const uint32_t *slots, uint32_t *scratch, uint32_t *ktab_pool,
                        uint8_t *kok_pool, hipStream_t stream);
 hipError_t cvk_verify_keyed(uint32_t n, const uint8_t *keys, const uint32_t *key_index, const uint32_t *slot_of_key,
@@ -272,6 +273,12 @@ int cv_open(uint32_t device_mask, cv_ctx **out) {
                 return CV_E_HIP;
             }
             ctx->devs.push_back(dev);
+            // Per-device basepoint rows (16.8 MB, built once per process): eager, so the first
+            // verify is not charged for them and no later call synchronises to build them.
+            if (v == 0 && cvk_prepare(dev.stream) != hipSuccess) {
+                cv_close(ctx);
+                return CV_E_HIP;
+            }
         }
     }
     if (ctx->devs.empty()) {

@@ -182,6 +182,13 @@ static hipError_t bw16_table(const uint32_t **out, hipStream_t st) {
 
 extern "C" {
 
+// Build the current device's per-process tables now (cv_open calls this per device), so the first
+// verify pays no table build and no hipStreamSynchronize runs inside a later stream capture.
+hipError_t cvk_prepare(hipStream_t stream) {
+    const uint32_t *bw16 = nullptr;
+    return bw16_table(&bw16, stream);
+}
+
 // Verify n signatures with the workspace ws (capacity ws_cap signatures, a multiple of 512); the
 // batch is processed in chunks of ws_cap.  bitmap gets ceil(n/64) words.  ws_tab holds 2 * ws_cap
 // tables (k*(-A), then k*R for the half-size group); ws_dig CV_HS_DIGWORDS * ws_cap words.  ev phases: prep | straus | finish, or in the

@@ -67,7 +67,9 @@ extern "C" {
 
 typedef struct cv_ctx cv_ctx;
 
-/* Open a context on the devices in device_mask (bit d = HIP device ordinal d; 0 = all devices). */
+/* Open a context on the devices in device_mask (bit d = HIP device ordinal d; 0 = all devices).
+ * The first open on a device also builds that device's basepoint rows (16.8 MB, kept for the
+ * process lifetime, shared by every context), so it takes a few milliseconds longer. */
 int cv_open(uint32_t device_mask, cv_ctx **out);
 void cv_close(cv_ctx *ctx);
 const char *cv_strerror(int code);
