@@ -168,8 +168,10 @@ constexpr size_t kTabBytes = 9 * 40 * 4;  // CV_TAB_WORDS: k*P, k = 0..8, cached
 // 66 KB of tables cost about as much as 7 plain verifies to build; cached keys cost nothing)
 constexpr size_t kAutoKeyedMax = 1u << 18;
 
-// Verify workspace capacity: batches above it run in chunks of this many signatures.
-constexpr uint32_t kVerifyChunk = 1u << 21;
+// Verify workspace capacity: batches above it run in chunks of this many signatures (~13.4 GB of
+// workspace at 2^22; same-box A/B at 8M signatures: 2^21 73.2, 2^22 72.4, 2^23 72.4 ms -- fewer
+// chunk tails to drain; whole-round chunks of 1,966,080 were slower, 73.4 ms).
+constexpr uint32_t kVerifyChunk = 1u << 22;
 
 hipError_t ensure_verify_ws(Device &d, size_t n) {
     uint32_t want = (uint32_t)std::min<size_t>(kVerifyChunk, (n + 511) / 512 * 512);

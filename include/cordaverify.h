@@ -201,7 +201,7 @@ int cv_calibrate(cv_ctx *ctx, int device, double *mad_per_s, double *femul_per_s
 int cv_calibrate_cycles(cv_ctx *ctx, int device, double *out);
 
 /* Diagnostics (no reference counterpart): shader cycles per wave of each phase of the throughput
- * prep kernel on a device-resident batch (n <= 2^21) — out[8] = {hash, lattice, digits, decode
+ * prep kernel on a device-resident batch (n <= 2^22) — out[8] = {hash, lattice, digits, decode
  * A+R, tables, total, waves, SHA-512 part of hash}.  Writes the device's verify workspace; not thread-safe with verifies
  * on the same device. */
 int cv_diag_prep_phases(cv_ctx *ctx, int device, size_t n, const void *d_pk, const void *d_sig,

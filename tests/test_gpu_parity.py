@@ -371,11 +371,11 @@ def test_full_width_and_half_size_schedules_agree(engine, corpus, oracle_c, mode
 
 
 @pytest.mark.parametrize("mode,n", [(0, 200_003), (1, 200_003), (2, 200_003), (3, 200_003),
-                                    (3, (1 << 21) + 200_003), (1, (1 << 21) + 200_003)])
+                                    (3, (1 << 22) + 200_003), (1, (1 << 22) + 200_003)])
 def test_split_launch_plans_agree(engine, corpus, mode, n):
     """The two-stream sub-chunk plan (internal switch cvk_set_split_mode: 0 off, 1 concurrent, 2 tail
     after head prep, 3 auto) over the golden corpus tiled to a ragged n through the device API — at
-    2^21 + 200,003 the batch is two workspace chunks and only the second one's last round is
+    2^22 + 200,003 the batch is two workspace chunks and only the second one's last round is
     near-empty: every verdict and key-status byte follows its record, bits past n stay clear."""
     import ctypes
     import torch
