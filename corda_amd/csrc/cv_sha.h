@@ -87,6 +87,21 @@ CV_HD uint32_t cv_funnel32(uint32_t hi, uint32_t lo, uint32_t sh) {
 #endif
 }
 CV_HD uint32_t cv_ror32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+// Three-input bitwise functions in one v_bitop3_b32 per 32 bits (truth table indexed by
+// S0<<2 | S1<<1 | S2): xor3 0x96, choose (x ? y : z) 0xCA, majority 0xE8.  The compiler emits two or
+// three two-input ops for each otherwise (and does not fuse the 64-bit forms at all).
+template <int TT> CV_HD uint32_t cv_bitop3(uint32_t a, uint32_t b, uint32_t c) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_bitop3_b32(a, b, c, TT);
+#else
+    return TT == 0x96 ? a ^ b ^ c : TT == 0xCA ? (a & b) | (~a & c) : (a & b) | (a & c) | (b & c);
+#endif
+}
+CV_HD uint32_t cv_xor3(uint32_t a, uint32_t b, uint32_t c) { return cv_bitop3<0x96>(a, b, c); }
+template <int TT> CV_HD uint64_t cv_bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
+    return (uint64_t)cv_bitop3<TT>((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32 |
+           cv_bitop3<TT>((uint32_t)a, (uint32_t)b, (uint32_t)c);
+}
 CV_HD uint32_t cv_bswap32(uint32_t x) {
     return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
 }
@@ -109,8 +124,8 @@ CV_HD void sha512_init(uint64_t st[8]) {
 #define CV_S512_SSIG1(x) (cv_rotr64<19>(x) ^ cv_rotr64<61>(x) ^ ((x) >> 6))
 #define CV_S512_ROUND(a, b, c, d, e, f, g, h, kw)                                                     \
     {                                                                                             \
-        const uint64_t t1_ = (h) + CV_S512_BSIG1(e) + (((e) & (f)) ^ (~(e) & (g))) + (kw);           \
-        const uint64_t t2_ = CV_S512_BSIG0(a) + (((a) & (b)) ^ ((a) & (c)) ^ ((b) & (c)));           \
+        const uint64_t t1_ = (h) + CV_S512_BSIG1(e) + cv_bitop3_64<0xCA>((e), (f), (g)) + (kw);      \
+        const uint64_t t2_ = CV_S512_BSIG0(a) + cv_bitop3_64<0xE8>((a), (b), (c));                  \
         (d) += t1_;                                                                               \
         (h) = t1_ + t2_;                                                                          \
     }
@@ -168,20 +183,24 @@ CV_HD uint32_t msg_dword_le(const uint8_t *msg, uint32_t mlen, uint32_t t) {
 // of the caller) — and a lane with no message byte in the window reads nothing, so a message that
 // ends at the very end of an allocation is never read past (the same guarantee as msg_dword_le).
 // One branch per block instead of two conditional loads per dword.
-CV_HD void sha512_msg_window(uint32_t dw[33], const uint8_t *msg, uint32_t mlen, uint32_t tstart) {
+template <int K>
+CV_HD void cv_msg_window(uint32_t dw[K], const uint8_t *msg, uint32_t mlen, uint32_t tstart) {
     const uint32_t sh = (uint32_t)((uintptr_t)msg & 3u);              // tstart is a multiple of 4
     const uint32_t rem = mlen > tstart ? mlen - tstart + sh : 0u;     // message bytes from the window base
-    const uint32_t kmax = rem >= 132 ? 33u : (rem + 3) >> 2;          // dwords holding message bytes
+    const uint32_t kmax = rem >= 4u * K ? (uint32_t)K : (rem + 3) >> 2; // dwords holding message bytes
 #pragma unroll
-    for (int k = 0; k < 33; k++) dw[k] = 0;
+    for (int k = 0; k < K; k++) dw[k] = 0;
     if (kmax > 0) {
         const uint32_t *p = reinterpret_cast<const uint32_t *>(msg + tstart - sh);
 #pragma unroll
-        for (int k = 0; k < 33; k++) {
+        for (int k = 0; k < K; k++) {
             const uint32_t kk = (uint32_t)k < kmax ? (uint32_t)k : kmax - 1;
             dw[k] = p[kk];
         }
     }
+}
+CV_HD void sha512_msg_window(uint32_t dw[33], const uint8_t *msg, uint32_t mlen, uint32_t tstart) {
+    cv_msg_window<33>(dw, msg, mlen, tstart);
 }
 
 // The 16 schedule words of SHA-512 block `blk` of pre[0:NPRE] || msg[0:mlen] || padding || length.
@@ -265,41 +284,51 @@ CV_HD void sha256_init(uint32_t st[8]) {
 
 __host__ __device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16]) {
     uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-#pragma unroll 16
+#pragma unroll
     for (int i = 0; i < 64; i++) {
         uint32_t wi;
         if (i < 16) {
             wi = w[i & 15];
         } else {
             const uint32_t x15 = w[(i - 15) & 15], x2 = w[(i - 2) & 15];
-            const uint32_t s0 = cv_ror32(x15, 7) ^ cv_ror32(x15, 18) ^ (x15 >> 3);
-            const uint32_t s1 = cv_ror32(x2, 17) ^ cv_ror32(x2, 19) ^ (x2 >> 10);
+            const uint32_t s0 = cv_xor3(cv_ror32(x15, 7), cv_ror32(x15, 18), x15 >> 3);
+            const uint32_t s1 = cv_xor3(cv_ror32(x2, 17), cv_ror32(x2, 19), x2 >> 10);
             wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
             w[i & 15] = wi;
         }
-        const uint32_t t1 = h + (cv_ror32(e, 6) ^ cv_ror32(e, 11) ^ cv_ror32(e, 25)) + ((e & f) ^ (~e & g)) +
+        const uint32_t t1 = h + cv_xor3(cv_ror32(e, 6), cv_ror32(e, 11), cv_ror32(e, 25)) + ((e & f) ^ (~e & g)) +
                             cv_k256(i) + wi;
-        const uint32_t t2 = (cv_ror32(a, 2) ^ cv_ror32(a, 13) ^ cv_ror32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+        const uint32_t t2 = cv_xor3(cv_ror32(a, 2), cv_ror32(a, 13), cv_ror32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
         h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
     }
     st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
 // SHA-256 of an arbitrary byte string in device memory; out = 8 big-endian state words.
-// Message words come from aligned dword loads (msg_dword_le, which also inserts the 0x80 pad).
+// Per 64-byte block the message comes from one window of 17 aligned dwords (cv_msg_window: one
+// branch per block, nothing read past the last message byte), funnel-shifted into the 16 schedule
+// words, with msg_dword_le's padding rules applied branch-free.
 __host__ __device__ __forceinline__ void sha256_bytes(uint32_t out[8], const uint8_t *p, uint32_t n) {
     uint32_t st[8];
     sha256_init(st);
     const uint32_t nblocks = (n + 1 + 8 + 63) / 64;
     const uint32_t total = nblocks * 64;
     const uint64_t bits = (uint64_t)n * 8;
+    const uint32_t sh8 = 8u * (uint32_t)((uintptr_t)p & 3u);
 #pragma nounroll
     for (uint32_t blk = 0; blk < nblocks; blk++) {
-        uint32_t w[16];
+        uint32_t dw[17], w[16];
+        cv_msg_window<17>(dw, p, n, blk * 64);
 #pragma unroll
         for (int j = 0; j < 16; j++) {
             const uint32_t u = blk * 64 + 4 * j;
-            uint32_t v = cv_bswap32(msg_dword_le(p, n, u));
+            uint32_t le = cv_funnel32(dw[j + 1], dw[j], sh8);
+            const uint32_t valid = n - u;                            // message bytes left at u
+            const uint32_t keep = valid >= 4 ? 0xffffffffu : ((1u << (8 * (valid & 3u))) - 1u);
+            const uint32_t pad = valid >= 4 ? 0u : (0x80u << (8 * (valid & 3u)));
+            le = (le & keep) | pad;
+            if (u > n) le = 0;
+            uint32_t v = cv_bswap32(le);
             if (u == total - 8) v = (uint32_t)(bits >> 32);
             if (u == total - 4) v = (uint32_t)bits;
             w[j] = v;

@@ -181,7 +181,7 @@ def test_sha512_and_sha256(host_harness):
     import hashlib
     H = host_harness
     rng = random.Random(7)
-    for ln in [0, 1, 31, 47, 48, 49, 63, 64, 111, 112, 113, 127, 128, 200, 300, 1000]:
+    for ln in [0, 1, 31, 47, 48, 49, 55, 56, 57, 63, 64, 111, 112, 113, 119, 120, 121, 127, 128, 200, 300, 1000]:
         pre = bytes(rng.randrange(256) for _ in range(64))
         m = bytes(rng.randrange(256) for _ in range(ln))
         o = _out(64)
@@ -196,6 +196,8 @@ def test_sha512_and_sha256(host_harness):
             buf = (ctypes.c_uint8 * (ln + 16)).from_buffer_copy(bytes(shift) + m + bytes(16 - shift))
             H.cvh_sha512(_b(pre), 64, ctypes.byref(buf, shift), ln, o)
             assert bytes(o) == hashlib.sha512(pre + m).digest()
+            H.cvh_sha256(ctypes.byref(buf, shift), ln, o2)
+            assert bytes(o2) == hashlib.sha256(m).digest()
 
 
 def test_verify_logic_on_golden_corpus(host_harness, corpus, manifest):
