@@ -23,15 +23,46 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_sign_kernel(
 }
 
 // ---------------------------------------------------------------- Merkle tx ids
-__global__ __launch_bounds__(CV_BLOCK) void cv_leaf_hash_kernel(uint32_t nleaves, const uint8_t *__restrict__ arena,
-                                                                const uint64_t *__restrict__ off,
-                                                                const uint32_t *__restrict__ len,
-                                                                uint32_t *__restrict__ leaf_digest) {
-    const uint32_t gid = blockIdx.x * CV_BLOCK + threadIdx.x;
-    if (gid >= nleaves) return;
+// One lane per leaf.  A lane runs as many SHA-256 blocks as its leaf needs and a wave as many as its
+// longest leaf, so each workgroup of CV_LEAF_BLOCK consecutive leaves first orders them by block
+// count (counting sort in LDS: one LDS atomic per leaf, one wave scan) and lane t hashes the t-th
+// shortest: every wave then holds leaves of similar length while the workgroup's leaves stay one
+// contiguous stretch of the arena.  Digests go to each leaf's own index, so the order is invisible.
+__global__ __launch_bounds__(CV_LEAF_BLOCK) void cv_leaf_hash_kernel(uint32_t nleaves, const uint8_t *__restrict__ arena,
+                                                                     const uint64_t *__restrict__ off,
+                                                                     const uint32_t *__restrict__ len,
+                                                                     uint32_t *__restrict__ leaf_digest) {
+    __shared__ uint32_t hist[64], base[64], perm[CV_LEAF_BLOCK];
+    const uint32_t t = threadIdx.x, first = blockIdx.x * CV_LEAF_BLOCK;
+    const uint32_t gid = first + t;
+    const uint32_t nlive = nleaves - first < CV_LEAF_BLOCK ? nleaves - first : CV_LEAF_BLOCK;
+    if (t < 64) hist[t] = 0;
+    __syncthreads();
+    uint32_t bucket = 0, pos = 0;
+    if (t < nlive) {
+        const uint32_t nb = (len[gid] + 9u + 63u) / 64u;           // SHA-256 blocks of this leaf
+        bucket = nb < 63u ? nb : 63u;
+        pos = atomicAdd(&hist[bucket], 1u);
+    }
+    __syncthreads();
+    if (t < 64) {                                                 // exclusive scan, one wave
+        const uint32_t own = hist[t];
+        uint32_t inc = own;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d, 64);
+            if ((int)t >= d) inc += y;
+        }
+        base[t] = inc - own;
+    }
+    __syncthreads();
+    if (t < nlive) perm[base[bucket] + pos] = gid;
+    __syncthreads();
+    if (t >= nlive) return;
+    const uint32_t leaf = perm[t];
     uint32_t d[8];
-    sha256_bytes(d, arena + off[gid], len[gid]);
-    uint4 *o = reinterpret_cast<uint4 *>(leaf_digest + (size_t)gid * 8);
+    sha256_bytes(d, arena + off[leaf], len[leaf]);
+    uint4 *o = reinterpret_cast<uint4 *>(leaf_digest + (size_t)leaf * 8);
     o[0] = make_uint4(d[0], d[1], d[2], d[3]);
     o[1] = make_uint4(d[4], d[5], d[6], d[7]);
 }

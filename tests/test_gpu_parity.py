@@ -174,6 +174,9 @@ def test_merkle_random_vs_oracle(engine, oracle_c):
     begin[1:] = np.cumsum(counts)
     nl = int(begin[-1])
     lens = rng.integers(0, 700, nl).astype(np.uint32)
+    # leaves past the leaf kernel's last length bucket (>= 63 SHA-256 blocks) mixed in: workgroups
+    # order their leaves by block count, so every bucket and a ragged last workgroup must hash right
+    lens[::97] = rng.integers(3900, 9000, lens[::97].size).astype(np.uint32)
     off = np.zeros(nl, np.uint64)
     off[1:] = np.cumsum(lens[:-1])
     arena = rng.integers(0, 256, int(lens.sum()) + 16, dtype=np.uint8)
