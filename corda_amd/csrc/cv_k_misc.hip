@@ -24,25 +24,32 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_sign_kernel(
 
 // ---------------------------------------------------------------- Merkle tx ids
 // One lane per leaf.  A lane runs as many SHA-256 blocks as its leaf needs and a wave as many as its
-// longest leaf, so each workgroup of CV_LEAF_BLOCK consecutive leaves first orders them by block
-// count (counting sort in LDS: one LDS atomic per leaf, one wave scan) and lane t hashes the t-th
-// shortest: every wave then holds leaves of similar length while the workgroup's leaves stay one
-// contiguous stretch of the arena.  Digests go to each leaf's own index, so the order is invisible.
+// longest leaf, so each workgroup takes CV_LEAF_SPAN consecutive leaves, orders them by block count
+// (counting sort in LDS: one LDS atomic per leaf, one wave scan) and hashes them in CV_LEAF_SPAN /
+// CV_LEAF_BLOCK passes, lane t of pass p taking the (p * CV_LEAF_BLOCK + t)-th shortest: every wave
+// then holds leaves of similar length while the workgroup's leaves stay one contiguous stretch of
+// the arena.  Digests go to each leaf's own index, so the order is invisible.
 __global__ __launch_bounds__(CV_LEAF_BLOCK) void cv_leaf_hash_kernel(uint32_t nleaves, const uint8_t *__restrict__ arena,
                                                                      const uint64_t *__restrict__ off,
                                                                      const uint32_t *__restrict__ len,
                                                                      uint32_t *__restrict__ leaf_digest) {
-    __shared__ uint32_t hist[64], base[64], perm[CV_LEAF_BLOCK];
-    const uint32_t t = threadIdx.x, first = blockIdx.x * CV_LEAF_BLOCK;
-    const uint32_t gid = first + t;
-    const uint32_t nlive = nleaves - first < CV_LEAF_BLOCK ? nleaves - first : CV_LEAF_BLOCK;
+    constexpr uint32_t PASSES = CV_LEAF_SPAN / CV_LEAF_BLOCK;
+    __shared__ uint32_t hist[64], base[64], perm[CV_LEAF_SPAN];
+    const uint32_t t = threadIdx.x, first = blockIdx.x * CV_LEAF_SPAN;
+    const uint32_t nlive = nleaves - first < CV_LEAF_SPAN ? nleaves - first : CV_LEAF_SPAN;
     if (t < 64) hist[t] = 0;
     __syncthreads();
-    uint32_t bucket = 0, pos = 0;
-    if (t < nlive) {
-        const uint32_t nb = (len[gid] + 9u + 63u) / 64u;           // SHA-256 blocks of this leaf
-        bucket = nb < 63u ? nb : 63u;
-        pos = atomicAdd(&hist[bucket], 1u);
+    uint32_t bucket[PASSES], pos[PASSES];
+#pragma unroll
+    for (uint32_t k = 0; k < PASSES; k++) {
+        const uint32_t j = k * CV_LEAF_BLOCK + t;
+        bucket[k] = 0;
+        pos[k] = 0;
+        if (j < nlive) {
+            const uint32_t nb = (len[first + j] + 9u + 63u) / 64u;   // SHA-256 blocks of this leaf
+            bucket[k] = nb < 63u ? nb : 63u;
+            pos[k] = atomicAdd(&hist[bucket[k]], 1u);
+        }
     }
     __syncthreads();
     if (t < 64) {                                                 // exclusive scan, one wave
@@ -56,15 +63,23 @@ __global__ __launch_bounds__(CV_LEAF_BLOCK) void cv_leaf_hash_kernel(uint32_t nl
         base[t] = inc - own;
     }
     __syncthreads();
-    if (t < nlive) perm[base[bucket] + pos] = gid;
+#pragma unroll
+    for (uint32_t k = 0; k < PASSES; k++) {
+        const uint32_t j = k * CV_LEAF_BLOCK + t;
+        if (j < nlive) perm[base[bucket[k]] + pos[k]] = first + j;
+    }
     __syncthreads();
-    if (t >= nlive) return;
-    const uint32_t leaf = perm[t];
-    uint32_t d[8];
-    sha256_bytes(d, arena + off[leaf], len[leaf]);
-    uint4 *o = reinterpret_cast<uint4 *>(leaf_digest + (size_t)leaf * 8);
-    o[0] = make_uint4(d[0], d[1], d[2], d[3]);
-    o[1] = make_uint4(d[4], d[5], d[6], d[7]);
+#pragma nounroll
+    for (uint32_t k = 0; k < PASSES; k++) {
+        const uint32_t j = k * CV_LEAF_BLOCK + t;
+        if (j >= nlive) break;
+        const uint32_t leaf = perm[j];
+        uint32_t d[8];
+        sha256_bytes(d, arena + off[leaf], len[leaf]);
+        uint4 *o = reinterpret_cast<uint4 *>(leaf_digest + (size_t)leaf * 8);
+        o[0] = make_uint4(d[0], d[1], d[2], d[3]);
+        o[1] = make_uint4(d[4], d[5], d[6], d[7]);
+    }
 }
 
 // one lane per transaction, in place over its leaf digests; ids are written as digest bytes

@@ -439,7 +439,7 @@ hipError_t cvk_merkle(uint32_t ntx, uint32_t nleaves, const uint8_t *arena, cons
                       const uint32_t *leaf_len, const uint32_t *tx_begin, uint32_t *leaf_digest, uint8_t *ids,
                       uint8_t *status, hipStream_t stream) {
     if (nleaves) {
-        hipLaunchKernelGGL(cv_leaf_hash_kernel, dim3((nleaves + CV_LEAF_BLOCK - 1) / CV_LEAF_BLOCK), dim3(CV_LEAF_BLOCK), 0, stream,
+        hipLaunchKernelGGL(cv_leaf_hash_kernel, dim3((nleaves + CV_LEAF_SPAN - 1) / CV_LEAF_SPAN), dim3(CV_LEAF_BLOCK), 0, stream,
                            nleaves, arena, leaf_off, leaf_len, leaf_digest);
     }
     if (ntx) {
