@@ -77,13 +77,55 @@ def log(*a):
 def pmc_traffic(n: int, hs: bool):
     """HBM bytes per launch of the dominant kernel from the committed PMC pass (profiles/pmc_hs_straus.json
     or pmc_straus.json, written by scripts/pmc.sh + tools/pmc_summary.py on the same build and
-    workload), scaled to n."""
-    p = os.path.join(REPO, "profiles", "pmc_hs_straus.json" if hs else "pmc_straus.json")
+    workload), scaled to n.  Returns (bytes, provenance): the figure is a committed measurement, not one
+    taken in this run (PMC counters need their own rocprofv3 pass)."""
+    name = "pmc_hs_straus.json" if hs else "pmc_straus.json"
+    p = os.path.join(REPO, "profiles", name)
     if not os.path.exists(p):
-        return None
+        return None, None
     with open(p) as f:
         d = json.load(f)
-    return d["hbm_bytes_per_launch"] * n / d["n"]
+    src = (f"profiles/{name}: FETCH_SIZE+WRITE_SIZE of one {d['n']}-signature launch "
+           f"({d.get('build', 'build of that commit')}), scaled to n; not measured in this run")
+    return d["hbm_bytes_per_launch"] * n / d["n"], src
+
+
+def pcie_h2d_probe(dev, mb: int = 256, reps: int = 5) -> float:
+    """Host-to-device copy rate from pinned memory (GB/s, best of reps): the ceiling of the host-buffer
+    path's input DMA."""
+    h = torch.empty(mb << 20, dtype=torch.uint8, pin_memory=True)
+    d = torch.empty(mb << 20, dtype=torch.uint8, device=dev)
+    best = 0.0
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        d.copy_(h, non_blocking=True)
+        e1.record()
+        e1.synchronize()
+        best = max(best, (mb << 20) / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+    return best
+
+
+def host_api_rate(eng, batch, steps: int, device_value: float, name: str):
+    """The drop-in path: the same batch handed over as host numpy buffers to
+    cv_ed25519_verify_batch — what the JVM shim calls for SignedTransaction.checkSignaturesAreValid
+    (SignedTransaction.kt:82-87) and the resolve loop (ResolveTransactionsFlow.kt:105-111).  Each step =
+    one synchronous call: pinned staging packed by host threads, DMA, kernels, bitmap back, pipelined
+    over sub-chunks inside the call.  value = signatures / wall time of the K calls."""
+    pk, sig, arena, off, ln = batch.to_host()
+    n = batch.n
+    in_bytes = pk.nbytes + sig.nbytes + off.nbytes + ln.nbytes + int(ln.astype(np.int64).sum())
+    bm, _ = eng.verify_batch(pk, sig, arena, off, ln, want_status=False)     # warm: staging allocated
+    t = time.perf_counter()
+    for _ in range(steps):
+        bm, _ = eng.verify_batch(pk, sig, arena, off, ln, want_status=False)
+    dt = time.perf_counter() - t
+    assert native.bitmap_to_bools(bm, n).all(), "host API rejected an honest signature"
+    v = n * steps / dt
+    return {"workload": name, "value": v, "unit": "verifies/s", "ms_per_step": dt / steps * 1e3, "steps": steps,
+            "sigs": n, "ratio_to_device_value": v / device_value, "device_value": device_value,
+            "input_bytes_per_call": in_bytes, "input_gb_per_s": in_bytes * steps / dt / 1e9,
+            "path": "cv_ed25519_verify_batch from pageable numpy buffers (pinned staging, pipelined sub-chunks)"}
 
 
 def affinity_cores() -> int:
@@ -138,6 +180,10 @@ def cpu_baseline(batch, rank_device: int, seconds: float):
     ratem = ns / (time.perf_counter() - t)
     return {"value": ratem, "unit": "verifies/s", "cores": threads, "kind": "port",
             "single_thread_value": rate1, "jvm_probe": jvm_probe(), "affinity_cores": affinity_cores(),
+            "extrapolated_all_cores": rate1 * affinity_cores(),
+            "extrapolated_all_cores_note": "EXTRAPOLATION, not measured: single_thread_value x affinity_cores "
+                                           "(BASELINE.md: nproc threads, extrapolated per core); the box grants "
+                                           "this process an OMP_NUM_THREADS share, which `value` is measured on",
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
             "sample": f"first {ns} signatures of the same batch ({batch.msg_len}-byte msgs) on {threads} host "
                       f"threads; single-thread rate from the first {n1}",
@@ -200,6 +246,12 @@ def notary_latency(eng, device: int, n: int, reps: int, cpu: bool, key_pool=None
         assert np.array_equal(v.astype(bool), expect)
         out["cpu_p50_ms"] = float(np.median(cl) * 1e3)
         out["cpu_threads"] = threads
+        t = time.perf_counter()
+        cv_oracle.verify_batch(pk[:512], sig[:512], arena, off[:512], ln[:512], 1)
+        per_sig = (time.perf_counter() - t) / 512
+        out["cpu_extrapolated_all_cores_ms"] = per_sig * n / affinity_cores() * 1e3
+        out["cpu_extrapolated_note"] = (f"EXTRAPOLATION: 1-thread time per signature x {n} / {affinity_cores()} "
+                                        "affinity cores (perfect scaling assumed)")
     return out
 
 
@@ -363,7 +415,7 @@ def c3_line(eng, local, rank, world, sh, dev, ntx, steps, warmup, mad_rate):
             "roofline": straus_roofline(eng, local, r["n"], float(ph[2]), float(ph.sum()), mad_rate)}
 
 
-def c5_line(eng, local, rank, sh, dev, n, steps, mad_rate):
+def c5_line(eng, local, rank, sh, dev, n, steps, mad_rate, host_api: bool = True):
     """C5 (BASELINE.json configs[4]) single-GPU shard: n single-signer signatures over 32-byte tx ids,
     verified in the engine's 2M-signature workspace chunks."""
     t0 = time.perf_counter()
@@ -380,8 +432,9 @@ def c5_line(eng, local, rank, sh, dev, n, steps, mad_rate):
     el = time.perf_counter() - t0
     assert bool((bm == -1).all()) or n % 64, "C5: verify rejected an honest signature"
     ph = np.mean(np.array([eng.verify_device_timed(local, n, *a, sh) for _ in range(2)]), axis=0)
+    host = host_api_rate(eng, b, 2, n * steps / el, CONFIG_NAME["c5"] + " (host buffers)") if host_api else None
     del b
-    return {"workload": CONFIG_NAME["c5"], "value": n * steps / el, "unit": "verifies/s",
+    return {"workload": CONFIG_NAME["c5"], "value": n * steps / el, "unit": "verifies/s", "host_api": host,
             "ms_per_step": el / steps * 1e3, "steps": steps, "sigs_per_gpu": n,
             "tx_ids_per_s": n * steps / el, "tx_ids_note": "single-signer: one tx id per signature",
             "phase_ms": {"scalars": float(ph[0]), "points": float(ph[1]), "hs_straus": float(ph[2])},
@@ -401,6 +454,9 @@ def main():
     ap.add_argument("--no-notary", action="store_true")
     ap.add_argument("--no-keyed", action="store_true")
     ap.add_argument("--no-sub", action="store_true", help="skip the C3 / C5-shard sub-lines")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-buffer (drop-in) sub-lines")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="device streams the K timed steps are dealt over (each its own workspace slot)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -448,33 +504,50 @@ def main():
                                 key_pool=args.key_pool or None, stream=sh)
     log(f"[rank {rank}] generated {n} signatures on GPU in {time.perf_counter() - t0:.2f}s")
     words = (n + 63) // 64
-    bitmap = torch.zeros(words, dtype=torch.int64, device=dev)
     if world > 1:
         assert n % 64 == 0, "per-GPU shard must be whole bitmap words"
+    # Steps are independent batches (a node's concurrent verify calls): step k goes on streams[k % S],
+    # each stream with its own bitmap; the engine gives each stream its own workspace slot, so step k+1's
+    # prep runs while step k's last Straus round drains.  Every step is a full verify of all n signatures.
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(max(1, args.streams) - 1)]
+    bitmaps = [torch.zeros(words, dtype=torch.int64, device=dev) for _ in streams]
+    bitmap = bitmaps[0]
 
-    def step():
+    def step(k, ns=len(streams)):
+        st, bm = streams[k % ns], bitmaps[k % ns]
         eng.verify_device(local, n, batch.pk.data_ptr(), batch.sig.data_ptr(), batch.arena.data_ptr(),
-                          batch.off.data_ptr(), batch.len.data_ptr(), bitmap.data_ptr(), 0, sh)
+                          batch.off.data_ptr(), batch.len.data_ptr(), bm.data_ptr(), 0, st.cuda_stream)
         if world > 1:
-            return D.gather_bitmap(bitmap, world * n)
-        return bitmap
+            with torch.cuda.stream(st):                       # the gather waits for this step's verify only
+                return D.gather_bitmap(bm, world * n)
+        return bm
 
-    for _ in range(args.warmup):
-        step()
+    def timed(ns):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        out = None
+        for k in range(args.steps):
+            out = step(k, ns)                                 # N>1: RCCL all-gather into the commit step
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        return time.perf_counter() - t0, out
+
+    for k in range(args.warmup):
+        step(k)
     torch.cuda.synchronize(dev)
 
-    # Timed region: K production verify calls on `stream` (the engine's own launch plan, incl. the
-    # two-stream sub-chunk overlap it picks for near-empty last rounds), stream-ordered, one sync at the end.
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        gathered = step()                                     # N>1: RCCL all-gather into the commit step
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    # Timed region: K production verify calls dealt over the streams (the engine's own launch plan,
+    # incl. the drain-overlap sub-chunks it picks for near-empty last rounds), one sync at the end.
+    elapsed, gathered = timed(len(streams))
+    serial_elapsed, _ = timed(1) if len(streams) > 1 else (elapsed, None)
+    full = torch.full_like(bitmap, -1)
+    if n % 64:
+        full[-1] = (1 << (n % 64)) - 1
+    for bm in bitmaps:
+        assert torch.equal(bm, full), "verify rejected an honest signature"
     prod_bitmap = bitmap.clone()
     # Roofline: K more calls of the same batch as whole-chunk launches, timed kernel by kernel with HIP
     # events recorded on `stream` between the launches (cv_ed25519_verify_device_timed waits for the last).
@@ -486,17 +559,14 @@ def main():
     torch.cuda.synchronize(dev)
     assert torch.equal(prod_bitmap, bitmap), "production and timed launch plans disagree"
     # correctness of the timed configuration: every generated signature is honest
-    full = torch.full_like(bitmap, -1)
-    if n % 64:
-        full[-1] = (1 << (n % 64)) - 1
     assert torch.equal(bitmap, full), "verify rejected an honest signature"
     ph = np.mean(np.array(phases), axis=0)
     hs = native.verify_mode() == 1
     kern_ms, straus_ms = float(ph.sum()), float(ph[2] if hs else ph[1])
     if world > 1:
-        tt = torch.tensor([elapsed, kern_ms, straus_ms], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed, kern_ms, straus_ms, serial_elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms, straus_ms = float(tt[0]), float(tt[1]), float(tt[2])
+        elapsed, kern_ms, straus_ms, serial_elapsed = float(tt[0]), float(tt[1]), float(tt[2]), float(tt[3])
         assert torch.equal(gathered.view(world, words)[rank], bitmap)
         assert bool((gathered == -1).all()), "a rank rejected an honest signature"
     value = world * n * args.steps / elapsed
@@ -533,9 +603,13 @@ def main():
             "data": "synthetic (keys, messages, signatures generated on-GPU from seeded RNG, RFC 8032 signing)",
             "config": {"workload": CONFIG_NAME[args.config], "sigs_per_gpu": n, "msg_bytes": msg_len,
                        "key_pool": args.key_pool or "distinct", "parallelism": f"shard-by-signature x{world}",
+                       "device_streams": len(streams),
                        "collective": "RCCL all_gather of verdict bitmaps" if world > 1 else "none"},
+            "single_stream_ms_per_step": serial_elapsed / args.steps * 1e3,
+            "single_stream_value": world * n * args.steps / serial_elapsed,
             "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": mad_rate / 1e12, "unit": "Tmac/s",
-                         "frac": achieved / mad_rate, "traffic": pmc_traffic(n, hs),
+                         "frac": achieved / mad_rate, "traffic": pmc_traffic(n, hs)[0],
+                         "traffic_source": pmc_traffic(n, hs)[1],
                          "kernel": kname, "kernel_ms": straus_ms, "work_per_unit": wdesc,
                          "phase_ms": phase_ms,
                          "group": {"kernels": gname, "kernel_ms": kern_ms,
@@ -551,10 +625,17 @@ def main():
                     "over the same calibration launch"}
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(batch, local, args.cpu_seconds)
+        if world == 1 and not args.no_host:
+            result["host_api"] = {"c2": host_api_rate(eng, batch, max(3, args.steps // 2), value,
+                                                      CONFIG_NAME[args.config] + " (host buffers)"),
+                                  "pcie_h2d_gb_per_s_pinned": pcie_h2d_probe(dev)}
         if world == 1 and not args.no_sub:
             del batch
             result["c3"] = c3_line(eng, local, rank, world, sh, dev, 1_000_000, 3, 1, mad_rate)
-            result["c5_shard"] = c5_line(eng, local, rank, sh, dev, 8_000_000, 3, mad_rate)
+            result["c5_shard"] = c5_line(eng, local, rank, sh, dev, 8_000_000, 3, mad_rate,
+                                         host_api=not args.no_host)
+            if result["c5_shard"].get("host_api") and "host_api" in result:
+                result["host_api"]["c5"] = result["c5_shard"]["host_api"]
         if not args.no_keyed and world == 1:
             result["keyed"] = keyed_rate(eng, local, n, msg_len, max(3, args.steps // 2), sh)
         if not args.no_notary:

@@ -1,6 +1,6 @@
-// cv_api.cpp — the C-ABI (include/cordaverify.h): contexts, per-device workspaces, host-buffer
-// batches sharded over the context's GPUs (one host thread + one HIP stream per device), and the
-// device-resident entry points used by bench.py.
+// cv_api.cpp — the C-ABI (include/cordaverify.h): contexts, per-device verify workspace slots, host-buffer
+// batches sharded over the context's GPUs (one host thread per device) and pipelined through pinned
+// staging, and the device-resident entry points used by bench.py.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -14,36 +14,7 @@
 #include <vector>
 
 #include "../../include/cordaverify.h"
-
-extern "C" {
-hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off,
-                      const uint32_t *len, uint64_t *bitmap, uint8_t *status, uint32_t *ws_hs, uint32_t *ws_tab,
-                      uint32_t *ws_R, uint8_t *ws_ok, uint32_t *ws_dig, uint32_t ws_cap, hipStream_t stream,
-                      hipEvent_t *ev);
-hipError_t cvk_sign(uint32_t n, const uint8_t *seed, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
-                    uint8_t *pk, uint8_t *sig, hipStream_t stream);
-hipError_t cvk_pmt_verify(uint32_t ntrees, const uint8_t *kind, const uint32_t *left, const uint32_t *right,
-                          const uint8_t *leaf_hash, const uint32_t *tree_begin, const uint8_t *root, const uint8_t *check,
-                          const uint32_t *check_begin, uint32_t *dig, uint8_t *flag, uint8_t *verdict, uint8_t *status,
-                          hipStream_t stream);
-hipError_t cvk_merkle(uint32_t ntx, uint32_t nleaves, const uint8_t *arena, const uint64_t *leaf_off,
-                      const uint32_t *leaf_len, const uint32_t *tx_begin, uint32_t *leaf_digest, uint8_t *ids,
-                      uint8_t *status, hipStream_t stream);
-hipError_t cvk_calibrate(uint32_t iters, int which, uint32_t blocks, void *scratch, hipStream_t stream);
-hipError_t cvk_prep_probe(uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off,
-                          const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t ws_cap, uint64_t *stamps,
-                          hipStream_t stream);
-hipError_t cvk_mad_clock(uint32_t iters, uint32_t blocks, uint64_t *out, hipStream_t stream);
-uint32_t cvk_get_tri_max(void);
-hipError_t cvk_prepare(hipStream_t stream);
-hipError_t cvk_keyprep(uint32_t nk, const uint8_t *keys, const uint32_t *slots, uint32_t *scratch, uint32_t *ktab_pool,
-                       uint8_t *kok_pool, hipStream_t stream);
-hipError_t cvk_verify_keyed(uint32_t n, const uint8_t *keys, const uint32_t *key_index, const uint32_t *slot_of_key,
-                            const uint32_t *ktab_pool, const uint8_t *kok_pool, const uint8_t *sig,
-                            const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
-                            uint8_t *status, uint32_t *ws_hs, uint32_t *ws_R, uint8_t *ws_ok, uint32_t ws_cap,
-                            hipStream_t stream, hipEvent_t *ev);
-}
+#include "cv_launch.h"
 
 namespace {
 
@@ -140,22 +111,43 @@ struct KeyCache {
     uint32_t cap = 0;
     std::unordered_map<std::array<uint8_t, 32>, uint32_t, KeyHash> map;
     uint64_t hits = 0, misses = 0, resets = 0;
+    // the last stream that used the pool, and an event after that use (pool_begin / pool_end)
+    hipStream_t last = nullptr;
+    hipEvent_t ev = nullptr;
+    PinBuf pin;                    // pinned staging of the device-API keyed call's slot_of_key upload
+    hipEvent_t pin_ev = nullptr;   // recorded after that upload
+    bool pin_busy = false;
 };
+
+// One verify workspace (per signature: hs 64 B, 2 tables 2 x 1440 B, R record 128 B, ok 1 B, half-size
+// digits 292 B) with what orders its use across streams, its drain-overlap helper, and the host
+// pipeline's staging for the sub-chunks that run on it.  A device has kSlots of them: device-API
+// calls on different streams take different slots and run concurrently; the host-buffer pipeline
+// deals its sub-chunks round-robin over the slots (each slot's stream: H2D -> verify -> D2H).
+struct Slot {
+    DevBuf ws_hs, ws_tab, ws_R, ws_ok, ws_dig;
+    uint32_t ws_cap = 0;
+    hipStream_t last = nullptr;   // the stream of the last launch group on this workspace
+    hipEvent_t ev = nullptr;      // recorded after that group
+    uint64_t stamp = 0;           // last use (least-recently-used choice)
+    CvkSplit split;               // drain-overlap helper stream + events (created on first need)
+    hipStream_t stream = nullptr; // the slot's own stream (slot 0: the device stream)
+    PinBuf pin_in;                // host-buffer staging of one (sub-)chunk: pk | sig | off | len | arena
+    DevBuf packed;                // its device copy
+    hipEvent_t h2d = nullptr;     // recorded after the last DMA out of pin_in
+    bool h2d_pending = false;
+};
+constexpr int kSlots = 3;
 
 struct Device {
     int ordinal = 0;
     hipStream_t stream = nullptr;
     DevBuf pk, sig, arena, off, len, bitmap, status, seed, tx_begin, digest, ids;
-    DevBuf packed;                       // host-buffer verify: pk | sig | off | len | arena in one block
-    PinBuf pin_in, pin_out;              // its pinned host staging (inputs; bitmap | status)
+    PinBuf pin_out;                      // host-buffer verify outputs: bitmap | status
     DevBuf pmt;                          // partial Merkle trees: inputs, outputs and workspace, packed
-    DevBuf ws_hs, ws_tab, ws_R, ws_ok, ws_dig;   // verify workspace per signature: hs 64 B, 2 tables 2 x 1440 B,
-                                         // R record 128 B, ok 1 B, half-size digits 260 B
-    uint32_t ws_cap = 0;
+    Slot slot[kSlots];
+    uint64_t clock = 0;
     KeyCache kc;
-    // the last stream that used the shared workspace / key pool, and an event after its use
-    hipStream_t ws_last = nullptr;
-    hipEvent_t ws_ev = nullptr;
 };
 
 // key-table pool capacity per device (keys); 66 KB of tables per key (1.1 GB at the default; the pool
@@ -163,6 +155,8 @@ struct Device {
 constexpr uint32_t kDefaultKeyCap = 1u << 14;
 constexpr size_t kKtabBytes = 16512 * 4;  // CV_KTAB_WORDS: 4 comb rows x 129 affine entries x 128 B
 constexpr size_t kTabBytes = 9 * 40 * 4;  // CV_TAB_WORDS: k*P, k = 0..8, cached form (cv_verify.h)
+// new keys' tables are computed in launches of at most this many keys (bounded keyprep scratch: 270 MB)
+constexpr size_t kKeyprepBatch = 4096;
 // cv_ed25519_verify_batch dedupes keys on the host up to this batch size, and takes the keyed
 // (per-key comb) path when the batch has at least eight signatures per distinct key on average (a key's
 // 66 KB of tables cost about as much as 7 plain verifies to build; cached keys cost nothing)
@@ -173,44 +167,125 @@ constexpr size_t kAutoKeyedMax = 1u << 18;
 // chunk tails to drain; whole-round chunks of 1,966,080 were slower, 73.4 ms).
 constexpr uint32_t kVerifyChunk = 1u << 22;
 
-hipError_t ensure_verify_ws(Device &d, size_t n) {
-    uint32_t want = (uint32_t)std::min<size_t>(kVerifyChunk, (n + 511) / 512 * 512);
-    if (want <= d.ws_cap) return hipSuccess;
-    hipError_t e;
-    if ((e = d.ws_hs.ensure((size_t)want * 64)) != hipSuccess) return e;
-    if ((e = d.ws_tab.ensure((size_t)want * 2 * kTabBytes)) != hipSuccess) return e;   // k*(-A), k*R
-    if ((e = d.ws_R.ensure((size_t)want * 128)) != hipSuccess) return e;
-    if ((e = d.ws_ok.ensure((size_t)want)) != hipSuccess) return e;
-    if ((e = d.ws_dig.ensure((size_t)want * 73 * 4)) != hipSuccess) return e;   // CV_HS_DIGWORDS
-    d.ws_cap = want;
+// Host-buffer pipeline (verify_shard_pipe): shards above g_pipe_min signatures are cut into a first
+// sub-chunk of g_pipe_first (short, so the GPU starts early) and then sub-chunks of g_pipe_chunk (the
+// last two balanced), dealt round-robin over the device's slots; g_pack_threads host threads pack each
+// sub-chunk into pinned staging while the earlier ones transfer and verify.
+static size_t g_pipe_min = 131072, g_pipe_first = 65536, g_pipe_chunk = 262144;
+static int g_pack_threads = 8;
+
+hipError_t slot_events(Slot &sl) {
+    hipError_t e = hipSuccess;
+    if (!sl.ev && (e = hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if (!sl.h2d && (e = hipEventCreateWithFlags(&sl.h2d, hipEventDisableTiming)) != hipSuccess) return e;
+    return e;
+}
+
+// the slot's own stream (created on first use; slot 0 shares the device stream)
+hipError_t slot_stream(Device &d, int k, hipStream_t *out) {
+    Slot &sl = d.slot[k];
+    if (!sl.stream) {
+        if (k == 0)
+            sl.stream = d.stream;
+        else {
+            const hipError_t e = hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking);
+            if (e != hipSuccess) {
+                sl.stream = nullptr;
+                return e;
+            }
+        }
+    }
+    *out = sl.stream;
     return hipSuccess;
 }
 
-// Every use of a device's shared state (the verify workspace, the key pool) is ordered across
-// streams: a launch group enqueued on stream s first waits for the previous group when that ran on
-// another stream (ws_begin), and marks its own end (ws_end).  Device-pointer calls may therefore be
-// made on any streams; they serialise on the workspace instead of racing on it.  Callers hold
-// ctx->mu around ws_begin .. ws_end.
-hipError_t ws_begin(Device &d, hipStream_t s) {
-    hipError_t e = hipSuccess;
-    if (!d.ws_ev && (e = hipEventCreateWithFlags(&d.ws_ev, hipEventDisableTiming)) != hipSuccess) return e;
-    if (d.ws_last && d.ws_last != s) e = hipStreamWaitEvent(s, d.ws_ev, 0);
-    return e;
-}
-hipError_t ws_end(Device &d, hipStream_t s) {
-    d.ws_last = s;
-    return hipEventRecord(d.ws_ev, s);
+// the drain-overlap helper of a slot (created on the first large device-API call that may split)
+hipError_t slot_split(Device &d, Slot &sl) {
+    if (sl.split.s2) return hipSuccess;
+    CvkSplit x;
+    hipError_t e = hipDeviceGetAttribute(&x.cus, hipDeviceAttributeMultiprocessorCount, d.ordinal);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&x.start, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&x.prep1, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&x.done2, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&x.s2, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        for (hipEvent_t v : {x.start, x.prep1, x.done2})
+            if (v) (void)hipEventDestroy(v);
+        return e;
+    }
+    sl.split = x;
+    return hipSuccess;
 }
 
-hipError_t launch_verify(Device &d, uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
-                         const uint64_t *off, const uint32_t *len, uint64_t *bitmap, uint8_t *status, hipStream_t s,
-                         hipEvent_t *ev = nullptr) {
-    hipError_t e = ensure_verify_ws(d, n);
-    if (e == hipSuccess) e = ws_begin(d, s);
+// The workspace slot for a launch group on stream s: the slot s used last (no cross-stream wait),
+// else the least recently used one (ws_begin then waits for that slot's previous group).
+Slot &pick_slot(Device &d, hipStream_t s) {
+    for (Slot &sl : d.slot)
+        if (sl.last == s) return sl;
+    Slot *best = &d.slot[0];
+    for (Slot &sl : d.slot)
+        if (sl.stamp < best->stamp) best = &sl;
+    return *best;
+}
+
+// Grows a slot's workspace to n signatures (capped at one chunk).  The old buffers may still be read
+// by a queued group, so that group is waited for first; ws_cap stays 0 until all five buffers exist
+// (a failed growth leaves a slot that the next call grows again, never a null workspace with a
+// stale capacity).
+hipError_t ensure_verify_ws(Slot &sl, size_t n) {
+    uint32_t want = (uint32_t)std::min<size_t>(kVerifyChunk, (n + 511) / 512 * 512);
+    if (want <= sl.ws_cap) return hipSuccess;
+    hipError_t e;
+    if (sl.last && sl.ev && (e = hipEventSynchronize(sl.ev)) != hipSuccess) return e;
+    sl.ws_cap = 0;
+    if ((e = sl.ws_hs.ensure((size_t)want * 64)) != hipSuccess) return e;
+    if ((e = sl.ws_tab.ensure((size_t)want * 2 * kTabBytes)) != hipSuccess) return e;   // k*(-A), k*R
+    if ((e = sl.ws_R.ensure((size_t)want * 128)) != hipSuccess) return e;
+    if ((e = sl.ws_ok.ensure((size_t)want)) != hipSuccess) return e;
+    if ((e = sl.ws_dig.ensure((size_t)want * 73 * 4)) != hipSuccess) return e;   // CV_HS_DIGWORDS
+    sl.ws_cap = want;
+    return hipSuccess;
+}
+
+// Every use of a shared device resource (a workspace slot, the key pool) is ordered across streams:
+// a launch group enqueued on stream s first waits for the previous group when that ran on another
+// stream (ws_begin), and marks its own end (ws_end).  Device-pointer calls may therefore be made on any
+// streams; two streams that hold different slots run concurrently, and a stream that takes over a slot
+// waits for it instead of racing on it.  Callers hold ctx->mu around ws_begin .. ws_end.
+hipError_t ws_begin(Device &d, Slot &sl, hipStream_t s) {
+    hipError_t e = slot_events(sl);
     if (e != hipSuccess) return e;
-    e = cvk_verify(n, pk, sig, arena, off, len, bitmap, status, d.ws_hs.as<uint32_t>(), d.ws_tab.as<uint32_t>(),
-                   d.ws_R.as<uint32_t>(), d.ws_ok.as<uint8_t>(), d.ws_dig.as<uint32_t>(), d.ws_cap, s, ev);
-    const hipError_t e2 = ws_end(d, s);
+    sl.stamp = ++d.clock;
+    if (sl.last && sl.last != s) e = hipStreamWaitEvent(s, sl.ev, 0);
+    return e;
+}
+hipError_t ws_end(Slot &sl, hipStream_t s) {
+    sl.last = s;
+    return hipEventRecord(sl.ev, s);
+}
+hipError_t pool_begin(KeyCache &kc, hipStream_t s) {
+    hipError_t e = hipSuccess;
+    if (!kc.ev && (e = hipEventCreateWithFlags(&kc.ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if (kc.last && kc.last != s) e = hipStreamWaitEvent(s, kc.ev, 0);
+    return e;
+}
+hipError_t pool_end(KeyCache &kc, hipStream_t s) {
+    kc.last = s;
+    return hipEventRecord(kc.ev, s);
+}
+
+// One verify launch group on slot sl, stream s.  split: the drain-overlap sub-chunks may be used.
+hipError_t launch_verify(Device &d, Slot &sl, uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
+                         const uint64_t *off, const uint32_t *len, uint64_t *bitmap, uint8_t *status, hipStream_t s,
+                         hipEvent_t *ev, bool split) {
+    hipError_t e = ensure_verify_ws(sl, n);
+    if (e == hipSuccess) e = ws_begin(d, sl, s);
+    if (e != hipSuccess) return e;
+    if (split && n >= 131072) (void)slot_split(d, sl);   // without a helper the chunk runs whole
+    e = cvk_verify(n, pk, sig, arena, off, len, bitmap, status, sl.ws_hs.as<uint32_t>(), sl.ws_tab.as<uint32_t>(),
+                   sl.ws_R.as<uint32_t>(), sl.ws_ok.as<uint8_t>(), sl.ws_dig.as<uint32_t>(), sl.ws_cap, s, ev,
+                   split && sl.split.s2 ? &sl.split : nullptr);
+    const hipError_t e2 = ws_end(sl, s);
     return e != hipSuccess ? e : e2;
 }
 
@@ -226,6 +301,17 @@ int hip_rc(hipError_t e) {
         if (e_ != hipSuccess) return hip_rc(e_); \
     } while (0)
 
+// Runs fn at scope exit unless dismissed (error paths that must drain queued DMAs out of pinned
+// staging before a later call reuses or frees it).
+template <class F> struct OnExit {
+    F fn;
+    bool armed = true;
+    ~OnExit() {
+        if (armed) fn();
+    }
+};
+template <class F> OnExit<F> on_exit(F fn) { return OnExit<F>{fn}; }
+
 }  // namespace
 
 struct cv_ctx {
@@ -236,7 +322,7 @@ struct cv_ctx {
 
 extern "C" {
 
-const char *cv_version(void) { return "cordaverify-mi355x 0.1 (gfx950)"; }
+const char *cv_version(void) { return "cordaverify-mi355x 0.2 (gfx950)"; }
 
 const char *cv_strerror(int code) {
     switch (code) {
@@ -256,6 +342,15 @@ const char *cv_strerror(int code) {
 // dedupe and key pools) runs and is tested on a one-GPU box.  0 / 1 = off.
 static int g_virtual_devices = 1;
 void cvk_set_virtual_devices(int k) { g_virtual_devices = (k >= 1 && k <= 16) ? k : 1; }
+
+// Tuning knob (internal): the host-buffer pipeline's shard threshold, first and steady sub-chunk sizes
+// (signatures; 0 keeps the current value) and packing threads.
+void cvk_set_pipe(size_t min_n, size_t first, size_t chunk, int threads) {
+    if (min_n) g_pipe_min = min_n;
+    if (first) g_pipe_first = std::max<size_t>(64, first / 64 * 64);
+    if (chunk) g_pipe_chunk = std::max<size_t>(64, chunk / 64 * 64);
+    if (threads > 0) g_pack_threads = std::min(threads, 64);
+}
 
 int cv_open(uint32_t device_mask, cv_ctx **out) {
     if (!out) return CV_E_ARGS;
@@ -295,15 +390,24 @@ void cv_close(cv_ctx *ctx) {
     if (!ctx) return;
     for (Device &d : ctx->devs) {
         (void)hipSetDevice(d.ordinal);
-        if (d.stream) (void)hipStreamSynchronize(d.stream);
+        (void)hipDeviceSynchronize();
         for (DevBuf *b : {&d.pk, &d.sig, &d.arena, &d.off, &d.len, &d.bitmap, &d.status, &d.seed, &d.tx_begin,
-                          &d.digest, &d.ids, &d.pmt, &d.ws_hs, &d.ws_tab, &d.ws_R, &d.ws_ok, &d.ws_dig, &d.kc.ktab, &d.kc.kok,
-                          &d.kc.keys, &d.kc.slots, &d.kc.slot_of_key, &d.kc.key_index, &d.kc.scratch})
+                          &d.digest, &d.ids, &d.pmt, &d.kc.ktab, &d.kc.kok, &d.kc.keys, &d.kc.slots,
+                          &d.kc.slot_of_key, &d.kc.key_index, &d.kc.scratch})
             b->release();
-        d.packed.release();
-        d.pin_in.release();
         d.pin_out.release();
-        if (d.ws_ev) (void)hipEventDestroy(d.ws_ev);
+        for (int k = 0; k < kSlots; k++) {
+            Slot &sl = d.slot[k];
+            for (DevBuf *b : {&sl.ws_hs, &sl.ws_tab, &sl.ws_R, &sl.ws_ok, &sl.ws_dig, &sl.packed}) b->release();
+            sl.pin_in.release();
+            for (hipEvent_t v : {sl.ev, sl.h2d, sl.split.start, sl.split.prep1, sl.split.done2})
+                if (v) (void)hipEventDestroy(v);
+            if (sl.split.s2) (void)hipStreamDestroy(sl.split.s2);
+            if (k > 0 && sl.stream) (void)hipStreamDestroy(sl.stream);
+        }
+        d.kc.pin.release();
+        if (d.kc.ev) (void)hipEventDestroy(d.kc.ev);
+        if (d.kc.pin_ev) (void)hipEventDestroy(d.kc.pin_ev);
         if (d.stream) (void)hipStreamDestroy(d.stream);
     }
     delete ctx;
@@ -317,29 +421,25 @@ static Device *find_dev(cv_ctx *ctx, int device) {
     return nullptr;
 }
 
+}  // extern "C"
+
 // ---------------------------------------------------------------- verify (host buffers)
-// One shard [b, e) of a batch on one device.  b is a multiple of 64, so the shard's bitmap words
-// are whole words of the caller's bitmap.  The inputs are packed into the device's pinned staging
-// buffer (pk | sig | off rebased to the shard's arena range | len | arena bytes, 16-B aligned parts),
-// moved by one DMA (two above 1 MB: the first overlaps packing the second part) into one device
-// block, verified, and the bitmap (+ status) come back by one DMA.
 static inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-// Host copies into the pinned staging buffer.  A large batch is packed by a few threads (one core
-// copies ~10 GB/s, below what the DMA takes): each segment is cut into >= 512 KB pieces dealt out
+// Host copies into pinned staging.  A large copy is done by several threads (one core copies
+// ~10 GB/s, below what the DMA takes): each segment is cut into >= 512 KB pieces dealt out
 // round-robin; `extra` runs on the calling thread meanwhile.
-extern "C++" {
 struct CopyJob {
     void *dst;
     const void *src;
     size_t len;
 };
-template <class F> static void par_copy(const std::vector<CopyJob> &jobs, F extra) {
+template <class F> static void par_copy(const std::vector<CopyJob> &jobs, int threads, F extra) {
     constexpr size_t kPiece = 512 * 1024;
-    constexpr int kThreads = 4;
     size_t total = 0;
     for (const CopyJob &j : jobs) total += j.len;
-    if (total < 2 * kPiece) {
+    threads = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads, total / kPiece));
+    if (threads <= 1) {
         for (const CopyJob &j : jobs)
             if (j.len) std::memcpy(j.dst, j.src, j.len);
         extra();
@@ -350,84 +450,230 @@ template <class F> static void par_copy(const std::vector<CopyJob> &jobs, F extr
         for (size_t o = 0; o < j.len; o += kPiece)
             pieces.push_back({static_cast<uint8_t *>(j.dst) + o, static_cast<const uint8_t *>(j.src) + o,
                               std::min(kPiece, j.len - o)});
-    auto work = [&pieces](int t) {
-        for (size_t k = (size_t)t; k < pieces.size(); k += kThreads)
+    auto work = [&pieces, threads](int t) {
+        for (size_t k = (size_t)t; k < pieces.size(); k += (size_t)threads)
             std::memcpy(pieces[k].dst, pieces[k].src, pieces[k].len);
     };
-    std::thread th[kThreads - 1];
-    for (int t = 1; t < kThreads; t++) th[t - 1] = std::thread(work, t);
+    std::vector<std::thread> th;
+    th.reserve((size_t)threads - 1);
+    for (int t = 1; t < threads; t++) th.emplace_back(work, t);
     extra();
     work(0);
     for (auto &x : th) x.join();
 }
-}  // extern "C++"
-static int verify_shard(Device &d, size_t b, size_t e, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
-                        const uint64_t *off, const uint32_t *len, uint64_t *bitmap, uint8_t *status) {
-    const size_t n = e - b;
-    if (n == 0) return CV_OK;
-    if (n > 0xffffffffull) return CV_E_TOO_LARGE;
-    CV_TRY(hipSetDevice(d.ordinal));
-    // arena sub-range used by this shard; offsets are rebased to it
-    uint64_t lo = UINT64_MAX, hi = 0;
+
+// Staging layout of records [b, e): pk | sig | off | len | arena, 16-B aligned parts.  The arena part is
+// the byte range [lo, hi) the records' messages span, with lo rounded down to 16 so the device arena
+// pointer keeps every message's alignment; the kernels get arena_dev - lo and the caller's offsets
+// unchanged.  When the messages are scattered (the range is more than twice their bytes + 1 MB), they
+// are gathered back to back instead and the offsets rewritten ("compact").
+struct Stage {
+    size_t n = 0, o_pk = 0, o_sig = 0, o_off = 0, o_len = 0, o_ar = 0, total = 0;
+    uint64_t lo = 0, hi = 0;
+    bool compact = false;
+};
+static Stage stage_plan(size_t b, size_t e, const uint64_t *off, const uint32_t *len) {
+    Stage st;
+    st.n = e - b;
+    uint64_t lo = UINT64_MAX, hi = 0, bytes = 0;
     for (size_t i = b; i < e; i++) {
         lo = std::min<uint64_t>(lo, off[i]);
         hi = std::max<uint64_t>(hi, off[i] + len[i]);
+        bytes += len[i];
     }
-    if (hi < lo) hi = lo;
+    if (hi < lo) lo = hi = 0;
+    lo &= ~(uint64_t)15;
+    st.compact = hi - lo > 2 * bytes + (1u << 20);
+    st.lo = st.compact ? 0 : lo;
+    st.hi = st.compact ? bytes : hi;
+    const size_t n = st.n;
+    st.o_pk = 0;
+    st.o_sig = al16(n * 32);
+    st.o_off = st.o_sig + al16(n * 64);
+    st.o_len = st.o_off + al16(n * 8);
+    st.o_ar = st.o_len + al16(n * 4);
+    st.total = st.o_ar + al16(st.hi - st.lo + 16);
+    return st;
+}
+// Packs records [b, e) into h by the plan (keys + signatures first when `first_part` is given: it runs
+// before the rest so their DMA can start early).
+template <class F>
+static void stage_pack(const Stage &st, uint8_t *h, size_t b, const uint8_t *pk, const uint8_t *sig,
+                       const uint8_t *arena, const uint64_t *off, const uint32_t *len, int threads, F first_part) {
+    const size_t n = st.n;
+    par_copy({{h + st.o_pk, pk + b * 32, n * 32}, {h + st.o_sig, sig + b * 64, n * 64}}, threads, [] {});
+    first_part();
+    uint64_t *hoff = reinterpret_cast<uint64_t *>(h + st.o_off);
+    uint8_t *har = h + st.o_ar;
+    if (st.compact) {
+        par_copy({{h + st.o_len, len + b, n * 4}}, 1, [] {});
+        uint64_t pos = 0;
+        for (size_t i = 0; i < n; i++) {
+            hoff[i] = pos;
+            if (len[b + i]) std::memcpy(har + pos, arena + off[b + i], len[b + i]);
+            pos += len[b + i];
+        }
+    } else {
+        par_copy({{h + st.o_off, off + b, n * 8}, {h + st.o_len, len + b, n * 4},
+                  {har, st.hi > st.lo ? arena + st.lo : nullptr, (size_t)(st.hi - st.lo)}},
+                 threads, [] {});
+    }
+    std::memset(har + (st.hi - st.lo), 0, 16);
+}
+
+// One shard [b, e) of a batch on one device, small form (the notary-sized batches): packed into slot 0's
+// pinned staging, moved by one DMA (two above 1 MB: the first overlaps packing the second part) into
+// one device block, verified, and the bitmap (+ status) come back by one DMA.  b is a multiple of 64,
+// so the shard's bitmap words are whole words of the caller's bitmap.
+static int verify_shard_small(Device &d, size_t b, size_t e, const uint8_t *pk, const uint8_t *sig,
+                              const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
+                              uint8_t *status, int threads) {
+    const size_t n = e - b;
+    const Stage st = stage_plan(b, e, off, len);
     const size_t words = (n + 63) / 64;
-    const size_t o_pk = 0, o_sig = al16(n * 32), o_off = o_sig + al16(n * 64), o_len = o_off + al16(n * 8);
-    const size_t o_ar = o_len + al16(n * 4), total = o_ar + al16(hi - lo + 16);
     const size_t o_bm = 0, o_st = al16(words * 8), total_out = o_st + al16(n);
-    CV_TRY(d.pin_in.ensure(total));
+    Slot &sl = d.slot[0];
+    hipStream_t s = nullptr;
+    CV_TRY(slot_stream(d, 0, &s));
+    // the staging of a previous call may still be in a DMA only if that call failed half way (it
+    // drains its queue on every error path below), so this wait is normally free
+    if (sl.h2d_pending) {
+        CV_TRY(hipEventSynchronize(sl.h2d));
+        sl.h2d_pending = false;
+    }
+    CV_TRY(slot_events(sl));
+    CV_TRY(sl.pin_in.ensure(st.total));
     CV_TRY(d.pin_out.ensure(total_out));
-    CV_TRY(d.packed.ensure(total));
+    CV_TRY(sl.packed.ensure(st.total));
     CV_TRY(d.bitmap.ensure(total_out));
-    hipStream_t s = d.stream;
-    // the staging buffers are reused by the next call: the previous call synchronised at its end
-    uint8_t *h = d.pin_in.as<uint8_t>();
-    uint64_t *hoff = reinterpret_cast<uint64_t *>(h + o_off);
-    uint8_t *dv = d.packed.as<uint8_t>();
+    uint8_t *h = sl.pin_in.as<uint8_t>();
+    uint8_t *dv = sl.packed.as<uint8_t>();
+    auto drain = on_exit([s] { (void)hipStreamSynchronize(s); });   // error paths: no DMA outlives the call
     // Two-stage staging above 1 MB of keys + signatures: they are packed and their DMA is issued
     // first, so it runs while the offsets, lengths and message bytes are packed (notary 65,536:
     // 1.29-1.34 -> 1.21-1.25 ms p50); below, one DMA (a second DMA's ~6 us would cost more than it hides).
-    const bool two_stage = o_off >= ((size_t)1 << 20);
-    par_copy({{h + o_pk, pk + b * 32, n * 32}, {h + o_sig, sig + b * 64, n * 64}}, [] {});
-    if (two_stage) CV_TRY(hipMemcpyAsync(dv, h, o_off, hipMemcpyHostToDevice, s));
-    par_copy({{h + o_len, len + b, n * 4},
-              {h + o_ar, hi > lo ? arena + lo : nullptr, (size_t)(hi - lo)}},
-             [&] {
-                 for (size_t i = 0; i < n; i++) hoff[i] = off[b + i] - lo;
-             });
-    std::memset(h + o_ar + (hi - lo), 0, 16);
+    const bool two_stage = st.o_off >= ((size_t)1 << 20);
+    hipError_t e1 = hipSuccess;
+    stage_pack(st, h, b, pk, sig, arena, off, len, threads, [&] {
+        if (two_stage) e1 = hipMemcpyAsync(dv, h, st.o_off, hipMemcpyHostToDevice, s);
+    });
+    CV_TRY(e1);
     if (two_stage)
-        CV_TRY(hipMemcpyAsync(dv + o_off, h + o_off, total - o_off, hipMemcpyHostToDevice, s));
+        CV_TRY(hipMemcpyAsync(dv + st.o_off, h + st.o_off, st.total - st.o_off, hipMemcpyHostToDevice, s));
     else
-        CV_TRY(hipMemcpyAsync(dv, h, total, hipMemcpyHostToDevice, s));
+        CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, s));
     uint8_t *dout = d.bitmap.as<uint8_t>();
-    CV_TRY(launch_verify(d, (uint32_t)n, dv + o_pk, dv + o_sig, dv + o_ar, reinterpret_cast<const uint64_t *>(dv + o_off),
-                         reinterpret_cast<const uint32_t *>(dv + o_len), reinterpret_cast<uint64_t *>(dout + o_bm),
-                         status ? dout + o_st : nullptr, s));
+    CV_TRY(launch_verify(d, sl, (uint32_t)n, dv + st.o_pk, dv + st.o_sig, dv + st.o_ar - st.lo,
+                         reinterpret_cast<const uint64_t *>(dv + st.o_off), reinterpret_cast<const uint32_t *>(dv + st.o_len),
+                         reinterpret_cast<uint64_t *>(dout + o_bm), status ? dout + o_st : nullptr, s, nullptr, true));
     CV_TRY(hipMemcpyAsync(d.pin_out.p, dout, status ? o_st + n : words * 8, hipMemcpyDeviceToHost, s));
     CV_TRY(hipStreamSynchronize(s));
+    drain.armed = false;
     std::memcpy(bitmap + b / 64, d.pin_out.as<uint8_t>() + o_bm, words * 8);
     if (status) std::memcpy(status + b, d.pin_out.as<uint8_t>() + o_st, n);
     return CV_OK;
 }
 
-}  // extern "C"
+// One shard [b, e) of a large batch, pipelined: sub-chunks (multiples of 64 signatures) go round-robin
+// over the device's kSlots slots.  Sub-chunk j is packed by the host threads into slot j % kSlots's
+// pinned staging (after that slot's previous DMA has left it), moved by one DMA on the slot's stream,
+// verified there with the slot's workspace, and its bitmap words (+ status) copied into the shard's
+// pinned output.  So packing sub-chunk j+1, the DMA of sub-chunk j and the kernels of sub-chunks j-1 and
+// j-2 overlap, and the slots' kernels fill each other's drains.
+static int verify_shard_pipe(Device &d, size_t b, size_t e, const uint8_t *pk, const uint8_t *sig,
+                             const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
+                             uint8_t *status, int threads) {
+    const size_t n = e - b;
+    const size_t words = (n + 63) / 64;
+    const size_t o_st = al16(words * 8), total_out = o_st + al16(n);
+    // the sub-chunk plan: [first, C, C, ..., the last two balanced], all but the last multiples of 64
+    std::vector<size_t> cut{b};
+    {
+        const size_t C = g_pipe_chunk;
+        size_t p = b + std::min(n, g_pipe_first);
+        cut.push_back(p);
+        while (p < e) {
+            const size_t rem = e - p;
+            const size_t m = rem <= C ? rem : rem < 2 * C ? (rem / 2 + 63) / 64 * 64 : C;
+            p += m;
+            cut.push_back(p);
+        }
+    }
+    hipStream_t ss[kSlots];
+    for (int k = 0; k < kSlots; k++) {
+        CV_TRY(slot_stream(d, k, &ss[k]));
+        CV_TRY(slot_events(d.slot[k]));
+    }
+    CV_TRY(d.pin_out.ensure(total_out));
+    CV_TRY(d.bitmap.ensure(total_out));
+    uint8_t *dout = d.bitmap.as<uint8_t>();
+    uint8_t *hout = d.pin_out.as<uint8_t>();
+    auto drain = on_exit([&] {
+        for (int k = 0; k < kSlots; k++) (void)hipStreamSynchronize(ss[k]);
+        for (Slot &sl : d.slot) sl.h2d_pending = false;
+    });
+    for (size_t j = 0; j + 1 < cut.size(); j++) {
+        const size_t c0 = cut[j], c1 = cut[j + 1], m = c1 - c0;
+        Slot &sl = d.slot[j % kSlots];
+        hipStream_t s = ss[j % kSlots];
+        const Stage st = stage_plan(c0, c1, off, len);
+        if (sl.h2d_pending) {                       // the slot's staging is free once its DMA is done
+            CV_TRY(hipEventSynchronize(sl.h2d));
+            sl.h2d_pending = false;
+        }
+        if (st.total > sl.pin_in.cap || st.total > sl.packed.cap) {
+            CV_TRY(hipStreamSynchronize(s));        // the device copy may still be read by a queued verify
+            CV_TRY(sl.pin_in.ensure(st.total));
+            CV_TRY(sl.packed.ensure(st.total));
+        }
+        uint8_t *h = sl.pin_in.as<uint8_t>();
+        uint8_t *dv = sl.packed.as<uint8_t>();
+        stage_pack(st, h, c0, pk, sig, arena, off, len, threads, [] {});
+        CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, s));
+        CV_TRY(hipEventRecord(sl.h2d, s));
+        sl.h2d_pending = true;
+        const size_t w0 = (c0 - b) / 64;
+        CV_TRY(launch_verify(d, sl, (uint32_t)m, dv + st.o_pk, dv + st.o_sig, dv + st.o_ar - st.lo,
+                             reinterpret_cast<const uint64_t *>(dv + st.o_off),
+                             reinterpret_cast<const uint32_t *>(dv + st.o_len),
+                             reinterpret_cast<uint64_t *>(dout) + w0, status ? dout + o_st + (c0 - b) : nullptr, s,
+                             nullptr, false));
+        CV_TRY(hipMemcpyAsync(hout + w0 * 8, dout + w0 * 8, ((m + 63) / 64) * 8, hipMemcpyDeviceToHost, s));
+        if (status) CV_TRY(hipMemcpyAsync(hout + o_st + (c0 - b), dout + o_st + (c0 - b), m, hipMemcpyDeviceToHost, s));
+    }
+    for (int k = 0; k < kSlots; k++) CV_TRY(hipStreamSynchronize(ss[k]));
+    drain.armed = false;
+    for (Slot &sl : d.slot) sl.h2d_pending = false;
+    std::memcpy(bitmap + b / 64, hout, words * 8);
+    if (status) std::memcpy(status + b, hout + o_st, n);
+    return CV_OK;
+}
 
-// Shards [0, n) over the context's devices (contiguous ranges, multiples of 64) and runs fn per shard.
+static int verify_shard(Device &d, size_t b, size_t e, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
+                        const uint64_t *off, const uint32_t *len, uint64_t *bitmap, uint8_t *status, int threads) {
+    const size_t n = e - b;
+    if (n == 0) return CV_OK;
+    if (n > 0xffffffffull) return CV_E_TOO_LARGE;
+    CV_TRY(hipSetDevice(d.ordinal));
+    if (n > g_pipe_min) return verify_shard_pipe(d, b, e, pk, sig, arena, off, len, bitmap, status, threads);
+    return verify_shard_small(d, b, e, pk, sig, arena, off, len, bitmap, status, threads);
+}
+
+// Shards [0, n) over the context's devices (contiguous ranges, multiples of 64) and runs fn per shard
+// (fn(device, b, e, packing threads)).
 template <class F> static int for_each_shard(cv_ctx *ctx, size_t n, F fn) {
     const size_t ndev = ctx->devs.size();
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int threads = (int)std::max<size_t>(1, std::min<size_t>((size_t)g_pack_threads, hw / ndev));
     size_t per = (n + ndev - 1) / ndev;
     per = (per + 63) / 64 * 64;
-    if (ndev == 1 || n <= 64) return fn(ctx->devs[0], 0, n);
+    if (ndev == 1 || n <= 64) return fn(ctx->devs[0], 0, n, threads);
     std::vector<int> rc(ndev, CV_OK);
     std::vector<std::thread> th;
     for (size_t k = 0; k < ndev; k++) {
         const size_t b = std::min(n, k * per), e = std::min(n, b + per);
         if (b >= e) continue;
-        th.emplace_back([&, k, b, e] { rc[k] = fn(ctx->devs[k], b, e); });
+        th.emplace_back([&, k, b, e] { rc[k] = fn(ctx->devs[k], b, e, threads); });
     }
     for (auto &t : th) t.join();
     for (int r : rc)
@@ -437,22 +683,33 @@ template <class F> static int for_each_shard(cv_ctx *ctx, size_t n, F fn) {
 
 // ---------------------------------------------------------------- keyed verify (per-key comb tables)
 // Makes the keys k (used[k] != 0, or all when used == nullptr) of keys[0..nk) resident in d's key
-// pool and fills slot_of_key[k]; one keyprep launch on s computes the tables of the new ones.
+// pool and fills slot_of_key[k]; keyprep launches on s compute the tables of the new ones (at most
+// kKeyprepBatch keys per launch, so the scratch stays bounded).  The caller holds the pool
+// (pool_begin).  Failure leaves an empty pool (capacity 0, no resident keys), never a key mapped to
+// a slot whose tables were not computed or a capacity without its buffers.
 static int key_resolve(Device &d, uint32_t cap, size_t nk, const uint8_t *keys, const uint8_t *used,
                        std::vector<uint32_t> &slot_of_key, hipStream_t s) {
     KeyCache &kc = d.kc;
+    auto fail = [&kc](hipError_t e) {
+        kc.map.clear();
+        kc.cap = 0;
+        kc.resets++;
+        return hip_rc(e);
+    };
     size_t nused = 0;
     for (size_t k = 0; k < nk; k++) nused += used ? (used[k] != 0) : 1;
     const size_t need = std::max<size_t>(cap, nused);
     if (kc.cap < need) {                      // (re)allocate the pool; resident tables are dropped
         if (need > 0xffffffffull / 2) return CV_E_TOO_LARGE;
-        CV_TRY(hipStreamSynchronize(s));
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return fail(e);
+        kc.map.clear();
+        kc.cap = 0;
         kc.ktab.release();
         kc.kok.release();
-        CV_TRY(kc.ktab.ensure(need * kKtabBytes));
-        CV_TRY(kc.kok.ensure(need));
+        if ((e = kc.ktab.ensure(need * kKtabBytes)) != hipSuccess) return fail(e);
+        if ((e = kc.kok.ensure(need)) != hipSuccess) return fail(e);
         kc.cap = (uint32_t)need;
-        kc.map.clear();
     }
     if (kc.map.size() + nused > kc.cap) {     // epoch reset: every key of this call gets a fresh slot
         kc.map.clear();
@@ -460,8 +717,11 @@ static int key_resolve(Device &d, uint32_t cap, size_t nk, const uint8_t *keys, 
     }
     std::vector<uint8_t> miss_keys;
     std::vector<uint32_t> miss_slots;
+    std::vector<std::array<uint8_t, 32>> miss;     // mapped only once their tables are enqueued
+    std::unordered_map<std::array<uint8_t, 32>, uint32_t, KeyHash> fresh;   // this call's new keys
     std::array<uint8_t, 32> key;
     slot_of_key.assign(nk, 0);
+    uint32_t next = (uint32_t)kc.map.size();
     for (size_t k = 0; k < nk; k++) {
         if (used && !used[k]) continue;
         std::memcpy(key.data(), keys + 32 * k, 32);
@@ -471,23 +731,43 @@ static int key_resolve(Device &d, uint32_t cap, size_t nk, const uint8_t *keys, 
             kc.hits++;
             continue;
         }
-        const uint32_t slot = (uint32_t)kc.map.size();
-        kc.map.emplace(key, slot);
+        auto f = fresh.find(key);
+        if (f != fresh.end()) {                   // a key repeated inside this call's key list
+            slot_of_key[k] = f->second;
+            continue;
+        }
+        const uint32_t slot = next++;
+        fresh.emplace(key, slot);
         slot_of_key[k] = slot;
         miss_keys.insert(miss_keys.end(), key.begin(), key.end());
         miss_slots.push_back(slot);
         kc.misses++;
     }
-    if (!miss_slots.empty()) {
-        const size_t m = miss_slots.size();
-        CV_TRY(kc.keys.ensure(m * 32));
-        CV_TRY(kc.slots.ensure(m * 4));
-        CV_TRY(kc.scratch.ensure(m * kKtabBytes));
-        CV_TRY(hipMemcpyAsync(kc.keys.p, miss_keys.data(), m * 32, hipMemcpyHostToDevice, s));
-        CV_TRY(hipMemcpyAsync(kc.slots.p, miss_slots.data(), m * 4, hipMemcpyHostToDevice, s));
-        CV_TRY(cvk_keyprep((uint32_t)m, kc.keys.as<uint8_t>(), kc.slots.as<uint32_t>(), kc.scratch.as<uint32_t>(),
-                           kc.ktab.as<uint32_t>(), kc.kok.as<uint8_t>(), s));
+    const size_t m = miss_slots.size();
+    for (size_t k0 = 0; k0 < m; k0 += kKeyprepBatch) {
+        const size_t mk = std::min(kKeyprepBatch, m - k0);
+        hipError_t e = kc.keys.ensure(mk * 32);
+        if (e == hipSuccess) e = kc.slots.ensure(mk * 4);
+        if (e == hipSuccess) e = kc.scratch.ensure(mk * kKtabBytes);
+        // the previous batch's keyprep may still read keys / slots / scratch: order the copies after it
+        // (same stream), and the host vectors stay alive until the synchronize below
+        if (e == hipSuccess) e = hipMemcpyAsync(kc.keys.p, miss_keys.data() + 32 * k0, mk * 32, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(kc.slots.p, miss_slots.data() + k0, mk * 4, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess)
+            e = cvk_keyprep((uint32_t)mk, kc.keys.as<uint8_t>(), kc.slots.as<uint32_t>(), kc.scratch.as<uint32_t>(),
+                            kc.ktab.as<uint32_t>(), kc.kok.as<uint8_t>(), s);
+        if (e == hipSuccess && k0 + mk < m) e = hipStreamSynchronize(s);   // buffers are reused by the next batch
+        if (e != hipSuccess) {
+            (void)hipStreamSynchronize(s);
+            return fail(e);
+        }
     }
+    if (m) {
+        // the pageable copies above read miss_keys / miss_slots asynchronously: keep them alive
+        const hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return fail(e);
+    }
+    for (auto &kv : fresh) kc.map.emplace(kv.first, kv.second);
     return CV_OK;
 }
 
@@ -509,7 +789,11 @@ static int verify_shard_keyed(uint32_t cap, Device &d, size_t b, size_t e, size_
     }
     if (hi < lo) hi = lo;
     hipStream_t s = d.stream;
-    CV_TRY(ws_begin(d, s));
+    Slot &sl = pick_slot(d, s);
+    CV_TRY(ensure_verify_ws(sl, n));
+    CV_TRY(ws_begin(d, sl, s));
+    CV_TRY(pool_begin(d.kc, s));
+    auto drain = on_exit([s] { (void)hipStreamSynchronize(s); });   // error paths: no copy outlives the call
     std::vector<uint32_t> sok;
     int rc = key_resolve(d, cap, nkeys, keys, used.data(), sok, s);
     if (rc != CV_OK) return rc;
@@ -531,16 +815,17 @@ static int verify_shard_keyed(uint32_t cap, Device &d, size_t b, size_t e, size_
     if (hi > lo) CV_TRY(hipMemcpyAsync(d.arena.p, arena + lo, hi - lo, hipMemcpyHostToDevice, s));
     CV_TRY(hipMemcpyAsync(d.off.p, off + b, n * 8, hipMemcpyHostToDevice, s));
     CV_TRY(hipMemcpyAsync(d.len.p, len + b, n * 4, hipMemcpyHostToDevice, s));
-    CV_TRY(ensure_verify_ws(d, n));
     CV_TRY(cvk_verify_keyed((uint32_t)n, d.pk.as<uint8_t>(), kc.key_index.as<uint32_t>(), kc.slot_of_key.as<uint32_t>(),
                             kc.ktab.as<uint32_t>(), kc.kok.as<uint8_t>(), d.sig.as<uint8_t>(),
                             d.arena.as<uint8_t>() - lo, d.off.as<uint64_t>(), d.len.as<uint32_t>(),
-                            d.bitmap.as<uint64_t>(), status ? d.status.as<uint8_t>() : nullptr, d.ws_hs.as<uint32_t>(),
-                            d.ws_R.as<uint32_t>(), d.ws_ok.as<uint8_t>(), d.ws_cap, s, nullptr));
-    CV_TRY(ws_end(d, s));
+                            d.bitmap.as<uint64_t>(), status ? d.status.as<uint8_t>() : nullptr, sl.ws_hs.as<uint32_t>(),
+                            sl.ws_R.as<uint32_t>(), sl.ws_ok.as<uint8_t>(), sl.ws_cap, s, nullptr));
+    CV_TRY(ws_end(sl, s));
+    CV_TRY(pool_end(kc, s));
     CV_TRY(hipMemcpyAsync(bitmap + b / 64, d.bitmap.p, words * 8, hipMemcpyDeviceToHost, s));
     if (status) CV_TRY(hipMemcpyAsync(status + b, d.status.p, n, hipMemcpyDeviceToHost, s));
     CV_TRY(hipStreamSynchronize(s));
+    drain.armed = false;
     return CV_OK;
 }
 
@@ -637,13 +922,13 @@ int cv_ed25519_verify_batch(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint
     // additions, then the inversion): notary batch of 4,096 with 64 signers 0.47 vs 0.34 ms distinct.
     if (n > cvk_get_tri_max() && dedupe_keys(n, pk, keys, key_index)) {
         const size_t nk = keys.size() / 32;
-        return for_each_shard(ctx, n, [&](Device &d, size_t b, size_t e) {
+        return for_each_shard(ctx, n, [&](Device &d, size_t b, size_t e, int) {
             return verify_shard_keyed(ctx->key_cap, d, b, e, nk, keys.data(), key_index.data(), sig, msg_arena, msg_off,
                                       msg_len, verdict_bitmap, status);
         });
     }
-    return for_each_shard(ctx, n, [&](Device &d, size_t b, size_t e) {
-        return verify_shard(d, b, e, pk, sig, msg_arena, msg_off, msg_len, verdict_bitmap, status);
+    return for_each_shard(ctx, n, [&](Device &d, size_t b, size_t e, int threads) {
+        return verify_shard(d, b, e, pk, sig, msg_arena, msg_off, msg_len, verdict_bitmap, status, threads);
     });
 }
 
@@ -654,7 +939,7 @@ int cv_ed25519_verify_batch_keyed(cv_ctx *ctx, size_t n, size_t nkeys, const uin
     if (n == 0) return CV_OK;
     if (!keys || !key_index || !sig || !msg_off || !msg_len || !verdict_bitmap || nkeys == 0) return CV_E_ARGS;
     std::lock_guard<std::mutex> g(ctx->mu);
-    return for_each_shard(ctx, n, [&](Device &d, size_t b, size_t e) {
+    return for_each_shard(ctx, n, [&](Device &d, size_t b, size_t e, int) {
         return verify_shard_keyed(ctx->key_cap, d, b, e, nkeys, keys, key_index, sig, msg_arena, msg_off, msg_len,
                                   verdict_bitmap, status);
     });
@@ -717,7 +1002,7 @@ int cv_ed25519_sign_batch(cv_ctx *ctx, size_t n, const uint8_t *seed, const uint
     if (n == 0) return CV_OK;
     if (!seed || !msg_off || !msg_len || !pk_out || !sig_out) return CV_E_ARGS;
     std::lock_guard<std::mutex> g(ctx->mu);
-    return for_each_shard(ctx, n, [&](Device &d, size_t b, size_t e) {
+    return for_each_shard(ctx, n, [&](Device &d, size_t b, size_t e, int) {
         return sign_shard(d, b, e, seed, msg_arena, msg_off, msg_len, pk_out, sig_out);
     });
 }
@@ -841,10 +1126,10 @@ int cv_ed25519_verify_device(cv_ctx *ctx, int device, size_t n, const void *d_pk
     std::lock_guard<std::mutex> g(ctx->mu);            // enqueue only; ordered on the workspace (ws_begin)
     CV_TRY(hipSetDevice(d->ordinal));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : d->stream;
-    CV_TRY(launch_verify(*d, (uint32_t)n, static_cast<const uint8_t *>(d_pk), static_cast<const uint8_t *>(d_sig),
-                         static_cast<const uint8_t *>(d_arena), static_cast<const uint64_t *>(d_off),
-                         static_cast<const uint32_t *>(d_len), static_cast<uint64_t *>(d_bitmap),
-                         static_cast<uint8_t *>(d_status), s));
+    CV_TRY(launch_verify(*d, pick_slot(*d, s), (uint32_t)n, static_cast<const uint8_t *>(d_pk),
+                         static_cast<const uint8_t *>(d_sig), static_cast<const uint8_t *>(d_arena),
+                         static_cast<const uint64_t *>(d_off), static_cast<const uint32_t *>(d_len),
+                         static_cast<uint64_t *>(d_bitmap), static_cast<uint8_t *>(d_status), s, nullptr, true));
     return CV_OK;
 }
 
@@ -860,16 +1145,17 @@ int cv_ed25519_verify_device_timed(cv_ctx *ctx, int device, size_t n, const void
     std::lock_guard<std::mutex> g(ctx->mu);
     CV_TRY(hipSetDevice(d->ordinal));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : d->stream;
+    Slot &sl = pick_slot(*d, s);
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     hipError_t e = hipSuccess;
     for (int k = 0; k < 4 && e == hipSuccess; k++) e = hipEventCreate(&ev[k]);
     // one workspace chunk at a time (chunk starts are multiples of 64: whole bitmap words)
     for (size_t c0 = 0; c0 < n && e == hipSuccess; c0 += kVerifyChunk) {
         const size_t m = std::min<size_t>(kVerifyChunk, n - c0);
-        e = launch_verify(*d, (uint32_t)m, static_cast<const uint8_t *>(d_pk) + c0 * 32,
+        e = launch_verify(*d, sl, (uint32_t)m, static_cast<const uint8_t *>(d_pk) + c0 * 32,
                           static_cast<const uint8_t *>(d_sig) + c0 * 64, static_cast<const uint8_t *>(d_arena),
                           static_cast<const uint64_t *>(d_off) + c0, static_cast<const uint32_t *>(d_len) + c0,
-                          static_cast<uint64_t *>(d_bitmap) + c0 / 64, nullptr, s, ev);
+                          static_cast<uint64_t *>(d_bitmap) + c0 / 64, nullptr, s, ev, false);
         if (e == hipSuccess) e = hipEventSynchronize(ev[3]);
         for (int k = 0; k < 3 && e == hipSuccess; k++) {
             float ms = 0.f;
@@ -902,26 +1188,43 @@ int cv_ed25519_verify_device_keyed(cv_ctx *ctx, int device, size_t n, size_t nke
     hipError_t e = hipSuccess;
     if (phase_ms)
         for (int k = 0; k < 5 && e == hipSuccess; k++) e = hipEventCreate(&ev[k]);
+    Slot &sl = pick_slot(*d, s);
+    if (e == hipSuccess) e = ensure_verify_ws(sl, n);
     if (e == hipSuccess && phase_ms) e = hipEventRecord(ev[0], s);
-    if (e == hipSuccess) e = ws_begin(*d, s);
+    if (e == hipSuccess) e = ws_begin(*d, sl, s);
+    if (e == hipSuccess) e = pool_begin(d->kc, s);
     std::vector<uint32_t> sok;
     int rc = e == hipSuccess ? key_resolve(*d, ctx->key_cap, nkeys, hkeys.data(), nullptr, sok, s) : hip_rc(e);
     KeyCache &kc = d->kc;
     if (rc == CV_OK) rc = hip_rc(kc.slot_of_key.ensure(nkeys * 4));
-    if (rc == CV_OK) rc = hip_rc(hipMemcpyAsync(kc.slot_of_key.p, sok.data(), nkeys * 4, hipMemcpyHostToDevice, s));
-    if (rc == CV_OK) rc = hip_rc(ensure_verify_ws(*d, n));
+    // slot_of_key goes up through the pool's pinned staging, which the previous keyed call's upload may
+    // still be reading: that call's pool event (after its verify) has passed once its upload has
+    if (rc == CV_OK && kc.pin_busy) rc = hip_rc(hipEventSynchronize(kc.pin_ev));
+    if (rc == CV_OK) rc = hip_rc(kc.pin.ensure(nkeys * 4));
+    if (rc == CV_OK) {
+        std::memcpy(kc.pin.p, sok.data(), nkeys * 4);
+        rc = hip_rc(hipMemcpyAsync(kc.slot_of_key.p, kc.pin.p, nkeys * 4, hipMemcpyHostToDevice, s));
+    }
+    if (rc == CV_OK && !kc.pin_ev) rc = hip_rc(hipEventCreateWithFlags(&kc.pin_ev, hipEventDisableTiming));
+    if (rc == CV_OK) rc = hip_rc(hipEventRecord(kc.pin_ev, s));
+    kc.pin_busy = rc == CV_OK;
     if (rc == CV_OK)
         rc = hip_rc(cvk_verify_keyed((uint32_t)n, static_cast<const uint8_t *>(d_keys),
                                      static_cast<const uint32_t *>(d_key_index), kc.slot_of_key.as<uint32_t>(),
                                      kc.ktab.as<uint32_t>(), kc.kok.as<uint8_t>(), static_cast<const uint8_t *>(d_sig),
                                      static_cast<const uint8_t *>(d_arena), static_cast<const uint64_t *>(d_off),
                                      static_cast<const uint32_t *>(d_len), static_cast<uint64_t *>(d_bitmap),
-                                     static_cast<uint8_t *>(d_status), d->ws_hs.as<uint32_t>(), d->ws_R.as<uint32_t>(),
-                                     d->ws_ok.as<uint8_t>(), d->ws_cap, s, phase_ms ? ev + 1 : nullptr));
-    if (d->ws_ev) {
-        const hipError_t e2 = ws_end(*d, s);
+                                     static_cast<uint8_t *>(d_status), sl.ws_hs.as<uint32_t>(), sl.ws_R.as<uint32_t>(),
+                                     sl.ws_ok.as<uint8_t>(), sl.ws_cap, s, phase_ms ? ev + 1 : nullptr));
+    if (sl.ev) {
+        const hipError_t e2 = ws_end(sl, s);
         if (rc == CV_OK) rc = hip_rc(e2);
     }
+    if (d->kc.ev) {
+        const hipError_t e2 = pool_end(d->kc, s);
+        if (rc == CV_OK) rc = hip_rc(e2);
+    }
+    if (rc != CV_OK) (void)hipStreamSynchronize(s);   // error paths: nothing queued outlives the call
     if (rc == CV_OK && phase_ms) {
         e = hipEventSynchronize(ev[4]);
         for (int k = 0; k < 4 && e == hipSuccess; k++) e = hipEventElapsedTime(&phase_ms[k], ev[k], ev[k + 1]);
@@ -975,6 +1278,27 @@ int cv_synchronize(cv_ctx *ctx, int device) {
 }
 
 // ---------------------------------------------------------------- calibration
+// scoped device scratch and events of the calibration / diagnostic calls (freed on every return path)
+struct ScopedMem {
+    void *p = nullptr;
+    ~ScopedMem() {
+        if (p) (void)hipFree(p);
+    }
+};
+struct ScopedEvents {
+    hipEvent_t e[2] = {nullptr, nullptr};
+    hipError_t create() {
+        hipError_t r = hipSuccess;
+        for (hipEvent_t &x : e)
+            if (r == hipSuccess) r = hipEventCreate(&x);
+        return r;
+    }
+    ~ScopedEvents() {
+        for (hipEvent_t x : e)
+            if (x) (void)hipEventDestroy(x);
+    }
+};
+
 int cv_calibrate(cv_ctx *ctx, int device, double *mad_per_s, double *femul_per_s) {
     if (!ctx) return CV_E_ARGS;
     Device *d = find_dev(ctx, device);
@@ -983,27 +1307,23 @@ int cv_calibrate(cv_ctx *ctx, int device, double *mad_per_s, double *femul_per_s
     hipDeviceProp_t prop;
     CV_TRY(hipGetDeviceProperties(&prop, d->ordinal));
     const uint32_t blocks = (uint32_t)prop.multiProcessorCount * 8;   // 8 waves per SIMD worth of work
-    void *scratch = nullptr;
-    CV_TRY(hipMalloc(&scratch, 64));
-    hipEvent_t e0, e1;
-    CV_TRY(hipEventCreate(&e0));
-    CV_TRY(hipEventCreate(&e1));
+    ScopedMem scratch;
+    ScopedEvents ev;
+    CV_TRY(hipMalloc(&scratch.p, 64));
+    CV_TRY(ev.create());
     double rates[2] = {0, 0};
     for (int which = 0; which < 2; which++) {
         const uint32_t iters = which == 0 ? 20000 : 2000;
-        CV_TRY(cvk_calibrate(iters / 10, which, blocks, scratch, d->stream));   // warm-up
-        CV_TRY(hipEventRecord(e0, d->stream));
-        CV_TRY(cvk_calibrate(iters, which, blocks, scratch, d->stream));
-        CV_TRY(hipEventRecord(e1, d->stream));
-        CV_TRY(hipEventSynchronize(e1));
+        CV_TRY(cvk_calibrate(iters / 10, which, blocks, scratch.p, d->stream));   // warm-up
+        CV_TRY(hipEventRecord(ev.e[0], d->stream));
+        CV_TRY(cvk_calibrate(iters, which, blocks, scratch.p, d->stream));
+        CV_TRY(hipEventRecord(ev.e[1], d->stream));
+        CV_TRY(hipEventSynchronize(ev.e[1]));
         float ms = 0;
-        CV_TRY(hipEventElapsedTime(&ms, e0, e1));
+        CV_TRY(hipEventElapsedTime(&ms, ev.e[0], ev.e[1]));
         const double per_thread = which == 0 ? 128.0 * iters : 4.0 * iters;
         rates[which] = per_thread * blocks * 256.0 / (ms * 1e-3);
     }
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    (void)hipFree(scratch);
     if (mad_per_s) *mad_per_s = rates[0];
     if (femul_per_s) *femul_per_s = rates[1];
     return CV_OK;
@@ -1021,24 +1341,20 @@ int cv_calibrate_cycles(cv_ctx *ctx, int device, double *out) {
     hipDeviceProp_t prop;
     CV_TRY(hipGetDeviceProperties(&prop, d->ordinal));
     const uint32_t blocks = (uint32_t)prop.multiProcessorCount * 8, iters = 20000;
-    uint64_t *buf = nullptr;
-    CV_TRY(hipMalloc(&buf, 64));
-    hipEvent_t e0, e1;
-    CV_TRY(hipEventCreate(&e0));
-    CV_TRY(hipEventCreate(&e1));
-    hipError_t e = cvk_mad_clock(iters / 10, blocks, buf, d->stream);
-    if (e == hipSuccess) e = hipEventRecord(e0, d->stream);
-    if (e == hipSuccess) e = cvk_mad_clock(iters, blocks, buf, d->stream);
-    if (e == hipSuccess) e = hipEventRecord(e1, d->stream);
-    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    ScopedMem buf;
+    ScopedEvents ev;
+    CV_TRY(hipMalloc(&buf.p, 64));
+    CV_TRY(ev.create());
+    uint64_t *clkbuf = static_cast<uint64_t *>(buf.p);
+    CV_TRY(cvk_mad_clock(iters / 10, blocks, clkbuf, d->stream));
+    CV_TRY(hipEventRecord(ev.e[0], d->stream));
+    CV_TRY(cvk_mad_clock(iters, blocks, clkbuf, d->stream));
+    CV_TRY(hipEventRecord(ev.e[1], d->stream));
+    CV_TRY(hipEventSynchronize(ev.e[1]));
     float ms = 0.f;
     uint64_t clk[2] = {0, 0};
-    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
-    if (e == hipSuccess) e = hipMemcpy(clk, buf, 16, hipMemcpyDeviceToHost);
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    (void)hipFree(buf);
-    if (e != hipSuccess) return hip_rc(e);
+    CV_TRY(hipEventElapsedTime(&ms, ev.e[0], ev.e[1]));
+    CV_TRY(hipMemcpy(clk, clkbuf, 16, hipMemcpyDeviceToHost));
     const double simds = 4.0 * prop.multiProcessorCount;
     const double rate = 128.0 * iters * blocks * 256.0 / (ms * 1e-3);
     const double ghz = clk[1] ? (double)clk[0] / ((double)clk[1] / 100e6) / 1e9 : 0.0;
@@ -1054,7 +1370,8 @@ int cv_calibrate_cycles(cv_ctx *ctx, int device, double *out) {
 
 // Per-phase shader cycles of the fused prep kernel (diagnostic build of the same code, one chunk):
 // out[k] = mean cycles per wave of phase k (hash, lattice, digits, decode A+R, tables), out[5] =
-// their sum, out[6] = waves measured, out[7] = the SHA-512 part of the hash phase.  The workspace is the device's verify workspace.
+// their sum, out[6] = waves measured, out[7] = the SHA-512 part of the hash phase.  The workspace is
+// the device stream's verify workspace slot.
 int cv_diag_prep_phases(cv_ctx *ctx, int device, size_t n, const void *d_pk, const void *d_sig, const void *d_arena,
                         const void *d_off, const void *d_len, double *out) {
     if (!ctx || !out || n == 0) return CV_E_ARGS;
@@ -1063,20 +1380,22 @@ int cv_diag_prep_phases(cv_ctx *ctx, int device, size_t n, const void *d_pk, con
     if (!d || !d_pk || !d_sig || !d_arena || !d_off || !d_len) return CV_E_ARGS;
     std::lock_guard<std::mutex> g(ctx->mu);
     CV_TRY(hipSetDevice(d->ordinal));
-    CV_TRY(ensure_verify_ws(*d, n));
+    Slot &sl = pick_slot(*d, d->stream);
+    CV_TRY(ensure_verify_ws(sl, n));
     const size_t waves = (n + 63) / 64;
-    uint64_t *st = nullptr;
-    CV_TRY(hipMalloc(&st, waves * 64));
-    CV_TRY(ws_begin(*d, d->stream));
+    ScopedMem st;
+    CV_TRY(hipMalloc(&st.p, waves * 64));
+    CV_TRY(ws_begin(*d, sl, d->stream));
     hipError_t e = cvk_prep_probe((uint32_t)n, static_cast<const uint8_t *>(d_pk), static_cast<const uint8_t *>(d_sig),
                                   static_cast<const uint8_t *>(d_arena), static_cast<const uint64_t *>(d_off),
-                                  static_cast<const uint32_t *>(d_len), d->ws_dig.as<uint32_t>(), d->ws_tab.as<uint32_t>(),
-                                  d->ws_cap, st, d->stream);
-    if (e == hipSuccess) e = ws_end(*d, d->stream);
+                                  static_cast<const uint32_t *>(d_len), sl.ws_dig.as<uint32_t>(), sl.ws_tab.as<uint32_t>(),
+                                  sl.ws_cap, static_cast<uint64_t *>(st.p), d->stream);
+    const hipError_t e2 = ws_end(sl, d->stream);
+    if (e == hipSuccess) e = e2;
     std::vector<uint64_t> h(waves * 8);
-    if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
-    if (e == hipSuccess) e = hipMemcpy(h.data(), st, waves * 64, hipMemcpyDeviceToHost);
-    (void)hipFree(st);
+    const hipError_t e3 = hipStreamSynchronize(d->stream);   // also on error: st is freed on return
+    if (e == hipSuccess) e = e3;
+    if (e == hipSuccess) e = hipMemcpy(h.data(), st.p, waves * 64, hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_rc(e);
     double sum[6] = {0, 0, 0, 0, 0, 0};
     for (size_t w = 0; w < waves; w++)

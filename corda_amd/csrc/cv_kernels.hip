@@ -24,6 +24,7 @@
 #include <mutex>
 
 #include "cv_kcommon.h"
+#include "cv_launch.h"
 
 // occupancy variant of the Straus kernel (waves per SIMD the register budget is built for);
 // tuned on the box with tools/ab_straus.py, default = the measured best
@@ -122,34 +123,6 @@ extern "C" void cvk_set_quad_max(uint32_t m) { g_quad_max = m; }
 static int g_split_mode = 3, g_split_pct = 10;
 extern "C" void cvk_set_split_mode(int m) { g_split_mode = (m >= 0 && m <= 3) ? m : 0; }
 extern "C" void cvk_set_split_pct(int p) { g_split_pct = (p >= 5 && p <= 50) ? p : 10; }
-struct SplitAux {
-    hipStream_t s2 = nullptr;
-    hipEvent_t start = nullptr, prep1 = nullptr, done2 = nullptr;
-    int cus = 0;
-    bool ready = false;
-    std::mutex mu;   // creation, and record/wait of the shared events, happen under it
-};
-static SplitAux g_split_aux[16];
-static hipError_t split_aux(SplitAux **out) {
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
-    if (dev < 0 || dev >= 16) return hipErrorInvalidDevice;
-    SplitAux &a = g_split_aux[dev];
-    // lazily created once per device; the lock makes two first callers (different threads) safe
-    std::lock_guard<std::mutex> lk(a.mu);
-    if (!a.ready) {
-        if (!a.s2 && (e = hipStreamCreateWithFlags(&a.s2, hipStreamNonBlocking)) != hipSuccess) return e;
-        if (!a.start && (e = hipEventCreateWithFlags(&a.start, hipEventDisableTiming)) != hipSuccess) return e;
-        if (!a.prep1 && (e = hipEventCreateWithFlags(&a.prep1, hipEventDisableTiming)) != hipSuccess) return e;
-        if (!a.done2 && (e = hipEventCreateWithFlags(&a.done2, hipEventDisableTiming)) != hipSuccess) return e;
-        if ((e = hipDeviceGetAttribute(&a.cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
-        a.ready = true;
-    }
-    *out = &a;
-    return hipSuccess;
-}
-
 static int g_comb_waves = 3;
 extern "C" void cvk_set_comb_waves(int w) { g_comb_waves = (w == 2) ? 2 : 3; }
 
@@ -196,7 +169,7 @@ hipError_t cvk_prepare(hipStream_t stream) {
 hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off,
                       const uint32_t *len, uint64_t *bitmap, uint8_t *status, uint32_t *ws_hs, uint32_t *ws_tab,
                       uint32_t *ws_R, uint8_t *ws_ok, uint32_t *ws_dig, uint32_t ws_cap, hipStream_t stream,
-                      hipEvent_t *ev) {
+                      hipEvent_t *ev, const CvkSplit *ax) {
     if (n == 0) return hipSuccess;
     if (ws_cap == 0 || ws_cap % 512) return hipErrorInvalidValue;
     // the radix-2^16 basepoint rows, for the throughput (n > quad max) and quad (n > tri max) forms
@@ -251,11 +224,8 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             continue;
         }
         if (g_verify_mode == 1 && !bw16) return hipErrorInvalidValue;   // (cannot happen: fetched above)
-        SplitAux *ax = nullptr;
         bool split = false;
-        if (!lat && g_verify_mode == 1 && g_hs_fused && g_split_mode && !ev && m >= 131072) {
-            hipError_t e = split_aux(&ax);
-            if (e != hipSuccess) return e;
+        if (ax && ax->s2 && !lat && g_verify_mode == 1 && g_hs_fused && g_split_mode && !ev && m >= 131072) {
             const uint32_t resident = (uint32_t)ax->cus * 4u * (uint32_t)g_hs_waves;   // waves in one round
             const uint32_t last = ((m + 63) / 64) % resident;
             split = g_split_mode != 3 || (resident && last && last * 100u <= resident * 12u);
@@ -268,7 +238,6 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             const uint32_t m1 = (uint32_t)(((uint64_t)m * (100 - g_split_pct) / 100) & ~(uint64_t)255);
             const uint32_t m2 = m - m1;                 // the tail keeps the batch's ragged end
             const uint32_t sub0[2] = {0, m1}, subn[2] = {m1, m2};
-            std::lock_guard<std::mutex> lk(ax->mu);
             (void)hipEventRecord(ax->start, stream);
             (void)hipStreamWaitEvent(ax->s2, ax->start, 0);
             for (int h = 0; h < 2; h++) {

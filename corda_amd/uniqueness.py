@@ -206,7 +206,13 @@ class PersistentUniquenessProvider:
                 self._db.executemany(f"INSERT OR REPLACE INTO {self.TABLE} VALUES (?, ?, ?, ?)", rows)
                 self._db.execute("COMMIT")
             except BaseException:
-                self._db.execute("ROLLBACK")
+                # a failed COMMIT (disk / fsync error) may already have rolled back: a second ROLLBACK
+                # would raise "no transaction is active" and replace the error the notary must report
+                if self._db.in_transaction:
+                    try:
+                        self._db.execute("ROLLBACK")
+                    except Exception:  # noqa: BLE001 - the original exception is the one to report
+                        pass
                 raise
         return out
 

@@ -1,0 +1,204 @@
+"""The pipelined host-buffer path (cv_ed25519_verify_batch above the pipeline threshold: sub-chunks dealt
+over the device's workspace slots, packing / DMA / kernels overlapped), the device API's workspace slots
+(calls on different streams run concurrently), and RCCL on the GPU (a 1-rank "nccl" group).
+
+Reference call sites the host path replaces: SignedTransaction.checkSignaturesAreValid
+(core/src/main/kotlin/net/corda/core/transactions/SignedTransaction.kt:82-87) and the resolve loop
+(core/src/main/kotlin/net/corda/flows/ResolveTransactionsFlow.kt:105-111); the commit-step gather
+replaces NotaryFlow.kt:133-141's single-node view."""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from corda_amd import native, workload
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+PIPE_DEFAULT = (131072, 65536, 262144, 8)
+
+
+def _bits(bitmap, n):
+    return native.bitmap_to_bools(np.asarray(bitmap, dtype=np.uint64), n)
+
+
+def _set_pipe(min_n, first, chunk, threads):
+    lib = native.load()
+    lib.cvk_set_pipe.argtypes = [ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int]
+    lib.cvk_set_pipe(min_n, first, chunk, threads)
+
+
+def _bad_key_records(corpus):
+    """golden records whose key is not a valid point (status CV_SIG_BAD_KEY, verdict 0)"""
+    return np.nonzero(corpus["status"] == 1)[0]
+
+
+def test_host_pipeline_large_exact_pattern(engine, corpus):
+    """2^22 + 200,003 distinct-key signatures over 300-byte messages through the
+    host-buffer C-ABI — the pipeline's sub-chunks cross the 2^22 workspace-chunk boundary and end ragged.
+    Every 16th S bit flipped (rejected), every 97th R byte flipped (rejected), every 1,009th key replaced
+    by a golden not-a-point key (rejected, status 1); everything else accepted; bits past n clear."""
+    n = (1 << 22) + 200_003
+    b = workload.make_batch(engine, 0, n, 300, seed=3101)
+    expect = workload.corrupt_fraction(b, 16)
+    idx = torch.arange(5, n, 97, device=DEV)
+    b.sig[idx, 3] ^= 0x40
+    expect[idx] = False
+    pk, sig, arena, off, ln = b.to_host()
+    del b
+    torch.cuda.empty_cache()
+    pk = pk.copy()
+    bad = _bad_key_records(corpus)
+    kidx = np.arange(11, n, 1009)
+    pk[kidx] = corpus["pk"][bad[kidx % len(bad)]]
+    exp = expect.cpu().numpy()
+    exp[kidx] = False
+    st_exp = np.zeros(n, np.uint8)
+    st_exp[kidx] = 1
+    bitmap, status = engine.verify_batch(pk, sig, arena, off, ln)
+    got = _bits(bitmap, n)
+    assert np.array_equal(got, exp), f"{int((got != exp).sum())} verdicts differ"
+    assert np.array_equal(status, st_exp)
+    assert int(bitmap[-1]) >> (n % 64) == 0
+
+
+@pytest.mark.parametrize("first,chunk", [(64, 64 * 17), (64 * 5, 64 * 3), (1024, 4096)])
+def test_host_pipeline_small_subchunks_golden(engine, corpus, first, chunk):
+    """The pipeline forced onto tiny sub-chunks (first / steady sizes, so one batch has hundreds of
+    them, in every kernel form from tri-chain to throughput) over the golden corpus tiled to a ragged
+    9,001 records in random order: every verdict and status byte equals the pinned corpus values."""
+    rng = np.random.default_rng(first + chunk)
+    n = 9001
+    sel = rng.integers(0, len(corpus["pk"]), n)
+    try:
+        _set_pipe(512, first, chunk, 3)
+        bitmap, status = engine.verify_batch(corpus["pk"][sel], corpus["sig"][sel], corpus["arena"],
+                                             corpus["off"][sel], corpus["len"][sel])
+    finally:
+        _set_pipe(*PIPE_DEFAULT)
+    assert np.array_equal(_bits(bitmap, n), corpus["verdict"][sel].astype(bool))
+    assert np.array_equal(status, corpus["status"][sel])
+    assert int(bitmap[-1]) >> (n % 64) == 0
+
+
+def test_host_pipeline_scattered_arena(engine, corpus, oracle_c):
+    """Messages scattered over a 96 MB arena in reverse order with gaps (the staging gathers them back
+    to back: the "compact" form), mixed lengths 0..700 bytes, corrupted S / R / keys: the pipelined and
+    the small host paths both equal the C oracle."""
+    rng = np.random.default_rng(77)
+    n = 200_000
+    lens = rng.integers(0, 701, n).astype(np.uint32)
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    arena = np.zeros(96 << 20, np.uint8)
+    gap = (arena.size - int(lens.sum()) - 64) // n
+    offs = np.zeros(n, np.uint64)
+    pos = arena.size - 32
+    for i in range(n):                               # last record first: offsets decrease
+        pos -= int(lens[i]) + int(rng.integers(0, gap + 1))
+        offs[i] = pos
+    arena[:] = rng.integers(0, 256, arena.size, dtype=np.uint8)
+    pk, sig = engine.sign_batch(seeds, arena, offs, lens)
+    sig[1::9, 40] ^= 0x04
+    sig[2::13, 7] ^= 0x01
+    pk[3::17, 30] ^= 0x20
+    ref, rst = oracle_c.verify_batch(pk, sig, arena, offs, lens, nthreads=8)
+    bitmap, status = engine.verify_batch(pk, sig, arena, offs, lens)
+    assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
+    assert np.array_equal(status, rst)
+    try:                                             # the same batch on the small (one-DMA) path
+        _set_pipe(1 << 30, 0, 0, 0)
+        b2, s2 = engine.verify_batch(pk, sig, arena, offs, lens)
+    finally:
+        _set_pipe(*PIPE_DEFAULT)
+    assert np.array_equal(b2, bitmap) and np.array_equal(s2, status)
+
+
+def test_device_api_streams_take_separate_slots(engine):
+    """Device-API calls on four streams (more streams than workspace slots), several rounds, interleaved
+    with a pipelined host-buffer call that uses every slot on its own streams: each bitmap is exact
+    (honest batch all ones; the others their corruption patterns)."""
+    n = 200_000
+    batches = [workload.make_batch(engine, 0, n, 32, seed=1200 + k) for k in range(4)]
+    expects = [torch.ones(n, dtype=torch.bool, device=DEV)] + [workload.corrupt_fraction(batches[k], k + 2)
+                                                               for k in range(1, 4)]
+    streams = [torch.cuda.Stream(DEV) for _ in range(4)]
+    bms = [torch.zeros((n + 63) // 64, dtype=torch.int64, device=DEV) for _ in range(4)]
+    hb = workload.make_batch(engine, 0, 300_000, 64, seed=1299)
+    hexp = workload.corrupt_fraction(hb, 5).cpu().numpy()
+    hpk, hsig, harena, hoff, hln = hb.to_host()
+    torch.cuda.synchronize()
+    for r in range(3):
+        for k in range(4):
+            b = batches[k]
+            engine.verify_device(0, n, b.pk.data_ptr(), b.sig.data_ptr(), b.arena.data_ptr(), b.off.data_ptr(),
+                                 b.len.data_ptr(), bms[k].data_ptr(), 0, streams[k].cuda_stream)
+            if r == 1 and k == 1:
+                hbm, _ = engine.verify_batch(hpk, hsig, harena, hoff, hln, want_status=False)
+                assert np.array_equal(_bits(hbm, hb.n), hexp)
+    torch.cuda.synchronize()
+    for k in range(4):
+        assert torch.equal(torch.from_numpy(_bits(bms[k].cpu().numpy().view(np.uint64), n)).to(DEV), expects[k])
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_rccl_one_rank_gather_and_sharded_notary(engine, corpus):
+    """the commit-step collective on the GPU.  A 1-rank "nccl" process group (RCCL) on
+    cuda:0: gather_bitmaps of device tensors returns the local bitmaps, and BatchingNotary(group=pg) on a
+    mixed batch (golden rejected records, a double spend, missing signers, a bad signature) decides
+    exactly what the same notary without a group decides.  librccl must be mapped into the process."""
+    import torch.distributed as dist
+    from corda_amd import distributed as D
+    from corda_amd.notary import BatchingNotary, SignRequest
+    from corda_amd.crypto import DigitalSignature, EdDSAPublicKey
+    from corda_amd.transactions import SignedTransaction
+    import test_gpu_mirror as M
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        pg = dist.group.WORLD
+        n = 1000
+        rng = np.random.default_rng(5)
+        local = torch.from_numpy(rng.integers(-2**62, 2**62, (2, D.shard_words(n, 1)), dtype=np.int64)).to(DEV)
+        glob = D.gather_bitmaps(local, n, pg)
+        torch.cuda.synchronize()
+        assert torch.equal(glob, local[:, : (n + 63) // 64])
+        with open("/proc/self/maps") as f:
+            assert "rccl" in f.read(), "librccl is not mapped: the collective did not go through RCCL"
+
+        seed = bytes(range(1, 33))
+        reqs = []
+        for i in range(6):
+            reqs.append(SignRequest(M.make_stx(engine, signer_idx=[130 + i], inputs=(b"rccl-state-%d" % i,)),
+                                    caller=f"p{i}"))
+        reqs.append(SignRequest(M.make_stx(engine, signer_idx=[140], inputs=(b"rccl-state-0",)), caller="double"))
+        reqs.append(SignRequest(M.make_stx(engine, signer_idx=[141], must_idx=[141, 142], inputs=(b"r-141",)),
+                                caller="missing"))
+        bad = M.make_stx(engine, signer_idx=[143], inputs=(b"r-143",))
+        reqs.append(SignRequest(SignedTransaction(bad._wtx, [DigitalSignature.WithKey(bad.sigs[0].by, b"\x05" * 64)],
+                                                  bad.id), caller="badsig"))
+        rej = np.nonzero(corpus["verdict"] == 0)[0][:5]
+        for j, i in enumerate(rej):                  # golden rejected records as a transaction's signature
+            st = M.make_stx(engine, signer_idx=[150 + j], inputs=(b"r-gold-%d" % j,))
+            key = EdDSAPublicKey(corpus["pk"][i].tobytes())
+            reqs.append(SignRequest(SignedTransaction(st._wtx, [DigitalSignature.WithKey(key, corpus["sig"][i].tobytes())],
+                                                      st.id), caller=f"gold{j}"))
+        got = BatchingNotary(seed, validating=True, engine=engine, group=pg).notarise(reqs)
+        want = BatchingNotary(seed, validating=True, engine=engine).notarise(reqs)
+        assert [r.ok for r in got] == [r.ok for r in want]
+        assert sum(r.ok for r in got) == 6
+        for g, w in zip(got, want):
+            assert type(g.error) is type(w.error) and type(g.failure) is type(w.failure)
+            if g.ok:
+                assert g.sig.bits == w.sig.bits
+    finally:
+        dist.destroy_process_group()

@@ -154,3 +154,30 @@ def test_persistent_concurrent_batches_never_double_spend(tmp_path):
         t.join()
     assert sum(wins) == len(p) <= len(pool)        # every state consumed at most once
     p.close()
+
+
+def test_failed_commit_reports_its_own_error(tmp_path):
+    """when COMMIT itself fails (a disk / fsync error) SQLite has already rolled the
+    transaction back; commit_batch must re-raise THAT error (not "no transaction is active" from a
+    second ROLLBACK), and nothing of the batch is stored."""
+    import sqlite3
+    p = PersistentUniquenessProvider(str(tmp_path / "failing.db"))
+    real = p._db
+
+    class FailingCommit:
+        def __getattr__(self, name):
+            return getattr(real, name)
+
+        def execute(self, sql, *a):
+            if sql == "COMMIT":
+                real.execute("ROLLBACK")
+                raise sqlite3.OperationalError("disk I/O error")
+            return real.execute(sql, *a)
+
+    p._db = FailingCommit()
+    with pytest.raises(sqlite3.OperationalError, match="disk I/O error"):
+        p.commit_batch([([generate_state_ref()], random_sha256(), "N")])
+    p._db = real
+    assert len(p) == 0
+    assert p.commit_batch([([generate_state_ref()], random_sha256(), "N")]) == [None]
+    p.close()
