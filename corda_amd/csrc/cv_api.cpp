@@ -5,8 +5,12 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
+#include <condition_variable>
 #include <cstring>
 #include <chrono>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <random>
 #include <thread>
@@ -137,7 +141,80 @@ struct Slot {
     hipEvent_t h2d = nullptr;     // recorded after the last DMA out of pin_in
     bool h2d_pending = false;
 };
-constexpr int kSlots = 3;
+constexpr int kSlots = 4;
+
+// A fixed set of host threads for index-parallel jobs (the host-buffer path's packing and range scans):
+// run(ntasks, fn) calls fn(i) for every i in [0, ntasks) on the helpers and the calling thread and
+// returns when all are done.  Created once per device, so a pipelined call does not pay a thread start
+// per sub-chunk (round-3 probe: ~14 thread starts per sub-chunk held C5's host path at 11 GB/s).
+class WorkerPool {
+  public:
+    explicit WorkerPool(int helpers) {
+        for (int t = 0; t < helpers; t++) th_.emplace_back([this] { loop(); });
+    }
+    ~WorkerPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    int threads() const { return (int)th_.size() + 1; }
+    void run(size_t ntasks, const std::function<void(size_t)> &fn) {
+        if (ntasks == 0) return;
+        if (th_.empty() || ntasks == 1) {
+            for (size_t i = 0; i < ntasks; i++) fn(i);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            job_ = &fn;
+            ntasks_ = ntasks;
+            next_.store(0);
+            busy_ = th_.size();
+            gen_++;
+        }
+        cv_.notify_all();
+        drain(fn, ntasks);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [this] { return busy_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    void drain(const std::function<void(size_t)> &fn, size_t ntasks) {
+        for (size_t i; (i = next_.fetch_add(1)) < ntasks;) fn(i);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(size_t)> *job;
+            size_t ntasks;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                job = job_;
+                ntasks = ntasks_;
+            }
+            drain(*job, ntasks);
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                if (--busy_ == 0) done_cv_.notify_one();
+            }
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(size_t)> *job_ = nullptr;
+    size_t ntasks_ = 0, busy_ = 0;
+    std::atomic<size_t> next_{0};
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
 
 struct Device {
     int ordinal = 0;
@@ -148,6 +225,14 @@ struct Device {
     Slot slot[kSlots];
     uint64_t clock = 0;
     KeyCache kc;
+    std::unique_ptr<WorkerPool> pool;    // host packing threads (created on the first large host batch)
+    WorkerPool &workers(int threads) {
+        if (!pool || pool->threads() != threads) {
+            pool.reset();
+            pool.reset(new WorkerPool(threads - 1));
+        }
+        return *pool;
+    }
 };
 
 // key-table pool capacity per device (keys); 66 KB of tables per key (1.1 GB at the default; the pool
@@ -173,6 +258,18 @@ constexpr uint32_t kVerifyChunk = 1u << 22;
 // sub-chunk into pinned staging while the earlier ones transfer and verify.
 static size_t g_pipe_min = 131072, g_pipe_first = 65536, g_pipe_chunk = 262144;
 static int g_pack_threads = 8;
+static int g_pipe_slots = 3;   // slots the pipeline deals its sub-chunks over (2..kSlots)
+// host-side time of the pipelined path, seconds (cvk_pipe_stats): range scans, packing, waits for a
+// slot's staging, enqueue (HIP calls), the final synchronisation; and calls / sub-chunks
+struct PipeStats {
+    double plan = 0, pack = 0, wait = 0, enq = 0, sync = 0;
+    uint64_t calls = 0, chunks = 0;
+};
+static PipeStats g_pipe_stats;
+static std::mutex g_pipe_stats_mu;
+static inline double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 hipError_t slot_events(Slot &sl) {
     hipError_t e = hipSuccess;
@@ -345,11 +442,29 @@ void cvk_set_virtual_devices(int k) { g_virtual_devices = (k >= 1 && k <= 16) ? 
 
 // Tuning knob (internal): the host-buffer pipeline's shard threshold, first and steady sub-chunk sizes
 // (signatures; 0 keeps the current value) and packing threads.
+void cvk_set_pipe_slots(int k) { g_pipe_slots = (k >= 2 && k <= kSlots) ? k : 3; }
 void cvk_set_pipe(size_t min_n, size_t first, size_t chunk, int threads) {
     if (min_n) g_pipe_min = min_n;
     if (first) g_pipe_first = std::max<size_t>(64, first / 64 * 64);
     if (chunk) g_pipe_chunk = std::max<size_t>(64, chunk / 64 * 64);
     if (threads > 0) g_pack_threads = std::min(threads, 64);
+}
+
+// Diagnostic knob: out[7] = {plan, pack, wait, enqueue, sync seconds, calls, sub-chunks} of the
+// pipelined host path since the last reset.
+void cvk_pipe_stats(double *out, int reset) {
+    std::lock_guard<std::mutex> g(g_pipe_stats_mu);
+    const PipeStats &p = g_pipe_stats;
+    if (out) {
+        out[0] = p.plan;
+        out[1] = p.pack;
+        out[2] = p.wait;
+        out[3] = p.enq;
+        out[4] = p.sync;
+        out[5] = (double)p.calls;
+        out[6] = (double)p.chunks;
+    }
+    if (reset) g_pipe_stats = PipeStats{};
 }
 
 int cv_open(uint32_t device_mask, cv_ctx **out) {
@@ -369,7 +484,7 @@ int cv_open(uint32_t device_mask, cv_ctx **out) {
                 cv_close(ctx);
                 return CV_E_HIP;
             }
-            ctx->devs.push_back(dev);
+            ctx->devs.push_back(std::move(dev));
             // Per-device basepoint rows (16.8 MB, built once per process): eager, so the first
             // verify is not charged for them and no later call synchronises to build them.
             if (v == 0 && cvk_prepare(dev.stream) != hipSuccess) {
@@ -426,40 +541,30 @@ static Device *find_dev(cv_ctx *ctx, int device) {
 // ---------------------------------------------------------------- verify (host buffers)
 static inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-// Host copies into pinned staging.  A large copy is done by several threads (one core copies
-// ~10 GB/s, below what the DMA takes): each segment is cut into >= 512 KB pieces dealt out
-// round-robin; `extra` runs on the calling thread meanwhile.
+// Host copies into pinned staging.  A large copy is done by the device's worker pool (one core copies
+// ~10-12 GB/s, below what the DMA takes): each segment is cut into 256 KB pieces the workers take in
+// turn.  Copies below 1 MB stay on the calling thread (a notary batch: waking workers costs more).
 struct CopyJob {
     void *dst;
     const void *src;
     size_t len;
 };
-template <class F> static void par_copy(const std::vector<CopyJob> &jobs, int threads, F extra) {
-    constexpr size_t kPiece = 512 * 1024;
+static void par_copy(const std::vector<CopyJob> &jobs, WorkerPool *pool) {
+    constexpr size_t kPiece = 256 * 1024;
     size_t total = 0;
     for (const CopyJob &j : jobs) total += j.len;
-    threads = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads, total / kPiece));
-    if (threads <= 1) {
+    if (!pool || pool->threads() <= 1 || total < 4 * kPiece) {
         for (const CopyJob &j : jobs)
             if (j.len) std::memcpy(j.dst, j.src, j.len);
-        extra();
         return;
     }
     std::vector<CopyJob> pieces;
+    pieces.reserve(total / kPiece + jobs.size());
     for (const CopyJob &j : jobs)
         for (size_t o = 0; o < j.len; o += kPiece)
             pieces.push_back({static_cast<uint8_t *>(j.dst) + o, static_cast<const uint8_t *>(j.src) + o,
                               std::min(kPiece, j.len - o)});
-    auto work = [&pieces, threads](int t) {
-        for (size_t k = (size_t)t; k < pieces.size(); k += (size_t)threads)
-            std::memcpy(pieces[k].dst, pieces[k].src, pieces[k].len);
-    };
-    std::vector<std::thread> th;
-    th.reserve((size_t)threads - 1);
-    for (int t = 1; t < threads; t++) th.emplace_back(work, t);
-    extra();
-    work(0);
-    for (auto &x : th) x.join();
+    pool->run(pieces.size(), [&pieces](size_t k) { std::memcpy(pieces[k].dst, pieces[k].src, pieces[k].len); });
 }
 
 // Staging layout of records [b, e): pk | sig | off | len | arena, 16-B aligned parts.  The arena part is
@@ -472,14 +577,35 @@ struct Stage {
     uint64_t lo = 0, hi = 0;
     bool compact = false;
 };
-static Stage stage_plan(size_t b, size_t e, const uint64_t *off, const uint32_t *len) {
+static Stage stage_plan(size_t b, size_t e, const uint64_t *off, const uint32_t *len, WorkerPool *pool = nullptr) {
     Stage st;
     st.n = e - b;
+    // the range scan, in slices of 64K records over the pool
+    constexpr size_t kSlice = 65536;
+    const size_t nslices = (st.n + kSlice - 1) / kSlice;
+    struct R {
+        uint64_t lo = UINT64_MAX, hi = 0, bytes = 0;
+    };
+    std::vector<R> part(std::max<size_t>(nslices, 1));
+    auto scan = [&](size_t k) {
+        R r;
+        const size_t i1 = std::min(e, b + (k + 1) * kSlice);
+        for (size_t i = b + k * kSlice; i < i1; i++) {
+            r.lo = std::min<uint64_t>(r.lo, off[i]);
+            r.hi = std::max<uint64_t>(r.hi, off[i] + len[i]);
+            r.bytes += len[i];
+        }
+        part[k] = r;
+    };
+    if (pool && nslices > 1)
+        pool->run(nslices, scan);
+    else
+        for (size_t k = 0; k < nslices; k++) scan(k);
     uint64_t lo = UINT64_MAX, hi = 0, bytes = 0;
-    for (size_t i = b; i < e; i++) {
-        lo = std::min<uint64_t>(lo, off[i]);
-        hi = std::max<uint64_t>(hi, off[i] + len[i]);
-        bytes += len[i];
+    for (const R &r : part) {
+        lo = std::min(lo, r.lo);
+        hi = std::max(hi, r.hi);
+        bytes += r.bytes;
     }
     if (hi < lo) lo = hi = 0;
     lo &= ~(uint64_t)15;
@@ -495,18 +621,18 @@ static Stage stage_plan(size_t b, size_t e, const uint64_t *off, const uint32_t 
     st.total = st.o_ar + al16(st.hi - st.lo + 16);
     return st;
 }
-// Packs records [b, e) into h by the plan (keys + signatures first when `first_part` is given: it runs
-// before the rest so their DMA can start early).
+// Packs records [b, e) into h by the plan (keys + signatures first: `first_part` runs after them, so
+// their DMA can start while the rest is packed).
 template <class F>
 static void stage_pack(const Stage &st, uint8_t *h, size_t b, const uint8_t *pk, const uint8_t *sig,
-                       const uint8_t *arena, const uint64_t *off, const uint32_t *len, int threads, F first_part) {
+                       const uint8_t *arena, const uint64_t *off, const uint32_t *len, WorkerPool *pool, F first_part) {
     const size_t n = st.n;
-    par_copy({{h + st.o_pk, pk + b * 32, n * 32}, {h + st.o_sig, sig + b * 64, n * 64}}, threads, [] {});
+    par_copy({{h + st.o_pk, pk + b * 32, n * 32}, {h + st.o_sig, sig + b * 64, n * 64}}, pool);
     first_part();
     uint64_t *hoff = reinterpret_cast<uint64_t *>(h + st.o_off);
     uint8_t *har = h + st.o_ar;
     if (st.compact) {
-        par_copy({{h + st.o_len, len + b, n * 4}}, 1, [] {});
+        par_copy({{h + st.o_len, len + b, n * 4}}, nullptr);
         uint64_t pos = 0;
         for (size_t i = 0; i < n; i++) {
             hoff[i] = pos;
@@ -516,7 +642,7 @@ static void stage_pack(const Stage &st, uint8_t *h, size_t b, const uint8_t *pk,
     } else {
         par_copy({{h + st.o_off, off + b, n * 8}, {h + st.o_len, len + b, n * 4},
                   {har, st.hi > st.lo ? arena + st.lo : nullptr, (size_t)(st.hi - st.lo)}},
-                 threads, [] {});
+                 pool);
     }
     std::memset(har + (st.hi - st.lo), 0, 16);
 }
@@ -529,7 +655,8 @@ static int verify_shard_small(Device &d, size_t b, size_t e, const uint8_t *pk, 
                               const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
                               uint8_t *status, int threads) {
     const size_t n = e - b;
-    const Stage st = stage_plan(b, e, off, len);
+    WorkerPool *pool = n >= 16384 ? &d.workers(threads) : nullptr;
+    const Stage st = stage_plan(b, e, off, len, pool);
     const size_t words = (n + 63) / 64;
     const size_t o_bm = 0, o_st = al16(words * 8), total_out = o_st + al16(n);
     Slot &sl = d.slot[0];
@@ -554,7 +681,7 @@ static int verify_shard_small(Device &d, size_t b, size_t e, const uint8_t *pk, 
     // 1.29-1.34 -> 1.21-1.25 ms p50); below, one DMA (a second DMA's ~6 us would cost more than it hides).
     const bool two_stage = st.o_off >= ((size_t)1 << 20);
     hipError_t e1 = hipSuccess;
-    stage_pack(st, h, b, pk, sig, arena, off, len, threads, [&] {
+    stage_pack(st, h, b, pk, sig, arena, off, len, pool, [&] {
         if (two_stage) e1 = hipMemcpyAsync(dv, h, st.o_off, hipMemcpyHostToDevice, s);
     });
     CV_TRY(e1);
@@ -574,33 +701,46 @@ static int verify_shard_small(Device &d, size_t b, size_t e, const uint8_t *pk, 
     return CV_OK;
 }
 
+// The pipeline's sub-chunk boundaries of [b, e): [first, C, C, ..., the last two balanced]; every
+// boundary but e is b + a multiple of 64 (whole bitmap words per sub-chunk).
+static std::vector<size_t> pipe_cuts(size_t b, size_t e, size_t first, size_t C) {
+    std::vector<size_t> cut{b};
+    if (e <= b) return cut;
+    first = std::max<size_t>(64, first / 64 * 64);
+    C = std::max<size_t>(64, C / 64 * 64);
+    size_t p = b + std::min(e - b, first);
+    cut.push_back(p);
+    while (p < e) {
+        const size_t rem = e - p;
+        const size_t m = rem <= C ? rem : rem < 2 * C ? (rem / 2 + 63) / 64 * 64 : C;
+        p += m;
+        cut.push_back(p);
+    }
+    return cut;
+}
+
 // One shard [b, e) of a large batch, pipelined: sub-chunks (multiples of 64 signatures) go round-robin
-// over the device's kSlots slots.  Sub-chunk j is packed by the host threads into slot j % kSlots's
-// pinned staging (after that slot's previous DMA has left it), moved by one DMA on the slot's stream,
-// verified there with the slot's workspace, and its bitmap words (+ status) copied into the shard's
-// pinned output.  So packing sub-chunk j+1, the DMA of sub-chunk j and the kernels of sub-chunks j-1 and
-// j-2 overlap, and the slots' kernels fill each other's drains.
+// over g_pipe_slots of the device's slots.  Sub-chunk j is packed by the host threads into slot
+// j % R's pinned staging (after that slot's previous DMA has left it), moved by one DMA on the slot's
+// stream and verified there with the slot's workspace, its bitmap words (+ status) landing in the
+// shard's device output.  So packing sub-chunk j+1, the DMA of sub-chunk j and the kernels of the
+// sub-chunks before it overlap, and the slots' kernels fill each other's drains.
+// No copy is ever enqueued behind a kernel that is still running: the DMA of sub-chunk j is enqueued
+// only after the host has seen the slot's previous verify finish, and the verdicts come back in ONE
+// copy after the last verify.  (A copy that waits for a kernel holds the DMA queue for the other
+// streams' copies behind it: with a bitmap copy after every sub-chunk, each sub-chunk's input DMA
+// waited for the previous sub-chunk's kernels and the pipeline ran at compute + transfer time,
+// C5 8M: 74 + 20 ms, tools/subchunk_probe.py.)
 static int verify_shard_pipe(Device &d, size_t b, size_t e, const uint8_t *pk, const uint8_t *sig,
                              const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
                              uint8_t *status, int threads) {
     const size_t n = e - b;
     const size_t words = (n + 63) / 64;
     const size_t o_st = al16(words * 8), total_out = o_st + al16(n);
-    // the sub-chunk plan: [first, C, C, ..., the last two balanced], all but the last multiples of 64
-    std::vector<size_t> cut{b};
-    {
-        const size_t C = g_pipe_chunk;
-        size_t p = b + std::min(n, g_pipe_first);
-        cut.push_back(p);
-        while (p < e) {
-            const size_t rem = e - p;
-            const size_t m = rem <= C ? rem : rem < 2 * C ? (rem / 2 + 63) / 64 * 64 : C;
-            p += m;
-            cut.push_back(p);
-        }
-    }
-    hipStream_t ss[kSlots];
-    for (int k = 0; k < kSlots; k++) {
+    const std::vector<size_t> cut = pipe_cuts(b, e, g_pipe_first, g_pipe_chunk);
+    const int nsl = g_pipe_slots;
+    hipStream_t ss[kSlots] = {};
+    for (int k = 0; k < nsl; k++) {
         CV_TRY(slot_stream(d, k, &ss[k]));
         CV_TRY(slot_events(d.slot[k]));
     }
@@ -609,18 +749,25 @@ static int verify_shard_pipe(Device &d, size_t b, size_t e, const uint8_t *pk, c
     uint8_t *dout = d.bitmap.as<uint8_t>();
     uint8_t *hout = d.pin_out.as<uint8_t>();
     auto drain = on_exit([&] {
-        for (int k = 0; k < kSlots; k++) (void)hipStreamSynchronize(ss[k]);
+        for (int k = 0; k < nsl; k++) (void)hipStreamSynchronize(ss[k]);
         for (Slot &sl : d.slot) sl.h2d_pending = false;
     });
+    WorkerPool *pool = &d.workers(threads);
+    PipeStats ps;
     for (size_t j = 0; j + 1 < cut.size(); j++) {
         const size_t c0 = cut[j], c1 = cut[j + 1], m = c1 - c0;
-        Slot &sl = d.slot[j % kSlots];
-        hipStream_t s = ss[j % kSlots];
-        const Stage st = stage_plan(c0, c1, off, len);
+        Slot &sl = d.slot[j % nsl];
+        hipStream_t s = ss[j % nsl];
+        double t0 = now_s();
+        const Stage st = stage_plan(c0, c1, off, len, pool);
+        double t1 = now_s();
+        ps.plan += t1 - t0;
         if (sl.h2d_pending) {                       // the slot's staging is free once its DMA is done
             CV_TRY(hipEventSynchronize(sl.h2d));
             sl.h2d_pending = false;
         }
+        t0 = now_s();
+        ps.wait += t0 - t1;
         if (st.total > sl.pin_in.cap || st.total > sl.packed.cap) {
             CV_TRY(hipStreamSynchronize(s));        // the device copy may still be read by a queued verify
             CV_TRY(sl.pin_in.ensure(st.total));
@@ -628,7 +775,15 @@ static int verify_shard_pipe(Device &d, size_t b, size_t e, const uint8_t *pk, c
         }
         uint8_t *h = sl.pin_in.as<uint8_t>();
         uint8_t *dv = sl.packed.as<uint8_t>();
-        stage_pack(st, h, c0, pk, sig, arena, off, len, threads, [] {});
+        stage_pack(st, h, c0, pk, sig, arena, off, len, pool, [] {});
+        t1 = now_s();
+        ps.pack += t1 - t0;
+        // the slot's device input block is free once its last launch group (sub-chunk j - R, or a
+        // device-API call) has finished: wait for that here, so the DMA below depends on nothing
+        if (sl.last) CV_TRY(hipEventSynchronize(sl.ev));
+        t0 = now_s();
+        ps.wait += t0 - t1;
+        t1 = t0;
         CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, s));
         CV_TRY(hipEventRecord(sl.h2d, s));
         sl.h2d_pending = true;
@@ -638,11 +793,26 @@ static int verify_shard_pipe(Device &d, size_t b, size_t e, const uint8_t *pk, c
                              reinterpret_cast<const uint32_t *>(dv + st.o_len),
                              reinterpret_cast<uint64_t *>(dout) + w0, status ? dout + o_st + (c0 - b) : nullptr, s,
                              nullptr, false));
-        CV_TRY(hipMemcpyAsync(hout + w0 * 8, dout + w0 * 8, ((m + 63) / 64) * 8, hipMemcpyDeviceToHost, s));
-        if (status) CV_TRY(hipMemcpyAsync(hout + o_st + (c0 - b), dout + o_st + (c0 - b), m, hipMemcpyDeviceToHost, s));
+        ps.enq += now_s() - t1;
+        ps.chunks++;
     }
-    for (int k = 0; k < kSlots; k++) CV_TRY(hipStreamSynchronize(ss[k]));
+    const double t0 = now_s();
+    for (int k = 0; k < nsl; k++) CV_TRY(hipStreamSynchronize(ss[k]));
+    CV_TRY(hipMemcpyAsync(hout, dout, status ? o_st + n : words * 8, hipMemcpyDeviceToHost, ss[0]));
+    CV_TRY(hipStreamSynchronize(ss[0]));
+    ps.sync += now_s() - t0;
     drain.armed = false;
+    {
+        std::lock_guard<std::mutex> g(g_pipe_stats_mu);
+        PipeStats &G = g_pipe_stats;
+        G.plan += ps.plan;
+        G.pack += ps.pack;
+        G.wait += ps.wait;
+        G.enq += ps.enq;
+        G.sync += ps.sync;
+        G.calls++;
+        G.chunks += ps.chunks;
+    }
     for (Slot &sl : d.slot) sl.h2d_pending = false;
     std::memcpy(bitmap + b / 64, hout, words * 8);
     if (status) std::memcpy(status + b, hout + o_st, n);

@@ -11,7 +11,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "_build", "libcvoracle.so")
+# CV_ORACLE_LIB: a prebuilt variant of the same C file (tests/sanitize: ASan + UBSan build)
+_LIB_PATH = os.environ.get("CV_ORACLE_LIB") or os.path.join(_HERE, "_build", "libcvoracle.so")
 _lib = None
 
 

@@ -43,6 +43,8 @@ def oracle_c():
 def host_harness():
     """The product's per-lane device code compiled for the CPU (tests/host_harness.cpp)."""
     import ctypes
+    if os.environ.get("CV_HOST_LIB"):        # a prebuilt variant (tests/sanitize: ASan + UBSan build)
+        return ctypes.CDLL(os.environ["CV_HOST_LIB"])
     lib = os.path.join(REPO, "tests", "_build", "libcvhost.so")
     src = os.path.join(REPO, "tests", "host_harness.cpp")
     deps = [src] + [os.path.join(REPO, "corda_amd", "csrc", f) for f in os.listdir(os.path.join(REPO, "corda_amd", "csrc"))

@@ -19,8 +19,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from corda_amd import native, workload  # noqa: E402
 
 SETTINGS = [  # (first, chunk, threads)
-    (65536, 262144, 8), (32768, 131072, 8), (65536, 524288, 8), (131072, 262144, 8),
-    (65536, 262144, 4), (65536, 262144, 12), (16384, 131072, 8),
+    (32768, 131072, 8), (65536, 262144, 8), (32768, 131072, 12), (32768, 131072, 16), (16384, 65536, 8),
+    (32768, 131072, 4),
 ]
 
 
@@ -32,6 +32,7 @@ def main():
     a = ap.parse_args()
     lib = native.load()
     lib.cvk_set_pipe.argtypes = [ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int]
+    lib.cvk_pipe_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
     eng = native.Engine(1)
     dev = torch.device("cuda", 0)
     for name, n, ml in (("c2", a.n2, 300), ("c5", a.n5, 32)):
@@ -52,6 +53,16 @@ def main():
         pk, sig, arena, off, ln = b.to_host()
         del b
         torch.cuda.empty_cache()
+        h = torch.empty(256 << 20, dtype=torch.uint8, pin_memory=True)
+        dd = torch.empty(256 << 20, dtype=torch.uint8, device=dev)
+        for _ in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            dd.copy_(h, non_blocking=True)
+            e1.record()
+            e1.synchronize()
+            print(json.dumps({"h2d_pinned_gb_per_s": (256 << 20) / e0.elapsed_time(e1) / 1e6}), flush=True)
+        del h, dd
         for first, chunk, th in SETTINGS + SETTINGS[:1]:
             lib.cvk_set_pipe(131072, first, chunk, th)
             eng.verify_batch(pk, sig, arena, off, ln, want_status=False)
@@ -61,8 +72,14 @@ def main():
                 bm, _ = eng.verify_batch(pk, sig, arena, off, ln, want_status=False)
                 ts.append(time.perf_counter() - t)
             assert native.bitmap_to_bools(bm, n).all()
+            st = (ctypes.c_double * 7)()
+            lib.cvk_pipe_stats(st, 1)
+            calls = max(st[5], 1)
             print(json.dumps({"shape": name, "first": first, "chunk": chunk, "threads": th,
-                              "ms_med": float(np.median(ts) * 1e3), "ms_min": float(np.min(ts) * 1e3)}), flush=True)
+                              "ms_med": float(np.median(ts) * 1e3), "ms_min": float(np.min(ts) * 1e3),
+                              "host_ms_per_call": {k: st[i] / calls * 1e3 for i, k in
+                                                   enumerate(("plan", "pack", "wait", "enqueue", "sync"))},
+                              "subchunks_per_call": st[6] / calls}), flush=True)
         # pack-only and copy-only rates of the host (what bounds the pipeline besides the GPU)
         t = time.perf_counter()
         _ = np.concatenate([pk.reshape(-1), sig.reshape(-1), arena])
