@@ -395,13 +395,62 @@ def run_c3(eng, local, rank, world, sh, dev, ntx: int, steps: int, warmup: int):
         mk.append(e0.elapsed_time(e1))
     ph = np.mean(np.array([eng.verify_device_timed(local, n, *sig_args, sh) for _ in range(max(2, steps))]), axis=0)
     merkle_ms = float(np.mean(mk))
+    comp = merkle_compressions(tb.leaf_len, tb.tx_begin)
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt[0])
     tb = None
     return {"n": n, "ntx": ntx, "elapsed": elapsed, "merkle_ms": merkle_ms, "phases": ph,
-            "leaves": nleaves}
+            "leaves": nleaves, "compressions": comp}
+
+
+# SHA-256 instruction floor per compression on gfx950 (VALU lane-instructions, every one a VOP3 at the
+# v_mad_u64_u32 issue rate): per round Sigma1 and Sigma0 as 3 v_alignbit + 1 v_bitop3 xor3 each, Ch and
+# Maj one v_bitop3 each, T1 two v_add3, a' one v_add3, e' one v_add = 14; per schedule word (48)
+# sigma0 / sigma1 as 2 v_alignbit + 1 shift + 1 v_bitop3 each, W two adds = 10; 16 v_perm byte swaps
+# of the message words; 8 state adds:  64*14 + 48*10 + 16 + 8 = 1,400.
+SHA256_FLOOR_INSTR = 64 * 14 + 48 * 10 + 16 + 8
+# PMC of the leaf kernel (tools/merkle_probe.py under rocprofv3 --pmc; file below): VALU
+# wave-instructions and the compressions of that run, for the instruction-efficiency figure
+MERKLE_PMC_FILE = "profiles/r03_pmc_merkle.json"
+
+
+def merkle_compressions(leaf_len: torch.Tensor, tx_begin: torch.Tensor) -> dict:
+    """SURVEY.md §8(d) Merkle unit, one SHA-256 compression: per leaf ceil((len + 9) / 64) blocks, per
+    internal node (odd levels duplicate the last node: cv_merkle_root_inplace) sha256(l || r) = 2
+    blocks.  Counted from the actual leaf lengths of the batch."""
+    leaf = int(((leaf_len.to(torch.int64) + 9 + 63) // 64).sum())
+    cnt = (tx_begin[1:] - tx_begin[:-1]).to(torch.int64)
+    nodes = torch.zeros_like(cnt)
+    while bool((cnt > 1).any()):
+        m = torch.where(cnt > 1, (cnt + 1) // 2, torch.zeros_like(cnt))
+        nodes += m
+        cnt = torch.where(cnt > 1, m, cnt)
+    internal = int(nodes.sum())
+    return {"leaf": leaf, "internal_nodes": internal, "total": leaf + 2 * internal}
+
+
+def merkle_roofline(comp: dict, ntx: int, merkle_ms: float, mad_rate: float) -> dict:
+    """VALU-issue roofline of the Merkle tx-id recompute (cv_leaf_hash_kernel + cv_merkle_tree_kernel):
+    compressions/s against the chip's VOP3 issue rate (measured v_mad_u64_u32 rate, lane-instr/s)
+    over the 1,400-instruction SHA-256 floor."""
+    rate = comp["total"] / (merkle_ms * 1e-3)
+    peak = mad_rate / SHA256_FLOOR_INSTR
+    out = {"bound": "valu", "unit": "compressions/s", "achieved": rate, "peak": peak, "frac": rate / peak,
+           "compressions_per_tx": comp["total"] / ntx, "leaf_compressions": comp["leaf"],
+           "internal_nodes": comp["internal_nodes"], "kernel_ms": merkle_ms,
+           "floor_instr_per_compression": SHA256_FLOOR_INSTR,
+           "peak_note": "measured v_mad_u64_u32 lane rate / SHA-256 VOP3 instruction floor (bench.py)"}
+    try:
+        with open(os.path.join(REPO, MERKLE_PMC_FILE)) as f:
+            pmc = json.load(f)
+        out["pmc"] = {"source": MERKLE_PMC_FILE, **{k: pmc[k] for k in
+                      ("valu_lane_slots_per_compression", "valu_active_lane_instr_per_compression",
+                       "lane_utilisation", "instr_efficiency_vs_floor") if k in pmc}}
+    except (OSError, ValueError, KeyError):
+        pass
+    return out
 
 
 def c3_line(eng, local, rank, world, sh, dev, ntx, steps, warmup, mad_rate):
@@ -412,7 +461,8 @@ def c3_line(eng, local, rank, world, sh, dev, ntx, steps, warmup, mad_rate):
             "steps": steps, "txs_per_gpu": ntx, "sigs_per_gpu": r["n"], "leaves_per_gpu": r["leaves"],
             "phase_ms": {"merkle": r["merkle_ms"], "scalars": float(ph[0]), "points": float(ph[1]),
                          "hs_straus": float(ph[2])},
-            "roofline": straus_roofline(eng, local, r["n"], float(ph[2]), float(ph.sum()), mad_rate)}
+            "roofline": straus_roofline(eng, local, r["n"], float(ph[2]), float(ph.sum()), mad_rate),
+            "merkle_roofline": merkle_roofline(r["compressions"], ntx, r["merkle_ms"], mad_rate)}
 
 
 def c5_line(eng, local, rank, sh, dev, n, steps, mad_rate, host_api: bool = True):
@@ -493,7 +543,8 @@ def main():
                 "tx_ids_per_s": world * ntx * args.steps / r["elapsed"],
                 "phase_ms": {"merkle": r["merkle_ms"], "scalars": float(ph[0]), "points": float(ph[1]),
                              "hs_straus": float(ph[2])},
-                "roofline": straus_roofline(eng, local, r["n"], float(ph[2]), float(ph.sum()), mad_rate)}), flush=True)
+                "roofline": straus_roofline(eng, local, r["n"], float(ph[2]), float(ph.sum()), mad_rate),
+                "merkle_roofline": merkle_roofline(r["compressions"], ntx, r["merkle_ms"], mad_rate)}), flush=True)
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()

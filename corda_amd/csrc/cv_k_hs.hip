@@ -14,6 +14,47 @@ __global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_scalars_kernel(uint32_t n,
     if (i < n) cv_scalars_lane<false, true>(i, cap, pk, sig, arena, off, len, ws_dig);
 }
 
+// The scalars in two launches (cvk_set_scalars_split): the SHA-512 challenge hash (+ effective S) and
+// the lattice + window digits each at the occupancy its own registers allow — inside one kernel the
+// hash's live state and the lattice's multi-word remainders shared one 168-VGPR budget and spilled.
+// h || s go through ws_hs as four 16-B planes (plane p at word (p * cap + i) * 4), so each store and
+// load of a wave is one contiguous 1-KB stretch.
+template <int WAVES>
+__global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_hash_kernel(uint32_t n, uint32_t cap, const uint8_t *__restrict__ pk,
+                                                              const uint8_t *__restrict__ sig,
+                                                              const uint8_t *__restrict__ arena,
+                                                              const uint64_t *__restrict__ off,
+                                                              const uint32_t *__restrict__ len,
+                                                              uint32_t *__restrict__ ws_hs) {
+    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    uint32_t aw[8], rw[8], sw[8], hs[CV_HS_WORDS];
+    load_words8(aw, pk + (size_t)i * 32);
+    load_words8(rw, sig + (size_t)i * 64);
+    load_words8(sw, sig + (size_t)i * 64 + 32);
+    cv_keyed_hs(aw, rw, sw, arena + off[i], len[i], hs);
+    uint4 *d = reinterpret_cast<uint4 *>(ws_hs);
+#pragma unroll
+    for (int q = 0; q < CV_HS_WORDS / 4; q++)
+        d[(size_t)q * cap + i] = make_uint4(hs[4 * q], hs[4 * q + 1], hs[4 * q + 2], hs[4 * q + 3]);
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_lattice_kernel(uint32_t n, uint32_t cap,
+                                                                 const uint32_t *__restrict__ ws_hs,
+                                                                 uint32_t *__restrict__ ws_dig) {
+    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    uint32_t hs[CV_HS_WORDS];
+    const uint4 *src = reinterpret_cast<const uint4 *>(ws_hs);
+#pragma unroll
+    for (int q = 0; q < CV_HS_WORDS / 4; q++) {
+        const uint4 v = src[(size_t)q * cap + i];
+        hs[4 * q] = v.x; hs[4 * q + 1] = v.y; hs[4 * q + 2] = v.z; hs[4 * q + 3] = v.w;
+    }
+    cv_hs_scalars<false, true>(hs, ws_dig + i, cap);
+}
+
 // points of the half-size group (throughput form): A and R decoded as one interleaved pair per lane,
 // both odd-multiple tables (cv_hs_points); ws_ok = key_ok AND r_ok, status = key status.
 template <bool SUB>
@@ -161,3 +202,8 @@ template __global__ void cv_prep_tp_kernel<false>(uint32_t n, uint32_t cap, uint
 template __global__ void cv_prep_tp_kernel<true>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
 template __global__ void cv_scalars_kernel<2>(uint32_t n, uint32_t cap, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig);
 template __global__ void cv_scalars_kernel<3>(uint32_t n, uint32_t cap, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig);
+template __global__ void cv_hash_kernel<3>(uint32_t n, uint32_t cap, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_hs);
+template __global__ void cv_hash_kernel<4>(uint32_t n, uint32_t cap, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_hs);
+template __global__ void cv_lattice_kernel<2>(uint32_t n, uint32_t cap, const uint32_t *ws_hs, uint32_t *ws_dig);
+template __global__ void cv_lattice_kernel<3>(uint32_t n, uint32_t cap, const uint32_t *ws_hs, uint32_t *ws_dig);
+template __global__ void cv_lattice_kernel<4>(uint32_t n, uint32_t cap, const uint32_t *ws_hs, uint32_t *ws_dig);

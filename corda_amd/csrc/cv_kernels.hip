@@ -47,10 +47,18 @@ extern "C" void cvk_set_scalars_waves(int v) { g_scalars_waves = (v == 2) ? 2 : 
 template <bool SUB>
 static void launch_points(uint32_t m, const uint8_t *pk, const uint8_t *sig, uint32_t *tabA, uint32_t *tabR, uint8_t *ok,
                           uint8_t *status, hipStream_t st);
+// 1 = the scalars as two launches (cv_hash_kernel -> ws_hs -> cv_lattice_kernel), each at its own
+// occupancy (g_hash_waves / g_lattice_waves per SIMD); 0 = one cv_scalars_kernel
+static int g_scalars_split = 0, g_hash_waves = 3, g_lattice_waves = 3;
+extern "C" void cvk_set_scalars_split(int v, int hash_waves, int lattice_waves) {
+    g_scalars_split = v ? 1 : 0;
+    g_hash_waves = hash_waves == 4 ? 4 : 3;
+    g_lattice_waves = (lattice_waves == 2 || lattice_waves == 4) ? lattice_waves : 3;
+}
 template <bool SUB>
 static void launch_prep_tp(uint32_t m, uint32_t cap, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
                            const uint64_t *off, const uint32_t *len, uint32_t *dig, uint32_t *tabA, uint32_t *tabR,
-                           uint8_t *ok, uint8_t *status, hipStream_t st, hipEvent_t mid) {
+                           uint8_t *ok, uint8_t *status, hipStream_t st, hipEvent_t mid, uint32_t *hs) {
     if (g_prep_tp && g_points_mode == 3) {
         const uint32_t nbp = (2 * m + CV_BLOCK - 1) / CV_BLOCK, nbs = (m + CV_BLOCK - 1) / CV_BLOCK;
         hipLaunchKernelGGL(cv_prep_tp_kernel<SUB>, dim3(nbp + nbs), dim3(CV_BLOCK), 0, st, m, cap, nbp, pk, sig, arena,
@@ -58,7 +66,19 @@ static void launch_prep_tp(uint32_t m, uint32_t cap, const uint8_t *pk, const ui
         if (mid) (void)hipEventRecord(mid, st);
         return;
     }
-    if (g_scalars_waves == 2)
+    if (g_scalars_split && hs) {
+        const dim3 g((m + CV_BLOCK - 1) / CV_BLOCK);
+        if (g_hash_waves == 4)
+            hipLaunchKernelGGL(cv_hash_kernel<4>, g, dim3(CV_BLOCK), 0, st, m, cap, pk, sig, arena, off, len, hs);
+        else
+            hipLaunchKernelGGL(cv_hash_kernel<3>, g, dim3(CV_BLOCK), 0, st, m, cap, pk, sig, arena, off, len, hs);
+        if (g_lattice_waves == 4)
+            hipLaunchKernelGGL(cv_lattice_kernel<4>, g, dim3(CV_BLOCK), 0, st, m, cap, hs, dig);
+        else if (g_lattice_waves == 2)
+            hipLaunchKernelGGL(cv_lattice_kernel<2>, g, dim3(CV_BLOCK), 0, st, m, cap, hs, dig);
+        else
+            hipLaunchKernelGGL(cv_lattice_kernel<3>, g, dim3(CV_BLOCK), 0, st, m, cap, hs, dig);
+    } else if (g_scalars_waves == 2)
         hipLaunchKernelGGL(cv_scalars_kernel<2>, dim3((m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, st, m, cap, pk,
                            sig, arena, off, len, dig);
     else
@@ -247,7 +267,7 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
                 launch_prep_tp<true>(mm, ws_cap, pk + (size_t)a * 32, sig + (size_t)a * 64, arena, off + a, len + a,
                                      ws_dig + sub0[h], ws_tab + (size_t)sub0[h] * CV_TAB_WORDS,
                                      ws_tabR + (size_t)sub0[h] * CV_TAB_WORDS, ws_ok + sub0[h],
-                                     status ? status + a : nullptr, st, nullptr);
+                                     status ? status + a : nullptr, st, nullptr, ws_hs + (size_t)sub0[h] * 4);
                 if (h == 0) (void)hipEventRecord(ax->prep1, st);
                 if (g_hs_waves == 2)
                     hipLaunchKernelGGL((cv_hs_straus_kernel<2, true>), dim3(bl), dim3(CV_BLOCK), 0, st, mm, ws_cap,
@@ -268,7 +288,7 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             // (fused prep: ev[1] and ev[2] both follow the one launch, so its time shows as "scalars")
             launch_prep_tp<false>(m, ws_cap, pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0,
                                   ws_dig, ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr, stream,
-                                  ev && c0 == 0 ? ev[1] : nullptr);
+                                  ev && c0 == 0 ? ev[1] : nullptr, ws_hs);
             if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
             if (g_hs_waves == 2)
                 hipLaunchKernelGGL(cv_hs_straus_kernel<2>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, ws_dig,

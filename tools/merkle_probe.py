@@ -47,9 +47,11 @@ def main():
         if r:
             ts.append(e0.elapsed_time(e1))
     same = bool(torch.equal(ids, tb.ids)) if not args.sort_leaves else None
+    import bench  # the repo root is on sys.path
+    comp = bench.merkle_compressions(ln, tb.tx_begin)
     print(json.dumps({"tag": args.tag, "ntx": args.ntx, "sorted": args.sort_leaves,
                       "median_ms": float(np.median(ts)), "min_ms": float(np.min(ts)),
-                      "ids_match_generation": same,
+                      "ids_match_generation": same, "compressions": comp,
                       "ids_sha256": hashlib.sha256(ids.cpu().numpy().tobytes()).hexdigest()[:16]}), flush=True)
 
 
