@@ -212,7 +212,9 @@ CV_HD constexpr int cv_sq_cols(int k, int q, int field) {
     return T[k][q][field];
 }
 
-template <int N, unsigned DBL = 0> CV_HD void fe_sq_n(fe (&h)[N], const fe (&f)[N]) {
+// rtk (0 or 1, run time): every chain additionally doubled (h = 2 f^2) — the per-lane doubling flag of
+// the quad formulas; a literal 0 folds away.
+template <int N, unsigned DBL = 0> CV_HD void fe_sq_n(fe (&h)[N], const fe (&f)[N], uint32_t rtk = 0) {
     // operand variants: left x1 / x2 (times 2 again for DBL chains), right x1 / x2 / x19 / x38
     uint32_t l1[N][10], l2[N][10], r2[N][10], r19[N][10], r38[N][10];
 #pragma unroll
@@ -221,7 +223,7 @@ template <int N, unsigned DBL = 0> CV_HD void fe_sq_n(fe (&h)[N], const fe (&f)[
         for (int i = 0; i < 10; i++)
             CV_ASSERT((uint64_t)f[m].v[i] * 10 < ((uint64_t)33 << CV_W(i)), "fe_sq: limb > 3.3M");
 #endif
-        const uint32_t k = (DBL >> m) & 1u;
+        const uint32_t k = ((DBL >> m) & 1u) + rtk;
 #pragma unroll
         for (int i = 0; i < 10; i++) {
             l1[m][i] = f[m].v[i] << k;
@@ -382,6 +384,22 @@ CV_HD void fe_sq_ilp(fe &h, const fe &f, bool dbl) {
         for (int i = 0; i < 10; i++) h_[i] += h_[i];
     }
     fe_reduce64(h, h_);
+}
+// h = f^2 (dbl = false) or 2 f^2 (dbl = true), sequential-carry form with a run-time doubling flag
+CV_HD void fe_sq_rt(fe &h, const fe &f, bool dbl) {
+    fe hh[1];
+    const fe ff[1] = {f};
+    fe_sq_n<1, 0>(hh, ff, dbl ? 1u : 0u);
+    h = hh[0];
+}
+// Field forms of the quad / tri latency kernels: SEQ = false the ILP forms (ten independent column
+// chains + a 64-bit carry tree), true the sequential-carry forms (fewer instructions, one dependent
+// chain per product)
+template <bool SEQ> CV_HD void fe_mul_q(fe &h, const fe &f, const fe &g) {
+    if constexpr (SEQ) fe_mul(h, f, g); else fe_mul_ilp(h, f, g);
+}
+template <bool SEQ> CV_HD void fe_sq_q(fe &h, const fe &f, bool dbl) {
+    if constexpr (SEQ) fe_sq_rt(h, f, dbl); else fe_sq_ilp(h, f, dbl);
 }
 // Mode dispatch for the long single chains (key decoding, inversion): LAT = true selects the latency
 // forms above (small batches, a lone wave per SIMD), false the sequential-carry forms (throughput).

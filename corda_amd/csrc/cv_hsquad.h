@@ -12,7 +12,7 @@
 // wave); blo / bhi = k*B and k*2^128*B rows (row 0 = identity), tabA = k*(-A), tabR = k*R (cached).
 // W16: w's radix-2^16 digit pairs every fourth window from the CV_BW16 rows (as cv_hs_straus<.., true>),
 // else radix-256 digits every other window from CV_BCOMB.  Returns E == O on every lane of the quad.
-template <bool W16 = false>
+template <bool W16 = false, bool SEQ = false>
 __device__ __forceinline__ bool cv_quad_hs_straus(const uint32_t *blo, const uint32_t *bhi, const uint32_t *dig,
                                                   size_t stride, const uint32_t *tabA, const uint32_t *tabR, int nw,
                                                   int r) {
@@ -23,16 +23,16 @@ __device__ __forceinline__ bool cv_quad_hs_straus(const uint32_t *blo, const uin
     for (int win = nw - 1; win >= 0; win--) {
         const uint32_t dw = dig[(size_t)win * stride];
         if (win != nw - 1) {
-            quad_dbl(P, r);
-            quad_dbl(P, r);
-            quad_dbl(P, r);
-            quad_dbl(P, r);
+            quad_dbl<SEQ>(P, r);
+            quad_dbl<SEQ>(P, r);
+            quad_dbl<SEQ>(P, r);
+            quad_dbl<SEQ>(P, r);
         }
         fe q;
         quad_cached_coord(q, tabR, cv_sfield(dw, 5, 5), r);
-        quad_add(P, q, r);
+        quad_add<SEQ>(P, q, r);
         quad_cached_coord(q, tabA, cv_sfield(dw, 0, 5), r);
-        quad_add(P, q, r);
+        quad_add<SEQ>(P, q, r);
         if (W16 ? ((win & 3) == 0 && win < 32) : ((win & 1) == 0 && win < 32)) {
             int dlo, dhi;
             if (W16) {
@@ -44,9 +44,9 @@ __device__ __forceinline__ bool cv_quad_hs_straus(const uint32_t *blo, const uin
                 dhi = cv_sfield(dw, 19, 9);
             }
             quad_precomp_coord(q, blo, CV_BTAB_STRIDE, dlo, r, true);
-            quad_add(P, q, r);
+            quad_add<SEQ>(P, q, r);
             quad_precomp_coord(q, bhi, CV_BTAB_STRIDE, dhi, r, true);
-            quad_add(P, q, r);
+            quad_add<SEQ>(P, q, r);
         }
     }
     fe X, Y, Z, d;
@@ -92,6 +92,7 @@ __device__ __forceinline__ void quad_any_coord(fe &q, const uint32_t *tab, bool 
 
 // this lane's coordinate of a full extended point in cached form (Y+X, Y-X, Z, 2dT), from each
 // lane's own coordinate of (X, Y, Z, T)
+template <bool SEQ = false>
 __device__ __forceinline__ void quad_to_cached(fe &q, const fe &P, int r) {
     fe x, y, s, d, t, d2;
     fe_const_d2(d2);
@@ -99,7 +100,7 @@ __device__ __forceinline__ void quad_to_cached(fe &q, const fe &P, int r) {
     fe_qp<CV_QP(1, 1, 1, 1)>(y, P);
     fe_add(s, y, x);
     fe_sub<2>(d, y, x);
-    fe_mul_ilp(t, P, d2);                   // lane 3: 2d T (other lanes discard it)
+    fe_mul_q<SEQ>(t, P, d2);                // lane 3: 2d T (other lanes discard it)
     fe_sel(q, P, t, r == 3);
     fe_sel(q, q, d, r == 1);
     fe_sel(q, q, s, r == 0);
@@ -113,6 +114,7 @@ template <int CTRL> __device__ __forceinline__ void fe_dpp_row(fe &h, const fe &
 
 // E = [v]R + [u]A + [w]B by four chains (quad c of the 16-lane group, coordinate r); returns E == O
 // on every lane.  tab / precomp / field: this quad's table and digit field (5 bits at `field`).
+template <bool SEQ = false>
 __device__ __forceinline__ bool cv_tri_hs_straus(const uint32_t *dig, size_t stride, const uint32_t *tab, bool precomp,
                                                  int field, int nw, int r) {
     fe P, q;
@@ -122,23 +124,23 @@ __device__ __forceinline__ bool cv_tri_hs_straus(const uint32_t *dig, size_t str
     for (int win = nw - 1; win >= 0; win--) {
         const uint32_t dw = dig[(size_t)win * stride];
         if (win != nw - 1) {
-            quad_dbl(P, r);
-            quad_dbl(P, r);
-            quad_dbl(P, r);
-            quad_dbl(P, r);
+            quad_dbl<SEQ>(P, r);
+            quad_dbl<SEQ>(P, r);
+            quad_dbl<SEQ>(P, r);
+            quad_dbl<SEQ>(P, r);
         }
         quad_any_coord(q, tab, precomp, cv_sfield(dw, field, 5), r);
-        quad_add(P, q, r);
+        quad_add<SEQ>(P, q, r);
     }
     // every quad adds the quad 4 lanes away, then the quad 8 lanes away (row rotations): each quad
     // ends with the sum of all four chains
     fe Q;
     fe_dpp_row<0x124>(Q, P);                             // row_ror:4
-    quad_to_cached(q, Q, r);
-    quad_add(P, q, r);
+    quad_to_cached<SEQ>(q, Q, r);
+    quad_add<SEQ>(P, q, r);
     fe_dpp_row<0x128>(Q, P);                             // row_ror:8
-    quad_to_cached(q, Q, r);
-    quad_add(P, q, r);
+    quad_to_cached<SEQ>(q, Q, r);
+    quad_add<SEQ>(P, q, r);
     fe X, Y, Z, d;
     fe_qp<CV_QP(0, 0, 0, 0)>(X, P);
     fe_qp<CV_QP(1, 1, 1, 1)>(Y, P);

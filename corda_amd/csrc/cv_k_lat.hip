@@ -57,6 +57,7 @@ __global__ __launch_bounds__(64, 1) void cv_prep_lat_kernel(uint32_t n, uint32_t
 // Half-size quad kernel (cv_hsquad.h): grid 4n lanes.  The chunk's bitmap words must be zero on
 // entry (the launcher clears them): each wave ORs its 16 verdict bits into its word.  Quads past n
 // replay signature n-1 (whole waves take part in the window-count reduction) and add no bits.
+template <bool SEQ>
 __global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_quad_kernel(uint32_t n, uint32_t cap,
                                                                      const uint32_t *__restrict__ ws_dig,
                                                                      const uint32_t *__restrict__ ws_tab,
@@ -79,7 +80,7 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_quad_kernel(uint32_t n,
     }
     nw = __builtin_amdgcn_readfirstlane(nw);
     // w's radix-2^16 pairs against the CV_BW16 rows k*B (row 0) and k*2^128*B (row 2)
-    const bool eq = cv_quad_hs_straus<true>(bw16, bw16 + 2 * CV_BW16_ROW, ws_dig + i, cap,
+    const bool eq = cv_quad_hs_straus<true, SEQ>(bw16, bw16 + 2 * CV_BW16_ROW, ws_dig + i, cap,
                                             ws_tab + (size_t)i * CV_TAB_WORDS, ws_tabR + (size_t)i * CV_TAB_WORDS, nw, r);
     const bool acc = eq && ws_ok[i] && i0 < n;
     const uint32_t bits = cv_quad_ballot_bits(__ballot(acc));
@@ -89,6 +90,7 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_quad_kernel(uint32_t n,
 
 // Tri-chain kernel (cv_hsquad.h): grid 16n lanes, 4 signatures per wave; digits from
 // cv_hs_scalars<true>.  Bitmap words zero on entry, as for the quad kernel.
+template <bool SEQ>
 __global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_tri_kernel(uint32_t n, uint32_t cap,
                                                                     const uint32_t *__restrict__ ws_dig,
                                                                     const uint32_t *__restrict__ ws_tab,
@@ -115,7 +117,7 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_tri_kernel(uint32_t n, 
                         : c == 1 ? ws_tab + (size_t)i * CV_TAB_WORDS
                                  : CV_BCOMB + (c == 2 ? 0 : 2 * ROW);
     const int field = c == 0 ? 5 : c == 1 ? 0 : c == 2 ? 10 : 15;
-    const bool eq = cv_tri_hs_straus(ws_dig + i, cap, tab, c >= 2, field, nw, r);
+    const bool eq = cv_tri_hs_straus<SEQ>(ws_dig + i, cap, tab, c >= 2, field, nw, r);
     const bool acc = eq && ws_ok[i] && i0 < n && (threadIdx.x & 15u) == 0;
     uint64_t b = __ballot(acc) & 0x0001000100010001ull;      // lanes 0, 16, 32, 48
     b = (b | (b >> 15)) & 0x0000000300000003ull;
@@ -125,3 +127,7 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_tri_kernel(uint32_t n, 
 
 template __global__ void cv_prep_lat_kernel<true>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
 template __global__ void cv_prep_lat_kernel<false>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
+template __global__ void cv_hs_straus_quad_kernel<false>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);
+template __global__ void cv_hs_straus_quad_kernel<true>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);
+template __global__ void cv_hs_straus_tri_kernel<false>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap);
+template __global__ void cv_hs_straus_tri_kernel<true>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap);

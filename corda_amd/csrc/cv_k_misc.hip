@@ -82,6 +82,78 @@ __global__ __launch_bounds__(CV_LEAF_BLOCK) void cv_leaf_hash_kernel(uint32_t nl
     }
 }
 
+// Balanced-pair form of the leaf kernel (cvk_set_leaf_mode(1)): the same per-workgroup counting sort,
+// then lane t hashes the t-th shortest AND the t-th longest leaf of the span back to back in one block
+// loop (the state restarts between them), so every lane's block count is about the span's mean and
+// a wave no longer runs as long as its longest leaf.  Span = 2 x block.
+__global__ __launch_bounds__(CV_LEAF_BLOCK) void cv_leaf_hash_pair_kernel(uint32_t nleaves, const uint8_t *__restrict__ arena,
+                                                                          const uint64_t *__restrict__ off,
+                                                                          const uint32_t *__restrict__ len,
+                                                                          uint32_t *__restrict__ leaf_digest) {
+    constexpr uint32_t SPAN = 2 * CV_LEAF_BLOCK;
+    __shared__ uint32_t hist[64], base[64], perm[SPAN];
+    const uint32_t t = threadIdx.x, first = blockIdx.x * SPAN;
+    const uint32_t nlive = nleaves - first < SPAN ? nleaves - first : SPAN;
+    if (t < 64) hist[t] = 0;
+    __syncthreads();
+    uint32_t bucket[2], pos[2];
+#pragma unroll
+    for (uint32_t k = 0; k < 2; k++) {
+        const uint32_t j = k * CV_LEAF_BLOCK + t;
+        bucket[k] = 0;
+        pos[k] = 0;
+        if (j < nlive) {
+            const uint32_t nb = sha256_nblocks(len[first + j]);
+            bucket[k] = nb < 63u ? nb : 63u;
+            pos[k] = atomicAdd(&hist[bucket[k]], 1u);
+        }
+    }
+    __syncthreads();
+    if (t < 64) {                                                 // exclusive scan, one wave
+        const uint32_t own = hist[t];
+        uint32_t inc = own;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d, 64);
+            if ((int)t >= d) inc += y;
+        }
+        base[t] = inc - own;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < 2; k++) {
+        const uint32_t j = k * CV_LEAF_BLOCK + t;
+        if (j < nlive) perm[base[bucket[k]] + pos[k]] = first + j;
+    }
+    __syncthreads();
+    // ranks t and nlive-1-t; the middle rank of an odd span is taken once (as A)
+    const bool has_a = 2 * t + 1 <= nlive, has_b = nlive - 1 - t > t && t < nlive;
+    const uint32_t la = has_a ? perm[t] : 0u, lb = has_b ? perm[nlive - 1 - t] : 0u;
+    const uint32_t na = has_a ? len[la] : 0u, nbl = has_b ? len[lb] : 0u;
+    const uint8_t *pa = arena + (has_a ? off[la] : 0), *pb = arena + (has_b ? off[lb] : 0);
+    const uint32_t ba = has_a ? sha256_nblocks(na) : 0u, bb = has_b ? sha256_nblocks(nbl) : 0u;
+    uint32_t st[8];
+    sha256_init(st);
+#pragma nounroll
+    for (uint32_t it = 0; it < ba + bb; it++) {
+        const bool in_a = it < ba;
+        uint32_t w[16];
+        sha256_block_words(w, in_a ? pa : pb, in_a ? na : nbl, in_a ? it : it - ba, 64 * (in_a ? ba : bb));
+        sha256_compress(st, w);
+        if (it + 1 == ba) {
+            uint4 *o = reinterpret_cast<uint4 *>(leaf_digest + (size_t)la * 8);
+            o[0] = make_uint4(st[0], st[1], st[2], st[3]);
+            o[1] = make_uint4(st[4], st[5], st[6], st[7]);
+            sha256_init(st);
+        }
+    }
+    if (has_b) {
+        uint4 *o = reinterpret_cast<uint4 *>(leaf_digest + (size_t)lb * 8);
+        o[0] = make_uint4(st[0], st[1], st[2], st[3]);
+        o[1] = make_uint4(st[4], st[5], st[6], st[7]);
+    }
+}
+
 // one lane per transaction, in place over its leaf digests; ids are written as digest bytes
 __global__ __launch_bounds__(CV_BLOCK) void cv_merkle_tree_kernel(uint32_t ntx, const uint32_t *__restrict__ tx_begin,
                                                                   uint32_t *__restrict__ leaf_digest,

@@ -115,8 +115,8 @@ __global__ void cv_bw16_init_kernel(uint32_t *tab);
 __global__ void cv_scalars_lat_kernel(uint32_t n, uint32_t cap, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig);
 __global__ void cv_points_pair_kernel(uint32_t n, const uint8_t *pk, const uint8_t *sig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
 template <bool B16> __global__ void cv_prep_lat_kernel(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
-__global__ void cv_hs_straus_quad_kernel(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);
-__global__ void cv_hs_straus_tri_kernel(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap);
+template <bool SEQ> __global__ void cv_hs_straus_quad_kernel(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);
+template <bool SEQ> __global__ void cv_hs_straus_tri_kernel(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap);
 __global__ void cv_sign_kernel( uint32_t n, const uint8_t *seed, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint8_t *pk_out, uint8_t *sig_out);
 // leaves per leaf-hash workgroup (sorted by SHA-256 block count inside it)
 #define CV_LEAF_BLOCK 256
@@ -124,6 +124,7 @@ __global__ void cv_sign_kernel( uint32_t n, const uint8_t *seed, const uint8_t *
 #define CV_LEAF_SPAN 512   // leaves sorted together per workgroup (a multiple of CV_LEAF_BLOCK)
 #endif
 __global__ void cv_leaf_hash_kernel(uint32_t nleaves, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *leaf_digest);
+__global__ void cv_leaf_hash_pair_kernel(uint32_t nleaves, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *leaf_digest);
 __global__ void cv_merkle_tree_kernel(uint32_t ntx, const uint32_t *tx_begin, uint32_t *leaf_digest, uint8_t *ids, uint8_t *status);
 __global__ void cv_pmt_verify_kernel(uint32_t ntrees, const uint8_t *kind, const uint32_t *left, const uint32_t *right, const uint8_t *leaf_hash, const uint32_t *tree_begin, const uint8_t *root, const uint8_t *check, const uint32_t *check_begin, uint32_t *dig, uint8_t *flag, uint8_t *verdict, uint8_t *status);
 __global__ void cv_mad_bench_kernel(uint32_t iters, uint64_t *out);

@@ -130,6 +130,11 @@ extern "C" uint32_t cvk_get_tri_max(void) { return g_tri_max; }
 static int g_prep_lat_fused = 1;
 extern "C" void cvk_set_prep_lat_fused(int v) { g_prep_lat_fused = v ? 1 : 0; }
 
+// field forms of the latency Straus kernels: bit 0 = tri, bit 1 = quad use the sequential-carry
+// multiplications (fewer instructions) instead of the ILP forms
+static int g_lat_seq = 0;
+extern "C" void cvk_set_lat_seq(int v) { g_lat_seq = v & 3; }
+
 // Batches of at most this many signatures run the quad kernels (set by cvk_set_quad_max; 0 = never)
 static uint32_t g_quad_max = 32768;
 extern "C" void cvk_set_quad_max(uint32_t m) { g_quad_max = m; }
@@ -234,11 +239,17 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             if (!(g_prep_lat_fused || tri))
                 (void)hipMemsetAsync(bitmap + (size_t)c0 / 64, 0, (size_t)((m + 63) / 64) * 8, stream);
             if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
-            if (tri)
-                hipLaunchKernelGGL(cv_hs_straus_tri_kernel, dim3((16 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
+            if (tri && (g_lat_seq & 1))
+                hipLaunchKernelGGL(cv_hs_straus_tri_kernel<true>, dim3((16 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
                                    stream, m, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
+            else if (tri)
+                hipLaunchKernelGGL(cv_hs_straus_tri_kernel<false>, dim3((16 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
+                                   stream, m, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
+            else if (g_lat_seq & 2)
+                hipLaunchKernelGGL(cv_hs_straus_quad_kernel<true>, dim3((4 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK),
+                                   0, stream, m, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64, bw16);
             else
-                hipLaunchKernelGGL(cv_hs_straus_quad_kernel, dim3((4 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK),
+                hipLaunchKernelGGL(cv_hs_straus_quad_kernel<false>, dim3((4 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK),
                                    0, stream, m, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64, bw16);
             if (ev && c0 == 0) (void)hipEventRecord(ev[3], stream);
             continue;
@@ -424,10 +435,19 @@ hipError_t cvk_pmt_verify(uint32_t ntrees, const uint8_t *kind, const uint32_t *
     return hipGetLastError();
 }
 
+}  // extern "C"
+// leaf hashing: 0 = length-sorted passes (cv_leaf_hash_kernel), 1 = balanced pairs (cv_leaf_hash_pair_kernel)
+static int g_leaf_mode = 0;
+extern "C" {
+void cvk_set_leaf_mode(int m) { g_leaf_mode = m == 1 ? 1 : 0; }
+
 hipError_t cvk_merkle(uint32_t ntx, uint32_t nleaves, const uint8_t *arena, const uint64_t *leaf_off,
                       const uint32_t *leaf_len, const uint32_t *tx_begin, uint32_t *leaf_digest, uint8_t *ids,
                       uint8_t *status, hipStream_t stream) {
-    if (nleaves) {
+    if (nleaves && g_leaf_mode == 1) {
+        hipLaunchKernelGGL(cv_leaf_hash_pair_kernel, dim3((nleaves + 2 * CV_LEAF_BLOCK - 1) / (2 * CV_LEAF_BLOCK)),
+                           dim3(CV_LEAF_BLOCK), 0, stream, nleaves, arena, leaf_off, leaf_len, leaf_digest);
+    } else if (nleaves) {
         hipLaunchKernelGGL(cv_leaf_hash_kernel, dim3((nleaves + CV_LEAF_SPAN - 1) / CV_LEAF_SPAN), dim3(CV_LEAF_BLOCK), 0, stream,
                            nleaves, arena, leaf_off, leaf_len, leaf_digest);
     }

@@ -23,21 +23,23 @@ template <int CTRL> __device__ __forceinline__ void fe_qp(fe &h, const fe &f) {
 
 // the second half of both formulas: R1 = (H, G, F, E) on lanes 0..3 (tight) ->
 // own coordinate of (X, Y, Z, T) = (E F, G H, F G, E H)
+template <bool SEQ = false>
 __device__ __forceinline__ void quad_finish_products(fe &P, const fe &R1) {
     fe op1, op2;
     fe_qp<CV_QP(3, 1, 2, 3)>(op1, R1);   // E, G, F, E
     fe_qp<CV_QP(2, 0, 1, 0)>(op2, R1);   // F, H, G, H
-    fe_mul_ilp(P, op1, op2);
+    fe_mul_q<SEQ>(P, op1, op2);
 }
 
 // P <- 2P.  P: own coordinate of an extended point (T is not read).
+template <bool SEQ = false>
 __device__ __forceinline__ void quad_dbl(fe &P, int r) {
     fe w, x, u, sq;
     fe_qp<CV_QP(0, 1, 2, 1)>(w, P);      // X, Y, Z, Y
     fe_qp<CV_QP(0, 0, 0, 0)>(x, P);      // X everywhere
 #pragma unroll
     for (int i = 0; i < 10; i++) u.v[i] = w.v[i] + (r == 3 ? x.v[i] : 0u);   // lane 3: X + Y (<= 2.02)
-    fe_sq_ilp(sq, u, r == 2);            // A = X^2, B = Y^2, C = 2 Z^2, S = (X + Y)^2   (tight)
+    fe_sq_q<SEQ>(sq, u, r == 2);         // A = X^2, B = Y^2, C = 2 Z^2, S = (X + Y)^2   (tight)
     fe a, b, hp, g, t, d, R1;
     fe_qp<CV_QP(0, 0, 0, 0)>(a, sq);
     fe_qp<CV_QP(1, 1, 1, 1)>(b, sq);
@@ -47,11 +49,12 @@ __device__ __forceinline__ void quad_dbl(fe &P, int r) {
     fe_sub<4>(d, sq, t);                 // lane 2: F' = C - G, lane 3: E = S - H'   (<= 6.03)
     fe_sel(R1, t, d, r >= 2);
     fe_carry(R1, R1);
-    quad_finish_products(P, R1);         // (E F', G H', F' G, E H') — the negated-(F, H) doubling, same point
+    quad_finish_products<SEQ>(P, R1);    // (E F', G H', F' G, E H') — the negated-(F, H) doubling, same point
 }
 
 // P <- P + Q, q = this lane's coordinate of Q in cached form (Y+X, Y-X, Z, 2dT); for an affine
 // "precomp" Q (y+x, y-x, 1, 2dxy) lane 2 passes the constant 1.
+template <bool SEQ = false>
 __device__ __forceinline__ void quad_add(fe &P, const fe &q, int r) {
     fe y, x, s, d, L, m;
     fe_qp<CV_QP(1, 1, 2, 3)>(y, P);      // Y, Y, Z, T
@@ -60,7 +63,7 @@ __device__ __forceinline__ void quad_add(fe &P, const fe &q, int r) {
     fe_sub<2>(d, y, x);                  // lane 1: Y - X      <= 3.01
     fe_sel(L, y, d, r == 1);
     fe_sel(L, L, s, r == 0);             // lanes 2, 3: Z, T
-    fe_mul_ilp(m, L, q);                 // a, b, dd = Z1 Z2, c = T1 2d T2
+    fe_mul_q<SEQ>(m, L, q);              // a, b, dd = Z1 Z2, c = T1 2d T2
     fe o1, o2, sum, diff, R1;
     fe_qp<CV_QP(0, 2, 2, 0)>(o1, m);     // a, dd, dd, a
     const uint32_t sh = (r == 1 || r == 2) ? 1u : 0u;
@@ -71,7 +74,7 @@ __device__ __forceinline__ void quad_add(fe &P, const fe &q, int r) {
     fe_sub<2>(diff, o1, o2);             // lane 2: F = 2dd - c, lane 3: E = a - b
     fe_sel(R1, diff, sum, r < 2);
     fe_carry(R1, R1);
-    quad_finish_products(P, R1);
+    quad_finish_products<SEQ>(P, R1);
 }
 
 // this lane's coordinate of +-k*(-A) from a per-signature cached table (40 words per entry, entry k = kP)

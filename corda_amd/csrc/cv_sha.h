@@ -308,31 +308,43 @@ __host__ __device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_
 // Per 64-byte block the message comes from one window of 17 aligned dwords (cv_msg_window: one
 // branch per block, nothing read past the last message byte), funnel-shifted into the 16 schedule
 // words, with msg_dword_le's padding rules applied branch-free.
+// The 16 schedule words of SHA-256 block `blk` of the n-byte message at p (padding and the bit
+// length applied branch-free; total = the padded length in bytes).
+__host__ __device__ __forceinline__ void sha256_block_words(uint32_t w[16], const uint8_t *p, uint32_t n, uint32_t blk,
+                                                            uint32_t total) {
+    const uint64_t bits = (uint64_t)n * 8;
+    const uint32_t sh8 = 8u * (uint32_t)((uintptr_t)p & 3u);
+    uint32_t dw[17];
+    cv_msg_window<17>(dw, p, n, blk * 64);
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint32_t u = blk * 64 + 4 * j;
+        uint32_t le = cv_funnel32(dw[j + 1], dw[j], sh8);
+        const uint32_t valid = n - u;                            // message bytes left at u
+        const uint32_t keep = valid >= 4 ? 0xffffffffu : ((1u << (8 * (valid & 3u))) - 1u);
+        const uint32_t pad = valid >= 4 ? 0u : (0x80u << (8 * (valid & 3u)));
+        le = (le & keep) | pad;
+        if (u > n) le = 0;
+        uint32_t v = cv_bswap32(le);
+        if (u == total - 8) v = (uint32_t)(bits >> 32);
+        if (u == total - 4) v = (uint32_t)bits;
+        w[j] = v;
+    }
+}
+CV_HD uint32_t sha256_nblocks(uint32_t n) { return (n + 1 + 8 + 63) / 64; }
+
+// SHA-256 of an arbitrary byte string in device memory; out = 8 big-endian state words.
+// Per 64-byte block the message comes from one window of 17 aligned dwords (cv_msg_window: one
+// branch per block, nothing read past the last message byte), funnel-shifted into the 16 schedule
+// words, with msg_dword_le's padding rules applied branch-free.
 __host__ __device__ __forceinline__ void sha256_bytes(uint32_t out[8], const uint8_t *p, uint32_t n) {
     uint32_t st[8];
     sha256_init(st);
-    const uint32_t nblocks = (n + 1 + 8 + 63) / 64;
-    const uint32_t total = nblocks * 64;
-    const uint64_t bits = (uint64_t)n * 8;
-    const uint32_t sh8 = 8u * (uint32_t)((uintptr_t)p & 3u);
+    const uint32_t nblocks = sha256_nblocks(n);
 #pragma nounroll
     for (uint32_t blk = 0; blk < nblocks; blk++) {
-        uint32_t dw[17], w[16];
-        cv_msg_window<17>(dw, p, n, blk * 64);
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const uint32_t u = blk * 64 + 4 * j;
-            uint32_t le = cv_funnel32(dw[j + 1], dw[j], sh8);
-            const uint32_t valid = n - u;                            // message bytes left at u
-            const uint32_t keep = valid >= 4 ? 0xffffffffu : ((1u << (8 * (valid & 3u))) - 1u);
-            const uint32_t pad = valid >= 4 ? 0u : (0x80u << (8 * (valid & 3u)));
-            le = (le & keep) | pad;
-            if (u > n) le = 0;
-            uint32_t v = cv_bswap32(le);
-            if (u == total - 8) v = (uint32_t)(bits >> 32);
-            if (u == total - 4) v = (uint32_t)bits;
-            w[j] = v;
-        }
+        uint32_t w[16];
+        sha256_block_words(w, p, n, blk, nblocks * 64);
         sha256_compress(st, w);
     }
 #pragma unroll

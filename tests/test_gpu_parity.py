@@ -4,6 +4,7 @@ Bit-exact bar: every verdict, every key-status byte, every tx id.  Sizes: the go
 oracle-checked random batches at sizes the oracle finishes in seconds; BASELINE sizes (1M) through
 size-independent properties (all honest accepted, an exact corruption pattern rejected).
 """
+import ctypes
 import hashlib
 import os
 
@@ -148,7 +149,17 @@ def test_key_pool_batch(engine, oracle_c):
         assert 0 < int(ref.sum()) < n
 
 
-def test_merkle_golden(engine, merkle_cases):
+@pytest.fixture(params=[0, 1], ids=["sorted_passes", "balanced_pairs"])
+def leaf_mode(request):
+    """Both leaf-hash kernels (cvk_set_leaf_mode): length-sorted passes and balanced pairs."""
+    lib = native.load()
+    lib.cvk_set_leaf_mode.argtypes = [ctypes.c_int]
+    lib.cvk_set_leaf_mode(request.param)
+    yield request.param
+    lib.cvk_set_leaf_mode(0)
+
+
+def test_merkle_golden(engine, merkle_cases, leaf_mode):
     m = merkle_cases
     ids, st = engine.merkle_tx_ids(m["arena"], m["leaf_off"], m["leaf_len"], m["tx_leaf_begin"])
     assert np.array_equal(st, m["status"])
@@ -156,7 +167,7 @@ def test_merkle_golden(engine, merkle_cases):
     assert ids[0].tobytes().hex().upper() == "F6D8FB3720114F8D040D64F633B0D9178EB09A55AA7D62FAE1A070D1BF561051"
 
 
-def test_merkle_sha256_multiblock_kat(engine):
+def test_merkle_sha256_multiblock_kat(engine, leaf_mode):
     """One-leaf tx over the 71,644-byte prospectus jar: id = SHA-256(jar) = decd0986... (SellerFlow.kt:23)."""
     here = os.path.dirname(os.path.abspath(__file__))
     data = np.fromfile(os.path.join(here, "golden", "bank-of-london-cp.jar.bin"), np.uint8)
@@ -165,7 +176,7 @@ def test_merkle_sha256_multiblock_kat(engine):
     assert ids[0].tobytes().hex() == "decd098666b9657314870e192ced0c3519c2c9d395507a238338f8d003929de9"
 
 
-def test_merkle_random_vs_oracle(engine, oracle_c):
+def test_merkle_random_vs_oracle(engine, oracle_c, leaf_mode):
     rng = np.random.default_rng(3)
     ntx = 3000
     counts = rng.integers(0, 12, ntx)

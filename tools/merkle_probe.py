@@ -24,8 +24,14 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--sort-leaves", action="store_true")
     ap.add_argument("--tag", default=os.environ.get("CV_LIB_PATH", "default"))
+    ap.add_argument("--leaf-mode", type=int, default=-1, help="cvk_set_leaf_mode (0 sorted passes, 1 pairs)")
     args = ap.parse_args()
     eng = native.Engine(1)
+    if args.leaf_mode >= 0:
+        import ctypes
+        lib = native.load()
+        lib.cvk_set_leaf_mode.argtypes = [ctypes.c_int]
+        lib.cvk_set_leaf_mode(args.leaf_mode)
     tb = workload.make_tx_batch(eng, 0, args.ntx, signers=1)
     off, ln = tb.leaf_off, tb.leaf_len
     if args.sort_leaves:
@@ -49,7 +55,7 @@ def main():
     same = bool(torch.equal(ids, tb.ids)) if not args.sort_leaves else None
     import bench  # the repo root is on sys.path
     comp = bench.merkle_compressions(ln, tb.tx_begin)
-    print(json.dumps({"tag": args.tag, "ntx": args.ntx, "sorted": args.sort_leaves,
+    print(json.dumps({"tag": args.tag, "leaf_mode": args.leaf_mode, "ntx": args.ntx, "sorted": args.sort_leaves,
                       "median_ms": float(np.median(ts)), "min_ms": float(np.min(ts)),
                       "ids_match_generation": same, "compressions": comp,
                       "ids_sha256": hashlib.sha256(ids.cpu().numpy().tobytes()).hexdigest()[:16]}), flush=True)

@@ -40,36 +40,61 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=100)
     ap.add_argument("--sizes", default="256,4096,65536")
+    ap.add_argument("--variants", default="base:",
+                    help="';'-free list 'NAME:SETTER=A/B,SETTER=C ...' separated by spaces; rounds interleave them")
+    ap.add_argument("--rounds", type=int, default=1)
     args = ap.parse_args()
+    import ctypes
+    lib = native.load()
+    variants = []
+    for v in args.variants.split():
+        name, _, body = v.partition(":")
+        variants.append((name, [(k, tuple(int(x) for x in a.split("/"))) for k, a in
+                                (kv.split("=") for kv in filter(None, body.split(",")))]))
+    used = {k for _, sets in variants for k, _ in sets}
+    reset = {"cvk_set_lat_seq": (0,), "cvk_set_tri_max": (4096,), "cvk_set_prep_lat_fused": (1,)}
+
+    def apply(sets):
+        for k in used:
+            getattr(lib, k).argtypes = [ctypes.c_int] * len(reset[k])
+            getattr(lib, k)(*reset[k])
+        for k, a in sets:
+            getattr(lib, k).argtypes = [ctypes.c_int] * len(a)
+            getattr(lib, k)(*a)
     eng = native.Engine(1)
     adv = adversarial_pool()
     dev = torch.device("cuda", 0)
     s = torch.cuda.Stream(dev)
     for n in (int(x) for x in args.sizes.split(",")):
         pk, sig, arena, off, ln, expect = build(eng, n, None, adv)
-        host = p50(lambda: eng.verify_batch(pk, sig, arena, off, ln, want_status=False), args.reps)
-        bm_h, _ = eng.verify_batch(pk, sig, arena, off, ln, want_status=False)
-        assert np.array_equal(native.bitmap_to_bools(bm_h, n), expect)
-        d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in
-             (("pk", pk), ("sig", sig), ("arena", arena), ("off", off.view(np.int64)), ("len", ln.view(np.int32)))}
-        bm = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
-        torch.cuda.synchronize()
+        for rnd in range(args.rounds):
+            for vname, sets in variants:
+                apply(sets)
+                host = p50(lambda: eng.verify_batch(pk, sig, arena, off, ln, want_status=False), args.reps)
+                bm_h, _ = eng.verify_batch(pk, sig, arena, off, ln, want_status=False)
+                assert np.array_equal(native.bitmap_to_bools(bm_h, n), expect)
+                d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in
+                     (("pk", pk), ("sig", sig), ("arena", arena), ("off", off.view(np.int64)), ("len", ln.view(np.int32)))}
+                bm = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+                torch.cuda.synchronize()
 
-        def dev_call():
-            eng.verify_device(0, n, d["pk"].data_ptr(), d["sig"].data_ptr(), d["arena"].data_ptr(),
-                              d["off"].data_ptr(), d["len"].data_ptr(), bm.data_ptr(), 0, s.cuda_stream)
-            s.synchronize()
+                def dev_call():
+                    eng.verify_device(0, n, d["pk"].data_ptr(), d["sig"].data_ptr(), d["arena"].data_ptr(),
+                                      d["off"].data_ptr(), d["len"].data_ptr(), bm.data_ptr(), 0, s.cuda_stream)
+                    s.synchronize()
 
-        device = p50(dev_call, args.reps)
-        assert np.array_equal(native.bitmap_to_bools(bm.cpu().numpy().view(np.uint64), n), expect)
-        ph = np.median(np.array([eng.verify_device_timed(0, n, d["pk"].data_ptr(), d["sig"].data_ptr(),
-                                                         d["arena"].data_ptr(), d["off"].data_ptr(),
-                                                         d["len"].data_ptr(), bm.data_ptr(), s.cuda_stream)
-                                 for _ in range(20)]), axis=0)
-        nbytes = pk.nbytes + sig.nbytes + arena.nbytes + off.nbytes + ln.nbytes
-        print(json.dumps({"n": n, "host_p50_p99_ms": host, "device_p50_p99_ms": device,
-                          "phase_ms": {"hash": float(ph[0]), "prep": float(ph[1]), "straus": float(ph[2])},
-                          "input_bytes": int(nbytes)}), flush=True)
+                device = p50(dev_call, args.reps)
+                assert np.array_equal(native.bitmap_to_bools(bm.cpu().numpy().view(np.uint64), n), expect)
+                ph = np.median(np.array([eng.verify_device_timed(0, n, d["pk"].data_ptr(), d["sig"].data_ptr(),
+                                                                 d["arena"].data_ptr(), d["off"].data_ptr(),
+                                                                 d["len"].data_ptr(), bm.data_ptr(), s.cuda_stream)
+                                         for _ in range(20)]), axis=0)
+                nbytes = pk.nbytes + sig.nbytes + arena.nbytes + off.nbytes + ln.nbytes
+                print(json.dumps({"variant": vname, "round": rnd, "n": n, "host_p50_p99_ms": host,
+                                  "device_p50_p99_ms": device,
+                                  "phase_ms": {"hash": float(ph[0]), "prep": float(ph[1]), "straus": float(ph[2])},
+                                  "input_bytes": int(nbytes)}), flush=True)
+        apply([])
     eng.close()
 
 
