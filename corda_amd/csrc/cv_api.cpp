@@ -258,13 +258,17 @@ constexpr uint32_t kVerifyChunk = 1u << 22;
 // sub-chunk into pinned staging while the earlier ones transfer and verify.
 static size_t g_pipe_min = 131072, g_pipe_first = 65536, g_pipe_chunk = 262144;
 static int g_pack_threads = 8;
+// small-form batches of at least this many signatures pack their staging on the device's worker pool
+static size_t g_small_pool_min = 16384;
 static int g_pipe_slots = 3;   // slots the pipeline deals its sub-chunks over (2..kSlots)
 // host-side time of the pipelined path, seconds (cvk_pipe_stats): range scans, packing, waits for a
 // slot's staging, enqueue (HIP calls), the final synchronisation; and calls / sub-chunks
 struct PipeStats {
     double plan = 0, pack = 0, wait = 0, enq = 0, sync = 0;
-    uint64_t calls = 0, chunks = 0;
+    uint64_t calls = 0, chunks = 0, direct = 0;
 };
+// 1 = pinned caller arrays are DMAed in place (stage_direct); 0 = always pack (A/B knob)
+static int g_direct_dma = 1;
 static PipeStats g_pipe_stats;
 static std::mutex g_pipe_stats_mu;
 static inline double now_s() {
@@ -442,6 +446,8 @@ void cvk_set_virtual_devices(int k) { g_virtual_devices = (k >= 1 && k <= 16) ? 
 
 // Tuning knob (internal): the host-buffer pipeline's shard threshold, first and steady sub-chunk sizes
 // (signatures; 0 keeps the current value) and packing threads.
+void cvk_set_direct_dma(int v) { g_direct_dma = v ? 1 : 0; }
+void cvk_set_small_pool_min(int n) { g_small_pool_min = n > 0 ? (size_t)n : 16384; }
 void cvk_set_pipe_slots(int k) { g_pipe_slots = (k >= 2 && k <= kSlots) ? k : 3; }
 void cvk_set_pipe(size_t min_n, size_t first, size_t chunk, int threads) {
     if (min_n) g_pipe_min = min_n;
@@ -465,6 +471,38 @@ void cvk_pipe_stats(double *out, int reset) {
         out[6] = (double)p.chunks;
     }
     if (reset) g_pipe_stats = PipeStats{};
+}
+// max(off[i] + len[i]) over n records (0 for n = 0): the arena bytes a batch reaches, for the Python
+// mirror's bounds check; slices of 2^20 records on up to 8 threads.
+uint64_t cvk_msg_end(size_t n, const uint64_t *off, const uint32_t *len) {
+    if (!n || !off || !len) return 0;
+    constexpr size_t kSlice = 1u << 20;
+    const size_t ns = (n + kSlice - 1) / kSlice;
+    std::vector<uint64_t> part(ns, 0);
+    auto scan = [&](size_t k) {
+        uint64_t hi = 0;
+        const size_t i1 = std::min(n, (k + 1) * kSlice);
+        for (size_t i = k * kSlice; i < i1; i++) hi = std::max<uint64_t>(hi, off[i] + len[i]);
+        part[k] = hi;
+    };
+    const size_t nt = std::min<size_t>(ns, 8);
+    if (nt <= 1) {
+        scan(0);
+    } else {
+        std::atomic<size_t> next{0};
+        std::vector<std::thread> th;
+        for (size_t t = 0; t < nt; t++)
+            th.emplace_back([&] {
+                for (size_t k; (k = next.fetch_add(1)) < ns;) scan(k);
+            });
+        for (auto &t : th) t.join();
+    }
+    return *std::max_element(part.begin(), part.end());
+}
+// sub-chunks of the pipelined path that were DMAed straight from pinned caller arrays (since the last reset)
+double cvk_pipe_direct_chunks(void) {
+    std::lock_guard<std::mutex> g(g_pipe_stats_mu);
+    return (double)g_pipe_stats.direct;
 }
 
 int cv_open(uint32_t device_mask, cv_ctx **out) {
@@ -529,6 +567,22 @@ void cv_close(cv_ctx *ctx) {
 }
 
 int cv_device_count(const cv_ctx *ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+
+int cv_host_alloc(cv_ctx *ctx, size_t bytes, void **out) {
+    if (!ctx || !out || bytes == 0) return CV_E_ARGS;
+    *out = nullptr;
+    CV_TRY(hipSetDevice(ctx->devs[0].ordinal));
+    void *p = nullptr;
+    const hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) return e == hipErrorOutOfMemory ? CV_E_OOM : CV_E_HIP;
+    *out = p;
+    return CV_OK;
+}
+
+void cv_host_free(cv_ctx *ctx, void *p) {
+    (void)ctx;
+    if (p) (void)hipHostFree(p);
+}
 
 static Device *find_dev(cv_ctx *ctx, int device) {
     for (Device &d : ctx->devs)
@@ -647,6 +701,46 @@ static void stage_pack(const Stage &st, uint8_t *h, size_t b, const uint8_t *pk,
     std::memset(har + (st.hi - st.lo), 0, 16);
 }
 
+// Is [p, p + bytes) page-locked host memory (hipHostMalloc / hipHostRegister)?  Both ends are looked
+// up; a failed lookup (pageable memory) clears the runtime's last-error state so no later
+// hipGetLastError reports it.
+static bool host_pinned(const void *p, size_t bytes) {
+    if (!p || bytes == 0) return p != nullptr;
+    const uint8_t *q[2] = {static_cast<const uint8_t *>(p), static_cast<const uint8_t *>(p) + bytes - 1};
+    for (const uint8_t *x : q) {
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, x) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (a.type != hipMemoryTypeHost) return false;
+    }
+    return true;
+}
+// Direct form of a stage: the record arrays of [b, e) and the arena range all pinned (and the arena
+// not compacted), so they can be DMAed from where they are.
+static bool stage_direct(const Stage &st, size_t b, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
+                         const uint64_t *off, const uint32_t *len) {
+    if (!g_direct_dma || st.compact) return false;
+    const size_t n = st.n;
+    return host_pinned(pk + b * 32, n * 32) && host_pinned(sig + b * 64, n * 64) && host_pinned(off + b, n * 8) &&
+           host_pinned(len + b, n * 4) && (st.hi == st.lo || host_pinned(arena + st.lo, st.hi - st.lo));
+}
+// The stage's DMAs straight from the caller's pinned arrays into the device block dv (the layout of
+// stage_pack), the arena's 16-byte tail zeroed on the device.
+static hipError_t stage_dma_direct(const Stage &st, uint8_t *dv, size_t b, const uint8_t *pk, const uint8_t *sig,
+                                   const uint8_t *arena, const uint64_t *off, const uint32_t *len, hipStream_t s) {
+    const size_t n = st.n;
+    hipError_t e = hipMemcpyAsync(dv + st.o_pk, pk + b * 32, n * 32, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(dv + st.o_sig, sig + b * 64, n * 64, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(dv + st.o_off, off + b, n * 8, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(dv + st.o_len, len + b, n * 4, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && st.hi > st.lo)
+        e = hipMemcpyAsync(dv + st.o_ar, arena + st.lo, st.hi - st.lo, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemsetAsync(dv + st.o_ar + (st.hi - st.lo), 0, 16, s);
+    return e;
+}
+
 // One shard [b, e) of a batch on one device, small form (the notary-sized batches): packed into slot 0's
 // pinned staging, moved by one DMA (two above 1 MB: the first overlaps packing the second part) into
 // one device block, verified, and the bitmap (+ status) come back by one DMA.  b is a multiple of 64,
@@ -655,7 +749,7 @@ static int verify_shard_small(Device &d, size_t b, size_t e, const uint8_t *pk, 
                               const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
                               uint8_t *status, int threads) {
     const size_t n = e - b;
-    WorkerPool *pool = n >= 16384 ? &d.workers(threads) : nullptr;
+    WorkerPool *pool = n >= g_small_pool_min ? &d.workers(threads) : nullptr;
     const Stage st = stage_plan(b, e, off, len, pool);
     const size_t words = (n + 63) / 64;
     const size_t o_bm = 0, o_st = al16(words * 8), total_out = o_st + al16(n);
@@ -680,15 +774,20 @@ static int verify_shard_small(Device &d, size_t b, size_t e, const uint8_t *pk, 
     // first, so it runs while the offsets, lengths and message bytes are packed (notary 65,536:
     // 1.29-1.34 -> 1.21-1.25 ms p50); below, one DMA (a second DMA's ~6 us would cost more than it hides).
     const bool two_stage = st.o_off >= ((size_t)1 << 20);
-    hipError_t e1 = hipSuccess;
-    stage_pack(st, h, b, pk, sig, arena, off, len, pool, [&] {
-        if (two_stage) e1 = hipMemcpyAsync(dv, h, st.o_off, hipMemcpyHostToDevice, s);
-    });
-    CV_TRY(e1);
-    if (two_stage)
-        CV_TRY(hipMemcpyAsync(dv + st.o_off, h + st.o_off, st.total - st.o_off, hipMemcpyHostToDevice, s));
-    else
-        CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, s));
+    if (stage_direct(st, b, pk, sig, arena, off, len)) {
+        // pinned caller arrays: no packing, the DMAs read them where they are
+        CV_TRY(stage_dma_direct(st, dv, b, pk, sig, arena, off, len, s));
+    } else {
+        hipError_t e1 = hipSuccess;
+        stage_pack(st, h, b, pk, sig, arena, off, len, pool, [&] {
+            if (two_stage) e1 = hipMemcpyAsync(dv, h, st.o_off, hipMemcpyHostToDevice, s);
+        });
+        CV_TRY(e1);
+        if (two_stage)
+            CV_TRY(hipMemcpyAsync(dv + st.o_off, h + st.o_off, st.total - st.o_off, hipMemcpyHostToDevice, s));
+        else
+            CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, s));
+    }
     uint8_t *dout = d.bitmap.as<uint8_t>();
     CV_TRY(launch_verify(d, sl, (uint32_t)n, dv + st.o_pk, dv + st.o_sig, dv + st.o_ar - st.lo,
                          reinterpret_cast<const uint64_t *>(dv + st.o_off), reinterpret_cast<const uint32_t *>(dv + st.o_len),
@@ -762,6 +861,26 @@ static int verify_shard_pipe(Device &d, size_t b, size_t e, const uint8_t *pk, c
         const Stage st = stage_plan(c0, c1, off, len, pool);
         double t1 = now_s();
         ps.plan += t1 - t0;
+        if (stage_direct(st, c0, pk, sig, arena, off, len)) {
+            // pinned caller arrays: this sub-chunk's DMAs read them in place (no staging, no packing);
+            // the slot's device block is free once its previous launch group has finished
+            if (sl.last) CV_TRY(hipEventSynchronize(sl.ev));
+            if (st.total > sl.packed.cap) CV_TRY(sl.packed.ensure(st.total));
+            t0 = now_s();
+            ps.wait += t0 - t1;
+            uint8_t *dv = sl.packed.as<uint8_t>();
+            CV_TRY(stage_dma_direct(st, dv, c0, pk, sig, arena, off, len, s));
+            const size_t w0 = (c0 - b) / 64;
+            CV_TRY(launch_verify(d, sl, (uint32_t)m, dv + st.o_pk, dv + st.o_sig, dv + st.o_ar - st.lo,
+                                 reinterpret_cast<const uint64_t *>(dv + st.o_off),
+                                 reinterpret_cast<const uint32_t *>(dv + st.o_len),
+                                 reinterpret_cast<uint64_t *>(dout) + w0, status ? dout + o_st + (c0 - b) : nullptr, s,
+                                 nullptr, false));
+            ps.enq += now_s() - t0;
+            ps.chunks++;
+            ps.direct++;
+            continue;
+        }
         if (sl.h2d_pending) {                       // the slot's staging is free once its DMA is done
             CV_TRY(hipEventSynchronize(sl.h2d));
             sl.h2d_pending = false;
@@ -812,6 +931,7 @@ static int verify_shard_pipe(Device &d, size_t b, size_t e, const uint8_t *pk, c
         G.sync += ps.sync;
         G.calls++;
         G.chunks += ps.chunks;
+        G.direct += ps.direct;
     }
     for (Slot &sl : d.slot) sl.h2d_pending = false;
     std::memcpy(bitmap + b / 64, hout, words * 8);

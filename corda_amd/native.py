@@ -8,6 +8,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import weakref
 from typing import Optional, Tuple
 
 import numpy as np
@@ -90,6 +91,13 @@ def load():
         lib.cv_merkle_tx_ids_ex.restype = ctypes.c_int
         lib.cv_ed25519_sign_batch.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]
         lib.cv_ed25519_sign_batch.restype = ctypes.c_int
+        lib.cv_host_alloc.argtypes = [_vp, _sz, ctypes.POINTER(_vp)]
+        lib.cv_host_alloc.restype = ctypes.c_int
+        lib.cv_host_free.argtypes = [_vp, _vp]
+        lib.cv_host_free.restype = None
+        if hasattr(lib, "cvk_msg_end"):
+            lib.cvk_msg_end.argtypes = [_sz, _vp, _vp]
+            lib.cvk_msg_end.restype = ctypes.c_uint64
         lib.cv_tx_verdicts.argtypes = [_sz, _vp, _vp, _vp]
         lib.cv_tx_verdicts.restype = ctypes.c_int
         if hasattr(lib, "cvk_set_verify_mode"):                 # internal tuning knobs (not C-ABI)
@@ -143,6 +151,13 @@ def _u8(a, shape_last=None) -> np.ndarray:
     return a
 
 
+def _msg_end(lib, off: np.ndarray, ln: np.ndarray) -> int:
+    """max(off + len) — the arena bytes the records reach (multi-threaded in the library for big n)."""
+    if hasattr(lib, "cvk_msg_end"):
+        return int(lib.cvk_msg_end(off.shape[0], _p(off), _p(ln)))
+    return int((off + ln).max())
+
+
 def _check(rc: int, what: str):
     if rc != CV_OK:
         raise CvError(rc, what)
@@ -187,6 +202,24 @@ class Engine:
         return self._lib.cv_device_count(self._h)
 
     # ------------------------------------------------------------ host-buffer API
+    def host_empty(self, shape, dtype=np.uint8) -> np.ndarray:
+        """An uninitialised numpy array in pinned host memory (cv_host_alloc), freed with its last view.
+        Host-buffer calls whose five input arrays are all pinned skip the engine's packing copy."""
+        shape = (shape,) if isinstance(shape, int) else tuple(shape)
+        nbytes = max(1, int(np.prod(shape)) * np.dtype(dtype).itemsize)
+        ptr = _vp()
+        _check(self._lib.cv_host_alloc(self._h, nbytes, ctypes.byref(ptr)), "cv_host_alloc")
+        buf = (ctypes.c_uint8 * nbytes).from_address(ptr.value)
+        weakref.finalize(buf, self._lib.cv_host_free, None, ctypes.c_void_p(ptr.value))
+        return np.frombuffer(buf, dtype=dtype, count=int(np.prod(shape))).reshape(shape)
+
+    def host_copy(self, a) -> np.ndarray:
+        """A pinned copy of array a (host_empty + copy)."""
+        a = np.ascontiguousarray(a)
+        out = self.host_empty(a.shape, a.dtype)
+        out[...] = a
+        return out
+
     def verify_batch(self, pk, sig, arena, off, ln, want_status: bool = True) -> Tuple[np.ndarray, Optional[np.ndarray]]:
         """pk (n,32) u8, sig (n,64) u8, arena u8, off u64[n], ln u32[n] -> (bitmap u64[ceil(n/64)], status u8[n])."""
         pk = _u8(pk)
@@ -199,7 +232,7 @@ class Engine:
         ln = np.ascontiguousarray(ln, dtype=np.uint32)
         if off.shape[0] != n or ln.shape[0] != n:
             raise ValueError("off/len must have n entries")
-        if n and int((off + ln).max()) > arena.size:
+        if n and _msg_end(self._lib, off, ln) > arena.size:
             raise ValueError("message range exceeds the arena")
         bitmap = np.zeros((n + 63) // 64, np.uint64)
         status = np.zeros(n, np.uint8) if want_status else None
@@ -222,7 +255,7 @@ class Engine:
         arena = _u8(arena) if arena is not None and np.asarray(arena).size else np.zeros(16, np.uint8)
         off = np.ascontiguousarray(off, dtype=np.uint64)
         ln = np.ascontiguousarray(ln, dtype=np.uint32)
-        if n and int((off + ln).max()) > arena.size:
+        if n and _msg_end(self._lib, off, ln) > arena.size:
             raise ValueError("message range exceeds the arena")
         bitmap = np.zeros((n + 63) // 64, np.uint64)
         status = np.zeros(n, np.uint8) if want_status else None

@@ -83,6 +83,15 @@ int cv_ed25519_verify_batch(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint
                             const uint8_t *msg_arena, const uint64_t *msg_off, const uint32_t *msg_len,
                             uint64_t *verdict_bitmap, uint8_t *status);
 
+/* Pinned host memory for the host-buffer API's inputs (hipHostMalloc).  When all five input arrays of
+ * cv_ed25519_verify_batch lie in pinned memory (from here, or any page-locked / registered host memory),
+ * the engine DMAs each sub-chunk's records straight out of them and skips its packing copy into its own
+ * staging: a JVM shim that builds its batches in buffers from cv_host_alloc (JNA Pointer ->
+ * ByteBuffer) feeds the GPU at PCIe rate.  The memory stays valid until cv_host_free; ctx only selects
+ * the allocator (any open context). */
+int cv_host_alloc(cv_ctx *ctx, size_t bytes, void **out);
+void cv_host_free(cv_ctx *ctx, void *p);
+
 /* Keyed batch: the distinct keys once, keys[nkeys][32], and per signature
  * key_index[n] into them.  Replaces the same N x PublicKey.verifyWithECDSA as
  * cv_ed25519_verify_batch — identical verdicts and status — for batches whose keys repeat (a notary

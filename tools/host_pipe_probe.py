@@ -19,8 +19,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from corda_amd import native, workload  # noqa: E402
 
 SETTINGS = [  # (first, chunk, threads)
-    (32768, 131072, 8), (65536, 262144, 8), (32768, 131072, 12), (32768, 131072, 16), (16384, 65536, 8),
-    (32768, 131072, 4),
+    (65536, 262144, 8), (65536, 262144, 16), (65536, 262144, 12), (32768, 131072, 16), (131072, 524288, 16),
+    (65536, 262144, 24),
 ]
 
 
@@ -80,6 +80,20 @@ def main():
                               "host_ms_per_call": {k: st[i] / calls * 1e3 for i, k in
                                                    enumerate(("plan", "pack", "wait", "enqueue", "sync"))},
                               "subchunks_per_call": st[6] / calls}), flush=True)
+        # the same call from pinned inputs (cv_host_alloc): sub-chunks DMAed in place, no packing
+        pinned = [eng.host_copy(x) for x in (pk, sig, arena, off, ln)]
+        for first, chunk in ((65536, 262144), (131072, 524288), (32768, 131072)):
+            lib.cvk_set_pipe(131072, first, chunk, 8)
+            eng.verify_batch(*pinned, want_status=False)
+            ts = []
+            for _ in range(a.reps):
+                t = time.perf_counter()
+                bm, _ = eng.verify_batch(*pinned, want_status=False)
+                ts.append(time.perf_counter() - t)
+            assert native.bitmap_to_bools(bm, n).all()
+            print(json.dumps({"shape": name, "pinned_inputs": True, "first": first, "chunk": chunk,
+                              "ms_med": float(np.median(ts) * 1e3), "ms_min": float(np.min(ts) * 1e3)}), flush=True)
+        del pinned
         # pack-only and copy-only rates of the host (what bounds the pipeline besides the GPU)
         t = time.perf_counter()
         _ = np.concatenate([pk.reshape(-1), sig.reshape(-1), arena])
