@@ -142,6 +142,7 @@ struct Slot {
     bool h2d_pending = false;
 };
 constexpr int kSlots = 4;
+constexpr int kRing = 6;   // input blocks of the host pipeline (more than slots: copies run ahead of kernels)
 
 // A fixed set of host threads for index-parallel jobs (the host-buffer path's packing and range scans):
 // run(ntasks, fn) calls fn(i) for every i in [0, ntasks) on the helpers and the calling thread and
@@ -226,6 +227,16 @@ struct Device {
     uint64_t clock = 0;
     KeyCache kc;
     std::unique_ptr<WorkerPool> pool;    // host packing threads (created on the first large host batch)
+    // The host pipeline's input ring (verify_shard_pipe): sub-chunk j's records go into device block
+    // j % kRing by the ONE copy stream (so every H2D copy runs on one DMA queue, never as a blit kernel
+    // beside the verify kernels), packed first into pinned staging block j % kRing when the caller's
+    // arrays are pageable.  in_ready[q]: after block q's copies (copy stream); in_free[q]: after the
+    // verify that read it (its slot stream).
+    hipStream_t copy = nullptr;
+    DevBuf inblk[kRing];
+    PinBuf instage[kRing];
+    hipEvent_t in_ready[kRing] = {}, in_free[kRing] = {};
+    bool in_used[kRing] = {}, stage_busy[kRing] = {};
     WorkerPool &workers(int threads) {
         if (!pool || pool->threads() != threads) {
             pool.reset();
@@ -558,6 +569,13 @@ void cv_close(cv_ctx *ctx) {
             if (sl.split.s2) (void)hipStreamDestroy(sl.split.s2);
             if (k > 0 && sl.stream) (void)hipStreamDestroy(sl.stream);
         }
+        for (int q = 0; q < kRing; q++) {
+            d.inblk[q].release();
+            d.instage[q].release();
+            for (hipEvent_t v : {d.in_ready[q], d.in_free[q]})
+                if (v) (void)hipEventDestroy(v);
+        }
+        if (d.copy) (void)hipStreamDestroy(d.copy);
         d.kc.pin.release();
         if (d.kc.ev) (void)hipEventDestroy(d.kc.ev);
         if (d.kc.pin_ev) (void)hipEventDestroy(d.kc.pin_ev);
@@ -727,7 +745,11 @@ static bool stage_direct(const Stage &st, size_t b, const uint8_t *pk, const uin
            host_pinned(len + b, n * 4) && (st.hi == st.lo || host_pinned(arena + st.lo, st.hi - st.lo));
 }
 // The stage's DMAs straight from the caller's pinned arrays into the device block dv (the layout of
-// stage_pack), the arena's 16-byte tail zeroed on the device.
+// stage_pack).  The 16 bytes after the arena part keep whatever the block held: the kernels read a
+// message only through dword windows clamped to its last byte and mask the bytes past it, so those
+// bytes never reach a verdict — and a fill there would be a blit KERNEL on the copy queue, which waits
+// for a free CU slot behind the running verify waves (it held the C2 copy stream for 2.5 ms,
+// profiles/r03d_timeline_pinned.txt).
 static hipError_t stage_dma_direct(const Stage &st, uint8_t *dv, size_t b, const uint8_t *pk, const uint8_t *sig,
                                    const uint8_t *arena, const uint64_t *off, const uint32_t *len, hipStream_t s) {
     const size_t n = st.n;
@@ -737,7 +759,6 @@ static hipError_t stage_dma_direct(const Stage &st, uint8_t *dv, size_t b, const
     if (e == hipSuccess) e = hipMemcpyAsync(dv + st.o_len, len + b, n * 4, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && st.hi > st.lo)
         e = hipMemcpyAsync(dv + st.o_ar, arena + st.lo, st.hi - st.lo, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemsetAsync(dv + st.o_ar + (st.hi - st.lo), 0, 16, s);
     return e;
 }
 
@@ -818,18 +839,17 @@ static std::vector<size_t> pipe_cuts(size_t b, size_t e, size_t first, size_t C)
     return cut;
 }
 
-// One shard [b, e) of a large batch, pipelined: sub-chunks (multiples of 64 signatures) go round-robin
-// over g_pipe_slots of the device's slots.  Sub-chunk j is packed by the host threads into slot
-// j % R's pinned staging (after that slot's previous DMA has left it), moved by one DMA on the slot's
-// stream and verified there with the slot's workspace, its bitmap words (+ status) landing in the
-// shard's device output.  So packing sub-chunk j+1, the DMA of sub-chunk j and the kernels of the
-// sub-chunks before it overlap, and the slots' kernels fill each other's drains.
-// No copy is ever enqueued behind a kernel that is still running: the DMA of sub-chunk j is enqueued
-// only after the host has seen the slot's previous verify finish, and the verdicts come back in ONE
-// copy after the last verify.  (A copy that waits for a kernel holds the DMA queue for the other
-// streams' copies behind it: with a bitmap copy after every sub-chunk, each sub-chunk's input DMA
-// waited for the previous sub-chunk's kernels and the pipeline ran at compute + transfer time,
-// C5 8M: 74 + 20 ms, tools/subchunk_probe.py.)
+// One shard [b, e) of a large batch, pipelined: sub-chunks (multiples of 64 signatures) go through a ring
+// of kRing device input blocks.  Sub-chunk j's records reach block j % kRing on the device's ONE copy
+// stream — straight from the caller's arrays when they are pinned (stage_direct), else packed by the
+// host threads into pinned staging block j % kRing first — and are verified on slot j % R's stream,
+// which waits for that copy (event) and marks the block free when its kernels are done.  The copy
+// stream waits (on the GPU) for the verify that last read a block before refilling it, so copies run
+// up to kRing sub-chunks ahead of the kernels and never queue behind a running kernel on a compute
+// stream.  One copy queue matters: with copies on every slot stream the runtime ran those of one
+// stream as blit kernels (`__amd_rocclr_copyBuffer`, ~37 GB/s, on the CUs beside the verify kernels)
+// and the C2 host call took 13.8-16 ms for 9.6 ms of kernels (profiles/r03c_timeline_*.txt).  The
+// verdicts come back in ONE copy after the last verify.
 static int verify_shard_pipe(Device &d, size_t b, size_t e, const uint8_t *pk, const uint8_t *sig,
                              const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
                              uint8_t *status, int threads) {
@@ -843,84 +863,81 @@ static int verify_shard_pipe(Device &d, size_t b, size_t e, const uint8_t *pk, c
         CV_TRY(slot_stream(d, k, &ss[k]));
         CV_TRY(slot_events(d.slot[k]));
     }
+    if (!d.copy) CV_TRY(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+    for (int q = 0; q < kRing; q++) {
+        if (!d.in_ready[q]) CV_TRY(hipEventCreateWithFlags(&d.in_ready[q], hipEventDisableTiming));
+        if (!d.in_free[q]) CV_TRY(hipEventCreateWithFlags(&d.in_free[q], hipEventDisableTiming));
+    }
     CV_TRY(d.pin_out.ensure(total_out));
     CV_TRY(d.bitmap.ensure(total_out));
     uint8_t *dout = d.bitmap.as<uint8_t>();
     uint8_t *hout = d.pin_out.as<uint8_t>();
     auto drain = on_exit([&] {
+        (void)hipStreamSynchronize(d.copy);
         for (int k = 0; k < nsl; k++) (void)hipStreamSynchronize(ss[k]);
-        for (Slot &sl : d.slot) sl.h2d_pending = false;
+        for (int q = 0; q < kRing; q++) d.in_used[q] = d.stage_busy[q] = false;
     });
     WorkerPool *pool = &d.workers(threads);
     PipeStats ps;
     for (size_t j = 0; j + 1 < cut.size(); j++) {
         const size_t c0 = cut[j], c1 = cut[j + 1], m = c1 - c0;
+        const int q = (int)(j % kRing);
         Slot &sl = d.slot[j % nsl];
         hipStream_t s = ss[j % nsl];
         double t0 = now_s();
         const Stage st = stage_plan(c0, c1, off, len, pool);
+        const bool direct = stage_direct(st, c0, pk, sig, arena, off, len);
         double t1 = now_s();
         ps.plan += t1 - t0;
-        if (stage_direct(st, c0, pk, sig, arena, off, len)) {
-            // pinned caller arrays: this sub-chunk's DMAs read them in place (no staging, no packing);
-            // the slot's device block is free once its previous launch group has finished
-            if (sl.last) CV_TRY(hipEventSynchronize(sl.ev));
-            if (st.total > sl.packed.cap) CV_TRY(sl.packed.ensure(st.total));
+        if (st.total > d.inblk[q].cap) {             // growing: the old block may still be read
+            if (d.in_used[q]) CV_TRY(hipEventSynchronize(d.in_free[q]));
+            CV_TRY(d.inblk[q].ensure(st.total));
+        }
+        if (d.in_used[q]) CV_TRY(hipStreamWaitEvent(d.copy, d.in_free[q], 0));
+        uint8_t *dv = d.inblk[q].as<uint8_t>();
+        if (direct) {
             t0 = now_s();
             ps.wait += t0 - t1;
-            uint8_t *dv = sl.packed.as<uint8_t>();
-            CV_TRY(stage_dma_direct(st, dv, c0, pk, sig, arena, off, len, s));
-            const size_t w0 = (c0 - b) / 64;
-            CV_TRY(launch_verify(d, sl, (uint32_t)m, dv + st.o_pk, dv + st.o_sig, dv + st.o_ar - st.lo,
-                                 reinterpret_cast<const uint64_t *>(dv + st.o_off),
-                                 reinterpret_cast<const uint32_t *>(dv + st.o_len),
-                                 reinterpret_cast<uint64_t *>(dout) + w0, status ? dout + o_st + (c0 - b) : nullptr, s,
-                                 nullptr, false));
-            ps.enq += now_s() - t0;
-            ps.chunks++;
+            CV_TRY(stage_dma_direct(st, dv, c0, pk, sig, arena, off, len, d.copy));
             ps.direct++;
-            continue;
+        } else {
+            // staging block q is free once its previous copy has left it
+            if (d.stage_busy[q]) {
+                CV_TRY(hipEventSynchronize(d.in_ready[q]));
+                d.stage_busy[q] = false;
+            }
+            CV_TRY(d.instage[q].ensure(st.total));
+            t0 = now_s();
+            ps.wait += t0 - t1;
+            uint8_t *h = d.instage[q].as<uint8_t>();
+            stage_pack(st, h, c0, pk, sig, arena, off, len, pool, [] {});
+            t1 = now_s();
+            ps.pack += t1 - t0;
+            t0 = t1;
+            CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, d.copy));
+            d.stage_busy[q] = true;
         }
-        if (sl.h2d_pending) {                       // the slot's staging is free once its DMA is done
-            CV_TRY(hipEventSynchronize(sl.h2d));
-            sl.h2d_pending = false;
-        }
-        t0 = now_s();
-        ps.wait += t0 - t1;
-        if (st.total > sl.pin_in.cap || st.total > sl.packed.cap) {
-            CV_TRY(hipStreamSynchronize(s));        // the device copy may still be read by a queued verify
-            CV_TRY(sl.pin_in.ensure(st.total));
-            CV_TRY(sl.packed.ensure(st.total));
-        }
-        uint8_t *h = sl.pin_in.as<uint8_t>();
-        uint8_t *dv = sl.packed.as<uint8_t>();
-        stage_pack(st, h, c0, pk, sig, arena, off, len, pool, [] {});
-        t1 = now_s();
-        ps.pack += t1 - t0;
-        // the slot's device input block is free once its last launch group (sub-chunk j - R, or a
-        // device-API call) has finished: wait for that here, so the DMA below depends on nothing
-        if (sl.last) CV_TRY(hipEventSynchronize(sl.ev));
-        t0 = now_s();
-        ps.wait += t0 - t1;
-        t1 = t0;
-        CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, s));
-        CV_TRY(hipEventRecord(sl.h2d, s));
-        sl.h2d_pending = true;
+        CV_TRY(hipEventRecord(d.in_ready[q], d.copy));
+        CV_TRY(hipStreamWaitEvent(s, d.in_ready[q], 0));
         const size_t w0 = (c0 - b) / 64;
         CV_TRY(launch_verify(d, sl, (uint32_t)m, dv + st.o_pk, dv + st.o_sig, dv + st.o_ar - st.lo,
                              reinterpret_cast<const uint64_t *>(dv + st.o_off),
                              reinterpret_cast<const uint32_t *>(dv + st.o_len),
                              reinterpret_cast<uint64_t *>(dout) + w0, status ? dout + o_st + (c0 - b) : nullptr, s,
                              nullptr, false));
-        ps.enq += now_s() - t1;
+        CV_TRY(hipEventRecord(d.in_free[q], s));
+        d.in_used[q] = true;
+        ps.enq += now_s() - t0;
         ps.chunks++;
     }
     const double t0 = now_s();
     for (int k = 0; k < nsl; k++) CV_TRY(hipStreamSynchronize(ss[k]));
     CV_TRY(hipMemcpyAsync(hout, dout, status ? o_st + n : words * 8, hipMemcpyDeviceToHost, ss[0]));
     CV_TRY(hipStreamSynchronize(ss[0]));
+    CV_TRY(hipStreamSynchronize(d.copy));
     ps.sync += now_s() - t0;
     drain.armed = false;
+    for (int q = 0; q < kRing; q++) d.in_used[q] = d.stage_busy[q] = false;
     {
         std::lock_guard<std::mutex> g(g_pipe_stats_mu);
         PipeStats &G = g_pipe_stats;
@@ -933,7 +950,6 @@ static int verify_shard_pipe(Device &d, size_t b, size_t e, const uint8_t *pk, c
         G.chunks += ps.chunks;
         G.direct += ps.direct;
     }
-    for (Slot &sl : d.slot) sl.h2d_pending = false;
     std::memcpy(bitmap + b / 64, hout, words * 8);
     if (status) std::memcpy(status + b, hout + o_st, n);
     return CV_OK;

@@ -132,7 +132,7 @@ extern "C" void cvk_set_prep_lat_fused(int v) { g_prep_lat_fused = v ? 1 : 0; }
 
 // field forms of the latency Straus kernels: bit 0 = tri, bit 1 = quad use the sequential-carry
 // multiplications (fewer instructions) instead of the ILP forms
-static int g_lat_seq = 0;
+static int g_lat_seq = 3;
 extern "C" void cvk_set_lat_seq(int v) { g_lat_seq = v & 3; }
 
 // Batches of at most this many signatures run the quad kernels (set by cvk_set_quad_max; 0 = never)
@@ -437,7 +437,7 @@ hipError_t cvk_pmt_verify(uint32_t ntrees, const uint8_t *kind, const uint32_t *
 
 }  // extern "C"
 // leaf hashing: 0 = length-sorted passes (cv_leaf_hash_kernel), 1 = balanced pairs (cv_leaf_hash_pair_kernel)
-static int g_leaf_mode = 0;
+static int g_leaf_mode = 1;
 extern "C" {
 void cvk_set_leaf_mode(int m) { g_leaf_mode = m == 1 ? 1 : 0; }
 

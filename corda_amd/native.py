@@ -30,7 +30,7 @@ EXPORTED = (
     "cv_tx_verdicts", "cv_ed25519_verify_device", "cv_ed25519_verify_device_timed", "cv_ed25519_sign_device", "cv_merkle_tx_ids_device",
     "cv_synchronize", "cv_calibrate", "cv_ed25519_verify_batch_keyed", "cv_key_cache_reserve", "cv_key_cache_stats",
     "cv_ed25519_verify_device_keyed", "cv_partial_merkle_verify", "cv_calibrate_cycles", "cv_diag_prep_phases",
-    "cv_diag_dedupe_keys",
+    "cv_diag_dedupe_keys", "cv_host_alloc", "cv_host_free",
 )
 
 

@@ -1,0 +1,12 @@
+#!/bin/bash
+# round-3 session 4: the copy-stream / input-ring host pipeline: pipeline tests, host probe (C2, C5,
+# pinned and pageable), timelines of pinned and pageable C2 calls
+cd "${GRAFT_REPO_ROOT:-.}" || exit 1
+T=${1:-r03d}
+O=gpurun_out/$T
+bash scripts/gpu_multi.sh "$T" --skip-check \
+  "timeout -k 10 300 python -u -m pytest tests/test_gpu_pipeline.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread" \
+  "timeout -k 10 400 python -u tools/host_pipe_probe.py --reps 3" \
+  "timeout -k 10 120 rocprofv3 --kernel-trace --memory-copy-trace -d $O/tl_pin -o t --output-format csv -- python3 tools/host_timeline.py --shape c2 --pinned 1" \
+  "timeout -k 10 120 rocprofv3 --kernel-trace --memory-copy-trace -d $O/tl_page -o t --output-format csv -- python3 tools/host_timeline.py --shape c2 --pinned 0" \
+  "python3 tools/host_timeline.py --summarize $O/tl_pin > $O/tl_pin.txt && python3 tools/host_timeline.py --summarize $O/tl_page > $O/tl_page.txt"

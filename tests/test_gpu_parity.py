@@ -156,7 +156,7 @@ def leaf_mode(request):
     lib.cvk_set_leaf_mode.argtypes = [ctypes.c_int]
     lib.cvk_set_leaf_mode(request.param)
     yield request.param
-    lib.cvk_set_leaf_mode(0)
+    lib.cvk_set_leaf_mode(1)              # the default
 
 
 def test_merkle_golden(engine, merkle_cases, leaf_mode):

@@ -46,6 +46,10 @@ def main():
         rec["lane_utilisation"] = tot_t / (64 * act) if act else None
         rec["valu_active_lane_instr_per_compression"] = tot_t / c
         rec["instr_efficiency_vs_floor"] = bench.SHA256_FLOOR_INSTR / (tot_t / c)
+        rec["lane_utilisation_per_kernel"] = {
+            k: d["SQ_THREAD_CYCLES_VALU"] / (64 * d["SQ_ACTIVE_INST_VALU"])
+            for k, d in rec["kernels"].items() if d.get("SQ_ACTIVE_INST_VALU")}
+    rec["leaf_mode"] = line.get("leaf_mode")
     print(json.dumps(rec, indent=1))
     if out:
         with open(out, "w") as f:
