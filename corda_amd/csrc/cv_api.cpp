@@ -267,11 +267,16 @@ constexpr uint32_t kVerifyChunk = 1u << 22;
 // sub-chunk of g_pipe_first (short, so the GPU starts early) and then sub-chunks of g_pipe_chunk (the
 // last two balanced), dealt round-robin over the device's slots; g_pack_threads host threads pack each
 // sub-chunk into pinned staging while the earlier ones transfer and verify.
-static size_t g_pipe_min = 131072, g_pipe_first = 65536, g_pipe_chunk = 262144;
+static size_t g_pipe_min = 131072, g_pipe_first = 32768, g_pipe_chunk = 262144;
 static int g_pack_threads = 8;
 // small-form batches of at least this many signatures pack their staging on the device's worker pool
 static size_t g_small_pool_min = 16384;
-static int g_pipe_slots = 3;   // slots the pipeline deals its sub-chunks over (2..kSlots)
+// compute slots the pipeline deals its sub-chunks over (2..kSlots).  2: with GPU_MAX_HW_QUEUES = 4
+// (HIP's default) the null stream, the device stream, one more slot stream and the copy stream each get
+// a hardware queue; a third slot stream shares one — with the copy stream, whose copies then waited
+// behind that slot's Straus kernel (2.4 ms stalls, profiles/r03e_timeline_pinned_nofill.txt)
+static int g_pipe_slots = 2;
+static int g_pipe_ramp = 1;    // sub-chunk sizes double from g_pipe_first up to g_pipe_chunk
 // host-side time of the pipelined path, seconds (cvk_pipe_stats): range scans, packing, waits for a
 // slot's staging, enqueue (HIP calls), the final synchronisation; and calls / sub-chunks
 struct PipeStats {
@@ -459,7 +464,8 @@ void cvk_set_virtual_devices(int k) { g_virtual_devices = (k >= 1 && k <= 16) ? 
 // (signatures; 0 keeps the current value) and packing threads.
 void cvk_set_direct_dma(int v) { g_direct_dma = v ? 1 : 0; }
 void cvk_set_small_pool_min(int n) { g_small_pool_min = n > 0 ? (size_t)n : 16384; }
-void cvk_set_pipe_slots(int k) { g_pipe_slots = (k >= 2 && k <= kSlots) ? k : 3; }
+void cvk_set_pipe_slots(int k) { g_pipe_slots = (k >= 2 && k <= kSlots) ? k : 2; }
+void cvk_set_pipe_ramp(int v) { g_pipe_ramp = v ? 1 : 0; }
 void cvk_set_pipe(size_t min_n, size_t first, size_t chunk, int threads) {
     if (min_n) g_pipe_min = min_n;
     if (first) g_pipe_first = std::max<size_t>(64, first / 64 * 64);
@@ -823,16 +829,21 @@ static int verify_shard_small(Device &d, size_t b, size_t e, const uint8_t *pk, 
 
 // The pipeline's sub-chunk boundaries of [b, e): [first, C, C, ..., the last two balanced]; every
 // boundary but e is b + a multiple of 64 (whole bitmap words per sub-chunk).
-static std::vector<size_t> pipe_cuts(size_t b, size_t e, size_t first, size_t C) {
+// With ramp, the sizes after the first double (first, 2 first, 4 first, ...) until they reach C: each
+// sub-chunk's copy then takes about as long as the kernels of the one before it, so the GPU is not left
+// waiting for a big second sub-chunk while a small first one has long finished.
+static std::vector<size_t> pipe_cuts(size_t b, size_t e, size_t first, size_t C, bool ramp = false) {
     std::vector<size_t> cut{b};
     if (e <= b) return cut;
     first = std::max<size_t>(64, first / 64 * 64);
     C = std::max<size_t>(64, C / 64 * 64);
     size_t p = b + std::min(e - b, first);
     cut.push_back(p);
+    size_t step = first;
     while (p < e) {
         const size_t rem = e - p;
-        const size_t m = rem <= C ? rem : rem < 2 * C ? (rem / 2 + 63) / 64 * 64 : C;
+        step = ramp ? std::min(C, 2 * step) : C;
+        const size_t m = rem <= step ? rem : rem < 2 * step ? (rem / 2 + 63) / 64 * 64 : step;
         p += m;
         cut.push_back(p);
     }
@@ -856,7 +867,7 @@ static int verify_shard_pipe(Device &d, size_t b, size_t e, const uint8_t *pk, c
     const size_t n = e - b;
     const size_t words = (n + 63) / 64;
     const size_t o_st = al16(words * 8), total_out = o_st + al16(n);
-    const std::vector<size_t> cut = pipe_cuts(b, e, g_pipe_first, g_pipe_chunk);
+    const std::vector<size_t> cut = pipe_cuts(b, e, g_pipe_first, g_pipe_chunk, g_pipe_ramp != 0);
     const int nsl = g_pipe_slots;
     hipStream_t ss[kSlots] = {};
     for (int k = 0; k < nsl; k++) {

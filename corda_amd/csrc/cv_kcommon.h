@@ -61,6 +61,9 @@ __device__ __forceinline__ void cv_scalars_lane(uint32_t i, uint32_t cap, const 
 // lane decoding the key A into k*(-A), the odd lane R into k*R, side by side (the same instructions
 // on both lanes: cv_hs_point_one) with the latency (ILP) field forms — half the serial chain of the
 // throughput form, whose single lane runs both decodes.  The even lane writes ok = key_ok AND r_ok.
+// LAT = false: the sequential-carry field forms for the lone wave's decode chain (as the latency Straus
+// kernels' SEQ forms), true: the ILP forms
+template <bool LAT = true>
 __device__ __forceinline__ void cv_points_pair_lane(uint32_t g, uint32_t n, const uint8_t *pk, const uint8_t *sig,
                                                     uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok,
                                                     uint8_t *status) {
@@ -69,7 +72,7 @@ __device__ __forceinline__ void cv_points_pair_lane(uint32_t g, uint32_t n, cons
     const bool is_r = (g & 1u) != 0;
     uint32_t w[8];
     load_words8(w, is_r ? sig + (size_t)i * 64 : pk + (size_t)i * 32);
-    const bool ok = cv_hs_point_one<true>(w, is_r, (is_r ? ws_tabR : ws_tab) + (size_t)i * CV_TAB_WORDS);
+    const bool ok = cv_hs_point_one<LAT>(w, is_r, (is_r ? ws_tabR : ws_tab) + (size_t)i * CV_TAB_WORDS);
     const bool r_ok = __shfl_xor((int)ok, 1) != 0;
     if (!is_r) {
         ws_ok[i] = (ok && r_ok) ? 1 : 0;
@@ -114,7 +117,7 @@ template <int WAVES, bool SUB = false> __global__ void cv_hs_straus_kernel(uint3
 __global__ void cv_bw16_init_kernel(uint32_t *tab);
 __global__ void cv_scalars_lat_kernel(uint32_t n, uint32_t cap, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig);
 __global__ void cv_points_pair_kernel(uint32_t n, const uint8_t *pk, const uint8_t *sig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
-template <bool B16> __global__ void cv_prep_lat_kernel(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
+template <bool B16, bool LAT = true> __global__ void cv_prep_lat_kernel(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
 template <bool SEQ> __global__ void cv_hs_straus_quad_kernel(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);
 template <bool SEQ> __global__ void cv_hs_straus_tri_kernel(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap);
 __global__ void cv_sign_kernel( uint32_t n, const uint8_t *seed, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint8_t *pk_out, uint8_t *sig_out);

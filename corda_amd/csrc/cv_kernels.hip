@@ -130,10 +130,11 @@ extern "C" uint32_t cvk_get_tri_max(void) { return g_tri_max; }
 static int g_prep_lat_fused = 1;
 extern "C" void cvk_set_prep_lat_fused(int v) { g_prep_lat_fused = v ? 1 : 0; }
 
-// field forms of the latency Straus kernels: bit 0 = tri, bit 1 = quad use the sequential-carry
-// multiplications (fewer instructions) instead of the ILP forms
+// field forms of the latency kernels: bit 0 = tri, bit 1 = quad Straus, bit 2 = the fused latency
+// prep's point decodes use the sequential-carry multiplications (fewer instructions) instead of the
+// ILP forms
 static int g_lat_seq = 3;
-extern "C" void cvk_set_lat_seq(int v) { g_lat_seq = v & 3; }
+extern "C" void cvk_set_lat_seq(int v) { g_lat_seq = v & 7; }
 
 // Batches of at most this many signatures run the quad kernels (set by cvk_set_quad_max; 0 = never)
 static uint32_t g_quad_max = 32768;
@@ -217,13 +218,23 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             if (!tri && !bw16) return hipErrorInvalidValue;   // (cannot happen: fetched above)
             if (g_prep_lat_fused || tri) {
                 const uint32_t nbp = (2 * m + 63) / 64, nbs = (m + 63) / 64;
-                if (tri)
-                    hipLaunchKernelGGL(cv_prep_lat_kernel<true>, dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp,
+                if (tri && (g_lat_seq & 4))
+                    hipLaunchKernelGGL((cv_prep_lat_kernel<true, false>), dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp,
+                                       pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0,
+                                       ws_dig, ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr,
+                                       bitmap + (size_t)c0 / 64);
+                else if (!tri && (g_lat_seq & 4))
+                    hipLaunchKernelGGL((cv_prep_lat_kernel<false, false>), dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp,
+                                       pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0,
+                                       ws_dig, ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr,
+                                       bitmap + (size_t)c0 / 64);
+                else if (tri)
+                    hipLaunchKernelGGL((cv_prep_lat_kernel<true, true>), dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp,
                                        pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0,
                                        ws_dig, ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr,
                                        bitmap + (size_t)c0 / 64);
                 else
-                    hipLaunchKernelGGL(cv_prep_lat_kernel<false>, dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp,
+                    hipLaunchKernelGGL((cv_prep_lat_kernel<false, true>), dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp,
                                        pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0,
                                        ws_dig, ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr,
                                        bitmap + (size_t)c0 / 64);

@@ -340,6 +340,39 @@ def test_lane_quad_and_tri_forms_agree(engine, corpus, oracle_c, quad_max, tri_m
         lib.cvk_set_tri_max(4096)
 
 
+@pytest.mark.parametrize("lat_seq", [0, 7])
+@pytest.mark.parametrize("n", [4096, 9001])
+def test_latency_field_forms_agree(engine, corpus, oracle_c, lat_seq, n):
+    """The latency kernels' two field forms (cvk_set_lat_seq: 0 = ILP forms everywhere, 7 = the
+    sequential-carry forms in the tri and quad Straus AND the fused prep's decodes): the golden corpus
+    tiled to n records (n = 4,096: tri chain, 9,001: quad) gives the pinned verdicts and statuses, and
+    a corrupted random batch of n the C oracle's."""
+    import ctypes
+    lib = native.load()
+    lib.cvk_set_lat_seq.argtypes = [ctypes.c_int]
+    lib.cvk_set_lat_seq(lat_seq)
+    try:
+        rng = np.random.default_rng(n + lat_seq)
+        sel = rng.integers(0, len(corpus["pk"]), n)
+        bitmap, status = engine.verify_batch(corpus["pk"][sel], corpus["sig"][sel], corpus["arena"],
+                                             corpus["off"][sel], corpus["len"][sel])
+        assert np.array_equal(_bits(bitmap, n), corpus["verdict"][sel].astype(bool))
+        assert np.array_equal(status, corpus["status"][sel])
+        seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+        arena = rng.integers(0, 256, n * 32 + 16, dtype=np.uint8)
+        off = np.arange(n, dtype=np.uint64) * 32
+        ln = np.full(n, 32, np.uint32)
+        pk, sig = engine.sign_batch(seeds, arena, off, ln)
+        sig[1::5, 35] ^= 4
+        pk[2::7, 3] ^= 0x40
+        bitmap, status = engine.verify_batch(pk, sig, arena, off, ln)
+        ref, rst = oracle_c.verify_batch(pk, sig, arena, off, ln, nthreads=8)
+        assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
+        assert np.array_equal(status, rst)
+    finally:
+        lib.cvk_set_lat_seq(3)
+
+
 # ---------------------------------------------------------------- both throughput schedules
 @pytest.mark.parametrize("mode", [0, 1])
 def test_full_width_and_half_size_schedules_agree(engine, corpus, oracle_c, mode):

@@ -18,7 +18,7 @@ from corda_amd import native, workload
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
-PIPE_DEFAULT = (131072, 65536, 262144, 8)
+PIPE_DEFAULT = (131072, 32768, 262144, 8)
 
 
 def _bits(bitmap, n):

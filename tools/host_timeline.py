@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--slots", type=int, default=0)
+    ap.add_argument("--ramp", type=int, default=-1)
     a = ap.parse_args()
     if a.summarize:
         summarize(a.summarize)
@@ -64,6 +65,8 @@ def main():
     lib.cvk_set_pipe(0, a.first, a.chunk, a.threads)
     if a.slots:
         lib.cvk_set_pipe_slots(a.slots)
+    if a.ramp >= 0:
+        lib.cvk_set_pipe_ramp(a.ramp)
     eng = native.Engine(1)
     n, ml = (1_000_000, 300) if a.shape == "c2" else (8_000_000, 32)
     b = workload.make_batch(eng, 0, n, ml, seed=11)
