@@ -285,6 +285,7 @@ struct PipeStats {
 };
 // 1 = pinned caller arrays are DMAed in place (stage_direct); 0 = always pack (A/B knob)
 static int g_direct_dma = 1;
+static size_t g_direct_small_min = 16384;   // the small path's direct-DMA threshold (signatures)
 static PipeStats g_pipe_stats;
 static std::mutex g_pipe_stats_mu;
 static inline double now_s() {
@@ -463,6 +464,7 @@ void cvk_set_virtual_devices(int k) { g_virtual_devices = (k >= 1 && k <= 16) ? 
 // Tuning knob (internal): the host-buffer pipeline's shard threshold, first and steady sub-chunk sizes
 // (signatures; 0 keeps the current value) and packing threads.
 void cvk_set_direct_dma(int v) { g_direct_dma = v ? 1 : 0; }
+void cvk_set_direct_small_min(int n) { g_direct_small_min = n > 0 ? (size_t)n : 16384; }
 void cvk_set_small_pool_min(int n) { g_small_pool_min = n > 0 ? (size_t)n : 16384; }
 void cvk_set_pipe_slots(int k) { g_pipe_slots = (k >= 2 && k <= kSlots) ? k : 2; }
 void cvk_set_pipe_ramp(int v) { g_pipe_ramp = v ? 1 : 0; }
@@ -801,7 +803,10 @@ static int verify_shard_small(Device &d, size_t b, size_t e, const uint8_t *pk, 
     // first, so it runs while the offsets, lengths and message bytes are packed (notary 65,536:
     // 1.29-1.34 -> 1.21-1.25 ms p50); below, one DMA (a second DMA's ~6 us would cost more than it hides).
     const bool two_stage = st.o_off >= ((size_t)1 << 20);
-    if (stage_direct(st, b, pk, sig, arena, off, len)) {
+    // below g_direct_small_min signatures one packed DMA beats five direct ones even from pinned
+    // arrays (notary 4,096: 0.328 ms p50 packed vs 0.342 direct; 65,536: 1.28 vs 1.10,
+    // profiles/r03h_bench.json)
+    if (n >= g_direct_small_min && stage_direct(st, b, pk, sig, arena, off, len)) {
         // pinned caller arrays: no packing, the DMAs read them where they are
         CV_TRY(stage_dma_direct(st, dv, b, pk, sig, arena, off, len, s));
     } else {

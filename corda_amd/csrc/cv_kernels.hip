@@ -133,7 +133,7 @@ extern "C" void cvk_set_prep_lat_fused(int v) { g_prep_lat_fused = v ? 1 : 0; }
 // field forms of the latency kernels: bit 0 = tri, bit 1 = quad Straus, bit 2 = the fused latency
 // prep's point decodes use the sequential-carry multiplications (fewer instructions) instead of the
 // ILP forms
-static int g_lat_seq = 3;
+static int g_lat_seq = 7;
 extern "C" void cvk_set_lat_seq(int v) { g_lat_seq = v & 7; }
 
 // Batches of at most this many signatures run the quad kernels (set by cvk_set_quad_max; 0 = never)

@@ -370,7 +370,7 @@ def test_latency_field_forms_agree(engine, corpus, oracle_c, lat_seq, n):
         assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
         assert np.array_equal(status, rst)
     finally:
-        lib.cvk_set_lat_seq(3)
+        lib.cvk_set_lat_seq(7)
 
 
 # ---------------------------------------------------------------- both throughput schedules

@@ -52,7 +52,7 @@ def main():
         variants.append((name, [(k, tuple(int(x) for x in a.split("/"))) for k, a in
                                 (kv.split("=") for kv in filter(None, body.split(",")))]))
     used = {k for _, sets in variants for k, _ in sets}
-    reset = {"cvk_set_small_pool_min": (16384,), "cvk_set_lat_seq": (3,), "cvk_set_tri_max": (4096,), "cvk_set_prep_lat_fused": (1,)}
+    reset = {"cvk_set_small_pool_min": (16384,), "cvk_set_lat_seq": (7,), "cvk_set_tri_max": (4096,), "cvk_set_prep_lat_fused": (1,)}
 
     def apply(sets):
         for k in used:
