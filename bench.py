@@ -130,6 +130,21 @@ def host_api_rate(eng, batch, steps: int, device_value: float, name: str):
         assert native.bitmap_to_bools(bm, n).all(), "host API rejected an honest signature"
         return dt
 
+    def timed_async(a):
+        """K calls with two in flight (cv_ed25519_verify_batch_async / cv_wait): submit k+1, then wait k."""
+        eng.wait(eng.verify_batch_async(*a, want_status=False))
+        t = time.perf_counter()
+        pend = []
+        for _ in range(steps):
+            pend.append(eng.verify_batch_async(*a, want_status=False))
+            if len(pend) == 2:
+                bm, _ = eng.wait(pend.pop(0))
+        for tk in pend:
+            bm, _ = eng.wait(tk)
+        dt = time.perf_counter() - t
+        assert native.bitmap_to_bools(bm, n).all(), "async host API rejected an honest signature"
+        return dt
+
     dt_page = timed((pk, sig, arena, off, ln))
     pinned = tuple(eng.host_copy(x) for x in (pk, sig, arena, off, ln))
     lib = native.load()
@@ -138,17 +153,26 @@ def host_api_rate(eng, batch, steps: int, device_value: float, name: str):
     lib.cvk_pipe_stats(None, 1)
     dt_pin = timed(pinned)
     direct = int(lib.cvk_pipe_direct_chunks())
+    dt_async = timed_async(pinned)
+    dt_async_page = timed_async((pk, sig, arena, off, ln))
     del pinned
-    v, vp = n * steps / dt_pin, n * steps / dt_page
-    return {"workload": name, "value": v, "unit": "verifies/s", "ms_per_step": dt_pin / steps * 1e3, "steps": steps,
+    v, vp, vs = n * steps / dt_async, n * steps / dt_page, n * steps / dt_pin
+    va = n * steps / dt_async_page
+    return {"workload": name, "value": v, "unit": "verifies/s", "ms_per_step": dt_async / steps * 1e3, "steps": steps,
             "sigs": n, "ratio_to_device_value": v / device_value, "device_value": device_value,
-            "input_bytes_per_call": in_bytes, "input_gb_per_s": in_bytes * steps / dt_pin / 1e9,
-            "direct_dma_subchunks": direct,
-            "path": "cv_ed25519_verify_batch from pinned host buffers (cv_host_alloc): sub-chunks DMAed in place",
+            "input_bytes_per_call": in_bytes, "input_gb_per_s": in_bytes * steps / dt_async / 1e9,
+            "path": "cv_ed25519_verify_batch_async from pinned host buffers (cv_host_alloc), two calls in flight "
+                    "(a batching node submits batch k+1 before waiting for batch k); sub-chunks DMAed in place",
+            "sync_pinned": {"value": vs, "ms_per_step": dt_pin / steps * 1e3, "ratio_to_device_value": vs / device_value,
+                            "direct_dma_subchunks": direct,
+                            "path": "cv_ed25519_verify_batch (synchronous, one call at a time) from pinned buffers"},
+            "async_pageable": {"value": va, "ms_per_step": dt_async_page / steps * 1e3,
+                               "ratio_to_device_value": va / device_value,
+                               "path": "cv_ed25519_verify_batch_async from pageable numpy buffers, two in flight"},
             "pageable": {"value": vp, "ms_per_step": dt_page / steps * 1e3, "ratio_to_device_value": vp / device_value,
                          "input_gb_per_s": in_bytes * steps / dt_page / 1e9,
-                         "path": "cv_ed25519_verify_batch from pageable numpy buffers (host threads pack pinned "
-                                 "staging per sub-chunk)"}}
+                         "path": "cv_ed25519_verify_batch (synchronous) from pageable numpy buffers (host threads "
+                                 "pack pinned staging per sub-chunk)"}}
 
 
 def affinity_cores() -> int:
@@ -520,7 +544,7 @@ def c5_line(eng, local, rank, sh, dev, n, steps, mad_rate, host_api: bool = True
     el = time.perf_counter() - t0
     assert bool((bm == -1).all()) or n % 64, "C5: verify rejected an honest signature"
     ph = np.mean(np.array([eng.verify_device_timed(local, n, *a, sh) for _ in range(2)]), axis=0)
-    host = host_api_rate(eng, b, 2, n * steps / el, CONFIG_NAME["c5"] + " (host buffers)") if host_api else None
+    host = host_api_rate(eng, b, 3, n * steps / el, CONFIG_NAME["c5"] + " (host buffers)") if host_api else None
     del b
     return {"workload": CONFIG_NAME["c5"], "value": n * steps / el, "unit": "verifies/s", "host_api": host,
             "ms_per_step": el / steps * 1e3, "steps": steps, "sigs_per_gpu": n,
@@ -715,7 +739,7 @@ def main():
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(batch, local, args.cpu_seconds)
         if world == 1 and not args.no_host:
-            result["host_api"] = {"c2": host_api_rate(eng, batch, max(3, args.steps // 2), value,
+            result["host_api"] = {"c2": host_api_rate(eng, batch, max(6, args.steps), value,
                                                       CONFIG_NAME[args.config] + " (host buffers)"),
                                   "pcie_h2d_gb_per_s_pinned": pcie_h2d_probe(dev)}
         if world == 1 and not args.no_sub:

@@ -143,6 +143,21 @@ struct Slot {
 };
 constexpr int kSlots = 4;
 constexpr int kRing = 6;   // input blocks of the host pipeline (more than slots: copies run ahead of kernels)
+constexpr int kOuts = 2;   // host pipeline calls in flight per device (cv_ed25519_verify_batch_async)
+
+// The verdict output of one pipelined host call on one device: bitmap words | status bytes on the
+// device, their pinned host copy, and the event after that copy.  pending: enqueued, not yet copied
+// into the caller's arrays (pipe_finish does that); gen counts the calls that used this slot.
+struct PipeOut {
+    DevBuf dout;
+    PinBuf hout;
+    hipEvent_t done = nullptr;
+    bool pending = false;
+    uint64_t gen = 0;
+    uint64_t *bitmap = nullptr;
+    uint8_t *status = nullptr;
+    size_t b = 0, n = 0, o_st = 0;
+};
 
 // A fixed set of host threads for index-parallel jobs (the host-buffer path's packing and range scans):
 // run(ntasks, fn) calls fn(i) for every i in [0, ntasks) on the helpers and the calling thread and
@@ -233,10 +248,13 @@ struct Device {
     // arrays are pageable.  in_ready[q]: after block q's copies (copy stream); in_free[q]: after the
     // verify that read it (its slot stream).
     hipStream_t copy = nullptr;
+    PipeOut out[kOuts];                  // the pipeline's verdict outputs, one per call in flight
+    int out_next = 0;
     DevBuf inblk[kRing];
     PinBuf instage[kRing];
     hipEvent_t in_ready[kRing] = {}, in_free[kRing] = {};
     bool in_used[kRing] = {}, stage_busy[kRing] = {};
+    int ring_next = 0;                   // the ring block the next sub-chunk takes
     WorkerPool &workers(int threads) {
         if (!pool || pool->threads() != threads) {
             pool.reset();
@@ -436,6 +454,9 @@ struct cv_ctx {
     std::vector<Device> devs;
     std::mutex mu;
     uint32_t key_cap = kDefaultKeyCap;
+    // cv_ed25519_verify_batch_async: ticket -> (device index, output slot, that slot's gen) per shard
+    uint64_t next_ticket = 0;
+    std::unordered_map<uint64_t, std::vector<std::array<uint64_t, 3>>> tickets;
 };
 
 extern "C" {
@@ -576,6 +597,11 @@ void cv_close(cv_ctx *ctx) {
                 if (v) (void)hipEventDestroy(v);
             if (sl.split.s2) (void)hipStreamDestroy(sl.split.s2);
             if (k > 0 && sl.stream) (void)hipStreamDestroy(sl.stream);
+        }
+        for (PipeOut &o : d.out) {
+            o.dout.release();
+            o.hout.release();
+            if (o.done) (void)hipEventDestroy(o.done);
         }
         for (int q = 0; q < kRing; q++) {
             d.inblk[q].release();
@@ -866,9 +892,25 @@ static std::vector<size_t> pipe_cuts(size_t b, size_t e, size_t first, size_t C,
 // stream as blit kernels (`__amd_rocclr_copyBuffer`, ~37 GB/s, on the CUs beside the verify kernels)
 // and the C2 host call took 13.8-16 ms for 9.6 ms of kernels (profiles/r03c_timeline_*.txt).  The
 // verdicts come back in ONE copy after the last verify.
-static int verify_shard_pipe(Device &d, size_t b, size_t e, const uint8_t *pk, const uint8_t *sig,
-                             const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
-                             uint8_t *status, int threads) {
+// Copies a finished pipelined call's verdicts into the caller's arrays (waits for them first).
+static int pipe_finish(PipeOut &po) {
+    if (!po.pending) return CV_OK;
+    po.pending = false;
+    CV_TRY(hipEventSynchronize(po.done));
+    const size_t words = (po.n + 63) / 64;
+    std::memcpy(po.bitmap + po.b / 64, po.hout.p, words * 8);
+    if (po.status) std::memcpy(po.status + po.b, po.hout.as<uint8_t>() + po.o_st, po.n);
+    return CV_OK;
+}
+
+// Enqueues the pipelined verify of shard [b, e) on device d with its verdicts going to output slot
+// po (which must not be pending); returns without waiting for the GPU.  The join: the device stream
+// (slot 0's) waits for the other slot streams' last launch groups, copies the verdicts to po's pinned
+// buffer and records po.done.  The ring's in_free / in_ready events stay valid across calls, so the
+// next call's copies and kernels queue right behind this one's (cv_ed25519_verify_batch_async).
+static int pipe_enqueue(Device &d, PipeOut &po, size_t b, size_t e, const uint8_t *pk, const uint8_t *sig,
+                        const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
+                        uint8_t *status, int threads) {
     const size_t n = e - b;
     const size_t words = (n + 63) / 64;
     const size_t o_st = al16(words * 8), total_out = o_st + al16(n);
@@ -884,22 +926,28 @@ static int verify_shard_pipe(Device &d, size_t b, size_t e, const uint8_t *pk, c
         if (!d.in_ready[q]) CV_TRY(hipEventCreateWithFlags(&d.in_ready[q], hipEventDisableTiming));
         if (!d.in_free[q]) CV_TRY(hipEventCreateWithFlags(&d.in_free[q], hipEventDisableTiming));
     }
-    CV_TRY(d.pin_out.ensure(total_out));
-    CV_TRY(d.bitmap.ensure(total_out));
-    uint8_t *dout = d.bitmap.as<uint8_t>();
-    uint8_t *hout = d.pin_out.as<uint8_t>();
+    if (!po.done) CV_TRY(hipEventCreateWithFlags(&po.done, hipEventDisableTiming));
+    CV_TRY(po.hout.ensure(total_out));
+    CV_TRY(po.dout.ensure(total_out));
+    uint8_t *dout = po.dout.as<uint8_t>();
+    // error paths: drain every queue, forget the ring's state and every pending output of this device
     auto drain = on_exit([&] {
         (void)hipStreamSynchronize(d.copy);
         for (int k = 0; k < nsl; k++) (void)hipStreamSynchronize(ss[k]);
         for (int q = 0; q < kRing; q++) d.in_used[q] = d.stage_busy[q] = false;
+        for (PipeOut &o : d.out)                  // an earlier call still in flight keeps its verdicts
+            if (&o != &po) (void)pipe_finish(o);
     });
     WorkerPool *pool = &d.workers(threads);
     PipeStats ps;
+    bool used[kSlots] = {};
     for (size_t j = 0; j + 1 < cut.size(); j++) {
         const size_t c0 = cut[j], c1 = cut[j + 1], m = c1 - c0;
-        const int q = (int)(j % kRing);
+        const int q = d.ring_next;
+        d.ring_next = (d.ring_next + 1) % kRing;
         Slot &sl = d.slot[j % nsl];
         hipStream_t s = ss[j % nsl];
+        used[j % nsl] = true;
         double t0 = now_s();
         const Stage st = stage_plan(c0, c1, off, len, pool);
         const bool direct = stage_direct(st, c0, pk, sig, arena, off, len);
@@ -946,14 +994,19 @@ static int verify_shard_pipe(Device &d, size_t b, size_t e, const uint8_t *pk, c
         ps.enq += now_s() - t0;
         ps.chunks++;
     }
-    const double t0 = now_s();
-    for (int k = 0; k < nsl; k++) CV_TRY(hipStreamSynchronize(ss[k]));
-    CV_TRY(hipMemcpyAsync(hout, dout, status ? o_st + n : words * 8, hipMemcpyDeviceToHost, ss[0]));
-    CV_TRY(hipStreamSynchronize(ss[0]));
-    CV_TRY(hipStreamSynchronize(d.copy));
-    ps.sync += now_s() - t0;
+    // join on the device stream (slot 0's), then the one verdict copy
+    for (int k = 1; k < nsl; k++)
+        if (used[k]) CV_TRY(hipStreamWaitEvent(ss[0], d.slot[k].ev, 0));
+    CV_TRY(hipMemcpyAsync(po.hout.p, dout, status ? o_st + n : words * 8, hipMemcpyDeviceToHost, ss[0]));
+    CV_TRY(hipEventRecord(po.done, ss[0]));
     drain.armed = false;
-    for (int q = 0; q < kRing; q++) d.in_used[q] = d.stage_busy[q] = false;
+    po.pending = true;
+    po.gen++;
+    po.bitmap = bitmap;
+    po.status = status;
+    po.b = b;
+    po.n = n;
+    po.o_st = o_st;
     {
         std::lock_guard<std::mutex> g(g_pipe_stats_mu);
         PipeStats &G = g_pipe_stats;
@@ -961,14 +1014,38 @@ static int verify_shard_pipe(Device &d, size_t b, size_t e, const uint8_t *pk, c
         G.pack += ps.pack;
         G.wait += ps.wait;
         G.enq += ps.enq;
-        G.sync += ps.sync;
         G.calls++;
         G.chunks += ps.chunks;
         G.direct += ps.direct;
     }
-    std::memcpy(bitmap + b / 64, hout, words * 8);
-    if (status) std::memcpy(status + b, hout + o_st, n);
     return CV_OK;
+}
+
+// The device's next free output slot: the older in-flight call is finished first if it still holds it.
+static PipeOut &pipe_out(Device &d, int *index = nullptr) {
+    PipeOut &po = d.out[d.out_next];
+    if (index) *index = d.out_next;
+    d.out_next = (d.out_next + 1) % kOuts;
+    return po;
+}
+
+// One shard [b, e) of a large batch, pipelined (see pipe_enqueue), synchronously: the verdicts are in
+// the caller's arrays on return.
+static int verify_shard_pipe(Device &d, size_t b, size_t e, const uint8_t *pk, const uint8_t *sig,
+                             const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
+                             uint8_t *status, int threads) {
+    PipeOut &po = pipe_out(d);
+    int rc = pipe_finish(po);
+    if (rc != CV_OK) return rc;
+    rc = pipe_enqueue(d, po, b, e, pk, sig, arena, off, len, bitmap, status, threads);
+    if (rc != CV_OK) return rc;
+    const double t0 = now_s();
+    rc = pipe_finish(po);
+    {
+        std::lock_guard<std::mutex> g(g_pipe_stats_mu);
+        g_pipe_stats.sync += now_s() - t0;
+    }
+    return rc;
 }
 
 static int verify_shard(Device &d, size_t b, size_t e, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
@@ -1252,6 +1329,56 @@ int cv_ed25519_verify_batch(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint
     return for_each_shard(ctx, n, [&](Device &d, size_t b, size_t e, int threads) {
         return verify_shard(d, b, e, pk, sig, msg_arena, msg_off, msg_len, verdict_bitmap, status, threads);
     });
+}
+
+int cv_ed25519_verify_batch_async(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint8_t *sig,
+                                  const uint8_t *msg_arena, const uint64_t *msg_off, const uint32_t *msg_len,
+                                  uint64_t *verdict_bitmap, uint8_t *status, uint64_t *ticket) {
+    if (!ctx || !ticket) return CV_E_ARGS;
+    *ticket = 0;
+    if (n == 0) return CV_OK;
+    if (!pk || !sig || !msg_off || !msg_len || !verdict_bitmap) return CV_E_ARGS;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    std::vector<std::array<uint64_t, 3>> parts(ctx->devs.size(), {UINT64_MAX, 0, 0});
+    const int rc = for_each_shard(ctx, n, [&](Device &d, size_t b, size_t e, int threads) {
+        if (e - b > 0xffffffffull) return CV_E_TOO_LARGE;
+        CV_TRY(hipSetDevice(d.ordinal));
+        int k = 0;
+        PipeOut &po = pipe_out(d, &k);
+        int r = pipe_finish(po);                  // the slot's previous call (its verdicts land first)
+        if (r == CV_OK) r = pipe_enqueue(d, po, b, e, pk, sig, msg_arena, msg_off, msg_len, verdict_bitmap, status, threads);
+        if (r == CV_OK) parts[(size_t)(&d - ctx->devs.data())] = {(uint64_t)(&d - ctx->devs.data()), (uint64_t)k, po.gen};
+        return r;
+    });
+    if (rc != CV_OK) return rc;
+    std::vector<std::array<uint64_t, 3>> live;
+    for (const auto &p : parts)
+        if (p[0] != UINT64_MAX) live.push_back(p);
+    *ticket = ++ctx->next_ticket;
+    ctx->tickets.emplace(*ticket, std::move(live));
+    return CV_OK;
+}
+
+int cv_wait(cv_ctx *ctx, uint64_t ticket) {
+    if (!ctx) return CV_E_ARGS;
+    if (ticket == 0) return CV_OK;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    auto it = ctx->tickets.find(ticket);
+    if (it == ctx->tickets.end()) return CV_E_ARGS;
+    int rc = CV_OK;
+    for (const auto &p : it->second) {
+        Device &d = ctx->devs[p[0]];
+        PipeOut &po = d.out[p[1]];
+        if (po.gen != p[2] || !po.pending) continue;   // already copied (its slot was reused)
+        if (hipSetDevice(d.ordinal) != hipSuccess) {
+            rc = CV_E_HIP;
+            continue;
+        }
+        const int r = pipe_finish(po);
+        if (r != CV_OK) rc = r;
+    }
+    ctx->tickets.erase(it);
+    return rc;
 }
 
 int cv_ed25519_verify_batch_keyed(cv_ctx *ctx, size_t n, size_t nkeys, const uint8_t *keys, const uint32_t *key_index,

@@ -30,7 +30,7 @@ EXPORTED = (
     "cv_tx_verdicts", "cv_ed25519_verify_device", "cv_ed25519_verify_device_timed", "cv_ed25519_sign_device", "cv_merkle_tx_ids_device",
     "cv_synchronize", "cv_calibrate", "cv_ed25519_verify_batch_keyed", "cv_key_cache_reserve", "cv_key_cache_stats",
     "cv_ed25519_verify_device_keyed", "cv_partial_merkle_verify", "cv_calibrate_cycles", "cv_diag_prep_phases",
-    "cv_diag_dedupe_keys", "cv_host_alloc", "cv_host_free",
+    "cv_diag_dedupe_keys", "cv_host_alloc", "cv_host_free", "cv_ed25519_verify_batch_async", "cv_wait",
 )
 
 
@@ -91,6 +91,11 @@ def load():
         lib.cv_merkle_tx_ids_ex.restype = ctypes.c_int
         lib.cv_ed25519_sign_batch.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]
         lib.cv_ed25519_sign_batch.restype = ctypes.c_int
+        lib.cv_ed25519_verify_batch_async.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                                      ctypes.POINTER(ctypes.c_uint64)]
+        lib.cv_ed25519_verify_batch_async.restype = ctypes.c_int
+        lib.cv_wait.argtypes = [_vp, ctypes.c_uint64]
+        lib.cv_wait.restype = ctypes.c_int
         lib.cv_host_alloc.argtypes = [_vp, _sz, ctypes.POINTER(_vp)]
         lib.cv_host_alloc.restype = ctypes.c_int
         lib.cv_host_free.argtypes = [_vp, _vp]
@@ -179,6 +184,7 @@ class Engine:
         self._lib = lib
         self._h = h
         self.mu = threading.Lock()
+        self._inflight = {}
 
     def close(self):
         if self._h:
@@ -239,6 +245,37 @@ class Engine:
         with self.mu:
             _check(self._lib.cv_ed25519_verify_batch(self._h, n, _p(pk), _p(sig), _p(arena), _p(off), _p(ln),
                                                      _p(bitmap), _p(status)), "cv_ed25519_verify_batch")
+        return bitmap, status
+
+    def verify_batch_async(self, pk, sig, arena, off, ln, want_status: bool = True) -> int:
+        """cv_ed25519_verify_batch_async: enqueue and return a ticket; wait(ticket) -> (bitmap, status).
+        The arrays are kept referenced here until the wait (the engine may DMA from them until then)."""
+        pk = _u8(pk)
+        sig = _u8(sig)
+        n = pk.shape[0]
+        if pk.size != n * 32 or sig.size != n * 64:
+            raise ValueError("pk must be (n,32) and sig (n,64)")
+        arena = _u8(arena) if arena is not None and np.asarray(arena).size else np.zeros(16, np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        ln = np.ascontiguousarray(ln, dtype=np.uint32)
+        if off.shape[0] != n or ln.shape[0] != n:
+            raise ValueError("off/len must have n entries")
+        if n and _msg_end(self._lib, off, ln) > arena.size:
+            raise ValueError("message range exceeds the arena")
+        bitmap = np.zeros((n + 63) // 64, np.uint64)
+        status = np.zeros(n, np.uint8) if want_status else None
+        t = ctypes.c_uint64()
+        with self.mu:
+            _check(self._lib.cv_ed25519_verify_batch_async(self._h, n, _p(pk), _p(sig), _p(arena), _p(off), _p(ln),
+                                                           _p(bitmap), _p(status), ctypes.byref(t)),
+                   "cv_ed25519_verify_batch_async")
+            self._inflight[t.value] = (bitmap, status, (pk, sig, arena, off, ln))
+        return t.value
+
+    def wait(self, ticket: int) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+        with self.mu:
+            bitmap, status, _ = self._inflight.pop(ticket, (None, None, None))
+            _check(self._lib.cv_wait(self._h, ctypes.c_uint64(ticket)), "cv_wait")
         return bitmap, status
 
     def verify_batch_keyed(self, keys, key_index, sig, arena, off, ln, want_status: bool = True):

@@ -83,6 +83,19 @@ int cv_ed25519_verify_batch(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint
                             const uint8_t *msg_arena, const uint64_t *msg_off, const uint32_t *msg_len,
                             uint64_t *verdict_bitmap, uint8_t *status);
 
+/* Asynchronous form of cv_ed25519_verify_batch (same records, same verdicts and status): enqueues the
+ * batch on the context's devices and returns a ticket; cv_wait(ticket) returns once verdict_bitmap and
+ * status hold the results.  Until then the caller keeps every array of the call alive and unmodified
+ * (pinned inputs are read by DMA after this call returns).  Two calls per device may be in flight: a
+ * third first completes the oldest (whose cv_wait then returns at once).  A node's batching loop
+ * submits batch k+1 before waiting for batch k, so its copies and kernels fill the first one's
+ * pipeline ramp and tail.  No host dedupe / keyed path here.  Tickets are waited at most once;
+ * cv_close drops results not yet waited for. */
+int cv_ed25519_verify_batch_async(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint8_t *sig,
+                                  const uint8_t *msg_arena, const uint64_t *msg_off, const uint32_t *msg_len,
+                                  uint64_t *verdict_bitmap, uint8_t *status, uint64_t *ticket);
+int cv_wait(cv_ctx *ctx, uint64_t ticket);
+
 /* Pinned host memory for the host-buffer API's inputs (hipHostMalloc).  When all five input arrays of
  * cv_ed25519_verify_batch lie in pinned memory (from here, or any page-locked / registered host memory),
  * the engine DMAs each sub-chunk's records straight out of them and skips its packing copy into its own

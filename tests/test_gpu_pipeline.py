@@ -254,3 +254,45 @@ def test_host_small_pinned_inputs_golden(engine, corpus, n):
     assert np.array_equal(_bits(bitmap, n), corpus["verdict"][sel].astype(bool))
     assert np.array_equal(status, corpus["status"][sel])
     assert int(bitmap[-1]) >> (n % 64) == 0 if n % 64 else True
+
+
+def test_async_calls_in_flight_match_sync(engine, corpus, oracle_c):
+    """cv_ed25519_verify_batch_async: three batches in flight (pageable 300,007 with corrupted S bytes,
+    pinned 262,145 with corrupted R bytes and golden not-a-point keys, a 4,096 golden tile) — more than
+    the two output slots per device, so the third submission completes the first — waited out of
+    order: each equals its synchronous cv_ed25519_verify_batch (verdicts and status), and the pinned
+    and golden ones their expected patterns."""
+    n1, n2, n3 = 300_007, 262_145, 4096
+    b1 = workload.make_batch(engine, 0, n1, 300, seed=71)
+    e1 = workload.corrupt_fraction(b1, 13).cpu().numpy()
+    a1 = b1.to_host()
+    b2 = workload.make_batch(engine, 0, n2, 32, seed=72)
+    idx = torch.arange(1, n2, 37, device=DEV)
+    b2.sig[idx, 2] ^= 0x08
+    e2 = torch.ones(n2, dtype=torch.bool, device=DEV)
+    e2[idx] = False
+    e2 = e2.cpu().numpy()
+    pk2, sig2, ar2, off2, ln2 = b2.to_host()
+    pk2 = pk2.copy()
+    bad = _bad_key_records(corpus)
+    kidx = np.arange(5, n2, 1013)
+    pk2[kidx] = corpus["pk"][bad[kidx % len(bad)]]
+    e2[kidx] = False
+    a2 = tuple(engine.host_copy(x) for x in (pk2, sig2, ar2, off2, ln2))
+    del b1, b2
+    rng = np.random.default_rng(9)
+    sel = rng.integers(0, len(corpus["pk"]), n3)
+    a3 = (corpus["pk"][sel], corpus["sig"][sel], corpus["arena"], corpus["off"][sel], corpus["len"][sel])
+    t1 = engine.verify_batch_async(*a1)
+    t2 = engine.verify_batch_async(*a2)
+    t3 = engine.verify_batch_async(*a3)
+    r3 = engine.wait(t3)
+    r1 = engine.wait(t1)
+    r2 = engine.wait(t2)
+    s1, s2, s3 = engine.verify_batch(*a1), engine.verify_batch(*a2), engine.verify_batch(*a3)
+    for r, s_ in ((r1, s1), (r2, s2), (r3, s3)):
+        assert np.array_equal(r[0], s_[0]) and np.array_equal(r[1], s_[1])
+    assert np.array_equal(_bits(r1[0], n1), e1)
+    assert np.array_equal(_bits(r2[0], n2), e2) and int(r2[1].sum()) == kidx.size
+    assert np.array_equal(_bits(r3[0], n3), corpus["verdict"][sel].astype(bool))
+    assert np.array_equal(r3[1], corpus["status"][sel])
