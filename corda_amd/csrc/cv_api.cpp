@@ -151,7 +151,9 @@ constexpr int kOuts = 2;   // host pipeline calls in flight per device (cv_ed255
 struct PipeOut {
     DevBuf dout;
     PinBuf hout;
-    hipEvent_t done = nullptr;
+    hipEvent_t done = nullptr;           // (unused since the host-side join; kept for cv_close)
+    hipEvent_t slot_done[kSlots] = {};   // after this call's last launch group on each slot stream
+    bool slot_used[kSlots] = {};
     bool pending = false;
     uint64_t gen = 0;
     uint64_t *bitmap = nullptr;
@@ -248,6 +250,7 @@ struct Device {
     // arrays are pageable.  in_ready[q]: after block q's copies (copy stream); in_free[q]: after the
     // verify that read it (its slot stream).
     hipStream_t copy = nullptr;
+    hipStream_t outs = nullptr;          // the pipeline's verdict copies (pipe_finish)
     PipeOut out[kOuts];                  // the pipeline's verdict outputs, one per call in flight
     int out_next = 0;
     DevBuf inblk[kRing];
@@ -295,6 +298,7 @@ static size_t g_small_pool_min = 16384;
 // behind that slot's Straus kernel (2.4 ms stalls, profiles/r03e_timeline_pinned_nofill.txt)
 static int g_pipe_slots = 2;
 static int g_pipe_ramp = 1;    // sub-chunk sizes double from g_pipe_first up to g_pipe_chunk
+static size_t g_async_chunk = 524288;   // sub-chunks of cv_ed25519_verify_batch_async (no ramp)
 // host-side time of the pipelined path, seconds (cvk_pipe_stats): range scans, packing, waits for a
 // slot's staging, enqueue (HIP calls), the final synchronisation; and calls / sub-chunks
 struct PipeStats {
@@ -489,6 +493,7 @@ void cvk_set_direct_small_min(int n) { g_direct_small_min = n > 0 ? (size_t)n : 
 void cvk_set_small_pool_min(int n) { g_small_pool_min = n > 0 ? (size_t)n : 16384; }
 void cvk_set_pipe_slots(int k) { g_pipe_slots = (k >= 2 && k <= kSlots) ? k : 2; }
 void cvk_set_pipe_ramp(int v) { g_pipe_ramp = v ? 1 : 0; }
+void cvk_set_async_chunk(int m) { g_async_chunk = m >= 64 ? (size_t)m / 64 * 64 : 524288; }
 void cvk_set_pipe(size_t min_n, size_t first, size_t chunk, int threads) {
     if (min_n) g_pipe_min = min_n;
     if (first) g_pipe_first = std::max<size_t>(64, first / 64 * 64);
@@ -602,7 +607,10 @@ void cv_close(cv_ctx *ctx) {
             o.dout.release();
             o.hout.release();
             if (o.done) (void)hipEventDestroy(o.done);
+            for (hipEvent_t v : o.slot_done)
+                if (v) (void)hipEventDestroy(v);
         }
+        if (d.outs) (void)hipStreamDestroy(d.outs);
         for (int q = 0; q < kRing; q++) {
             d.inblk[q].release();
             d.instage[q].release();
@@ -893,11 +901,18 @@ static std::vector<size_t> pipe_cuts(size_t b, size_t e, size_t first, size_t C,
 // and the C2 host call took 13.8-16 ms for 9.6 ms of kernels (profiles/r03c_timeline_*.txt).  The
 // verdicts come back in ONE copy after the last verify.
 // Copies a finished pipelined call's verdicts into the caller's arrays (waits for them first).
-static int pipe_finish(PipeOut &po) {
+static int pipe_finish(Device &d, PipeOut &po) {
     if (!po.pending) return CV_OK;
     po.pending = false;
-    CV_TRY(hipEventSynchronize(po.done));
+    // host-side join: the call's last launch group on every slot stream, then ONE verdict copy on the
+    // device's output stream (which carries nothing else, so it neither waits behind the next call's
+    // input copies nor holds a compute stream the next call's kernels run on)
+    for (int k = 0; k < kSlots; k++)
+        if (po.slot_used[k]) CV_TRY(hipEventSynchronize(po.slot_done[k]));
+    if (!d.outs) CV_TRY(hipStreamCreateWithFlags(&d.outs, hipStreamNonBlocking));
     const size_t words = (po.n + 63) / 64;
+    CV_TRY(hipMemcpyAsync(po.hout.p, po.dout.p, po.status ? po.o_st + po.n : words * 8, hipMemcpyDeviceToHost, d.outs));
+    CV_TRY(hipStreamSynchronize(d.outs));
     std::memcpy(po.bitmap + po.b / 64, po.hout.p, words * 8);
     if (po.status) std::memcpy(po.status + po.b, po.hout.as<uint8_t>() + po.o_st, po.n);
     return CV_OK;
@@ -908,13 +923,16 @@ static int pipe_finish(PipeOut &po) {
 // (slot 0's) waits for the other slot streams' last launch groups, copies the verdicts to po's pinned
 // buffer and records po.done.  The ring's in_free / in_ready events stay valid across calls, so the
 // next call's copies and kernels queue right behind this one's (cv_ed25519_verify_batch_async).
+// async: the sub-chunk plan of cv_ed25519_verify_batch_async (g_async_chunk, no ramp — with a call in
+// flight ahead of it the GPU is busy anyway, and bigger launches run closer to the kernels' rate)
 static int pipe_enqueue(Device &d, PipeOut &po, size_t b, size_t e, const uint8_t *pk, const uint8_t *sig,
                         const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
-                        uint8_t *status, int threads) {
+                        uint8_t *status, int threads, bool async = false) {
     const size_t n = e - b;
     const size_t words = (n + 63) / 64;
     const size_t o_st = al16(words * 8), total_out = o_st + al16(n);
-    const std::vector<size_t> cut = pipe_cuts(b, e, g_pipe_first, g_pipe_chunk, g_pipe_ramp != 0);
+    const std::vector<size_t> cut = async ? pipe_cuts(b, e, g_async_chunk, g_async_chunk, false)
+                                          : pipe_cuts(b, e, g_pipe_first, g_pipe_chunk, g_pipe_ramp != 0);
     const int nsl = g_pipe_slots;
     hipStream_t ss[kSlots] = {};
     for (int k = 0; k < nsl; k++) {
@@ -926,7 +944,8 @@ static int pipe_enqueue(Device &d, PipeOut &po, size_t b, size_t e, const uint8_
         if (!d.in_ready[q]) CV_TRY(hipEventCreateWithFlags(&d.in_ready[q], hipEventDisableTiming));
         if (!d.in_free[q]) CV_TRY(hipEventCreateWithFlags(&d.in_free[q], hipEventDisableTiming));
     }
-    if (!po.done) CV_TRY(hipEventCreateWithFlags(&po.done, hipEventDisableTiming));
+    for (int k = 0; k < nsl; k++)
+        if (!po.slot_done[k]) CV_TRY(hipEventCreateWithFlags(&po.slot_done[k], hipEventDisableTiming));
     CV_TRY(po.hout.ensure(total_out));
     CV_TRY(po.dout.ensure(total_out));
     uint8_t *dout = po.dout.as<uint8_t>();
@@ -936,7 +955,7 @@ static int pipe_enqueue(Device &d, PipeOut &po, size_t b, size_t e, const uint8_
         for (int k = 0; k < nsl; k++) (void)hipStreamSynchronize(ss[k]);
         for (int q = 0; q < kRing; q++) d.in_used[q] = d.stage_busy[q] = false;
         for (PipeOut &o : d.out)                  // an earlier call still in flight keeps its verdicts
-            if (&o != &po) (void)pipe_finish(o);
+            if (&o != &po) (void)pipe_finish(d, o);
     });
     WorkerPool *pool = &d.workers(threads);
     PipeStats ps;
@@ -994,11 +1013,12 @@ static int pipe_enqueue(Device &d, PipeOut &po, size_t b, size_t e, const uint8_
         ps.enq += now_s() - t0;
         ps.chunks++;
     }
-    // join on the device stream (slot 0's), then the one verdict copy
-    for (int k = 1; k < nsl; k++)
-        if (used[k]) CV_TRY(hipStreamWaitEvent(ss[0], d.slot[k].ev, 0));
-    CV_TRY(hipMemcpyAsync(po.hout.p, dout, status ? o_st + n : words * 8, hipMemcpyDeviceToHost, ss[0]));
-    CV_TRY(hipEventRecord(po.done, ss[0]));
+    // completion marks per slot stream (pipe_finish joins on the host); no GPU-side join, which would
+    // hold the next call's kernels on that stream until this call had finished
+    for (int k = 0; k < kSlots; k++) {
+        po.slot_used[k] = k < nsl && used[k];
+        if (po.slot_used[k]) CV_TRY(hipEventRecord(po.slot_done[k], ss[k]));
+    }
     drain.armed = false;
     po.pending = true;
     po.gen++;
@@ -1035,12 +1055,12 @@ static int verify_shard_pipe(Device &d, size_t b, size_t e, const uint8_t *pk, c
                              const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
                              uint8_t *status, int threads) {
     PipeOut &po = pipe_out(d);
-    int rc = pipe_finish(po);
+    int rc = pipe_finish(d, po);
     if (rc != CV_OK) return rc;
     rc = pipe_enqueue(d, po, b, e, pk, sig, arena, off, len, bitmap, status, threads);
     if (rc != CV_OK) return rc;
     const double t0 = now_s();
-    rc = pipe_finish(po);
+    rc = pipe_finish(d, po);
     {
         std::lock_guard<std::mutex> g(g_pipe_stats_mu);
         g_pipe_stats.sync += now_s() - t0;
@@ -1345,8 +1365,9 @@ int cv_ed25519_verify_batch_async(cv_ctx *ctx, size_t n, const uint8_t *pk, cons
         CV_TRY(hipSetDevice(d.ordinal));
         int k = 0;
         PipeOut &po = pipe_out(d, &k);
-        int r = pipe_finish(po);                  // the slot's previous call (its verdicts land first)
-        if (r == CV_OK) r = pipe_enqueue(d, po, b, e, pk, sig, msg_arena, msg_off, msg_len, verdict_bitmap, status, threads);
+        int r = pipe_finish(d, po);               // the slot's previous call (its verdicts land first)
+        if (r == CV_OK)
+            r = pipe_enqueue(d, po, b, e, pk, sig, msg_arena, msg_off, msg_len, verdict_bitmap, status, threads, true);
         if (r == CV_OK) parts[(size_t)(&d - ctx->devs.data())] = {(uint64_t)(&d - ctx->devs.data()), (uint64_t)k, po.gen};
         return r;
     });
@@ -1374,7 +1395,7 @@ int cv_wait(cv_ctx *ctx, uint64_t ticket) {
             rc = CV_E_HIP;
             continue;
         }
-        const int r = pipe_finish(po);
+        const int r = pipe_finish(d, po);
         if (r != CV_OK) rc = r;
     }
     ctx->tickets.erase(it);

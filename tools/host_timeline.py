@@ -20,6 +20,7 @@ import numpy as np
 
 
 def summarize(d, gap_ms=3.0):
+    gap_ms = float(os.environ.get("TL_GAP_MS", gap_ms))
     ev = []
     for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
@@ -53,6 +54,7 @@ def main():
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--slots", type=int, default=0)
     ap.add_argument("--ramp", type=int, default=-1)
+    ap.add_argument("--n", type=int, default=0, help="signatures (overrides the shape's)")
     a = ap.parse_args()
     if a.summarize:
         summarize(a.summarize)
@@ -69,6 +71,8 @@ def main():
         lib.cvk_set_pipe_ramp(a.ramp)
     eng = native.Engine(1)
     n, ml = (1_000_000, 300) if a.shape == "c2" else (8_000_000, 32)
+    if a.n:
+        n = a.n
     b = workload.make_batch(eng, 0, n, ml, seed=11)
     arrs = b.to_host()
     del b
