@@ -298,7 +298,7 @@ static size_t g_small_pool_min = 16384;
 // behind that slot's Straus kernel (2.4 ms stalls, profiles/r03e_timeline_pinned_nofill.txt)
 static int g_pipe_slots = 2;
 static int g_pipe_ramp = 1;    // sub-chunk sizes double from g_pipe_first up to g_pipe_chunk
-static size_t g_async_chunk = 524288;   // sub-chunks of cv_ed25519_verify_batch_async (no ramp)
+static size_t g_async_chunk = 262144;   // sub-chunks of cv_ed25519_verify_batch_async (no ramp)
 // host-side time of the pipelined path, seconds (cvk_pipe_stats): range scans, packing, waits for a
 // slot's staging, enqueue (HIP calls), the final synchronisation; and calls / sub-chunks
 struct PipeStats {
@@ -493,7 +493,7 @@ void cvk_set_direct_small_min(int n) { g_direct_small_min = n > 0 ? (size_t)n : 
 void cvk_set_small_pool_min(int n) { g_small_pool_min = n > 0 ? (size_t)n : 16384; }
 void cvk_set_pipe_slots(int k) { g_pipe_slots = (k >= 2 && k <= kSlots) ? k : 2; }
 void cvk_set_pipe_ramp(int v) { g_pipe_ramp = v ? 1 : 0; }
-void cvk_set_async_chunk(int m) { g_async_chunk = m >= 64 ? (size_t)m / 64 * 64 : 524288; }
+void cvk_set_async_chunk(int m) { g_async_chunk = m >= 64 ? (size_t)m / 64 * 64 : 262144; }
 void cvk_set_pipe(size_t min_n, size_t first, size_t chunk, int threads) {
     if (min_n) g_pipe_min = min_n;
     if (first) g_pipe_first = std::max<size_t>(64, first / 64 * 64);
