@@ -931,7 +931,10 @@ static int pipe_enqueue(Device &d, PipeOut &po, size_t b, size_t e, const uint8_
     const size_t n = e - b;
     const size_t words = (n + 63) / 64;
     const size_t o_st = al16(words * 8), total_out = o_st + al16(n);
-    const std::vector<size_t> cut = async ? pipe_cuts(b, e, g_async_chunk, g_async_chunk, false)
+    // async sub-chunks: g_async_chunk, up to twice that for big shards (n / 16; same-box sweep:
+    // C2 1M best at 262,144, C5 8M at 524,288, profiles/r03l_async_chunk_sweep.log)
+    const size_t ach = std::max(g_async_chunk, std::min(2 * g_async_chunk, n / 16 / 64 * 64));
+    const std::vector<size_t> cut = async ? pipe_cuts(b, e, ach, ach, false)
                                           : pipe_cuts(b, e, g_pipe_first, g_pipe_chunk, g_pipe_ramp != 0);
     const int nsl = g_pipe_slots;
     hipStream_t ss[kSlots] = {};
@@ -1371,7 +1374,21 @@ int cv_ed25519_verify_batch_async(cv_ctx *ctx, size_t n, const uint8_t *pk, cons
         if (r == CV_OK) parts[(size_t)(&d - ctx->devs.data())] = {(uint64_t)(&d - ctx->devs.data()), (uint64_t)k, po.gen};
         return r;
     });
-    if (rc != CV_OK) return rc;
+    if (rc != CV_OK) {
+        // a shard failed: the shards that did enqueue are waited for and dropped here — nothing may
+        // read the caller's arrays or write its bitmap after an error return
+        for (const auto &p : parts) {
+            if (p[0] == UINT64_MAX) continue;
+            Device &d = ctx->devs[p[0]];
+            PipeOut &po = d.out[p[1]];
+            (void)hipSetDevice(d.ordinal);
+            for (int k = 0; k < kSlots; k++)
+                if (po.slot_used[k]) (void)hipEventSynchronize(po.slot_done[k]);
+            if (d.copy) (void)hipStreamSynchronize(d.copy);
+            po.pending = false;
+        }
+        return rc;
+    }
     std::vector<std::array<uint64_t, 3>> live;
     for (const auto &p : parts)
         if (p[0] != UINT64_MAX) live.push_back(p);
