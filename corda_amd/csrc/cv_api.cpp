@@ -52,25 +52,29 @@ struct DevBuf {
 // input copies cost ~0.1 ms of a 0.4-0.7 ms notary batch, tools/notary_probe.py).
 struct PinBuf {
     void *p = nullptr;
+    void *dev = nullptr;   // the device's address of p (hipHostGetDevicePointer)
     size_t cap = 0;
+    unsigned flags = hipHostMallocDefault;
     hipError_t ensure(size_t bytes) {
         if (bytes <= cap) return hipSuccess;
         if (p) (void)hipHostFree(p);
-        p = nullptr;
+        p = dev = nullptr;
         cap = 0;
         const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 16);
-        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        hipError_t e = hipHostMalloc(&p, want, flags);
+        if (e == hipSuccess && (e = hipHostGetDevicePointer(&dev, p, 0)) != hipSuccess) (void)hipHostFree(p);
         if (e != hipSuccess) {
-            p = nullptr;
+            p = dev = nullptr;
             return e;
         }
         cap = want;
         return hipSuccess;
     }
     template <class T> T *as() const { return static_cast<T *>(p); }
+    template <class T> T *dev_as() const { return static_cast<T *>(dev); }
     void release() {
         if (p) (void)hipHostFree(p);
-        p = nullptr;
+        p = dev = nullptr;
         cap = 0;
     }
 };
@@ -239,6 +243,9 @@ struct Device {
     hipStream_t stream = nullptr;
     DevBuf pk, sig, arena, off, len, bitmap, status, seed, tx_begin, digest, ids;
     PinBuf pin_out;                      // host-buffer verify outputs: bitmap | status
+    // zero-copy notary path (verify_shard_small_zc): fine-grained pinned host memory the kernels read
+    // (packed records) and store into (verdict nibbles | status) over PCIe
+    PinBuf zc_in, zc_out;
     DevBuf pmt;                          // partial Merkle trees: inputs, outputs and workspace, packed
     Slot slot[kSlots];
     uint64_t clock = 0;
@@ -308,6 +315,12 @@ struct PipeStats {
 // 1 = pinned caller arrays are DMAed in place (stage_direct); 0 = always pack (A/B knob)
 static int g_direct_dma = 1;
 static size_t g_direct_small_min = 16384;   // the small path's direct-DMA threshold (signatures)
+// 1 = tri-form batches from host buffers take the zero-copy path (verify_shard_small_zc); 0 = DMA in/out
+static int g_small_zc = 1;
+// host-side time of the zero-copy path, seconds (cvk_small_stats): range scan + setup (buffers,
+// workspace), packing, launches, the synchronisation (≈ the kernels), the bitmap assembly; and calls
+static double g_small_t[5];
+static uint64_t g_small_calls;
 static PipeStats g_pipe_stats;
 static std::mutex g_pipe_stats_mu;
 static inline double now_s() {
@@ -490,6 +503,19 @@ void cvk_set_virtual_devices(int k) { g_virtual_devices = (k >= 1 && k <= 16) ? 
 // (signatures; 0 keeps the current value) and packing threads.
 void cvk_set_direct_dma(int v) { g_direct_dma = v ? 1 : 0; }
 void cvk_set_direct_small_min(int n) { g_direct_small_min = n > 0 ? (size_t)n : 16384; }
+void cvk_set_small_zc(int v) { g_small_zc = v ? 1 : 0; }
+// out[6] = plan+setup, pack, launch, sync, assemble (seconds, summed) and calls; reset clears them
+void cvk_small_stats(double *out, int reset) {
+    std::lock_guard<std::mutex> g(g_pipe_stats_mu);
+    if (out) {
+        for (int k = 0; k < 5; k++) out[k] = g_small_t[k];
+        out[5] = (double)g_small_calls;
+    }
+    if (reset) {
+        for (double &t : g_small_t) t = 0;
+        g_small_calls = 0;
+    }
+}
 void cvk_set_small_pool_min(int n) { g_small_pool_min = n > 0 ? (size_t)n : 16384; }
 void cvk_set_pipe_slots(int k) { g_pipe_slots = (k >= 2 && k <= kSlots) ? k : 2; }
 void cvk_set_pipe_ramp(int v) { g_pipe_ramp = v ? 1 : 0; }
@@ -594,6 +620,8 @@ void cv_close(cv_ctx *ctx) {
                           &d.kc.slot_of_key, &d.kc.key_index, &d.kc.scratch})
             b->release();
         d.pin_out.release();
+        d.zc_in.release();
+        d.zc_out.release();
         for (int k = 0; k < kSlots; k++) {
             Slot &sl = d.slot[k];
             for (DevBuf *b : {&sl.ws_hs, &sl.ws_tab, &sl.ws_R, &sl.ws_ok, &sl.ws_dig, &sl.packed}) b->release();
@@ -804,6 +832,63 @@ static hipError_t stage_dma_direct(const Stage &st, uint8_t *dv, size_t b, const
     return e;
 }
 
+// Zero-copy form of the small path for tri-chain batches (n <= cvk_get_tri_max(): the notary batches).
+// The records are packed into fine-grained pinned host memory that the fused prep kernel reads over
+// PCIe, and the kernels store the status bytes and one verdict byte per wave (4 bits) into pinned host
+// memory: no DMA in, no copy out.  Measured on the box, notary 4,096 (profiles/r03j_timeline_notary4096.txt),
+// the DMA path paid 19.8 us of H2D + 11.6 us from the DMA's completion to the prep's start + 9.6 us for
+// the verdict copy (a blit kernel after the Straus kernel).
+static int verify_shard_small_zc(Device &d, const Stage &st, size_t b, const uint8_t *pk, const uint8_t *sig,
+                                 const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
+                                 uint8_t *status, WorkerPool *pool, double t_plan) {
+    double t[6];
+    t[0] = t_plan;
+    const size_t n = st.n, words = (n + 63) / 64, nnib = words * 16, waves = (n + 3) / 4;
+    Slot &sl = d.slot[0];
+    hipStream_t s = nullptr;
+    CV_TRY(slot_stream(d, 0, &s));
+    CV_TRY(slot_events(sl));
+    d.zc_in.flags = d.zc_out.flags = hipHostMallocCoherent | hipHostMallocMapped;
+    CV_TRY(d.zc_in.ensure(st.total));
+    CV_TRY(d.zc_out.ensure(al16(nnib) + al16(n)));
+    CV_TRY(ensure_verify_ws(sl, n));
+    if (!cvk_tri_zc_ok((uint32_t)n, sl.ws_cap)) return CV_E_HIP;   // (cannot happen: checked by the caller)
+    uint8_t *h = d.zc_in.as<uint8_t>();
+    const uint8_t *dv = d.zc_in.dev_as<uint8_t>();
+    t[1] = now_s();
+    stage_pack(st, h, b, pk, sig, arena, off, len, pool, [] {});
+    uint8_t *nib = d.zc_out.as<uint8_t>();
+    std::memset(nib + waves, 0, nnib - waves);   // bytes of waves past the batch: no wave stores them
+    t[2] = now_s();
+    auto drain = on_exit([s] { (void)hipStreamSynchronize(s); });   // error paths: no kernel outlives the call
+    CV_TRY(ws_begin(d, sl, s));
+    const hipError_t e = cvk_verify_tri_zc(
+        (uint32_t)n, dv + st.o_pk, dv + st.o_sig, dv + st.o_ar - st.lo, reinterpret_cast<const uint64_t *>(dv + st.o_off),
+        reinterpret_cast<const uint32_t *>(dv + st.o_len), d.zc_out.dev_as<uint8_t>(),
+        status ? d.zc_out.dev_as<uint8_t>() + al16(nnib) : nullptr, sl.ws_tab.as<uint32_t>(), sl.ws_ok.as<uint8_t>(),
+        sl.ws_dig.as<uint32_t>(), sl.ws_cap, s);
+    const hipError_t e2 = ws_end(sl, s);
+    CV_TRY(e);
+    CV_TRY(e2);
+    t[3] = now_s();
+    CV_TRY(hipStreamSynchronize(s));
+    drain.armed = false;
+    t[4] = now_s();
+    for (size_t w = 0; w < words; w++) {
+        uint64_t x = 0;
+        for (int j = 0; j < 16; j++) x |= (uint64_t)(nib[16 * w + j] & 15u) << (4 * j);
+        bitmap[b / 64 + w] = x;
+    }
+    if (status) std::memcpy(status + b, nib + al16(nnib), n);
+    t[5] = now_s();
+    {
+        std::lock_guard<std::mutex> g(g_pipe_stats_mu);
+        for (int k = 0; k < 5; k++) g_small_t[k] += t[k + 1] - t[k];
+        g_small_calls++;
+    }
+    return CV_OK;
+}
+
 // One shard [b, e) of a batch on one device, small form (the notary-sized batches): packed into slot 0's
 // pinned staging, moved by one DMA (two above 1 MB: the first overlaps packing the second part) into
 // one device block, verified, and the bitmap (+ status) come back by one DMA.  b is a multiple of 64,
@@ -813,7 +898,10 @@ static int verify_shard_small(Device &d, size_t b, size_t e, const uint8_t *pk, 
                               uint8_t *status, int threads) {
     const size_t n = e - b;
     WorkerPool *pool = n >= g_small_pool_min ? &d.workers(threads) : nullptr;
+    const double t_plan = now_s();
     const Stage st = stage_plan(b, e, off, len, pool);
+    if (g_small_zc && cvk_tri_zc_ok((uint32_t)n, (uint32_t)n))
+        return verify_shard_small_zc(d, st, b, pk, sig, arena, off, len, bitmap, status, pool, t_plan);
     const size_t words = (n + 63) / 64;
     const size_t o_bm = 0, o_st = al16(words * 8), total_out = o_st + al16(n);
     Slot &sl = d.slot[0];

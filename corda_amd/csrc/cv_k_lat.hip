@@ -48,7 +48,7 @@ __global__ __launch_bounds__(64, 1) void cv_prep_lat_kernel(uint32_t n, uint32_t
         const uint32_t i = (blockIdx.x - nbp) * 64 + threadIdx.x;
         // the chunk's verdict words start at zero for the Straus kernel's atomicOr (it runs after this
         // launch on the same stream): one lane per word, instead of a separate memset launch
-        if (i < n && (i & 63u) == 0) bitmap[i >> 6] = 0;
+        if (bitmap && i < n && (i & 63u) == 0) bitmap[i >> 6] = 0;
         // tri (B16): radix-16 halves of w; quad: the radix-2^16 pairs of the throughput group
         if (i < n) cv_scalars_lane<B16, !B16>(i, cap, pk, sig, arena, off, len, ws_dig);
     }
@@ -89,14 +89,17 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_quad_kernel(uint32_t n,
 }
 
 // Tri-chain kernel (cv_hsquad.h): grid 16n lanes, 4 signatures per wave; digits from
-// cv_hs_scalars<true>.  Bitmap words zero on entry, as for the quad kernel.
+// cv_hs_scalars<true>.  Bitmap words zero on entry, as for the quad kernel — or, with nib set (the
+// zero-copy host path, cvk_verify_tri_zc), each wave stores its 4 verdict bits as one byte nib[wave]
+// (a plain store into pinned host memory: no atomics over PCIe, no bitmap to clear).
 template <bool SEQ>
 __global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_tri_kernel(uint32_t n, uint32_t cap,
                                                                     const uint32_t *__restrict__ ws_dig,
                                                                     const uint32_t *__restrict__ ws_tab,
                                                                     const uint32_t *__restrict__ ws_tabR,
                                                                     const uint8_t *__restrict__ ws_ok,
-                                                                    uint64_t *__restrict__ bitmap) {
+                                                                    uint64_t *__restrict__ bitmap,
+                                                                    uint8_t *__restrict__ nib) {
     constexpr int ROW = CV_BTAB_ENTRIES * CV_BTAB_STRIDE;
     const uint32_t lane0 = blockIdx.x * CV_BLOCK + (threadIdx.x & ~63u);
     const uint32_t sig0 = lane0 >> 4;                        // first signature of this wave
@@ -122,14 +125,19 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_tri_kernel(uint32_t n, 
     uint64_t b = __ballot(acc) & 0x0001000100010001ull;      // lanes 0, 16, 32, 48
     b = (b | (b >> 15)) & 0x0000000300000003ull;
     b = (b | (b >> 30)) & 0xfull;
-    if ((threadIdx.x & 63u) == 0 && b) atomicOr((unsigned long long *)(bitmap + sig0 / 64), (unsigned long long)b << (sig0 & 63));
+    if ((threadIdx.x & 63u) == 0) {
+        if (nib)
+            nib[sig0 >> 2] = (uint8_t)b;
+        else if (b)
+            atomicOr((unsigned long long *)(bitmap + sig0 / 64), (unsigned long long)b << (sig0 & 63));
+    }
 }
 
 template __global__ void cv_prep_lat_kernel<true, true>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
 template __global__ void cv_prep_lat_kernel<false, true>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
 template __global__ void cv_hs_straus_quad_kernel<false>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);
 template __global__ void cv_hs_straus_quad_kernel<true>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);
-template __global__ void cv_hs_straus_tri_kernel<false>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap);
-template __global__ void cv_hs_straus_tri_kernel<true>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap);
+template __global__ void cv_hs_straus_tri_kernel<false>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, uint8_t *nib);
+template __global__ void cv_hs_straus_tri_kernel<true>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, uint8_t *nib);
 template __global__ void cv_prep_lat_kernel<true, false>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
 template __global__ void cv_prep_lat_kernel<false, false>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);

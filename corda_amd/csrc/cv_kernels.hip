@@ -140,6 +140,12 @@ extern "C" void cvk_set_lat_seq(int v) { g_lat_seq = v & 7; }
 static uint32_t g_quad_max = 32768;
 extern "C" void cvk_set_quad_max(uint32_t m) { g_quad_max = m; }
 
+// Does a batch of n take the tri-chain form with these settings (the zero-copy host path's condition:
+// one chunk, half-size mode, latency forms on)?
+extern "C" int cvk_tri_zc_ok(uint32_t n, uint32_t ws_cap) {
+    return n > 0 && n <= g_tri_max && n <= g_quad_max && n <= ws_cap && g_verify_mode == 1 && g_hs_quad;
+}
+
 // ---------------------------------------------------------------- two-stream sub-chunk overlap
 // A chunk of the half-size group is cut into a head and a tail sub-chunk; the tail runs on a helper
 // stream so its waves fill the partial last rounds (drain) of the head's kernels.  mode 0 = off,
@@ -186,6 +192,34 @@ extern "C" {
 hipError_t cvk_prepare(hipStream_t stream) {
     const uint32_t *bw16 = nullptr;
     return bw16_table(&bw16, stream);
+}
+
+// Zero-copy form of the tri-chain group (notary batches from host buffers, cv_api.cpp
+// verify_shard_small): pk/sig/arena/off/len are device-visible pinned HOST memory that the fused prep
+// reads over PCIe, status and nib are pinned host memory the kernels store into — no DMA in or out,
+// so the call is one packing memcpy, two launches and one synchronisation.  nib gets one byte per
+// wave (4 verdict bits, nib[i / 4] bit i % 4); the caller assembles the bitmap words.  Requires the
+// tri form (n <= cvk_get_tri_max(), half-size mode) and n <= ws_cap: hipErrorInvalidValue otherwise.
+hipError_t cvk_verify_tri_zc(uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
+                             const uint64_t *off, const uint32_t *len, uint8_t *nib, uint8_t *status,
+                             uint32_t *ws_tab, uint8_t *ws_ok, uint32_t *ws_dig, uint32_t ws_cap, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    if (!cvk_tri_zc_ok(n, ws_cap) || !nib) return hipErrorInvalidValue;
+    uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
+    const uint32_t nbp = (2 * n + 63) / 64, nbs = (n + 63) / 64;
+    if (g_lat_seq & 4)
+        hipLaunchKernelGGL((cv_prep_lat_kernel<true, false>), dim3(nbp + nbs), dim3(64), 0, stream, n, ws_cap, nbp, pk,
+                           sig, arena, off, len, ws_dig, ws_tab, ws_tabR, ws_ok, status, nullptr);
+    else
+        hipLaunchKernelGGL((cv_prep_lat_kernel<true, true>), dim3(nbp + nbs), dim3(64), 0, stream, n, ws_cap, nbp, pk,
+                           sig, arena, off, len, ws_dig, ws_tab, ws_tabR, ws_ok, status, nullptr);
+    if (g_lat_seq & 1)
+        hipLaunchKernelGGL(cv_hs_straus_tri_kernel<true>, dim3((16 * n + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
+                           stream, n, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, nullptr, nib);
+    else
+        hipLaunchKernelGGL(cv_hs_straus_tri_kernel<false>, dim3((16 * n + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
+                           stream, n, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, nullptr, nib);
+    return hipGetLastError();
 }
 
 // Verify n signatures with the workspace ws (capacity ws_cap signatures, a multiple of 512); the
@@ -252,10 +286,10 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
             if (tri && (g_lat_seq & 1))
                 hipLaunchKernelGGL(cv_hs_straus_tri_kernel<true>, dim3((16 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
-                                   stream, m, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
+                                   stream, m, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64, nullptr);
             else if (tri)
                 hipLaunchKernelGGL(cv_hs_straus_tri_kernel<false>, dim3((16 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
-                                   stream, m, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64);
+                                   stream, m, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64, nullptr);
             else if (g_lat_seq & 2)
                 hipLaunchKernelGGL(cv_hs_straus_quad_kernel<true>, dim3((4 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK),
                                    0, stream, m, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, bitmap + (size_t)c0 / 64, bw16);

@@ -256,6 +256,35 @@ def test_host_small_pinned_inputs_golden(engine, corpus, n):
     assert int(bitmap[-1]) >> (n % 64) == 0 if n % 64 else True
 
 
+@pytest.mark.parametrize("n", [1, 3, 4, 63, 64, 65, 1000, 4096])
+def test_host_small_zero_copy_golden(engine, corpus, n):
+    """The zero-copy notary path (tri-form batches: the prep kernel reads the packed records from pinned
+    host memory over PCIe, the kernels store one verdict byte per wave and the status bytes into pinned
+    host memory) against the DMA form and the golden verdicts/status: the golden corpus tiled to n
+    records in random order, pageable and pinned inputs, ragged ends (n % 4, n % 64)."""
+    rng = np.random.default_rng(1000 + n)
+    sel = rng.integers(0, len(corpus["pk"]), n)
+    arr = (corpus["pk"][sel], corpus["sig"][sel], corpus["arena"], corpus["off"][sel], corpus["len"][sel])
+    lib = native.load()
+    lib.cvk_set_small_zc.argtypes = [ctypes.c_int]
+    out = {}
+    try:
+        for zc in (0, 1):
+            lib.cvk_set_small_zc(zc)
+            out[zc] = engine.verify_batch(*arr)
+            out[zc, "pinned"] = engine.verify_batch(*[engine.host_copy(x) for x in arr])
+            out[zc, "nostatus"] = engine.verify_batch(*arr, want_status=False)
+    finally:
+        lib.cvk_set_small_zc(1)
+    exp = corpus["verdict"][sel].astype(bool)
+    for k, (bitmap, status) in out.items():
+        assert np.array_equal(_bits(bitmap, n), exp), k
+        assert int(bitmap[-1]) >> (n % 64) == 0 if n % 64 else True
+        if status is not None:
+            assert np.array_equal(status, corpus["status"][sel]), k
+    assert np.array_equal(out[0][0], out[1][0])
+
+
 def test_async_calls_in_flight_match_sync(engine, corpus, oracle_c):
     """cv_ed25519_verify_batch_async: three batches in flight (pageable 300,007 with corrupted S bytes,
     pinned 262,145 with corrupted R bytes and golden not-a-point keys, a 4,096 golden tile) — more than

@@ -52,7 +52,7 @@ def main():
         variants.append((name, [(k, tuple(int(x) for x in a.split("/"))) for k, a in
                                 (kv.split("=") for kv in filter(None, body.split(",")))]))
     used = {k for _, sets in variants for k, _ in sets}
-    reset = {"cvk_set_small_pool_min": (16384,), "cvk_set_lat_seq": (7,), "cvk_set_tri_max": (4096,), "cvk_set_prep_lat_fused": (1,)}
+    reset = {"cvk_set_small_pool_min": (16384,), "cvk_set_small_zc": (1,), "cvk_set_lat_seq": (7,), "cvk_set_tri_max": (4096,), "cvk_set_prep_lat_fused": (1,)}
 
     def apply(sets):
         for k in used:
@@ -70,7 +70,13 @@ def main():
         for rnd in range(args.rounds):
             for vname, sets in variants:
                 apply(sets)
+                st = (ctypes.c_double * 6)()
+                lib.cvk_small_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
+                lib.cvk_small_stats(None, 1)
                 host = p50(lambda: eng.verify_batch(pk, sig, arena, off, ln, want_status=False), args.reps)
+                lib.cvk_small_stats(st, 1)
+                zc_us = {k: round(st[i] / max(st[5], 1) * 1e6, 1) for i, k in
+                         enumerate(("plan_setup", "pack", "launch", "sync", "assemble"))} if st[5] else None
                 bm_h, _ = eng.verify_batch(pk, sig, arena, off, ln, want_status=False)
                 assert np.array_equal(native.bitmap_to_bools(bm_h, n), expect)
                 d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in
@@ -93,7 +99,7 @@ def main():
                 print(json.dumps({"variant": vname, "round": rnd, "n": n, "host_p50_p99_ms": host,
                                   "device_p50_p99_ms": device,
                                   "phase_ms": {"hash": float(ph[0]), "prep": float(ph[1]), "straus": float(ph[2])},
-                                  "input_bytes": int(nbytes)}), flush=True)
+                                  "input_bytes": int(nbytes), "zc_host_us_mean": zc_us}), flush=True)
         apply([])
     eng.close()
 
