@@ -52,14 +52,15 @@ def main():
         variants.append((name, [(k, tuple(int(x) for x in a.split("/"))) for k, a in
                                 (kv.split("=") for kv in filter(None, body.split(",")))]))
     used = {k for _, sets in variants for k, _ in sets}
-    reset = {"cvk_set_small_pool_min": (16384,), "cvk_set_small_zc": (1,), "cvk_set_lat_seq": (7,), "cvk_set_tri_max": (4096,), "cvk_set_prep_lat_fused": (1,)}
+    argt = {"cvk_set_pipe": [ctypes.c_size_t] * 3 + [ctypes.c_int]}
+    reset = {"cvk_set_pipe": (131072, 32768, 262144, 8), "cvk_set_small_pool_min": (16384,), "cvk_set_small_zc": (1,), "cvk_set_lat_seq": (7,), "cvk_set_tri_max": (4096,), "cvk_set_prep_lat_fused": (1,)}
 
     def apply(sets):
         for k in used:
-            getattr(lib, k).argtypes = [ctypes.c_int] * len(reset[k])
+            getattr(lib, k).argtypes = argt.get(k, [ctypes.c_int] * len(reset[k]))
             getattr(lib, k)(*reset[k])
         for k, a in sets:
-            getattr(lib, k).argtypes = [ctypes.c_int] * len(a)
+            getattr(lib, k).argtypes = argt.get(k, [ctypes.c_int] * len(a))
             getattr(lib, k)(*a)
     eng = native.Engine(1)
     adv = adversarial_pool()
