@@ -107,7 +107,7 @@ def pcie_h2d_probe(dev, mb: int = 256, reps: int = 5) -> float:
     return best
 
 
-def host_api_rate(eng, batch, steps: int, device_value: float, name: str):
+def host_api_rate(eng, batch, steps: int, device_value: float, name: str, async_steps: int = 0):
     """The drop-in path: the same batch handed over as host numpy buffers to
     cv_ed25519_verify_batch — what the JVM shim calls for SignedTransaction.checkSignaturesAreValid
     (SignedTransaction.kt:82-87) and the resolve loop (ResolveTransactionsFlow.kt:105-111).  Each step =
@@ -116,7 +116,9 @@ def host_api_rate(eng, batch, steps: int, device_value: float, name: str):
       pinned    the inputs live in pinned host memory (cv_host_alloc — how the JVM shim builds its
                 batches): every sub-chunk is DMAed straight out of them (no packing copy)
       pageable  ordinary numpy buffers: host threads pack each sub-chunk into pinned staging first
-    `value` is the pinned form (the shim's production layout); the pageable form is reported beside it."""
+    `value` is the pinned form (the shim's production layout); the pageable form is reported beside it.
+    async_steps (default: steps) = calls of the two async forms: with two calls in flight the first
+    call's ramp and the last call's tail are not overlapped, so a short loop understates the loop's rate."""
     pk, sig, arena, off, ln = batch.to_host()
     n = batch.n
     in_bytes = pk.nbytes + sig.nbytes + off.nbytes + ln.nbytes + int(ln.astype(np.int64).sum())
@@ -130,12 +132,14 @@ def host_api_rate(eng, batch, steps: int, device_value: float, name: str):
         assert native.bitmap_to_bools(bm, n).all(), "host API rejected an honest signature"
         return dt
 
+    asteps = async_steps or steps
+
     def timed_async(a):
         """K calls with two in flight (cv_ed25519_verify_batch_async / cv_wait): submit k+1, then wait k."""
         eng.wait(eng.verify_batch_async(*a, want_status=False))
         t = time.perf_counter()
         pend = []
-        for _ in range(steps):
+        for _ in range(asteps):
             pend.append(eng.verify_batch_async(*a, want_status=False))
             if len(pend) == 2:
                 bm, _ = eng.wait(pend.pop(0))
@@ -156,17 +160,17 @@ def host_api_rate(eng, batch, steps: int, device_value: float, name: str):
     dt_async = timed_async(pinned)
     dt_async_page = timed_async((pk, sig, arena, off, ln))
     del pinned
-    v, vp, vs = n * steps / dt_async, n * steps / dt_page, n * steps / dt_pin
-    va = n * steps / dt_async_page
-    return {"workload": name, "value": v, "unit": "verifies/s", "ms_per_step": dt_async / steps * 1e3, "steps": steps,
+    v, vp, vs = n * asteps / dt_async, n * steps / dt_page, n * steps / dt_pin
+    va = n * asteps / dt_async_page
+    return {"workload": name, "value": v, "unit": "verifies/s", "ms_per_step": dt_async / asteps * 1e3, "steps": asteps,
             "sigs": n, "ratio_to_device_value": v / device_value, "device_value": device_value,
-            "input_bytes_per_call": in_bytes, "input_gb_per_s": in_bytes * steps / dt_async / 1e9,
+            "input_bytes_per_call": in_bytes, "input_gb_per_s": in_bytes * asteps / dt_async / 1e9,
             "path": "cv_ed25519_verify_batch_async from pinned host buffers (cv_host_alloc), two calls in flight "
                     "(a batching node submits batch k+1 before waiting for batch k); sub-chunks DMAed in place",
             "sync_pinned": {"value": vs, "ms_per_step": dt_pin / steps * 1e3, "ratio_to_device_value": vs / device_value,
                             "direct_dma_subchunks": direct,
                             "path": "cv_ed25519_verify_batch (synchronous, one call at a time) from pinned buffers"},
-            "async_pageable": {"value": va, "ms_per_step": dt_async_page / steps * 1e3,
+            "async_pageable": {"value": va, "ms_per_step": dt_async_page / asteps * 1e3,
                                "ratio_to_device_value": va / device_value,
                                "path": "cv_ed25519_verify_batch_async from pageable numpy buffers, two in flight"},
             "pageable": {"value": vp, "ms_per_step": dt_page / steps * 1e3, "ratio_to_device_value": vp / device_value,
@@ -544,7 +548,8 @@ def c5_line(eng, local, rank, sh, dev, n, steps, mad_rate, host_api: bool = True
     el = time.perf_counter() - t0
     assert bool((bm == -1).all()) or n % 64, "C5: verify rejected an honest signature"
     ph = np.mean(np.array([eng.verify_device_timed(local, n, *a, sh) for _ in range(2)]), axis=0)
-    host = host_api_rate(eng, b, 3, n * steps / el, CONFIG_NAME["c5"] + " (host buffers)") if host_api else None
+    host = host_api_rate(eng, b, 3, n * steps / el, CONFIG_NAME["c5"] + " (host buffers)",
+                         async_steps=8) if host_api else None
     del b
     return {"workload": CONFIG_NAME["c5"], "value": n * steps / el, "unit": "verifies/s", "host_api": host,
             "ms_per_step": el / steps * 1e3, "steps": steps, "sigs_per_gpu": n,
@@ -567,8 +572,9 @@ def main():
     ap.add_argument("--no-keyed", action="store_true")
     ap.add_argument("--no-sub", action="store_true", help="skip the C3 / C5-shard sub-lines")
     ap.add_argument("--no-host", action="store_true", help="skip the host-buffer (drop-in) sub-lines")
-    ap.add_argument("--streams", type=int, default=2,
-                    help="device streams the K timed steps are dealt over (each its own workspace slot)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="device streams the K timed steps are dealt over (each its own workspace slot); the "
+                         "line also reports the other form (1 <-> 2 streams) beside it")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -622,7 +628,12 @@ def main():
     # Steps are independent batches (a node's concurrent verify calls): step k goes on streams[k % S],
     # each stream with its own bitmap; the engine gives each stream its own workspace slot, so step k+1's
     # prep runs while step k's last Straus round drains.  Every step is a full verify of all n signatures.
-    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(max(1, args.streams) - 1)]
+    # (round-3 same-box interleaved A/B, tools/stream_ab.py, profiles/r03n_stream_ab.log: one stream with
+    # the engine's drain-overlap split 9.99 ms per call, two streams 10.12, two without the split 10.03,
+    # three 9.95 — within a box's noise of each other; over six bench runs two streams won three by ~1 %
+    # and lost three by 3-4 %, so the line's value is the one-stream form and the other is reported beside)
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(max(2, args.streams) - 1)]
+    nstreams = max(1, args.streams)
     bitmaps = [torch.zeros(words, dtype=torch.int64, device=dev) for _ in streams]
     bitmap = bitmaps[0]
 
@@ -654,8 +665,9 @@ def main():
 
     # Timed region: K production verify calls dealt over the streams (the engine's own launch plan,
     # incl. the drain-overlap sub-chunks it picks for near-empty last rounds), one sync at the end.
-    elapsed, gathered = timed(len(streams))
-    serial_elapsed, _ = timed(1) if len(streams) > 1 else (elapsed, None)
+    elapsed, gathered = timed(nstreams)
+    other_streams = 2 if nstreams == 1 else 1
+    other_elapsed, _ = timed(other_streams)
     full = torch.full_like(bitmap, -1)
     if n % 64:
         full[-1] = (1 << (n % 64)) - 1
@@ -677,9 +689,9 @@ def main():
     hs = native.verify_mode() == 1
     kern_ms, straus_ms = float(ph.sum()), float(ph[2] if hs else ph[1])
     if world > 1:
-        tt = torch.tensor([elapsed, kern_ms, straus_ms, serial_elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed, kern_ms, straus_ms, other_elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms, straus_ms, serial_elapsed = float(tt[0]), float(tt[1]), float(tt[2]), float(tt[3])
+        elapsed, kern_ms, straus_ms, other_elapsed = float(tt[0]), float(tt[1]), float(tt[2]), float(tt[3])
         assert torch.equal(gathered.view(world, words)[rank], bitmap)
         assert bool((gathered == -1).all()), "a rank rejected an honest signature"
     value = world * n * args.steps / elapsed
@@ -716,10 +728,10 @@ def main():
             "data": "synthetic (keys, messages, signatures generated on-GPU from seeded RNG, RFC 8032 signing)",
             "config": {"workload": CONFIG_NAME[args.config], "sigs_per_gpu": n, "msg_bytes": msg_len,
                        "key_pool": args.key_pool or "distinct", "parallelism": f"shard-by-signature x{world}",
-                       "device_streams": len(streams),
+                       "device_streams": nstreams,
                        "collective": "RCCL all_gather of verdict bitmaps" if world > 1 else "none"},
-            "single_stream_ms_per_step": serial_elapsed / args.steps * 1e3,
-            "single_stream_value": world * n * args.steps / serial_elapsed,
+            f"{'two' if other_streams == 2 else 'single'}_stream_ms_per_step": other_elapsed / args.steps * 1e3,
+            f"{'two' if other_streams == 2 else 'single'}_stream_value": world * n * args.steps / other_elapsed,
             "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": mad_rate / 1e12, "unit": "Tmac/s",
                          "frac": achieved / mad_rate, "traffic": pmc_traffic(n, hs)[0],
                          "traffic_source": pmc_traffic(n, hs)[1],
