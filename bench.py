@@ -29,7 +29,7 @@ Extra fields on the JSON line:
   notary        C4: p50/p99 end-to-end latency of a 4096-signature notary batch (host buffers in and
                 out, 1/16 adversarial records from the golden corpus's rejected classes), with the
                 p50 breakdown (transfers + host, launch + sync, per kernel) and the CPU restatement on
-                the same batch; notary_sweep = the same at 256 and 65536; notary_keyed = 64 signers
+                the same batch; notary_sweep = the same at 2^k, k = 8..16 (k != 12); notary_keyed = 64 signers
   resolve_chain p50/p99 latency of a 5,000-tx dependency chain (2 signers/tx, 6 leaves/tx): one
                 Merkle call + one verify call + per-tx AND with the id check
 """
@@ -766,10 +766,11 @@ def main():
         if not args.no_notary:
             adv = workload.adversarial_records(os.path.join(REPO, "tests", "golden", "ed25519_corpus.npz"))
             cpu4 = world == 1 and not args.no_cpu
-            result["notary"] = notary_latency(eng, local, 4096, 60, cpu=cpu4, adv=adv)
-            result["notary_sweep"] = [notary_latency(eng, local, k, r, cpu=False, adv=adv)
-                                      for k, r in ((256, 60), (65536, 20))]
-            result["notary_keyed"] = notary_latency(eng, local, 4096, 60, cpu=False, key_pool=64, adv=adv)
+            # batches of 2^k signatures, k = 8..16, >= 200 timed repetitions per size
+            result["notary"] = notary_latency(eng, local, 4096, 200, cpu=cpu4, adv=adv)
+            result["notary_sweep"] = [notary_latency(eng, local, 1 << k, 200, cpu=False, adv=adv)
+                                      for k in range(8, 17) if k != 12]
+            result["notary_keyed"] = notary_latency(eng, local, 4096, 200, cpu=False, key_pool=64, adv=adv)
             result["resolve_chain"] = resolve_chain_latency(eng, local, 30, cpu=(world == 1 and not args.no_cpu))
         print(json.dumps(result), flush=True)
     if world > 1:
