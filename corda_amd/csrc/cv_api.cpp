@@ -315,6 +315,9 @@ struct PipeStats {
 // 1 = pinned caller arrays are DMAed in place (stage_direct); 0 = always pack (A/B knob)
 static int g_direct_dma = 1;
 static size_t g_direct_small_min = 16384;   // the small path's direct-DMA threshold (signatures)
+// 1 = cv_open creates the host pipeline's streams (slot 1, copy, verdict copy) right after the device
+// stream; 0 = on first use (A/B knob, read by cv_open)
+static int g_eager_streams = 1;
 // 1 = tri-form batches from host buffers take the zero-copy path (verify_shard_small_zc); 0 = DMA in/out
 static int g_small_zc = 1;
 // host-side time of the zero-copy path, seconds (cvk_small_stats): range scan + setup (buffers,
@@ -504,6 +507,7 @@ void cvk_set_virtual_devices(int k) { g_virtual_devices = (k >= 1 && k <= 16) ? 
 void cvk_set_direct_dma(int v) { g_direct_dma = v ? 1 : 0; }
 void cvk_set_direct_small_min(int n) { g_direct_small_min = n > 0 ? (size_t)n : 16384; }
 void cvk_set_small_zc(int v) { g_small_zc = v ? 1 : 0; }
+void cvk_set_eager_streams(int v) { g_eager_streams = v ? 1 : 0; }
 // out[6] = plan+setup, pack, launch, sync, assemble (seconds, summed) and calls; reset clears them
 void cvk_small_stats(double *out, int reset) {
     std::lock_guard<std::mutex> g(g_pipe_stats_mu);
@@ -594,6 +598,22 @@ int cv_open(uint32_t device_mask, cv_ctx **out) {
                 return CV_E_HIP;
             }
             ctx->devs.push_back(std::move(dev));
+            // The host pipeline's concurrently busy streams — slot 0 (the device stream), slot 1, the copy
+            // stream and the verdict-copy stream — are created back to back here, before any helper
+            // stream, so the runtime spreads them over distinct hardware queues (GPU_MAX_HW_QUEUES = 4 by
+            // default).  Created lazily, after the device API's split helpers or a caller's own streams,
+            // the copy stream could share a queue with a compute stream and its copies wait behind that
+            // stream's kernels.
+            if (g_eager_streams) {
+                Device &dd = ctx->devs.back();
+                hipStream_t s1 = nullptr;
+                if (slot_stream(dd, 1, &s1) != hipSuccess ||
+                    hipStreamCreateWithFlags(&dd.copy, hipStreamNonBlocking) != hipSuccess ||
+                    hipStreamCreateWithFlags(&dd.outs, hipStreamNonBlocking) != hipSuccess) {
+                    cv_close(ctx);
+                    return CV_E_HIP;
+                }
+            }
             // Per-device basepoint rows (16.8 MB, built once per process): eager, so the first
             // verify is not charged for them and no later call synchronises to build them.
             if (v == 0 && cvk_prepare(dev.stream) != hipSuccess) {
