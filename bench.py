@@ -42,6 +42,14 @@ import os
 import sys
 import time
 
+# Hardware queues per device for this process (read by the HIP runtime when it starts, so before torch
+# initialises it): the engine's host pipeline keeps four streams busy and the device-API steps below run
+# on two caller streams with a drain-split helper each; with HIP's default of four queues some of them
+# share a queue and a stream's kernels wait behind another's (DESIGN.md "Negative results": one vs two
+# streams flipped from box to box with the queue placement; with eight, two streams won on every box).
+# INTEGRATION.md gives a node the same setting.  An explicit GPU_MAX_HW_QUEUES in the environment wins.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -572,7 +580,7 @@ def main():
     ap.add_argument("--no-keyed", action="store_true")
     ap.add_argument("--no-sub", action="store_true", help="skip the C3 / C5-shard sub-lines")
     ap.add_argument("--no-host", action="store_true", help="skip the host-buffer (drop-in) sub-lines")
-    ap.add_argument("--streams", type=int, default=1,
+    ap.add_argument("--streams", type=int, default=2,
                     help="device streams the K timed steps are dealt over (each its own workspace slot); the "
                          "line also reports the other form (1 <-> 2 streams) beside it")
     args = ap.parse_args()
@@ -628,10 +636,10 @@ def main():
     # Steps are independent batches (a node's concurrent verify calls): step k goes on streams[k % S],
     # each stream with its own bitmap; the engine gives each stream its own workspace slot, so step k+1's
     # prep runs while step k's last Straus round drains.  Every step is a full verify of all n signatures.
-    # (round-3 same-box interleaved A/B, tools/stream_ab.py, profiles/r03n_stream_ab.log: one stream with
-    # the engine's drain-overlap split 9.99 ms per call, two streams 10.12, two without the split 10.03,
-    # three 9.95 — within a box's noise of each other; over six bench runs two streams won three by ~1 %
-    # and lost three by 3-4 %, so the line's value is the one-stream form and the other is reported beside)
+    # (round 3: with HIP's default four hardware queues one vs two streams flipped from box to box with
+    # the queues the streams landed on, profiles/r03n_stream_ab.log, r03o_stream_ab_q4.log; with eight
+    # (set above) two streams won on every run, 8.86-9.04 vs 9.18-9.23 ms per call on one box,
+    # profiles/r03p_bench_q8_streams.log.  The other form is reported beside the value.)
     streams = [stream] + [torch.cuda.Stream(dev) for _ in range(max(2, args.streams) - 1)]
     nstreams = max(1, args.streams)
     bitmaps = [torch.zeros(words, dtype=torch.int64, device=dev) for _ in streams]
