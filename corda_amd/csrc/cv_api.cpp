@@ -318,8 +318,12 @@ static size_t g_direct_small_min = 16384;   // the small path's direct-DMA thres
 // 1 = cv_open creates the host pipeline's streams (slot 1, copy, verdict copy) right after the device
 // stream; 0 = on first use (A/B knob, read by cv_open)
 static int g_eager_streams = 1;
-// 1 = tri-form batches from host buffers take the zero-copy path (verify_shard_small_zc); 0 = DMA in/out
-static int g_small_zc = 1;
+// tri-form batches from host buffers: 0 = DMA in / copy out (verify_shard_small), 1 = zero-copy (the prep
+// reads the pinned staging over PCIe, verdicts stored into pinned host memory), 2 = zero-copy out with a
+// gather kernel moving the staging into device memory first (verify_shard_small_zc), 3 = auto: 2 from
+// 2,048 signatures, 1 below (same-box A/B, profiles/r03p_notary_zc_gather_ab.log: 4,096 0.289 ms p50 with
+// the gather against 0.291-0.298 without; 256 0.251 against 0.249)
+static int g_small_zc = 3;
 // host-side time of the zero-copy path, seconds (cvk_small_stats): range scan + setup (buffers,
 // workspace), packing, launches, the synchronisation (≈ the kernels), the bitmap assembly; and calls
 static double g_small_t[5];
@@ -506,7 +510,7 @@ void cvk_set_virtual_devices(int k) { g_virtual_devices = (k >= 1 && k <= 16) ? 
 // (signatures; 0 keeps the current value) and packing threads.
 void cvk_set_direct_dma(int v) { g_direct_dma = v ? 1 : 0; }
 void cvk_set_direct_small_min(int n) { g_direct_small_min = n > 0 ? (size_t)n : 16384; }
-void cvk_set_small_zc(int v) { g_small_zc = v ? 1 : 0; }
+void cvk_set_small_zc(int v) { g_small_zc = (v >= 0 && v <= 3) ? v : 3; }
 void cvk_set_eager_streams(int v) { g_eager_streams = v ? 1 : 0; }
 // out[6] = plan+setup, pack, launch, sync, assemble (seconds, summed) and calls; reset clears them
 void cvk_small_stats(double *out, int reset) {
@@ -860,7 +864,7 @@ static hipError_t stage_dma_direct(const Stage &st, uint8_t *dv, size_t b, const
 // the verdict copy (a blit kernel after the Straus kernel).
 static int verify_shard_small_zc(Device &d, const Stage &st, size_t b, const uint8_t *pk, const uint8_t *sig,
                                  const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
-                                 uint8_t *status, WorkerPool *pool, double t_plan) {
+                                 uint8_t *status, WorkerPool *pool, double t_plan, bool gather) {
     double t[6];
     t[0] = t_plan;
     const size_t n = st.n, words = (n + 63) / 64, nnib = words * 16, waves = (n + 3) / 4;
@@ -874,7 +878,8 @@ static int verify_shard_small_zc(Device &d, const Stage &st, size_t b, const uin
     CV_TRY(ensure_verify_ws(sl, n));
     if (!cvk_tri_zc_ok((uint32_t)n, sl.ws_cap)) return CV_E_HIP;   // (cannot happen: checked by the caller)
     uint8_t *h = d.zc_in.as<uint8_t>();
-    const uint8_t *dv = d.zc_in.dev_as<uint8_t>();
+    if (gather) CV_TRY(sl.packed.ensure(al16(st.total)));
+    const uint8_t *dv = gather ? sl.packed.as<uint8_t>() : d.zc_in.dev_as<uint8_t>();
     t[1] = now_s();
     stage_pack(st, h, b, pk, sig, arena, off, len, pool, [] {});
     uint8_t *nib = d.zc_out.as<uint8_t>();
@@ -886,7 +891,8 @@ static int verify_shard_small_zc(Device &d, const Stage &st, size_t b, const uin
         (uint32_t)n, dv + st.o_pk, dv + st.o_sig, dv + st.o_ar - st.lo, reinterpret_cast<const uint64_t *>(dv + st.o_off),
         reinterpret_cast<const uint32_t *>(dv + st.o_len), d.zc_out.dev_as<uint8_t>(),
         status ? d.zc_out.dev_as<uint8_t>() + al16(nnib) : nullptr, sl.ws_tab.as<uint32_t>(), sl.ws_ok.as<uint8_t>(),
-        sl.ws_dig.as<uint32_t>(), sl.ws_cap, s);
+        sl.ws_dig.as<uint32_t>(), sl.ws_cap, s, gather ? d.zc_in.dev : nullptr, gather ? sl.packed.p : nullptr,
+        gather ? al16(st.total) : 0);
     const hipError_t e2 = ws_end(sl, s);
     CV_TRY(e);
     CV_TRY(e2);
@@ -921,7 +927,8 @@ static int verify_shard_small(Device &d, size_t b, size_t e, const uint8_t *pk, 
     const double t_plan = now_s();
     const Stage st = stage_plan(b, e, off, len, pool);
     if (g_small_zc && cvk_tri_zc_ok((uint32_t)n, (uint32_t)n))
-        return verify_shard_small_zc(d, st, b, pk, sig, arena, off, len, bitmap, status, pool, t_plan);
+        return verify_shard_small_zc(d, st, b, pk, sig, arena, off, len, bitmap, status, pool, t_plan,
+                                     g_small_zc == 2 || (g_small_zc == 3 && n >= 2048));
     const size_t words = (n + 63) / 64;
     const size_t o_bm = 0, o_st = al16(words * 8), total_out = o_st + al16(n);
     Slot &sl = d.slot[0];

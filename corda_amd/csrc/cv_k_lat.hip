@@ -133,6 +133,14 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_hs_straus_tri_kernel(uint32_t n, 
     }
 }
 
+// Host -> device gather of q 16-byte pieces (the zero-copy notary path's records, cvk_verify_tri_zc):
+// grid-stride, one 16-B load per lane per pass, so a batch's whole staging is in flight over PCIe at once.
+__global__ __launch_bounds__(256) void cv_gather16_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst,
+                                                          size_t q) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < q; i += stride) dst[i] = src[i];
+}
+
 template __global__ void cv_prep_lat_kernel<true, true>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
 template __global__ void cv_prep_lat_kernel<false, true>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
 template __global__ void cv_hs_straus_quad_kernel<false>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);

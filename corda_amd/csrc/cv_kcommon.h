@@ -119,6 +119,7 @@ __global__ void cv_scalars_lat_kernel(uint32_t n, uint32_t cap, const uint8_t *p
 __global__ void cv_points_pair_kernel(uint32_t n, const uint8_t *pk, const uint8_t *sig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
 template <bool B16, bool LAT = true> __global__ void cv_prep_lat_kernel(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
 template <bool SEQ> __global__ void cv_hs_straus_quad_kernel(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);
+__global__ void cv_gather16_kernel(const uint4 *src, uint4 *dst, size_t q);
 template <bool SEQ> __global__ void cv_hs_straus_tri_kernel(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, uint8_t *nib);
 __global__ void cv_sign_kernel( uint32_t n, const uint8_t *seed, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint8_t *pk_out, uint8_t *sig_out);
 // leaves per leaf-hash workgroup (sorted by SHA-256 block count inside it)

@@ -200,11 +200,25 @@ hipError_t cvk_prepare(hipStream_t stream) {
 // so the call is one packing memcpy, two launches and one synchronisation.  nib gets one byte per
 // wave (4 verdict bits, nib[i / 4] bit i % 4); the caller assembles the bitmap words.  Requires the
 // tri form (n <= cvk_get_tri_max(), half-size mode) and n <= ws_cap: hipErrorInvalidValue otherwise.
+//
+// copy_src / copy_dst / copy_bytes (optional, 16-B aligned, copy_bytes a multiple of 16): a gather kernel
+// first moves the packed records from pinned host memory into device memory with every lane of the
+// grid reading its own 16-B pieces (many PCIe reads in flight at once), and pk..len point into copy_dst —
+// instead of the prep's lanes reading them over PCIe one dependent load at a time.
 hipError_t cvk_verify_tri_zc(uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
                              const uint64_t *off, const uint32_t *len, uint8_t *nib, uint8_t *status,
-                             uint32_t *ws_tab, uint8_t *ws_ok, uint32_t *ws_dig, uint32_t ws_cap, hipStream_t stream) {
+                             uint32_t *ws_tab, uint8_t *ws_ok, uint32_t *ws_dig, uint32_t ws_cap, hipStream_t stream,
+                             const void *copy_src, void *copy_dst, size_t copy_bytes) {
     if (n == 0) return hipSuccess;
     if (!cvk_tri_zc_ok(n, ws_cap) || !nib) return hipErrorInvalidValue;
+    if (copy_bytes) {
+        if (!copy_src || !copy_dst || copy_bytes % 16 || ((uintptr_t)copy_src | (uintptr_t)copy_dst) % 16)
+            return hipErrorInvalidValue;
+        const size_t q = copy_bytes / 16;
+        const uint32_t blocks = (uint32_t)std::min<size_t>((q + 255) / 256, 2048);
+        hipLaunchKernelGGL(cv_gather16_kernel, dim3(blocks), dim3(256), 0, stream,
+                           static_cast<const uint4 *>(copy_src), static_cast<uint4 *>(copy_dst), q);
+    }
     uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
     const uint32_t nbp = (2 * n + 63) / 64, nbs = (n + 63) / 64;
     if (g_lat_seq & 4)

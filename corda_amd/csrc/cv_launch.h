@@ -39,7 +39,8 @@ uint32_t cvk_get_tri_max(void);
 int cvk_tri_zc_ok(uint32_t n, uint32_t ws_cap);
 hipError_t cvk_verify_tri_zc(uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
                              const uint64_t *off, const uint32_t *len, uint8_t *nib, uint8_t *status,
-                             uint32_t *ws_tab, uint8_t *ws_ok, uint32_t *ws_dig, uint32_t ws_cap, hipStream_t stream);
+                             uint32_t *ws_tab, uint8_t *ws_ok, uint32_t *ws_dig, uint32_t ws_cap, hipStream_t stream,
+                             const void *copy_src, void *copy_dst, size_t copy_bytes);
 hipError_t cvk_prepare(hipStream_t stream);
 hipError_t cvk_keyprep(uint32_t nk, const uint8_t *keys, const uint32_t *slots, uint32_t *scratch, uint32_t *ktab_pool,
                        uint8_t *kok_pool, hipStream_t stream);

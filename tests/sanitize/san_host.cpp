@@ -34,7 +34,7 @@ uint32_t cvk_get_tri_max(void) { return 4096; }
 int cvk_tri_zc_ok(uint32_t, uint32_t) { return 0; }
 hipError_t cvk_verify_tri_zc(uint32_t, const uint8_t *, const uint8_t *, const uint8_t *, const uint64_t *,
                              const uint32_t *, uint8_t *, uint8_t *, uint32_t *, uint8_t *, uint32_t *, uint32_t,
-                             hipStream_t) {
+                             hipStream_t, const void *, void *, size_t) {
     return hipErrorNoDevice;
 }
 hipError_t cvk_prepare(hipStream_t) { return hipErrorNoDevice; }

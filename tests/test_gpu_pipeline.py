@@ -259,8 +259,8 @@ def test_host_small_pinned_inputs_golden(engine, corpus, n):
 @pytest.mark.parametrize("n", [1, 3, 4, 63, 64, 65, 1000, 4096])
 def test_host_small_zero_copy_golden(engine, corpus, n):
     """The zero-copy notary path (tri-form batches: the prep kernel reads the packed records from pinned
-    host memory over PCIe, the kernels store one verdict byte per wave and the status bytes into pinned
-    host memory) against the DMA form and the golden verdicts/status: the golden corpus tiled to n
+    host memory over PCIe — or a gather kernel moves them to device memory first, form 2 — and the
+    kernels store one verdict byte per wave and the status bytes into pinned host memory) against the DMA form and the golden verdicts/status: the golden corpus tiled to n
     records in random order, pageable and pinned inputs, ragged ends (n % 4, n % 64)."""
     rng = np.random.default_rng(1000 + n)
     sel = rng.integers(0, len(corpus["pk"]), n)
@@ -269,20 +269,20 @@ def test_host_small_zero_copy_golden(engine, corpus, n):
     lib.cvk_set_small_zc.argtypes = [ctypes.c_int]
     out = {}
     try:
-        for zc in (0, 1):
+        for zc in (0, 1, 2):
             lib.cvk_set_small_zc(zc)
             out[zc] = engine.verify_batch(*arr)
             out[zc, "pinned"] = engine.verify_batch(*[engine.host_copy(x) for x in arr])
             out[zc, "nostatus"] = engine.verify_batch(*arr, want_status=False)
     finally:
-        lib.cvk_set_small_zc(1)
+        lib.cvk_set_small_zc(3)
     exp = corpus["verdict"][sel].astype(bool)
     for k, (bitmap, status) in out.items():
         assert np.array_equal(_bits(bitmap, n), exp), k
         assert int(bitmap[-1]) >> (n % 64) == 0 if n % 64 else True
         if status is not None:
             assert np.array_equal(status, corpus["status"][sel]), k
-    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][0], out[2][0])
 
 
 def test_async_calls_in_flight_match_sync(engine, corpus, oracle_c):
