@@ -30,7 +30,7 @@ __global__ __launch_bounds__(64) void cv_points_pair_kernel(uint32_t n, const ui
 // max(scalars, points) instead of their sum.  One wave per 64-thread block, the whole register
 // file for it (no spills in either role).
 template <bool B16, bool LAT>
-__global__ __launch_bounds__(64, 1) void cv_prep_lat_kernel(uint32_t n, uint32_t cap, uint32_t nbp,
+__global__ __launch_bounds__(64, 1) void cv_prep_lat_kernel(uint32_t n, uint32_t cap, uint32_t nbp, uint32_t pts4,
                                                             const uint8_t *__restrict__ pk,
                                                             const uint8_t *__restrict__ sig,
                                                             const uint8_t *__restrict__ arena,
@@ -43,7 +43,11 @@ __global__ __launch_bounds__(64, 1) void cv_prep_lat_kernel(uint32_t n, uint32_t
                                                             uint8_t *__restrict__ status,
                                                             uint64_t *__restrict__ bitmap) {
     if (blockIdx.x < nbp) {
-        cv_points_pair_lane<LAT>(blockIdx.x * 64 + threadIdx.x, n, pk, sig, ws_tab, ws_tabR, ws_ok, status);
+        // pts4 (kernel argument, uniform): four lanes per signature (split tables), else lane pairs
+        if (pts4)
+            cv_points_quad_lane<LAT>(blockIdx.x * 64 + threadIdx.x, n, pk, sig, ws_tab, ws_tabR, ws_ok, status);
+        else
+            cv_points_pair_lane<LAT>(blockIdx.x * 64 + threadIdx.x, n, pk, sig, ws_tab, ws_tabR, ws_ok, status);
     } else {
         const uint32_t i = (blockIdx.x - nbp) * 64 + threadIdx.x;
         // the chunk's verdict words start at zero for the Straus kernel's atomicOr (it runs after this
@@ -141,11 +145,11 @@ __global__ __launch_bounds__(256) void cv_gather16_kernel(const uint4 *__restric
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < q; i += stride) dst[i] = src[i];
 }
 
-template __global__ void cv_prep_lat_kernel<true, true>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
-template __global__ void cv_prep_lat_kernel<false, true>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
+template __global__ void cv_prep_lat_kernel<true, true>(uint32_t n, uint32_t cap, uint32_t nbp, uint32_t pts4, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
+template __global__ void cv_prep_lat_kernel<false, true>(uint32_t n, uint32_t cap, uint32_t nbp, uint32_t pts4, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
 template __global__ void cv_hs_straus_quad_kernel<false>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);
 template __global__ void cv_hs_straus_quad_kernel<true>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);
 template __global__ void cv_hs_straus_tri_kernel<false>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, uint8_t *nib);
 template __global__ void cv_hs_straus_tri_kernel<true>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, uint8_t *nib);
-template __global__ void cv_prep_lat_kernel<true, false>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
-template __global__ void cv_prep_lat_kernel<false, false>(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
+template __global__ void cv_prep_lat_kernel<true, false>(uint32_t n, uint32_t cap, uint32_t nbp, uint32_t pts4, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
+template __global__ void cv_prep_lat_kernel<false, false>(uint32_t n, uint32_t cap, uint32_t nbp, uint32_t pts4, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);

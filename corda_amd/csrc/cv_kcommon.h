@@ -80,6 +80,29 @@ __device__ __forceinline__ void cv_points_pair_lane(uint32_t g, uint32_t n, cons
     }
 }
 
+// points of the latency prep with FOUR lanes per signature (cvk_set_lat_points_quad): lanes 4i + {0, 1}
+// decode A / R and build entries 0, 1, 3, 5, 7 of their table, lanes 4i + {2, 3} decode the same points
+// (the redundant decode costs no time: the lanes are idle otherwise) and build entries 2, 4, 6, 8 —
+// each lane's chain is the decode + 1 doubling + 3 additions instead of + 1 + 6
+// (ge_cached_multiples8_half).  Lane 4i writes ok = key_ok AND r_ok.
+template <bool LAT = true>
+__device__ __forceinline__ void cv_points_quad_lane(uint32_t g, uint32_t n, const uint8_t *pk, const uint8_t *sig,
+                                                    uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok,
+                                                    uint8_t *status) {
+    const uint32_t i = g >> 2;
+    if (i >= n) return;                       // the four lanes of a signature leave together
+    const bool is_r = (g & 1u) != 0;
+    const int half = (int)((g >> 1) & 1u);
+    uint32_t w[8];
+    load_words8(w, is_r ? sig + (size_t)i * 64 : pk + (size_t)i * 32);
+    const bool ok = cv_hs_point_one<LAT>(w, is_r, (is_r ? ws_tabR : ws_tab) + (size_t)i * CV_TAB_WORDS, half);
+    const bool r_ok = __shfl_xor((int)ok, 1) != 0;
+    if (!is_r && half == 0) {
+        ws_ok[i] = (ok && r_ok) ? 1 : 0;
+        if (status) status[i] = ok ? 0 : 1;
+    }
+}
+
 // points of the half-size group, lane-pair throughput form: lane g of the grid handles signature
 // g/2, the even lane decoding A into k*(-A), the odd lane R into k*R (sequential-carry field forms)
 __device__ __forceinline__ void cv_points_one_lane(uint32_t g, uint32_t n, const uint8_t *pk, const uint8_t *sig,
@@ -117,7 +140,7 @@ template <int WAVES, bool SUB = false> __global__ void cv_hs_straus_kernel(uint3
 __global__ void cv_bw16_init_kernel(uint32_t *tab);
 __global__ void cv_scalars_lat_kernel(uint32_t n, uint32_t cap, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig);
 __global__ void cv_points_pair_kernel(uint32_t n, const uint8_t *pk, const uint8_t *sig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
-template <bool B16, bool LAT = true> __global__ void cv_prep_lat_kernel(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
+template <bool B16, bool LAT = true> __global__ void cv_prep_lat_kernel(uint32_t n, uint32_t cap, uint32_t nbp, uint32_t pts4, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
 template <bool SEQ> __global__ void cv_hs_straus_quad_kernel(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);
 __global__ void cv_gather16_kernel(const uint4 *src, uint4 *dst, size_t q);
 template <bool SEQ> __global__ void cv_hs_straus_tri_kernel(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, uint8_t *nib);

@@ -136,6 +136,11 @@ extern "C" void cvk_set_prep_lat_fused(int v) { g_prep_lat_fused = v ? 1 : 0; }
 static int g_lat_seq = 7;
 extern "C" void cvk_set_lat_seq(int v) { g_lat_seq = v & 7; }
 
+// latency prep points with four lanes per signature (split odd-multiple tables, cv_points_quad_lane):
+// 0 = never (lane pairs), 1 = tri-form batches, 2 = tri and quad forms
+static int g_lat_points_quad = 1;
+extern "C" void cvk_set_lat_points_quad(int v) { g_lat_points_quad = (v >= 0 && v <= 2) ? v : 1; }
+
 // Batches of at most this many signatures run the quad kernels (set by cvk_set_quad_max; 0 = never)
 static uint32_t g_quad_max = 32768;
 extern "C" void cvk_set_quad_max(uint32_t m) { g_quad_max = m; }
@@ -220,13 +225,14 @@ hipError_t cvk_verify_tri_zc(uint32_t n, const uint8_t *pk, const uint8_t *sig, 
                            static_cast<const uint4 *>(copy_src), static_cast<uint4 *>(copy_dst), q);
     }
     uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
-    const uint32_t nbp = (2 * n + 63) / 64, nbs = (n + 63) / 64;
+    const uint32_t pts4 = g_lat_points_quad >= 1 ? 1u : 0u;
+    const uint32_t nbp = ((pts4 ? 4 : 2) * n + 63) / 64, nbs = (n + 63) / 64;
     if (g_lat_seq & 4)
-        hipLaunchKernelGGL((cv_prep_lat_kernel<true, false>), dim3(nbp + nbs), dim3(64), 0, stream, n, ws_cap, nbp, pk,
-                           sig, arena, off, len, ws_dig, ws_tab, ws_tabR, ws_ok, status, nullptr);
+        hipLaunchKernelGGL((cv_prep_lat_kernel<true, false>), dim3(nbp + nbs), dim3(64), 0, stream, n, ws_cap, nbp,
+                           pts4, pk, sig, arena, off, len, ws_dig, ws_tab, ws_tabR, ws_ok, status, nullptr);
     else
-        hipLaunchKernelGGL((cv_prep_lat_kernel<true, true>), dim3(nbp + nbs), dim3(64), 0, stream, n, ws_cap, nbp, pk,
-                           sig, arena, off, len, ws_dig, ws_tab, ws_tabR, ws_ok, status, nullptr);
+        hipLaunchKernelGGL((cv_prep_lat_kernel<true, true>), dim3(nbp + nbs), dim3(64), 0, stream, n, ws_cap, nbp,
+                           pts4, pk, sig, arena, off, len, ws_dig, ws_tab, ws_tabR, ws_ok, status, nullptr);
     if (g_lat_seq & 1)
         hipLaunchKernelGGL(cv_hs_straus_tri_kernel<true>, dim3((16 * n + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
                            stream, n, ws_cap, ws_dig, ws_tab, ws_tabR, ws_ok, nullptr, nib);
@@ -265,24 +271,25 @@ hipError_t cvk_verify(uint32_t n, const uint8_t *pk, const uint8_t *sig, const u
             const bool tri = m <= g_tri_max;
             if (!tri && !bw16) return hipErrorInvalidValue;   // (cannot happen: fetched above)
             if (g_prep_lat_fused || tri) {
-                const uint32_t nbp = (2 * m + 63) / 64, nbs = (m + 63) / 64;
+                const uint32_t pts4 = (g_lat_points_quad == 2 || (g_lat_points_quad == 1 && tri)) ? 1u : 0u;
+                const uint32_t nbp = ((pts4 ? 4 : 2) * m + 63) / 64, nbs = (m + 63) / 64;
                 if (tri && (g_lat_seq & 4))
-                    hipLaunchKernelGGL((cv_prep_lat_kernel<true, false>), dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp,
+                    hipLaunchKernelGGL((cv_prep_lat_kernel<true, false>), dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp, pts4,
                                        pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0,
                                        ws_dig, ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr,
                                        bitmap + (size_t)c0 / 64);
                 else if (!tri && (g_lat_seq & 4))
-                    hipLaunchKernelGGL((cv_prep_lat_kernel<false, false>), dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp,
+                    hipLaunchKernelGGL((cv_prep_lat_kernel<false, false>), dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp, pts4,
                                        pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0,
                                        ws_dig, ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr,
                                        bitmap + (size_t)c0 / 64);
                 else if (tri)
-                    hipLaunchKernelGGL((cv_prep_lat_kernel<true, true>), dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp,
+                    hipLaunchKernelGGL((cv_prep_lat_kernel<true, true>), dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp, pts4,
                                        pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0,
                                        ws_dig, ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr,
                                        bitmap + (size_t)c0 / 64);
                 else
-                    hipLaunchKernelGGL((cv_prep_lat_kernel<false, true>), dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp,
+                    hipLaunchKernelGGL((cv_prep_lat_kernel<false, true>), dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp, pts4,
                                        pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0,
                                        ws_dig, ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr,
                                        bitmap + (size_t)c0 / 64);

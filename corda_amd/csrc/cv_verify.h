@@ -140,6 +140,45 @@ __host__ __device__ __forceinline__ void ge_cached_multiples8(uint32_t *tab, con
     }
 }
 
+// Half of ge_cached_multiples8's table, the same instructions on both halves (two lanes per point in
+// the latency prep, no divergence): both compute 2P and its cached form c2, then three additions
+// Q += x with x = c1 (half 0: 3P) or c2 (half 1: 4P = 2P + 2P by the complete addition), then Q += c2
+// twice — half 0 stores entries 0, 1, 3, 5, 7, half 1 entries 2, 4, 6, 8.  Each lane's chain is
+// 1 doubling + 3 additions instead of 1 + 6.
+__host__ __device__ __forceinline__ void ge_cached_multiples8_half(uint32_t *tab, const ge_p3 &P1, bool half1) {
+    ge_cached c1, c2, c;
+    ge_p3 Q;
+    ge_p1p1 t;
+    ge_p3_to_cached(c1, P1);
+    ge_p3_dbl(t, P1);
+    ge_p1p1_to_p3(Q, t);
+    ge_p3_to_cached(c2, Q);
+    if (half1) {
+        ge_cached_store(tab + 80, c2);
+    } else {
+        ge_cached_identity(c);
+        ge_cached_store(tab, c);
+        ge_cached_store(tab + 40, c1);
+    }
+    // step 1 operand: c1 (half 0) or c2 (half 1), limb-wise select
+    ge_cached x;
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        x.YplusX.v[i] = half1 ? c2.YplusX.v[i] : c1.YplusX.v[i];
+        x.YminusX.v[i] = half1 ? c2.YminusX.v[i] : c1.YminusX.v[i];
+        x.Z.v[i] = half1 ? c2.Z.v[i] : c1.Z.v[i];
+        x.T2d.v[i] = half1 ? c2.T2d.v[i] : c1.T2d.v[i];
+    }
+    const int k0 = half1 ? 4 : 3;
+#pragma unroll
+    for (int s = 0; s < 3; s++) {
+        ge_add(t, Q, s == 0 ? x : c2);
+        ge_p1p1_to_p3(Q, t);
+        ge_p3_to_cached(c, Q);
+        ge_cached_store(tab + 40 * (k0 + 2 * s), c);
+    }
+}
+
 // Phase 1.  Returns key_ok.  hs = h || s (16 words), tab = CV_TAB_WORDS words (16-B aligned).
 template <bool LAT = false> __host__ __device__ __forceinline__ bool cv_verify_prep(const uint32_t aw[8], const uint32_t rw[8], const uint32_t sw[8],
                                                const uint8_t *msg, uint32_t mlen, uint32_t *hs, uint32_t *tab) {
@@ -895,14 +934,18 @@ __host__ __device__ __forceinline__ bool cv_hs_points(const uint32_t aw[8], cons
 // side): is_r = false decodes the key A into k*(-A), true decodes R (canonical) into k*R.  Both lanes
 // run the same instructions.  Returns the lane's decode verdict (key_ok or r_ok).
 template <bool LAT = true>
-__host__ __device__ __forceinline__ bool cv_hs_point_one(const uint32_t w[8], bool is_r, uint32_t *tab) {
+__host__ __device__ __forceinline__ bool cv_hs_point_one(const uint32_t w[8], bool is_r, uint32_t *tab,
+                                                         int half = -1) {
     ge_p3 P, nP;
     bool ok = ge_decode_0_1_0<LAT>(P, w);
     ok = ok && (!is_r || cv_r_canonical(w));
     if (!ok) ge_p3_identity(P);
     ge_p3_neg(nP, P);
     if (!is_r) P = nP;
-    ge_cached_multiples8(tab, P);
+    if (half < 0)
+        ge_cached_multiples8(tab, P);
+    else
+        ge_cached_multiples8_half(tab, P, half == 1);   // two lanes per point, half of the table each
     return ok;
 }
 

@@ -303,4 +303,41 @@ int cvh_verify_hs_fused(const uint8_t *pk, const uint8_t *sig, const uint8_t *ms
     return ok ? 1 : 0;
 }
 
+// The latency prep's split odd-multiple table (two lanes per point, ge_cached_multiples8_half) against
+// the one-lane table, for the point a 32-byte encoding decodes to (as key: k*(-A); as R: k*R; the
+// identity when it does not decode).  Returns the number of differing words of the 9-entry table.
+int cvh_table_split_mismatch(const uint8_t *enc32, int is_r) {
+    uint32_t w[8];
+    words_from_bytes(w, enc32, 8);
+    uint32_t full[CV_TAB_WORDS], split[CV_TAB_WORDS];
+    for (int i = 0; i < CV_TAB_WORDS; i++) full[i] = 0xdeadbeefu, split[i] = 0x0badf00du;
+    const bool ok1 = cv_hs_point_one<false>(w, is_r != 0, full);
+    const bool ok2 = cv_hs_point_one<false>(w, is_r != 0, split, 0);
+    const bool ok3 = cv_hs_point_one<false>(w, is_r != 0, split, 1);
+    int bad = (ok1 != ok2 || ok1 != ok3) ? 1000 : 0;
+    // the same point in each entry (projective: the split halves reach 4P, 6P, 8P by additions, so
+    // their Z differs from the one-lane doublings'): (Y+X)/Z, (Y-X)/Z, 2dT/Z agree
+    for (int k = 0; k < 9; k++) {
+        ge_cached a, b;
+        ge_cached_load(a, full + 40 * k);
+        ge_cached_load(b, split + 40 * k);
+        const fe *fa[3] = {&a.YplusX, &a.YminusX, &a.T2d}, *fb[3] = {&b.YplusX, &b.YminusX, &b.T2d};
+        for (int c = 0; c < 3; c++) {
+            fe l, r;
+            uint32_t lw[8], rw2[8];
+            fe_mul(l, *fa[c], b.Z);
+            fe_mul(r, *fb[c], a.Z);
+            fe_to_words(lw, l);
+            fe_to_words(rw2, r);
+            for (int q = 0; q < 8; q++) bad += lw[q] != rw2[q];
+        }
+        uint32_t zw[8];
+        fe_to_words(zw, b.Z);
+        bool zero = true;
+        for (int q = 0; q < 8; q++) zero = zero && zw[q] == 0;
+        bad += zero;   // Z != 0
+    }
+    return bad;
+}
+
 }  // extern "C"

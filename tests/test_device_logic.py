@@ -361,3 +361,18 @@ def test_slide_replay_structured(host_harness):
     for s in cases:
         sb = (s & full).to_bytes(32, "little")
         assert H.cvh_slide_drops(_b(sb)) == int(E.slide_drops_carry(sb)), hex(s)
+
+
+def test_split_odd_multiple_tables(host_harness, corpus):
+    """The latency prep's four-lanes-per-signature form builds each point's 9-entry table k*P in two
+    halves (entries 0,1,3,5,7 and 2,4,6,8, the same instruction stream on both lanes): every entry of
+    the halves is the same point as the one-lane table's (projectively: (Y+X)/Z, (Y-X)/Z, 2dT/Z, Z != 0)
+    and the decode flags agree, for every golden key and R (valid, non-canonical, small-order,
+    undecodable -> identity) and 200 random encodings."""
+    host_harness.cvh_table_split_mismatch.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    encs = [(bytes(corpus["pk"][i]), 0) for i in range(len(corpus["pk"]))]
+    encs += [(bytes(corpus["sig"][i][:32]), 1) for i in range(len(corpus["sig"]))]
+    rng = np.random.default_rng(77)
+    encs += [(rng.integers(0, 256, 32, dtype=np.uint8).tobytes(), int(k & 1)) for k in range(200)]
+    bad = [(e.hex(), r) for e, r in encs if host_harness.cvh_table_split_mismatch(e, r) != 0]
+    assert not bad, bad[:5]

@@ -53,7 +53,7 @@ def main():
                                 (kv.split("=") for kv in filter(None, body.split(",")))]))
     used = {k for _, sets in variants for k, _ in sets}
     argt = {"cvk_set_pipe": [ctypes.c_size_t] * 3 + [ctypes.c_int]}
-    reset = {"cvk_set_pipe": (131072, 32768, 262144, 8), "cvk_set_small_pool_min": (16384,), "cvk_set_small_zc": (3,), "cvk_set_lat_seq": (7,), "cvk_set_tri_max": (4096,), "cvk_set_prep_lat_fused": (1,)}
+    reset = {"cvk_set_pipe": (131072, 32768, 262144, 8), "cvk_set_small_pool_min": (16384,), "cvk_set_small_zc": (3,), "cvk_set_lat_points_quad": (1,), "cvk_set_lat_seq": (7,), "cvk_set_tri_max": (4096,), "cvk_set_prep_lat_fused": (1,)}
 
     def apply(sets):
         for k in used:
