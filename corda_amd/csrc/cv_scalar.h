@@ -171,33 +171,39 @@ __host__ __device__ __forceinline__ void sc_muladd(uint32_t out[8], const uint32
 // The 256-bit value lives in four 64-bit registers read through select trees (never a dynamically
 // indexed array, which the GPU would keep in scratch memory).
 CV_HD uint64_t cv_sel4(const uint64_t u[4], int q) { return (q & 2) ? ((q & 1) ? u[3] : u[2]) : ((q & 1) ? u[1] : u[0]); }
-// bits [j, j + 64) of U, zeros past bit 255 (0 <= j < 256)
-CV_HD uint64_t cv_u_window(const uint64_t u[4], int j) {
-    const int q = j >> 6, b = j & 63;
-    const uint64_t lo = cv_sel4(u, q), hi = q < 3 ? cv_sel4(u, q + 1) : 0ull;
-    return b ? (lo >> b) | (hi << (64 - b)) : lo;
-}
 __host__ __device__ __forceinline__ bool slide_drops_carry(const uint32_t s[8]) {
     if (!(s[7] >> 31)) return false;
     uint64_t u[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) u[k] = s[2 * k] | ((uint64_t)s[2 * k + 1] << 32);
-    int j = 0;
+    // the scan position is base + p, with w = bits [base, base + 64) of S (base a multiple of 64, so a
+    // word of u, no shifts): a window step costs one ctz and a shift, and w is re-read only when the scan
+    // crosses into the next word — about 5 times per scalar instead of twice per window (round 3: the
+    // C4 mix's slide replays set the notary prep's critical path at 4,096)
+    int base = 0, p = 0;
+    uint64_t w = u[0];
     bool carry = false;
-    while (j < 256) {
-        const uint64_t w = cv_u_window(u, j);
+    for (;;) {
         // carry pending: first zero bit (the carry's landing place); none: first set bit
-        const uint64_t look = carry ? ~w : w;
-        if (look == 0) {                               // not in this 64-bit window (runs of ones
-            j += 64;                                   // end at bit 256 at the latest: zero padding)
+        const uint64_t look = (carry ? ~w : w) >> p;
+        if (look == 0) {                               // none in [base + p, base + 64): next word
+            base += 64;                                // (a carry whose run of ones reaches bit 256
+            if (base >= 256) return carry;             //  is dropped)
+            w = cv_sel4(u, base >> 6);
+            p = 0;
             continue;
         }
-        j += __builtin_ctzll(look);                    // the window start
-        if (j >= 256) return carry;                    // a carry ran past bit 255: dropped
-        carry = j + 4 < 256 && ((cv_u_window(u, j) >> 4) & 1u);
-        j += 5;
+        const int t = __builtin_ctzll(look);
+        const int q = base + p + t + 4;                // the window starts at q - 4 (< 256)
+        carry = q < 256 && ((p + t + 4 < 64) ? ((w >> (p + t + 4)) & 1u) : ((cv_sel4(u, q >> 6) >> (q & 63)) & 1u));
+        p += t + 5;
+        if (p >= 64) {
+            base += 64;
+            p -= 64;
+            if (base >= 256) return carry;
+            w = cv_sel4(u, base >> 6);
+        }
     }
-    return carry;
 }
 
 // Effective [S]B scalar of eddsa-0.1.0, reduced mod L: (S - 2^256 * drop) mod L.
