@@ -872,7 +872,7 @@ static int verify_shard_small_zc(Device &d, const Stage &st, size_t b, const uin
     hipStream_t s = nullptr;
     CV_TRY(slot_stream(d, 0, &s));
     CV_TRY(slot_events(sl));
-    d.zc_in.flags = d.zc_out.flags = hipHostMallocCoherent | hipHostMallocMapped;
+    d.zc_in.flags = d.zc_out.flags = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
     CV_TRY(d.zc_in.ensure(st.total));
     CV_TRY(d.zc_out.ensure(al16(nnib) + al16(n)));
     CV_TRY(ensure_verify_ws(sl, n));
