@@ -287,6 +287,20 @@ CV_HD void digits65536_pairs(uint32_t out[8], const uint32_t n[8]) {
 #define CV_HS_MAXWIN 36                 // |u|, |v| < 2^140 -> at most 36 signed radix-16 windows
 #define CV_HS_MAXIT 200                 // Euclid steps (the Fibonacci worst case is ~185)
 
+// a / b for the lattice's quotient estimates, b > 0: on the GPU one v_rcp_f64 refined by two Newton
+// steps (relative error ~2^-52, against the IEEE division's ~15-instruction scale/fma/fixup sequence);
+// every use tolerates it — the Lehmer loop re-checks each quotient (0 <= remainder < divisor, else it
+// stops early and the exact loop continues), the exact loop scales its estimate by 1 - 2^-44
+CV_HD double cv_qdiv(double a, double b) {
+#ifdef __HIP_DEVICE_COMPILE__
+    double r = __builtin_amdgcn_rcp(b);
+    r = fma(fma(-b, r, 1.0), r, r);
+    r = fma(fma(-b, r, 1.0), r, r);
+    return a * r;
+#else
+    return a / b;
+#endif
+}
 CV_HD double cv_words_to_double(const uint32_t a[8]) {
     double d = (double)a[7];
 #pragma unroll
@@ -397,7 +411,7 @@ __host__ __device__ __forceinline__ bool sc_halfsize(uint32_t u[8], uint32_t v[8
 #pragma nounroll
         for (int k = 0; k < 40; k++) {
             if (!(x1 >= 0x1p27)) break;
-            const double q = floor(x0 / x1);
+            const double q = floor(cv_qdiv(x0, x1));
             const double nx = fma(-q, x1, x0);
             const double n0 = fma(-q, a10, a00), n1 = fma(-q, a11, a01);
             const double e = fabs(n0) + fabs(n1);
@@ -447,7 +461,7 @@ __host__ __device__ __forceinline__ bool sc_halfsize(uint32_t u[8], uint32_t v[8
         }
         CV_STAT(g_exact++;)
         // quotient estimate, never above floor(r0 / r1): the doubles carry < 2^-49 relative error
-        double q = (cv_words_to_double(r0) / cv_words_to_double(r1)) * (1.0 - 0x1p-44);
+        double q = cv_qdiv(cv_words_to_double(r0), cv_words_to_double(r1)) * (1.0 - 0x1p-44);
         q = q < 1.0 ? 1.0 : (q > 4294967295.0 ? 4294967295.0 : q);
         const uint32_t qi = (uint32_t)q;
         cv_submul8(r0, r1, qi);
