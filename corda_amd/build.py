@@ -22,12 +22,15 @@ ARCH = os.environ.get("CV_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # kernel translation units (cv_kcommon.h) compile in parallel; cv_kernels.hip holds the launchers
-SOURCES = ["cv_k_hs.hip", "cv_k_lat.hip", "cv_k_full.hip", "cv_k_misc.hip", "cv_kernels.hip", "cv_api.cpp"]
+SOURCES = ["cv_k_hs.hip", "cv_k_hss.hip", "cv_k_lat.hip", "cv_k_full.hip", "cv_k_misc.hip", "cv_kernels.hip",
+           "cv_api.cpp"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
           "-Wno-unused-variable"]
 # kernels: LLVM's max-ILP machine scheduler (A/B on one MI355X, 3 alternating rounds: C2 1M verify
 # 11.34 -> 11.15 ms median; the iterative-ILP strategy was 5 % slower) — DESIGN.md "Kernels"
 KERNEL_FLAGS = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+# per-translation-unit extra flags (CV_HSS_FLAGS overrides the Straus kernel's, for A/Bs)
+SRC_FLAGS = {"cv_k_hss.hip": os.environ["CV_HSS_FLAGS"].split() if os.environ.get("CV_HSS_FLAGS") else []}
 
 
 def _deps():
@@ -58,7 +61,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
         op = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
         objs.append(op)
         if force or _stale(op, [sp] + deps):
-            cmd = [HIPCC] + CFLAGS + KERNEL_FLAGS + ["-c", sp, "-o", op]
+            cmd = [HIPCC] + CFLAGS + KERNEL_FLAGS + SRC_FLAGS.get(src, []) + ["-c", sp, "-o", op]
             if src.endswith(".cpp"):
                 cmd = [HIPCC, "-x", "hip"] + CFLAGS + ["-c", sp, "-o", op]
             cmds.append(cmd)
