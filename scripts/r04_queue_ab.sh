@@ -10,7 +10,7 @@ for r in 1 2 3; do
     echo "[queue_ab] round $r queues $q"
     GPU_MAX_HW_QUEUES=$q timeout -k 10 240 python -u bench.py --steps 20 --warmup 3 --no-cpu --no-notary \
       --no-keyed --no-sub --no-host > "$OUT/q${q}_r${r}.json" 2> "$OUT/q${q}_r${r}.err" || exit $?
-    python -c "import json,sys; d=json.load(open('$OUT/q${q}_r${r}.json')); print(q, d['ms_per_step'], [v for k,v in d.items() if k.endswith('ms_per_step') and k!='ms_per_step'])" q=$q 2>/dev/null || tail -3 "$OUT/q${q}_r${r}.json"
+    python -c "import json,sys; d=json.load(open(sys.argv[1])); print('queues', sys.argv[2], 'ms_per_step', round(d['ms_per_step'],3), {k: round(v,3) for k,v in d.items() if k.endswith('stream_ms_per_step')})" "$OUT/q${q}_r${r}.json" $q
   done
 done
 echo "[queue_ab] done"
