@@ -19,36 +19,35 @@ Extra fields on the JSON line:
                 MACs per verify, DESIGN.md "Half-size scalars") against the measured v_mad_u64_u32
                 peak of this GPU, kernel time from HIP events on whole-chunk launches of the same
                 batch; "group" = the whole launch group against its own MAC count
-  cpu_baseline  oracle/ C restatement of eddsa-0.1.0 verify (rank 0, N=1 only, bounded sample)
   roofline.cycle_basis  the same peak priced per shader cycle (SIMDs x 64 / cycles per wave-level
                 v_mad_u64_u32 x the clock measured over the calibration launch), and against 2.4 GHz
   cpu_baseline  oracle/ C restatement of eddsa-0.1.0 verify (rank 0, N=1 only, bounded sample) on the
                 host cores this process may use (capped by the box's OMP_NUM_THREADS share)
   c3, c5_shard  BASELINE configs C3 (1M txs x 8 signers: Merkle tx-id recompute + 8M verifies) and
                 C5 (8M-signature shard) on the same GPU: value, tx_ids_per_s, phases, roofline
+  host_api      the drop-in (host-buffer) path at C2, C5, C3 and keyed C2 (1,024-key pool), against the
+                device-resident rates of the same run
   notary        C4: p50/p99 end-to-end latency of a 4096-signature notary batch (host buffers in and
                 out, 1/16 adversarial records from the golden corpus's rejected classes), with the
                 p50 breakdown (transfers + host, launch + sync, per kernel) and the CPU restatement on
                 the same batch; notary_sweep = the same at 2^k, k = 8..16 (k != 12); notary_keyed = 64 signers
   resolve_chain p50/p99 latency of a 5,000-tx dependency chain (2 signers/tx, 6 leaves/tx): one
                 Merkle call + one verify call + per-tx AND with the id check
+The printed line keeps every headline value and stays under ~4 KB; per-kernel breakdowns and the full
+sub-line dicts go to gpurun_out/bench_detail.json (--detail PATH).
 """
 from __future__ import annotations
 
 import argparse
-import ctypes
 import json
 import os
 import sys
 import time
 
-# Hardware queues per device for this process (read by the HIP runtime when it starts, so before torch
-# initialises it): the engine's host pipeline keeps four streams busy and the device-API steps below run
-# on two caller streams with a drain-split helper each; with HIP's default of four queues some of them
-# share a queue and a stream's kernels wait behind another's (DESIGN.md "Negative results": one vs two
-# streams flipped from box to box with the queue placement; with eight, two streams won on every box).
-# INTEGRATION.md gives a node the same setting.  An explicit GPU_MAX_HW_QUEUES in the environment wins.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# Hardware queues per device (HIP reads GPU_MAX_HW_QUEUES when it starts): recorded in the line, not set
+# here.  Round 4 same-box A/B of this line at 4 (HIP's default, what the GPU box exports) vs 8 queues:
+# 9.22 vs 9.30 ms per C2 call, medians of 3 alternating fresh-process runs (profiles/r04_queue_ab.log).
+HW_QUEUES = os.environ.get("GPU_MAX_HW_QUEUES")
 
 import numpy as np
 import torch
@@ -159,12 +158,9 @@ def host_api_rate(eng, batch, steps: int, device_value: float, name: str, async_
 
     dt_page = timed((pk, sig, arena, off, ln))
     pinned = tuple(eng.host_copy(x) for x in (pk, sig, arena, off, ln))
-    lib = native.load()
-    lib.cvk_pipe_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    lib.cvk_pipe_direct_chunks.restype = ctypes.c_double
-    lib.cvk_pipe_stats(None, 1)
+    eng.stats("pipe", reset=True)
     dt_pin = timed(pinned)
-    direct = int(lib.cvk_pipe_direct_chunks())
+    direct = int(eng.stats("pipe")["direct_subchunks"])
     dt_async = timed_async(pinned)
     dt_async_page = timed_async((pk, sig, arena, off, ln))
     del pinned
@@ -185,6 +181,111 @@ def host_api_rate(eng, batch, steps: int, device_value: float, name: str, async_
                          "input_gb_per_s": in_bytes * steps / dt_page / 1e9,
                          "path": "cv_ed25519_verify_batch (synchronous) from pageable numpy buffers (host threads "
                                  "pack pinned staging per sub-chunk)"}}
+
+
+def host_c3_rate(eng, local, sh, ntx: int, steps: int, device_value: float, pcie_gbs: float):
+    """C3 through the drop-in boundary: per step, the Merkle ids of 1M transactions from
+    host leaf buffers (cv_merkle_tx_ids_async), the verify of their 8M signatures over those ids
+    (cv_ed25519_verify_batch_async: the messages are the ids the Merkle call returned), and per transaction
+    id == claimed AND all signature bits (cv_tx_verdicts).  Inputs in pinned host memory (cv_host_alloc, how
+    the JVM shim builds its batches).  Pipelined like a node's loop: the Merkle call of step k+1 is submitted
+    behind the verify of step k, so its leaf copies overlap that verify's kernels; three id buffers rotate
+    (the verify of step k-1 may still read its ids while step k+1's are written)."""
+    signers = 8
+    tb = workload.make_tx_batch(eng, local, ntx, signers, seed=20261016, stream=sh)
+    n = ntx * signers
+    pin = lambda t: eng.host_copy(t.cpu().numpy())  # noqa: E731
+    arena, leaf_off = pin(tb.leaf_arena), eng.host_copy(tb.leaf_off.cpu().numpy().astype(np.uint64))
+    leaf_len, tx_begin = eng.host_copy(tb.leaf_len.cpu().numpy().astype(np.uint32)), \
+        eng.host_copy(tb.tx_begin.cpu().numpy().astype(np.uint32))
+    claimed = tb.ids.cpu().numpy().view(np.uint64).reshape(ntx, 4)
+    pk, sig = pin(tb.sigs.pk), pin(tb.sigs.sig)
+    leaf_bytes = int(tb.leaf_len.to(torch.int64).sum())
+    del tb
+    torch.cuda.empty_cache()
+    msg_off = eng.host_copy((np.arange(n, dtype=np.uint64) // signers) * 32)
+    msg_len = eng.host_copy(np.full(n, 32, np.uint32))
+    sig_begin = np.arange(0, n + 1, signers, dtype=np.uint32)
+    bufs = [eng.host_empty(ntx * 32 + 16) for _ in range(3)]      # id arenas (the verify's messages)
+    for b in bufs:
+        b[-16:] = 0
+
+    def run(k_steps):
+        ok_all = True
+        tm = eng.merkle_tx_ids_async(arena, leaf_off, leaf_len, tx_begin, ids=bufs[0][:ntx * 32].reshape(ntx, 32))
+        tv_prev = None
+        for k in range(k_steps):
+            ids, st = eng.wait(tm)
+            tv = eng.verify_batch_async(pk, sig, bufs[k % 3], msg_off, msg_len, want_status=False)
+            if k + 1 < k_steps:
+                nb = bufs[(k + 1) % 3]
+                tm = eng.merkle_tx_ids_async(arena, leaf_off, leaf_len, tx_begin, ids=nb[:ntx * 32].reshape(ntx, 32))
+            id_ok = (ids.view(np.uint64).reshape(ntx, 4) == claimed).all(axis=1) & (st == 0)
+            if tv_prev is not None:
+                bm, _ = eng.wait(tv_prev[0])
+                ok_all &= bool((native.tx_verdicts(bm, sig_begin).astype(bool) & tv_prev[1]).all())
+            tv_prev = (tv, id_ok)
+        bm, _ = eng.wait(tv_prev[0])
+        ok_all &= bool((native.tx_verdicts(bm, sig_begin).astype(bool) & tv_prev[1]).all())
+        return ok_all
+
+    assert run(2), "host C3 step rejected an honest transaction"        # warm: staging / device blocks
+    t = time.perf_counter()
+    ok = run(steps)
+    dt = time.perf_counter() - t
+    assert ok, "host C3 step rejected an honest transaction"
+    in_bytes = leaf_bytes + ntx * 6 * 12 + (ntx + 1) * 4 + n * (32 + 64 + 8 + 4) + ntx * 32
+    v = n * steps / dt
+    return {"value": v, "unit": "verifies/s", "tx_ids_per_s": ntx * steps / dt, "ms_per_step": dt / steps * 1e3,
+            "steps": steps, "ratio_to_device_value": v / device_value, "device_value": device_value,
+            "input_bytes_per_step": in_bytes, "pcie_floor_ms_per_step": in_bytes / (pcie_gbs * 1e9) * 1e3,
+            "path": "cv_merkle_tx_ids_async (leaves) + cv_ed25519_verify_batch_async (sigs over the returned ids) "
+                    "+ cv_tx_verdicts and the id check, pinned host buffers, Merkle k+1 submitted behind verify k"}
+
+
+def host_keyed_rate(eng, local, sh, n: int, msg_len: int, steps: int, device_value: float, pcie_gbs: float):
+    """The keyed path through host buffers: C2 with a 1,024-key pool handed to
+    cv_ed25519_verify_batch(_async) as plain records — the engine dedupes the keys itself (host threads,
+    per device shard) and runs the keyed pipeline (key indices instead of keys staged per sub-chunk).  value =
+    async form from pinned buffers, two calls in flight.  PCIe carries ~376 B per signature at C2 (300-B
+    message + signature + offset/length + key index), so the host form is bounded by the H2D rate, not by the
+    comb kernel's 250 M/s."""
+    b = workload.make_batch(eng, local, n, msg_len, seed=4243, key_pool=1024, stream=sh)
+    pk, sig, arena, off, ln = (eng.host_copy(x) for x in b.to_host())
+    del b
+    torch.cuda.empty_cache()
+
+    def loop(k_steps, sync):
+        pend, bm = [], None
+        for _ in range(k_steps):
+            if sync:
+                bm, _ = eng.verify_batch(pk, sig, arena, off, ln, want_status=False)
+                continue
+            pend.append(eng.verify_batch_async(pk, sig, arena, off, ln, want_status=False))
+            if len(pend) == 2:
+                bm, _ = eng.wait(pend.pop(0))
+        for tk in pend:
+            bm, _ = eng.wait(tk)
+        return bm
+
+    eng.stats("route", reset=True)
+    loop(2, False)
+    assert eng.stats("route")["keyed_shards"] >= 1, "the host keyed path was not taken"
+    t = time.perf_counter()
+    bm = loop(steps, False)
+    dt = time.perf_counter() - t
+    assert native.bitmap_to_bools(bm, n).all(), "host keyed path rejected an honest signature"
+    t = time.perf_counter()
+    loop(max(2, steps // 2), True)
+    dts = (time.perf_counter() - t) / max(2, steps // 2)
+    per_sig = msg_len + 64 + 8 + 4 + 4
+    v = n * steps / dt
+    return {"value": v, "unit": "verifies/s", "ms_per_step": dt / steps * 1e3, "steps": steps,
+            "ratio_to_device_value": v / device_value, "device_value": device_value,
+            "sync_pinned_value": n / dts, "pcie_bound_value": pcie_gbs * 1e9 / per_sig,
+            "ratio_to_pcie_bound": v / (pcie_gbs * 1e9 / per_sig),
+            "path": "cv_ed25519_verify_batch_async on plain records with a 1,024-key pool from pinned buffers, two "
+                    "in flight; host dedupe + keyed pipeline"}
 
 
 def affinity_cores() -> int:
@@ -580,6 +681,8 @@ def main():
     ap.add_argument("--no-keyed", action="store_true")
     ap.add_argument("--no-sub", action="store_true", help="skip the C3 / C5-shard sub-lines")
     ap.add_argument("--no-host", action="store_true", help="skip the host-buffer (drop-in) sub-lines")
+    ap.add_argument("--detail", default="", help="where the full measurement dict goes (default "
+                                                     "gpurun_out/bench_detail.json)")
     ap.add_argument("--streams", type=int, default=2,
                     help="device streams the K timed steps are dealt over (each its own workspace slot); the "
                          "line also reports the other form (1 <-> 2 streams) beside it")
@@ -694,8 +797,7 @@ def main():
     # correctness of the timed configuration: every generated signature is honest
     assert torch.equal(bitmap, full), "verify rejected an honest signature"
     ph = np.mean(np.array(phases), axis=0)
-    hs = native.verify_mode() == 1
-    kern_ms, straus_ms = float(ph.sum()), float(ph[2] if hs else ph[1])
+    kern_ms, straus_ms = float(ph.sum()), float(ph[2])
     if world > 1:
         tt = torch.tensor([elapsed, kern_ms, straus_ms, other_elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -706,21 +808,61 @@ def main():
 
     if rank == 0:
         mad_rate, femul_rate = eng.calibrate(local)
-        w_straus = W_MAC_HS_STRAUS if hs else W_MAC_STRAUS
-        w_group = W_MAC_HS_GROUP if hs else W_MAC_PER_VERIFY
-        achieved = n * w_straus / (straus_ms * 1e-3)
-        group = n * w_group / (kern_ms * 1e-3)
-        if hs:
-            phase_ms = {"scalars": float(ph[0]), "points": float(ph[1]), "hs_straus": float(ph[2])}
-            kname, gname = "cv_hs_straus_kernel", "scalars + points + hs_straus"
-            wdesc = (f"{w_straus} 32x32->64 MAC per verify in the half-size Straus phase at {HS_NW} windows "
-                     f"(512 S + 1023 M: 16 basepoint madds from the radix-2^16 rows)")
-            gdesc = f"{w_group} MAC per verify (half-size schedule: Straus + 2 decodes + 2 tables)"
-        else:
-            phase_ms = {"prep": float(ph[0]), "straus": float(ph[1]), "finish": float(ph[2])}
-            kname, gname = "cv_straus_kernel", "prep + straus + finish"
-            wdesc = f"{w_straus} 32x32->64 MAC per verify in the Straus phase (1008 S + 1491 M)"
-            gdesc = f"{W_MAC_PER_VERIFY:.3g} MAC per verify (SURVEY.md 8d)"
+        achieved = n * W_MAC_HS_STRAUS / (straus_ms * 1e-3)
+        group = n * W_MAC_HS_GROUP / (kern_ms * 1e-3)
+        traffic, traffic_src = pmc_traffic(n, True)
+        cyc = eng.calibrate_cycles(local)
+        other_key = f"{'two' if other_streams == 2 else 'single'}_stream"
+        # everything measured, in full: written to the detail file; the printed line is a digest of it
+        D_ = {"roofline": {
+            "bound": "valu", "achieved": achieved / 1e12, "peak": mad_rate / 1e12, "unit": "Tmac/s",
+            "frac": achieved / mad_rate, "traffic": traffic, "traffic_source": traffic_src,
+            "kernel": "cv_hs_straus_kernel", "kernel_ms": straus_ms,
+            "work_per_unit": (f"{W_MAC_HS_STRAUS} 32x32->64 MAC per verify in the half-size Straus phase at {HS_NW} "
+                              f"windows (512 S + 1023 M: 16 basepoint madds from the radix-2^16 rows)"),
+            "phase_ms": {"scalars": float(ph[0]), "points": float(ph[1]), "hs_straus": float(ph[2])},
+            "group": {"kernels": "scalars + points + hs_straus", "kernel_ms": kern_ms, "achieved": group / 1e12,
+                      "frac": group / mad_rate,
+                      "work_per_unit": f"{W_MAC_HS_GROUP} MAC per verify (half-size schedule: Straus + 2 decodes + 2 tables)"},
+            "fe_mul_per_s": femul_rate,
+            "cycle_basis": {
+                "clock_ghz": cyc["clock_ghz"], "cycles_per_wave_mad": cyc["cycles_per_wave_instr"],
+                "peak_at_measured_clock": cyc["mac_per_s"] / 1e12, "peak_at_2p4ghz": cyc["mac_per_s_at_2p4ghz"] / 1e12,
+                "frac_vs_measured_clock": achieved / cyc["mac_per_s"],
+                "frac_vs_2p4ghz": achieved / cyc["mac_per_s_at_2p4ghz"],
+                "note": "peak = SIMDs x 64 lanes / cycles-per-wave-mad x clock; clock from s_memtime/s_memrealtime "
+                        "over the same calibration launch"}}}
+        if world == 1 and not args.no_cpu:
+            D_["cpu_baseline"] = cpu_baseline(batch, local, args.cpu_seconds)
+        pcie = pcie_h2d_probe(dev)
+        if world == 1 and not args.no_host:
+            D_["host_api"] = {"c2": host_api_rate(eng, batch, max(6, args.steps), value,
+                                                  CONFIG_NAME[args.config] + " (host buffers)"),
+                              "pcie_h2d_gb_per_s_pinned": pcie}
+        if world == 1 and not args.no_sub:
+            del batch
+            torch.cuda.empty_cache()
+            D_["c3"] = c3_line(eng, local, rank, world, sh, dev, 1_000_000, 3, 1, mad_rate)
+            if not args.no_host:
+                D_["host_api"]["c3"] = host_c3_rate(eng, local, sh, 1_000_000, 4, D_["c3"]["value"], pcie)
+            D_["c5_shard"] = c5_line(eng, local, rank, sh, dev, 8_000_000, 3, mad_rate, host_api=not args.no_host)
+            if D_["c5_shard"].get("host_api") and "host_api" in D_:
+                D_["host_api"]["c5"] = D_["c5_shard"].pop("host_api")
+        if not args.no_keyed and world == 1:
+            D_["keyed"] = keyed_rate(eng, local, n, msg_len, max(3, args.steps // 2), sh)
+            if not args.no_host:
+                D_["host_api"]["keyed"] = host_keyed_rate(eng, local, sh, n, msg_len, 8, D_["keyed"]["value"], pcie)
+        if not args.no_notary:
+            adv = workload.adversarial_records(os.path.join(REPO, "tests", "golden", "ed25519_corpus.npz"))
+            cpu4 = world == 1 and not args.no_cpu
+            # SURVEY.md 8(d) C4: batches of 2^k signatures, k = 8..16, >= 200 timed repetitions per size
+            D_["notary"] = notary_latency(eng, local, 4096, 200, cpu=cpu4, adv=adv)
+            D_["notary_sweep"] = [notary_latency(eng, local, 1 << k, 200, cpu=False, adv=adv)
+                                  for k in range(8, 17) if k != 12]
+            D_["notary_keyed"] = notary_latency(eng, local, 4096, 200, cpu=False, key_pool=64, adv=adv)
+            D_["resolve_chain"] = resolve_chain_latency(eng, local, 30, cpu=(world == 1 and not args.no_cpu))
+        r3 = lambda x: None if x is None else float(f"{x:.4g}")  # noqa: E731
+        R = D_["roofline"]
         result = {
             "metric": "Ed25519 verifies/sec (node)",
             "value": value,
@@ -736,50 +878,65 @@ def main():
             "data": "synthetic (keys, messages, signatures generated on-GPU from seeded RNG, RFC 8032 signing)",
             "config": {"workload": CONFIG_NAME[args.config], "sigs_per_gpu": n, "msg_bytes": msg_len,
                        "key_pool": args.key_pool or "distinct", "parallelism": f"shard-by-signature x{world}",
-                       "device_streams": nstreams,
+                       "device_streams": nstreams, "gpu_max_hw_queues": HW_QUEUES or "unset (HIP default 4)",
                        "collective": "RCCL all_gather of verdict bitmaps" if world > 1 else "none"},
-            f"{'two' if other_streams == 2 else 'single'}_stream_ms_per_step": other_elapsed / args.steps * 1e3,
-            f"{'two' if other_streams == 2 else 'single'}_stream_value": world * n * args.steps / other_elapsed,
-            "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": mad_rate / 1e12, "unit": "Tmac/s",
-                         "frac": achieved / mad_rate, "traffic": pmc_traffic(n, hs)[0],
-                         "traffic_source": pmc_traffic(n, hs)[1],
-                         "kernel": kname, "kernel_ms": straus_ms, "work_per_unit": wdesc,
-                         "phase_ms": phase_ms,
-                         "group": {"kernels": gname, "kernel_ms": kern_ms,
-                                   "achieved": group / 1e12, "frac": group / mad_rate, "work_per_unit": gdesc},
-                         "fe_mul_per_s": femul_rate},
+            f"{other_key}_ms_per_step": r3(other_elapsed / args.steps * 1e3),
+            f"{other_key}_value": r3(world * n * args.steps / other_elapsed),
+            "roofline": {"bound": "valu", "achieved": r3(R["achieved"]), "peak": r3(R["peak"]), "unit": "Tmac/s",
+                         "frac": r3(R["frac"]), "traffic": r3(traffic), "kernel": R["kernel"], "kernel_ms": r3(straus_ms),
+                         "frac_vs_2p4ghz": r3(R["cycle_basis"]["frac_vs_2p4ghz"]),
+                         "clock_ghz": r3(cyc["clock_ghz"]), "group_frac": r3(R["group"]["frac"]),
+                         "phase_ms": {k: r3(v) for k, v in R["phase_ms"].items()},
+                         "work_per_unit": f"{W_MAC_HS_STRAUS} MAC/verify", "traffic_source": "profiles/pmc_hs_straus.json"},
         }
-        cyc = eng.calibrate_cycles(local)
-        result["roofline"]["cycle_basis"] = {
-            "clock_ghz": cyc["clock_ghz"], "cycles_per_wave_mad": cyc["cycles_per_wave_instr"],
-            "peak_at_measured_clock": cyc["mac_per_s"] / 1e12, "peak_at_2p4ghz": cyc["mac_per_s_at_2p4ghz"] / 1e12,
-            "frac_vs_measured_clock": achieved / cyc["mac_per_s"], "frac_vs_2p4ghz": achieved / cyc["mac_per_s_at_2p4ghz"],
-            "note": "peak = SIMDs x 64 lanes / cycles-per-wave-mad x clock; clock from s_memtime/s_memrealtime "
-                    "over the same calibration launch"}
-        if world == 1 and not args.no_cpu:
-            result["cpu_baseline"] = cpu_baseline(batch, local, args.cpu_seconds)
-        if world == 1 and not args.no_host:
-            result["host_api"] = {"c2": host_api_rate(eng, batch, max(6, args.steps), value,
-                                                      CONFIG_NAME[args.config] + " (host buffers)"),
-                                  "pcie_h2d_gb_per_s_pinned": pcie_h2d_probe(dev)}
-        if world == 1 and not args.no_sub:
-            del batch
-            result["c3"] = c3_line(eng, local, rank, world, sh, dev, 1_000_000, 3, 1, mad_rate)
-            result["c5_shard"] = c5_line(eng, local, rank, sh, dev, 8_000_000, 3, mad_rate,
-                                         host_api=not args.no_host)
-            if result["c5_shard"].get("host_api") and "host_api" in result:
-                result["host_api"]["c5"] = result["c5_shard"]["host_api"]
-        if not args.no_keyed and world == 1:
-            result["keyed"] = keyed_rate(eng, local, n, msg_len, max(3, args.steps // 2), sh)
-        if not args.no_notary:
-            adv = workload.adversarial_records(os.path.join(REPO, "tests", "golden", "ed25519_corpus.npz"))
-            cpu4 = world == 1 and not args.no_cpu
-            # SURVEY.md 8(d) C4: batches of 2^k signatures, k = 8..16, >= 200 timed repetitions per size
-            result["notary"] = notary_latency(eng, local, 4096, 200, cpu=cpu4, adv=adv)
-            result["notary_sweep"] = [notary_latency(eng, local, 1 << k, 200, cpu=False, adv=adv)
-                                      for k in range(8, 17) if k != 12]
-            result["notary_keyed"] = notary_latency(eng, local, 4096, 200, cpu=False, key_pool=64, adv=adv)
-            result["resolve_chain"] = resolve_chain_latency(eng, local, 30, cpu=(world == 1 and not args.no_cpu))
+        if "cpu_baseline" in D_:
+            c = D_["cpu_baseline"]
+            result["cpu_baseline"] = {"value": r3(c["value"]), "unit": c["unit"], "cores": c["cores"], "kind": c["kind"],
+                                      "sample": c["sample"], "single_thread_value": r3(c["single_thread_value"])}
+        if "host_api" in D_:
+            H = D_["host_api"]
+            h = {"pcie_h2d_gb_per_s": r3(pcie)}
+            for k in ("c2", "c5", "c3", "keyed"):
+                if k in H:
+                    h[k] = {"value": r3(H[k]["value"]), "ratio": r3(H[k]["ratio_to_device_value"]),
+                            "ms_per_step": r3(H[k]["ms_per_step"])}
+            for k in ("c2", "c5"):
+                if k in H:
+                    h[k]["sync_pinned_ratio"] = r3(H[k]["sync_pinned"]["ratio_to_device_value"])
+                    h[k]["pageable_ratio"] = r3(H[k]["pageable"]["ratio_to_device_value"])
+            if "keyed" in H:
+                h["keyed"]["pcie_bound_value"] = r3(H["keyed"]["pcie_bound_value"])
+                h["keyed"]["ratio_to_pcie_bound"] = r3(H["keyed"]["ratio_to_pcie_bound"])
+            if "c3" in H:
+                h["c3"]["pcie_floor_ms_per_step"] = r3(H["c3"]["pcie_floor_ms_per_step"])
+            result["host_api"] = h
+        if "c3" in D_:
+            c = D_["c3"]
+            result["c3"] = {"value": r3(c["value"]), "tx_ids_per_s": r3(c["tx_ids_per_s"]), "ms_per_step": r3(c["ms_per_step"]),
+                            "merkle_ms": r3(c["phase_ms"]["merkle"]), "merkle_frac": r3(c["merkle_roofline"]["frac"]),
+                            "hs_straus_frac": r3(c["roofline"]["frac"])}
+        if "c5_shard" in D_:
+            result["c5_shard"] = {"value": r3(D_["c5_shard"]["value"]), "hs_straus_frac": r3(D_["c5_shard"]["roofline"]["frac"])}
+        if "keyed" in D_:
+            result["keyed"] = {"value": r3(D_["keyed"]["value"]), "comb_ms": r3(D_["keyed"]["phase_ms"]["comb"])}
+        if "notary" in D_:
+            N = D_["notary"]
+            result["notary"] = {"batch": 4096, "p50_ms": r3(N["p50_ms"]), "p99_ms": r3(N["p99_ms"]),
+                                "pinned_p50_ms": r3(N["pinned_inputs"]["p50_ms"]), "cpu_p50_ms": r3(N.get("cpu_p50_ms")),
+                                "cpu_threads": N.get("cpu_threads"),
+                                "kernels_ms": {k: r3(v) for k, v in N.get("breakdown_p50_ms", {}).get("kernels", {}).items()}}
+            result["notary_sweep_p50_p99_ms"] = {str(x["batch"]): [r3(x["p50_ms"]), r3(x["p99_ms"])] for x in D_["notary_sweep"]}
+            result["notary_keyed_p50_ms"] = r3(D_["notary_keyed"]["p50_ms"])
+            result["resolve_chain"] = {"p50_ms": r3(D_["resolve_chain"]["p50_ms"]),
+                                       "cpu_p50_ms": r3(D_["resolve_chain"].get("cpu_p50_ms"))}
+        detail = args.detail or os.path.join(REPO, "gpurun_out", "bench_detail.json")
+        try:
+            os.makedirs(os.path.dirname(detail), exist_ok=True)
+            with open(detail, "w") as f:
+                json.dump({"line": result, "detail": D_}, f, indent=1)
+            result["detail_file"] = os.path.relpath(detail, REPO)
+        except OSError as ex:
+            log(f"could not write {detail}: {ex}")
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

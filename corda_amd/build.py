@@ -22,7 +22,7 @@ ARCH = os.environ.get("CV_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # kernel translation units (cv_kcommon.h) compile in parallel; cv_kernels.hip holds the launchers
-SOURCES = ["cv_k_hs.hip", "cv_k_hss.hip", "cv_k_lat.hip", "cv_k_full.hip", "cv_k_misc.hip", "cv_kernels.hip",
+SOURCES = ["cv_k_hs.hip", "cv_k_hss.hip", "cv_k_lat.hip", "cv_k_keyed.hip", "cv_k_misc.hip", "cv_kernels.hip",
            "cv_api.cpp"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
           "-Wno-unused-variable"]

@@ -1,6 +1,8 @@
-// cv_api.cpp — the C-ABI (include/cordaverify.h): contexts, per-device verify workspace slots, host-buffer
-// batches sharded over the context's GPUs (one host thread per device) and pipelined through pinned
-// staging, and the device-resident entry points used by bench.py.
+// cv_api.cpp — the C-ABI (include/cordaverify.h): contexts and their options, per-device executors (one lock,
+// one persistent worker thread and a load count per device; batches routed whole to one device or cut over
+// several), verify workspace slots, the host-buffer pipeline (copy stream + input ring, direct DMA from pinned
+// buffers) for plain, keyed and Merkle batches with synchronous and asynchronous forms, and the
+// device-resident entry points used by bench.py.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -9,6 +11,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <chrono>
+#include <deque>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -115,60 +118,69 @@ struct KeyHash {
     size_t operator()(const std::array<uint8_t, 32> &k) const { return (size_t)key_hash32(k.data()); }
 };
 struct KeyCache {
-    DevBuf ktab, kok, keys, slots, slot_of_key, key_index, scratch;
+    DevBuf ktab, kok, keys, slots, scratch;
     uint32_t cap = 0;
     std::unordered_map<std::array<uint8_t, 32>, uint32_t, KeyHash> map;
     uint64_t hits = 0, misses = 0, resets = 0;
     // the last stream that used the pool, and an event after that use (pool_begin / pool_end)
     hipStream_t last = nullptr;
     hipEvent_t ev = nullptr;
-    PinBuf pin;                    // pinned staging of the device-API keyed call's slot_of_key upload
-    hipEvent_t pin_ev = nullptr;   // recorded after that upload
+    hipEvent_t kp_ev = nullptr;    // after the last keyprep launch (the pipeline's other slot streams wait on it)
+    // the device-API keyed call's slot_of_key: device copy, pinned staging, event after its upload
+    DevBuf slot_of_key;
+    PinBuf pin;
+    hipEvent_t pin_ev = nullptr;
     bool pin_busy = false;
 };
 
 // One verify workspace (per signature: hs 64 B, 2 tables 2 x 1440 B, R record 128 B, ok 1 B, half-size
-// digits 292 B) with what orders its use across streams, its drain-overlap helper, and the host
-// pipeline's staging for the sub-chunks that run on it.  A device has kSlots of them: device-API
-// calls on different streams take different slots and run concurrently; the host-buffer pipeline
-// deals its sub-chunks round-robin over the slots (each slot's stream: H2D -> verify -> D2H).
+// digits 292 B) with what orders its use across streams, its drain-overlap helper, and the Merkle leaf
+// digests of the sub-chunks that run on it.  A device has kSlots of them: device-API calls on different
+// streams take different slots and run concurrently; the host-buffer pipeline deals its sub-chunks
+// round-robin over two slots.
 struct Slot {
-    DevBuf ws_hs, ws_tab, ws_R, ws_ok, ws_dig;
+    DevBuf ws_hs, ws_tab, ws_R, ws_ok, ws_dig, mdig;
     uint32_t ws_cap = 0;
     hipStream_t last = nullptr;   // the stream of the last launch group on this workspace
     hipEvent_t ev = nullptr;      // recorded after that group
     uint64_t stamp = 0;           // last use (least-recently-used choice)
     CvkSplit split;               // drain-overlap helper stream + events (created on first need)
     hipStream_t stream = nullptr; // the slot's own stream (slot 0: the device stream)
-    PinBuf pin_in;                // host-buffer staging of one (sub-)chunk: pk | sig | off | len | arena
+    PinBuf pin_in;                // small-path staging of one batch: pk | sig | off | len | arena
     DevBuf packed;                // its device copy
-    hipEvent_t h2d = nullptr;     // recorded after the last DMA out of pin_in
-    bool h2d_pending = false;
 };
 constexpr int kSlots = 4;
-constexpr int kRing = 6;   // input blocks of the host pipeline (more than slots: copies run ahead of kernels)
-constexpr int kOuts = 2;   // host pipeline calls in flight per device (cv_ed25519_verify_batch_async)
+constexpr int kPipeSlots = 2;   // compute slots the pipeline deals its sub-chunks over (see pipe_enqueue)
+constexpr int kRing = 6;        // input blocks of the host pipeline (more than slots: copies run ahead of kernels)
+constexpr int kOuts = 4;        // pipelined host calls in flight per device (async verify + Merkle calls)
 
-// The verdict output of one pipelined host call on one device: bitmap words | status bytes on the
-// device, their pinned host copy, and the event after that copy.  pending: enqueued, not yet copied
-// into the caller's arrays (pipe_finish does that); gen counts the calls that used this slot.
+// The output of one pipelined host call on one device: its results on the device (dout), the pinned
+// copy they come back through, and what pipe_finish copies where.  pending: enqueued, results not yet in
+// the caller's arrays; gen counts the calls that used this output.  mu serialises finishing it (cv_wait
+// runs without the device lock) against reusing it (under the device lock; order: device -> output).
 struct PipeOut {
+    std::mutex mu;
     DevBuf dout;
     PinBuf hout;
-    hipEvent_t done = nullptr;           // (unused since the host-side join; kept for cv_close)
-    hipEvent_t slot_done[kSlots] = {};   // after this call's last launch group on each slot stream
-    bool slot_used[kSlots] = {};
+    hipEvent_t slot_done[kPipeSlots] = {};   // after this call's last launch group on each slot stream
+    bool slot_used[kPipeSlots] = {};
     bool pending = false;
     uint64_t gen = 0;
-    uint64_t *bitmap = nullptr;
-    uint8_t *status = nullptr;
-    size_t b = 0, n = 0, o_st = 0;
+    struct Seg {
+        void *dst;
+        size_t off, len;
+    };
+    Seg seg[2] = {};
+    int nseg = 0;
+    // keyed calls: the call's distinct keys and their pool slots on the device (kdev: keys | slot_of_key,
+    // uploaded through kstage), the auto path's key_index (pinned, DMAed per sub-chunk)
+    DevBuf kdev;
+    PinBuf kstage, kidx;
 };
 
-// A fixed set of host threads for index-parallel jobs (the host-buffer path's packing and range scans):
-// run(ntasks, fn) calls fn(i) for every i in [0, ntasks) on the helpers and the calling thread and
-// returns when all are done.  Created once per device, so a pipelined call does not pay a thread start
-// per sub-chunk (round-3 probe: ~14 thread starts per sub-chunk held C5's host path at 11 GB/s).
+// A fixed set of host threads for index-parallel jobs (the host-buffer path's packing, range scans and key
+// dedupe): run(ntasks, fn) calls fn(i) for every i in [0, ntasks) on the helpers and the calling thread and
+// returns when all are done.  One per device, used under the device lock.
 class WorkerPool {
   public:
     explicit WorkerPool(int helpers) {
@@ -238,11 +250,58 @@ class WorkerPool {
     bool stop_ = false;
 };
 
+// One persistent thread per device that runs the shards other threads hand it (dispatch), in order.
+class DeviceWorker {
+  public:
+    DeviceWorker() : th_([this] { loop(); }) {}
+    ~DeviceWorker() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_one();
+        th_.join();
+    }
+    void post(std::function<void()> f) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            q_.push_back(std::move(f));
+        }
+        cv_.notify_one();
+    }
+
+  private:
+    void loop() {
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+                if (q_.empty()) return;   // stop requested and nothing left
+                f = std::move(q_.front());
+                q_.pop_front();
+            }
+            f();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+    bool stop_ = false;
+    std::thread th_;
+};
+
 struct Device {
     int ordinal = 0;
+    // mu: held for the whole of a synchronous shard and while an asynchronous one is enqueued; load: the
+    // shards in progress or queued on this device (routing); worker: runs shards handed over by dispatch
+    std::mutex mu;
+    std::atomic<int> load{0};
+    std::unique_ptr<DeviceWorker> worker;
+    std::mutex worker_mu;   // creation of the worker
     hipStream_t stream = nullptr;
     DevBuf pk, sig, arena, off, len, bitmap, status, seed, tx_begin, digest, ids;
-    PinBuf pin_out;                      // host-buffer verify outputs: bitmap | status
+    PinBuf pin_out;                      // small-path verify outputs: bitmap | status
     // zero-copy notary path (verify_shard_small_zc): fine-grained pinned host memory the kernels read
     // (packed records) and store into (verdict nibbles | status) over PCIe
     PinBuf zc_in, zc_out;
@@ -251,26 +310,32 @@ struct Device {
     uint64_t clock = 0;
     KeyCache kc;
     std::unique_ptr<WorkerPool> pool;    // host packing threads (created on the first large host batch)
-    // The host pipeline's input ring (verify_shard_pipe): sub-chunk j's records go into device block
-    // j % kRing by the ONE copy stream (so every H2D copy runs on one DMA queue, never as a blit kernel
-    // beside the verify kernels), packed first into pinned staging block j % kRing when the caller's
-    // arrays are pageable.  in_ready[q]: after block q's copies (copy stream); in_free[q]: after the
-    // verify that read it (its slot stream).
+    // The host pipeline's input ring: sub-chunk j's records go into device block j % kRing by the ONE copy
+    // stream (so every H2D copy runs on one DMA queue, never as a blit kernel beside the verify kernels),
+    // packed first into pinned staging block j % kRing when the caller's arrays are pageable.  in_ready[q]:
+    // after block q's copies (copy stream); in_free[q]: after the kernels that read it (its slot stream).
     hipStream_t copy = nullptr;
-    hipStream_t outs = nullptr;          // the pipeline's verdict copies (pipe_finish)
-    PipeOut out[kOuts];                  // the pipeline's verdict outputs, one per call in flight
+    hipStream_t outs = nullptr;          // the pipeline's result copies (pipe_finish)
+    PipeOut out[kOuts];
     int out_next = 0;
     DevBuf inblk[kRing];
     PinBuf instage[kRing];
     hipEvent_t in_ready[kRing] = {}, in_free[kRing] = {};
     bool in_used[kRing] = {}, stage_busy[kRing] = {};
-    int ring_next = 0;                   // the ring block the next sub-chunk takes
+    int ring_next = 0;
     WorkerPool &workers(int threads) {
         if (!pool || pool->threads() != threads) {
             pool.reset();
             pool.reset(new WorkerPool(threads - 1));
         }
         return *pool;
+    }
+    void post(std::function<void()> f) {
+        {
+            std::lock_guard<std::mutex> g(worker_mu);
+            if (!worker) worker.reset(new DeviceWorker());
+        }
+        worker->post(std::move(f));
     }
 };
 
@@ -281,55 +346,53 @@ constexpr size_t kKtabBytes = 16512 * 4;  // CV_KTAB_WORDS: 4 comb rows x 129 af
 constexpr size_t kTabBytes = 9 * 40 * 4;  // CV_TAB_WORDS: k*P, k = 0..8, cached form (cv_verify.h)
 // new keys' tables are computed in launches of at most this many keys (bounded keyprep scratch: 270 MB)
 constexpr size_t kKeyprepBatch = 4096;
-// cv_ed25519_verify_batch dedupes keys on the host up to this batch size, and takes the keyed
-// (per-key comb) path when the batch has at least eight signatures per distinct key on average (a key's
-// 66 KB of tables cost about as much as 7 plain verifies to build; cached keys cost nothing)
-constexpr size_t kAutoKeyedMax = 1u << 18;
 
 // Verify workspace capacity: batches above it run in chunks of this many signatures (~13.4 GB of
 // workspace at 2^22; same-box A/B at 8M signatures: 2^21 73.2, 2^22 72.4, 2^23 72.4 ms -- fewer
 // chunk tails to drain; whole-round chunks of 1,966,080 were slower, 73.4 ms).
 constexpr uint32_t kVerifyChunk = 1u << 22;
 
-// Host-buffer pipeline (verify_shard_pipe): shards above g_pipe_min signatures are cut into a first
-// sub-chunk of g_pipe_first (short, so the GPU starts early) and then sub-chunks of g_pipe_chunk (the
-// last two balanced), dealt round-robin over the device's slots; g_pack_threads host threads pack each
-// sub-chunk into pinned staging while the earlier ones transfer and verify.
-static size_t g_pipe_min = 131072, g_pipe_first = 32768, g_pipe_chunk = 262144;
-static int g_pack_threads = 8;
-// small-form batches of at least this many signatures pack their staging on the device's worker pool
-static size_t g_small_pool_min = 16384;
-// compute slots the pipeline deals its sub-chunks over (2..kSlots).  2: with GPU_MAX_HW_QUEUES = 4
-// (HIP's default) the null stream, the device stream, one more slot stream and the copy stream each get
-// a hardware queue; a third slot stream shares one — with the copy stream, whose copies then waited
-// behind that slot's Straus kernel (2.4 ms stalls, profiles/r03e_timeline_pinned_nofill.txt)
-static int g_pipe_slots = 2;
-static int g_pipe_ramp = 1;    // sub-chunk sizes double from g_pipe_first up to g_pipe_chunk
-static size_t g_async_chunk = 262144;   // sub-chunks of cv_ed25519_verify_batch_async (no ramp)
-// host-side time of the pipelined path, seconds (cvk_pipe_stats): range scans, packing, waits for a
-// slot's staging, enqueue (HIP calls), the final synchronisation; and calls / sub-chunks
-struct PipeStats {
-    double plan = 0, pack = 0, wait = 0, enq = 0, sync = 0;
-    uint64_t calls = 0, chunks = 0, direct = 0;
+// ---------------------------------------------------------------- options (cv_set_option)
+struct OptDesc {
+    int64_t def, lo, hi;
 };
-// 1 = pinned caller arrays are DMAed in place (stage_direct); 0 = always pack (A/B knob)
-static int g_direct_dma = 1;
-static size_t g_direct_small_min = 16384;   // the small path's direct-DMA threshold (signatures)
-// 1 = cv_open creates the host pipeline's streams (slot 1, copy, verdict copy) right after the device
-// stream; 0 = on first use (A/B knob, read by cv_open)
-static int g_eager_streams = 1;
-// tri-form batches from host buffers: 0 = DMA in / copy out (verify_shard_small), 1 = zero-copy (the prep
-// reads the pinned staging over PCIe, verdicts stored into pinned host memory), 2 = zero-copy out with a
-// gather kernel moving the staging into device memory first (verify_shard_small_zc), 3 = auto: 2 from
-// 2,048 signatures, 1 below (same-box A/B, profiles/r03p_notary_zc_gather_ab.log: 4,096 0.289 ms p50 with
-// the gather against 0.291-0.298 without; 256 0.251 against 0.249)
-static int g_small_zc = 3;
-// host-side time of the zero-copy path, seconds (cvk_small_stats): range scan + setup (buffers,
-// workspace), packing, launches, the synchronisation (≈ the kernels), the bitmap assembly; and calls
-static double g_small_t[5];
-static uint64_t g_small_calls;
-static PipeStats g_pipe_stats;
-static std::mutex g_pipe_stats_mu;
+static const OptDesc kOpt[CV_OPT_COUNT] = {
+    {0, 0, 0},                          // (unused: options start at 1)
+    {4096, 0, 1 << 20},                 // CV_OPT_TRI_MAX
+    {32768, 0, 1 << 22},                // CV_OPT_QUAD_MAX
+    {1, 0, 2},                          // CV_OPT_DRAIN_SPLIT
+    {10, 5, 50},                        // CV_OPT_DRAIN_SPLIT_PCT
+    {131072, 64, (int64_t)1 << 40},     // CV_OPT_PIPE_MIN
+    {32768, 64, 1 << 24},               // CV_OPT_PIPE_FIRST
+    {262144, 64, 1 << 24},              // CV_OPT_PIPE_CHUNK
+    {262144, 64, 1 << 24},              // CV_OPT_ASYNC_CHUNK
+    {8, 1, 64},                         // CV_OPT_HOST_THREADS
+    {3, 0, 3},                          // CV_OPT_SMALL_ZERO_COPY
+    {16384, 1, (int64_t)1 << 40},       // CV_OPT_SMALL_DIRECT_MIN
+    {1, 0, 1},                          // CV_OPT_AUTO_KEYED
+    {4096, 64, (int64_t)1 << 40},       // CV_OPT_SHARD_MIN
+    {262144, 64, (int64_t)1 << 40},     // CV_OPT_SPREAD_MIN
+    {262144, 1, 1 << 24},               // CV_OPT_MERKLE_CHUNK
+};
+
+// A snapshot of a context's options, taken once per call.
+struct Opts {
+    CvkPlan plan;
+    size_t pipe_min, pipe_first, pipe_chunk, async_chunk, small_direct_min, shard_min, spread_min, merkle_chunk;
+    int threads, small_zc, auto_keyed;
+};
+
+// host-side time of the pipelined path (cv_diag_stats CV_STATS_PIPE), of the zero-copy small path
+// (CV_STATS_SMALL) and the routing counters (CV_STATS_ROUTE)
+struct Stats {
+    double pipe[5] = {};   // plan, pack, wait, enqueue, sync (seconds)
+    uint64_t pipe_calls = 0, pipe_chunks = 0, pipe_direct = 0;
+    double small[5] = {};  // plan + setup, pack, launch, sync, assemble
+    uint64_t small_calls = 0;
+    uint64_t calls = 0, routed_whole = 0, split_calls = 0, shards = 0, keyed_calls = 0, keyed_chunks = 0,
+             merkle_calls = 0, merkle_chunks = 0;
+};
+
 static inline double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -337,7 +400,6 @@ static inline double now_s() {
 hipError_t slot_events(Slot &sl) {
     hipError_t e = hipSuccess;
     if (!sl.ev && (e = hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming)) != hipSuccess) return e;
-    if (!sl.h2d && (e = hipEventCreateWithFlags(&sl.h2d, hipEventDisableTiming)) != hipSuccess) return e;
     return e;
 }
 
@@ -365,11 +427,10 @@ hipError_t slot_split(Device &d, Slot &sl) {
     CvkSplit x;
     hipError_t e = hipDeviceGetAttribute(&x.cus, hipDeviceAttributeMultiprocessorCount, d.ordinal);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&x.start, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&x.prep1, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&x.done2, hipEventDisableTiming);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&x.s2, hipStreamNonBlocking);
     if (e != hipSuccess) {
-        for (hipEvent_t v : {x.start, x.prep1, x.done2})
+        for (hipEvent_t v : {x.start, x.done2})
             if (v) (void)hipEventDestroy(v);
         return e;
     }
@@ -411,7 +472,7 @@ hipError_t ensure_verify_ws(Slot &sl, size_t n) {
 // a launch group enqueued on stream s first waits for the previous group when that ran on another
 // stream (ws_begin), and marks its own end (ws_end).  Device-pointer calls may therefore be made on any
 // streams; two streams that hold different slots run concurrently, and a stream that takes over a slot
-// waits for it instead of racing on it.  Callers hold ctx->mu around ws_begin .. ws_end.
+// waits for it instead of racing on it.  Callers hold the device lock around ws_begin .. ws_end.
 hipError_t ws_begin(Device &d, Slot &sl, hipStream_t s) {
     hipError_t e = slot_events(sl);
     if (e != hipSuccess) return e;
@@ -435,16 +496,15 @@ hipError_t pool_end(KeyCache &kc, hipStream_t s) {
 }
 
 // One verify launch group on slot sl, stream s.  split: the drain-overlap sub-chunks may be used.
-hipError_t launch_verify(Device &d, Slot &sl, uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
-                         const uint64_t *off, const uint32_t *len, uint64_t *bitmap, uint8_t *status, hipStream_t s,
-                         hipEvent_t *ev, bool split) {
+hipError_t launch_verify(Device &d, const CvkPlan &plan, Slot &sl, uint32_t n, const uint8_t *pk, const uint8_t *sig,
+                         const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
+                         uint8_t *status, hipStream_t s, hipEvent_t *ev, bool split) {
     hipError_t e = ensure_verify_ws(sl, n);
     if (e == hipSuccess) e = ws_begin(d, sl, s);
     if (e != hipSuccess) return e;
-    if (split && n >= 131072) (void)slot_split(d, sl);   // without a helper the chunk runs whole
-    e = cvk_verify(n, pk, sig, arena, off, len, bitmap, status, sl.ws_hs.as<uint32_t>(), sl.ws_tab.as<uint32_t>(),
-                   sl.ws_R.as<uint32_t>(), sl.ws_ok.as<uint8_t>(), sl.ws_dig.as<uint32_t>(), sl.ws_cap, s, ev,
-                   split && sl.split.s2 ? &sl.split : nullptr);
+    if (split && plan.split && n >= 131072) (void)slot_split(d, sl);   // without a helper the chunk runs whole
+    e = cvk_verify(&plan, n, pk, sig, arena, off, len, bitmap, status, sl.ws_tab.as<uint32_t>(), sl.ws_ok.as<uint8_t>(),
+                   sl.ws_dig.as<uint32_t>(), sl.ws_cap, s, ev, split && sl.split.s2 ? &sl.split : nullptr);
     const hipError_t e2 = ws_end(sl, s);
     return e != hipSuccess ? e : e2;
 }
@@ -475,17 +535,43 @@ template <class F> OnExit<F> on_exit(F fn) { return OnExit<F>{fn}; }
 }  // namespace
 
 struct cv_ctx {
-    std::vector<Device> devs;
-    std::mutex mu;
-    uint32_t key_cap = kDefaultKeyCap;
-    // cv_ed25519_verify_batch_async: ticket -> (device index, output slot, that slot's gen) per shard
+    std::vector<std::unique_ptr<Device>> devs;
+    std::atomic<int64_t> opt[CV_OPT_COUNT];
+    std::atomic<uint32_t> key_cap{kDefaultKeyCap};
+    std::atomic<uint32_t> rr{0};            // routing: where the search for the least loaded device starts
+    // asynchronous calls: ticket -> (device index, output index, that output's gen) per shard
+    std::mutex tk_mu;
     uint64_t next_ticket = 0;
     std::unordered_map<uint64_t, std::vector<std::array<uint64_t, 3>>> tickets;
+    std::mutex st_mu;
+    Stats stats;
+    cv_ctx() {
+        for (int k = 0; k < CV_OPT_COUNT; k++) opt[k].store(kOpt[k].def);
+    }
+    Opts opts() const {
+        Opts o;
+        o.plan.tri_max = (uint32_t)opt[CV_OPT_TRI_MAX].load();
+        o.plan.quad_max = (uint32_t)opt[CV_OPT_QUAD_MAX].load();
+        o.plan.split = (int)opt[CV_OPT_DRAIN_SPLIT].load();
+        o.plan.split_pct = (int)opt[CV_OPT_DRAIN_SPLIT_PCT].load();
+        o.pipe_min = (size_t)opt[CV_OPT_PIPE_MIN].load();
+        o.pipe_first = (size_t)opt[CV_OPT_PIPE_FIRST].load() / 64 * 64;
+        o.pipe_chunk = (size_t)opt[CV_OPT_PIPE_CHUNK].load() / 64 * 64;
+        o.async_chunk = (size_t)opt[CV_OPT_ASYNC_CHUNK].load() / 64 * 64;
+        o.threads = (int)opt[CV_OPT_HOST_THREADS].load();
+        o.small_zc = (int)opt[CV_OPT_SMALL_ZERO_COPY].load();
+        o.small_direct_min = (size_t)opt[CV_OPT_SMALL_DIRECT_MIN].load();
+        o.auto_keyed = (int)opt[CV_OPT_AUTO_KEYED].load();
+        o.shard_min = (size_t)opt[CV_OPT_SHARD_MIN].load();
+        o.spread_min = (size_t)opt[CV_OPT_SPREAD_MIN].load();
+        o.merkle_chunk = (size_t)opt[CV_OPT_MERKLE_CHUNK].load();
+        return o;
+    }
 };
 
 extern "C" {
 
-const char *cv_version(void) { return "cordaverify-mi355x 0.2 (gfx950)"; }
+const char *cv_version(void) { return "cordaverify-mi355x 0.3 (gfx950)"; }
 
 const char *cv_strerror(int code) {
     switch (code) {
@@ -499,58 +585,13 @@ const char *cv_strerror(int code) {
     }
 }
 
-// Test knob (internal, not in the header): every device of the next cv_open appears k times in the
-// context — k independent Device slots (own stream, buffers, workspace, key pool) on one GPU — so the
-// multi-device host path (for_each_shard: one thread per slot, 64-aligned shard ranges, per-slot
-// dedupe and key pools) runs and is tested on a one-GPU box.  0 / 1 = off.
-static int g_virtual_devices = 1;
-void cvk_set_virtual_devices(int k) { g_virtual_devices = (k >= 1 && k <= 16) ? k : 1; }
+// Test hook (internal, not in the header): every device of the next cv_open appears k times in the
+// context — k independent Device slots (own lock, worker, stream, buffers, workspace, key pool) on one
+// GPU — so the multi-device host path (routing, shards, per-device dedupe and key pools) runs and is
+// tested on a one-GPU box.  0 / 1 = off.
+static std::atomic<int> g_virtual_devices{1};
+void cvk_set_virtual_devices(int k) { g_virtual_devices.store((k >= 1 && k <= 16) ? k : 1); }
 
-// Tuning knob (internal): the host-buffer pipeline's shard threshold, first and steady sub-chunk sizes
-// (signatures; 0 keeps the current value) and packing threads.
-void cvk_set_direct_dma(int v) { g_direct_dma = v ? 1 : 0; }
-void cvk_set_direct_small_min(int n) { g_direct_small_min = n > 0 ? (size_t)n : 16384; }
-void cvk_set_small_zc(int v) { g_small_zc = (v >= 0 && v <= 3) ? v : 3; }
-void cvk_set_eager_streams(int v) { g_eager_streams = v ? 1 : 0; }
-// out[6] = plan+setup, pack, launch, sync, assemble (seconds, summed) and calls; reset clears them
-void cvk_small_stats(double *out, int reset) {
-    std::lock_guard<std::mutex> g(g_pipe_stats_mu);
-    if (out) {
-        for (int k = 0; k < 5; k++) out[k] = g_small_t[k];
-        out[5] = (double)g_small_calls;
-    }
-    if (reset) {
-        for (double &t : g_small_t) t = 0;
-        g_small_calls = 0;
-    }
-}
-void cvk_set_small_pool_min(int n) { g_small_pool_min = n > 0 ? (size_t)n : 16384; }
-void cvk_set_pipe_slots(int k) { g_pipe_slots = (k >= 2 && k <= kSlots) ? k : 2; }
-void cvk_set_pipe_ramp(int v) { g_pipe_ramp = v ? 1 : 0; }
-void cvk_set_async_chunk(int m) { g_async_chunk = m >= 64 ? (size_t)m / 64 * 64 : 262144; }
-void cvk_set_pipe(size_t min_n, size_t first, size_t chunk, int threads) {
-    if (min_n) g_pipe_min = min_n;
-    if (first) g_pipe_first = std::max<size_t>(64, first / 64 * 64);
-    if (chunk) g_pipe_chunk = std::max<size_t>(64, chunk / 64 * 64);
-    if (threads > 0) g_pack_threads = std::min(threads, 64);
-}
-
-// Diagnostic knob: out[7] = {plan, pack, wait, enqueue, sync seconds, calls, sub-chunks} of the
-// pipelined host path since the last reset.
-void cvk_pipe_stats(double *out, int reset) {
-    std::lock_guard<std::mutex> g(g_pipe_stats_mu);
-    const PipeStats &p = g_pipe_stats;
-    if (out) {
-        out[0] = p.plan;
-        out[1] = p.pack;
-        out[2] = p.wait;
-        out[3] = p.enq;
-        out[4] = p.sync;
-        out[5] = (double)p.calls;
-        out[6] = (double)p.chunks;
-    }
-    if (reset) g_pipe_stats = PipeStats{};
-}
 // max(off[i] + len[i]) over n records (0 for n = 0): the arena bytes a batch reaches, for the Python
 // mirror's bounds check; slices of 2^20 records on up to 8 threads.
 uint64_t cvk_msg_end(size_t n, const uint64_t *off, const uint32_t *len) {
@@ -578,10 +619,58 @@ uint64_t cvk_msg_end(size_t n, const uint64_t *off, const uint32_t *len) {
     }
     return *std::max_element(part.begin(), part.end());
 }
-// sub-chunks of the pipelined path that were DMAed straight from pinned caller arrays (since the last reset)
-double cvk_pipe_direct_chunks(void) {
-    std::lock_guard<std::mutex> g(g_pipe_stats_mu);
-    return (double)g_pipe_stats.direct;
+
+int cv_set_option(cv_ctx *ctx, int option, int64_t value) {
+    if (!ctx || option <= 0 || option >= CV_OPT_COUNT) return CV_E_ARGS;
+    if (value < kOpt[option].lo || value > kOpt[option].hi) return CV_E_ARGS;
+    ctx->opt[option].store(value);
+    return CV_OK;
+}
+
+int cv_get_option(cv_ctx *ctx, int option, int64_t *value) {
+    if (!ctx || !value || option <= 0 || option >= CV_OPT_COUNT) return CV_E_ARGS;
+    *value = ctx->opt[option].load();
+    return CV_OK;
+}
+
+int cv_diag_stats(cv_ctx *ctx, int which, double *out, size_t nout, int reset) {
+    if (!ctx || (nout && !out)) return CV_E_ARGS;
+    std::lock_guard<std::mutex> g(ctx->st_mu);
+    Stats &s = ctx->stats;
+    double v[8] = {};
+    size_t nv = 0;
+    if (which == CV_STATS_PIPE) {
+        for (int k = 0; k < 5; k++) v[k] = s.pipe[k];
+        v[5] = (double)s.pipe_calls;
+        v[6] = (double)s.pipe_chunks;
+        v[7] = (double)s.pipe_direct;
+        nv = 8;
+    } else if (which == CV_STATS_SMALL) {
+        for (int k = 0; k < 5; k++) v[k] = s.small[k];
+        v[5] = (double)s.small_calls;
+        nv = 6;
+    } else if (which == CV_STATS_ROUTE) {
+        const uint64_t r[8] = {s.calls, s.routed_whole, s.split_calls, s.shards, s.keyed_calls, s.keyed_chunks,
+                               s.merkle_calls, s.merkle_chunks};
+        for (int k = 0; k < 8; k++) v[k] = (double)r[k];
+        nv = 8;
+    } else {
+        return CV_E_ARGS;
+    }
+    for (size_t k = 0; k < nout && k < nv; k++) out[k] = v[k];
+    if (reset) {
+        if (which == CV_STATS_PIPE) {
+            std::fill(s.pipe, s.pipe + 5, 0.0);
+            s.pipe_calls = s.pipe_chunks = s.pipe_direct = 0;
+        } else if (which == CV_STATS_SMALL) {
+            std::fill(s.small, s.small + 5, 0.0);
+            s.small_calls = 0;
+        } else {
+            s.calls = s.routed_whole = s.split_calls = s.shards = s.keyed_calls = s.keyed_chunks = s.merkle_calls =
+                s.merkle_chunks = 0;
+        }
+    }
+    return (int)nv;
 }
 
 int cv_open(uint32_t device_mask, cv_ctx **out) {
@@ -591,36 +680,29 @@ int cv_open(uint32_t device_mask, cv_ctx **out) {
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return CV_E_NO_DEVICE;
     cv_ctx *ctx = new (std::nothrow) cv_ctx();
     if (!ctx) return CV_E_OOM;
+    const int virt = g_virtual_devices.load();
     for (int d = 0; d < count && d < 32; d++) {
         if (device_mask && !(device_mask & (1u << d))) continue;
-        for (int v = 0; v < g_virtual_devices; v++) {
-            Device dev;
-            dev.ordinal = d;
-            if (hipSetDevice(d) != hipSuccess ||
-                hipStreamCreateWithFlags(&dev.stream, hipStreamNonBlocking) != hipSuccess) {
+        for (int v = 0; v < virt; v++) {
+            ctx->devs.emplace_back(new Device());
+            Device &dd = *ctx->devs.back();
+            dd.ordinal = d;
+            // The host pipeline's concurrently busy streams — slot 0 (the device stream), slot 1, the copy
+            // stream and the result-copy stream — are created back to back here, before any helper stream,
+            // so the runtime spreads them over distinct hardware queues (GPU_MAX_HW_QUEUES = 4 by default).
+            // Created lazily, after the device API's split helpers or a caller's own streams, the copy
+            // stream could share a queue with a compute stream and its copies wait behind that stream's
+            // kernels (C5 host path 86-90 -> 75 ms, profiles/r03p_c5host_eager_streams_ab.log).
+            hipStream_t s1 = nullptr;
+            if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&dd.stream, hipStreamNonBlocking) != hipSuccess ||
+                slot_stream(dd, 1, &s1) != hipSuccess || hipStreamCreateWithFlags(&dd.copy, hipStreamNonBlocking) != hipSuccess ||
+                hipStreamCreateWithFlags(&dd.outs, hipStreamNonBlocking) != hipSuccess) {
                 cv_close(ctx);
                 return CV_E_HIP;
             }
-            ctx->devs.push_back(std::move(dev));
-            // The host pipeline's concurrently busy streams — slot 0 (the device stream), slot 1, the copy
-            // stream and the verdict-copy stream — are created back to back here, before any helper
-            // stream, so the runtime spreads them over distinct hardware queues (GPU_MAX_HW_QUEUES = 4 by
-            // default).  Created lazily, after the device API's split helpers or a caller's own streams,
-            // the copy stream could share a queue with a compute stream and its copies wait behind that
-            // stream's kernels.
-            if (g_eager_streams) {
-                Device &dd = ctx->devs.back();
-                hipStream_t s1 = nullptr;
-                if (slot_stream(dd, 1, &s1) != hipSuccess ||
-                    hipStreamCreateWithFlags(&dd.copy, hipStreamNonBlocking) != hipSuccess ||
-                    hipStreamCreateWithFlags(&dd.outs, hipStreamNonBlocking) != hipSuccess) {
-                    cv_close(ctx);
-                    return CV_E_HIP;
-                }
-            }
             // Per-device basepoint rows (16.8 MB, built once per process): eager, so the first
             // verify is not charged for them and no later call synchronises to build them.
-            if (v == 0 && cvk_prepare(dev.stream) != hipSuccess) {
+            if (v == 0 && cvk_prepare(dd.stream) != hipSuccess) {
                 cv_close(ctx);
                 return CV_E_HIP;
             }
@@ -636,21 +718,23 @@ int cv_open(uint32_t device_mask, cv_ctx **out) {
 
 void cv_close(cv_ctx *ctx) {
     if (!ctx) return;
-    for (Device &d : ctx->devs) {
+    for (auto &dp : ctx->devs) {
+        Device &d = *dp;
+        d.worker.reset();   // joins the worker (its queue is empty: every call returned before close)
         (void)hipSetDevice(d.ordinal);
         (void)hipDeviceSynchronize();
         for (DevBuf *b : {&d.pk, &d.sig, &d.arena, &d.off, &d.len, &d.bitmap, &d.status, &d.seed, &d.tx_begin,
                           &d.digest, &d.ids, &d.pmt, &d.kc.ktab, &d.kc.kok, &d.kc.keys, &d.kc.slots,
-                          &d.kc.slot_of_key, &d.kc.key_index, &d.kc.scratch})
+                          &d.kc.slot_of_key, &d.kc.scratch})
             b->release();
         d.pin_out.release();
         d.zc_in.release();
         d.zc_out.release();
         for (int k = 0; k < kSlots; k++) {
             Slot &sl = d.slot[k];
-            for (DevBuf *b : {&sl.ws_hs, &sl.ws_tab, &sl.ws_R, &sl.ws_ok, &sl.ws_dig, &sl.packed}) b->release();
+            for (DevBuf *b : {&sl.ws_hs, &sl.ws_tab, &sl.ws_R, &sl.ws_ok, &sl.ws_dig, &sl.mdig, &sl.packed}) b->release();
             sl.pin_in.release();
-            for (hipEvent_t v : {sl.ev, sl.h2d, sl.split.start, sl.split.prep1, sl.split.done2})
+            for (hipEvent_t v : {sl.ev, sl.split.start, sl.split.done2})
                 if (v) (void)hipEventDestroy(v);
             if (sl.split.s2) (void)hipStreamDestroy(sl.split.s2);
             if (k > 0 && sl.stream) (void)hipStreamDestroy(sl.stream);
@@ -658,7 +742,9 @@ void cv_close(cv_ctx *ctx) {
         for (PipeOut &o : d.out) {
             o.dout.release();
             o.hout.release();
-            if (o.done) (void)hipEventDestroy(o.done);
+            o.kdev.release();
+            o.kstage.release();
+            o.kidx.release();
             for (hipEvent_t v : o.slot_done)
                 if (v) (void)hipEventDestroy(v);
         }
@@ -671,9 +757,10 @@ void cv_close(cv_ctx *ctx) {
         }
         if (d.copy) (void)hipStreamDestroy(d.copy);
         d.kc.pin.release();
-        if (d.kc.ev) (void)hipEventDestroy(d.kc.ev);
-        if (d.kc.pin_ev) (void)hipEventDestroy(d.kc.pin_ev);
+        for (hipEvent_t v : {d.kc.ev, d.kc.pin_ev, d.kc.kp_ev})
+            if (v) (void)hipEventDestroy(v);
         if (d.stream) (void)hipStreamDestroy(d.stream);
+        d.pool.reset();
     }
     delete ctx;
 }
@@ -683,7 +770,7 @@ int cv_device_count(const cv_ctx *ctx) { return ctx ? (int)ctx->devs.size() : 0;
 int cv_host_alloc(cv_ctx *ctx, size_t bytes, void **out) {
     if (!ctx || !out || bytes == 0) return CV_E_ARGS;
     *out = nullptr;
-    CV_TRY(hipSetDevice(ctx->devs[0].ordinal));
+    CV_TRY(hipSetDevice(ctx->devs[0]->ordinal));
     void *p = nullptr;
     const hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
     if (e != hipSuccess) return e == hipErrorOutOfMemory ? CV_E_OOM : CV_E_HIP;
@@ -697,14 +784,104 @@ void cv_host_free(cv_ctx *ctx, void *p) {
 }
 
 static Device *find_dev(cv_ctx *ctx, int device) {
-    for (Device &d : ctx->devs)
-        if (d.ordinal == device) return &d;
+    for (auto &d : ctx->devs)
+        if (d->ordinal == device) return d.get();
     return nullptr;
 }
 
 }  // extern "C"
 
-// ---------------------------------------------------------------- verify (host buffers)
+// ---------------------------------------------------------------- routing (dispatch)
+// Runs fn(device, b, e, packing threads) over shards of [0, n) and returns the first error.  The shard
+// plan (DESIGN.md "Routing"):
+//   - one device, or n <= shard_min: the whole batch on ONE device — the least loaded (shards in progress
+//     or queued on it), ties broken by a rotating start, so concurrent notary batches land on different
+//     GPUs instead of each being cut eight ways (a shard below the tri-chain size costs the kernel
+//     chain's floor, ~0.22 ms, whatever its size);
+//   - n >= spread_min: contiguous shards over ALL devices (a throughput batch);
+//   - between: over the devices idle at submission, at most ceil(n / shard_min) of them, at least one
+//     (the least loaded) — a lone caller's mid-size batch spreads, a loaded node's does not.
+// Shard starts are multiples of `align` (64 for verify: whole bitmap words).  The caller's thread runs
+// the first shard; the others go to their devices' workers.  A shard runs under its device's lock;
+// nothing holds a lock while waiting for another, so concurrent calls cannot deadlock.
+template <class F>
+static int dispatch(cv_ctx *ctx, const Opts &o, size_t n, size_t align, F fn) {
+    const size_t ndev = ctx->devs.size();
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int threads = (int)std::max<size_t>(1, std::min<size_t>((size_t)o.threads, std::max<size_t>(1, hw / ndev)));
+    std::vector<size_t> pick;
+    const uint32_t start = ctx->rr.fetch_add(1);
+    if (ndev == 1) {
+        pick.push_back(0);
+    } else if (n >= o.spread_min) {
+        for (size_t k = 0; k < ndev; k++) pick.push_back(k);
+    } else {
+        const size_t kmax = n <= o.shard_min ? 1 : (n + o.shard_min - 1) / o.shard_min;
+        for (size_t j = 0; j < ndev && pick.size() < kmax; j++) {
+            const size_t k = (start + j) % ndev;
+            if (ctx->devs[k]->load.load() == 0) pick.push_back(k);
+        }
+        if (pick.empty()) {
+            size_t best = start % ndev;
+            for (size_t j = 0; j < ndev; j++) {
+                const size_t k = (start + j) % ndev;
+                if (ctx->devs[k]->load.load() < ctx->devs[best]->load.load()) best = k;
+            }
+            pick.push_back(best);
+        }
+    }
+    const size_t ns = pick.size();
+    size_t per = (n + ns - 1) / ns;
+    per = (per + align - 1) / align * align;
+    struct ShardPart {
+        size_t dev, b, e;
+    };
+    std::vector<ShardPart> parts;
+    for (size_t j = 0; j < ns; j++) {
+        const size_t b = std::min(n, j * per), e = std::min(n, b + per);
+        if (b < e || j == 0) parts.push_back({pick[j], b, e});
+    }
+    {
+        std::lock_guard<std::mutex> g(ctx->st_mu);
+        ctx->stats.calls++;
+        ctx->stats.shards += parts.size();
+        if (parts.size() == 1) ctx->stats.routed_whole++;
+        else ctx->stats.split_calls++;
+    }
+    for (const ShardPart &p : parts) ctx->devs[p.dev]->load.fetch_add(1);
+    std::vector<int> rc(parts.size(), CV_OK);
+    auto run = [&](size_t j) {
+        Device &d = *ctx->devs[parts[j].dev];
+        {
+            std::lock_guard<std::mutex> g(d.mu);
+            rc[j] = fn(d, parts[j].b, parts[j].e, threads);
+        }
+        d.load.fetch_sub(1);
+    };
+    if (parts.size() == 1) {
+        run(0);
+        return rc[0];
+    }
+    std::mutex m;
+    std::condition_variable cv;
+    size_t left = parts.size() - 1;
+    for (size_t j = 1; j < parts.size(); j++)
+        ctx->devs[parts[j].dev]->post([&, j] {
+            run(j);
+            std::lock_guard<std::mutex> g(m);
+            if (--left == 0) cv.notify_one();
+        });
+    run(0);
+    {
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [&] { return left == 0; });
+    }
+    for (int r : rc)
+        if (r != CV_OK) return r;
+    return CV_OK;
+}
+
+// ---------------------------------------------------------------- host staging
 static inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 // Host copies into pinned staging.  A large copy is done by the device's worker pool (one core copies
@@ -733,28 +910,17 @@ static void par_copy(const std::vector<CopyJob> &jobs, WorkerPool *pool) {
     pool->run(pieces.size(), [&pieces](size_t k) { std::memcpy(pieces[k].dst, pieces[k].src, pieces[k].len); });
 }
 
-// Staging layout of records [b, e): pk | sig | off | len | arena, 16-B aligned parts.  The arena part is
-// the byte range [lo, hi) the records' messages span, with lo rounded down to 16 so the device arena
-// pointer keeps every message's alignment; the kernels get arena_dev - lo and the caller's offsets
-// unchanged.  When the messages are scattered (the range is more than twice their bytes + 1 MB), they
-// are gathered back to back instead and the offsets rewritten ("compact").
-struct Stage {
-    size_t n = 0, o_pk = 0, o_sig = 0, o_off = 0, o_len = 0, o_ar = 0, total = 0;
-    uint64_t lo = 0, hi = 0;
-    bool compact = false;
+// The byte range [lo, hi) of records [b, e) in an arena (min offset, max end) and their total bytes; the
+// scan runs in slices of 64K records over the pool.
+struct Span {
+    uint64_t lo = UINT64_MAX, hi = 0, bytes = 0;
 };
-static Stage stage_plan(size_t b, size_t e, const uint64_t *off, const uint32_t *len, WorkerPool *pool = nullptr) {
-    Stage st;
-    st.n = e - b;
-    // the range scan, in slices of 64K records over the pool
+static Span arena_span(size_t b, size_t e, const uint64_t *off, const uint32_t *len, WorkerPool *pool) {
     constexpr size_t kSlice = 65536;
-    const size_t nslices = (st.n + kSlice - 1) / kSlice;
-    struct R {
-        uint64_t lo = UINT64_MAX, hi = 0, bytes = 0;
-    };
-    std::vector<R> part(std::max<size_t>(nslices, 1));
+    const size_t nslices = (e - b + kSlice - 1) / kSlice;
+    std::vector<Span> part(std::max<size_t>(nslices, 1));
     auto scan = [&](size_t k) {
-        R r;
+        Span r;
         const size_t i1 = std::min(e, b + (k + 1) * kSlice);
         for (size_t i = b + k * kSlice; i < i1; i++) {
             r.lo = std::min<uint64_t>(r.lo, off[i]);
@@ -767,33 +933,58 @@ static Stage stage_plan(size_t b, size_t e, const uint64_t *off, const uint32_t 
         pool->run(nslices, scan);
     else
         for (size_t k = 0; k < nslices; k++) scan(k);
-    uint64_t lo = UINT64_MAX, hi = 0, bytes = 0;
-    for (const R &r : part) {
-        lo = std::min(lo, r.lo);
-        hi = std::max(hi, r.hi);
-        bytes += r.bytes;
+    Span s;
+    for (const Span &r : part) {
+        s.lo = std::min(s.lo, r.lo);
+        s.hi = std::max(s.hi, r.hi);
+        s.bytes += r.bytes;
     }
-    if (hi < lo) lo = hi = 0;
-    lo &= ~(uint64_t)15;
-    st.compact = hi - lo > 2 * bytes + (1u << 20);
+    if (s.hi < s.lo) s.lo = s.hi = 0;
+    return s;
+}
+
+// Staging layout of signature records [b, e): pk | kidx | sig | off | len | arena, 16-B aligned parts (pk
+// absent in keyed staging, kidx present only there).  The arena part is the byte range [lo, hi) the records'
+// messages span, with lo rounded down to 16 so the device arena pointer keeps every message's alignment;
+// the kernels get arena_dev - lo and the caller's offsets unchanged.  When the messages are scattered (the
+// range is more than twice their bytes + 1 MB), they are gathered back to back instead and the offsets
+// rewritten ("compact").
+struct Stage {
+    size_t n = 0, o_pk = 0, o_kidx = 0, o_sig = 0, o_off = 0, o_len = 0, o_ar = 0, total = 0;
+    uint64_t lo = 0, hi = 0;
+    bool compact = false, keyed = false;
+};
+static Stage stage_plan(size_t b, size_t e, const uint64_t *off, const uint32_t *len, WorkerPool *pool = nullptr,
+                        bool keyed = false) {
+    Stage st;
+    st.n = e - b;
+    st.keyed = keyed;
+    const Span sp = arena_span(b, e, off, len, pool);
+    const uint64_t lo = sp.lo & ~(uint64_t)15;
+    st.compact = sp.hi - lo > 2 * sp.bytes + (1u << 20);
     st.lo = st.compact ? 0 : lo;
-    st.hi = st.compact ? bytes : hi;
+    st.hi = st.compact ? sp.bytes : sp.hi;
     const size_t n = st.n;
     st.o_pk = 0;
-    st.o_sig = al16(n * 32);
+    st.o_kidx = keyed ? 0 : al16(n * 32);
+    st.o_sig = st.o_kidx + (keyed ? al16(n * 4) : 0);
     st.o_off = st.o_sig + al16(n * 64);
     st.o_len = st.o_off + al16(n * 8);
     st.o_ar = st.o_len + al16(n * 4);
     st.total = st.o_ar + al16(st.hi - st.lo + 16);
     return st;
 }
-// Packs records [b, e) into h by the plan (keys + signatures first: `first_part` runs after them, so
-// their DMA can start while the rest is packed).
+// Packs records [b, e) into h by the plan (keys / key indices + signatures first: `first_part` runs after
+// them, so their DMA can start while the rest is packed).
 template <class F>
-static void stage_pack(const Stage &st, uint8_t *h, size_t b, const uint8_t *pk, const uint8_t *sig,
-                       const uint8_t *arena, const uint64_t *off, const uint32_t *len, WorkerPool *pool, F first_part) {
+static void stage_pack(const Stage &st, uint8_t *h, size_t b, const uint8_t *pk, const uint32_t *kidx,
+                       const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                       WorkerPool *pool, F first_part) {
     const size_t n = st.n;
-    par_copy({{h + st.o_pk, pk + b * 32, n * 32}, {h + st.o_sig, sig + b * 64, n * 64}}, pool);
+    if (st.keyed)
+        par_copy({{h + st.o_kidx, kidx + b, n * 4}, {h + st.o_sig, sig + b * 64, n * 64}}, pool);
+    else
+        par_copy({{h + st.o_pk, pk + b * 32, n * 32}, {h + st.o_sig, sig + b * 64, n * 64}}, pool);
     first_part();
     uint64_t *hoff = reinterpret_cast<uint64_t *>(h + st.o_off);
     uint8_t *har = h + st.o_ar;
@@ -831,12 +1022,13 @@ static bool host_pinned(const void *p, size_t bytes) {
 }
 // Direct form of a stage: the record arrays of [b, e) and the arena range all pinned (and the arena
 // not compacted), so they can be DMAed from where they are.
-static bool stage_direct(const Stage &st, size_t b, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
-                         const uint64_t *off, const uint32_t *len) {
-    if (!g_direct_dma || st.compact) return false;
+static bool stage_direct(const Stage &st, size_t b, const uint8_t *pk, const uint32_t *kidx, const uint8_t *sig,
+                         const uint8_t *arena, const uint64_t *off, const uint32_t *len) {
+    if (st.compact) return false;
     const size_t n = st.n;
-    return host_pinned(pk + b * 32, n * 32) && host_pinned(sig + b * 64, n * 64) && host_pinned(off + b, n * 8) &&
-           host_pinned(len + b, n * 4) && (st.hi == st.lo || host_pinned(arena + st.lo, st.hi - st.lo));
+    return (st.keyed ? host_pinned(kidx + b, n * 4) : host_pinned(pk + b * 32, n * 32)) &&
+           host_pinned(sig + b * 64, n * 64) && host_pinned(off + b, n * 8) && host_pinned(len + b, n * 4) &&
+           (st.hi == st.lo || host_pinned(arena + st.lo, st.hi - st.lo));
 }
 // The stage's DMAs straight from the caller's pinned arrays into the device block dv (the layout of
 // stage_pack).  The 16 bytes after the arena part keep whatever the block held: the kernels read a
@@ -844,10 +1036,12 @@ static bool stage_direct(const Stage &st, size_t b, const uint8_t *pk, const uin
 // bytes never reach a verdict — and a fill there would be a blit KERNEL on the copy queue, which waits
 // for a free CU slot behind the running verify waves (it held the C2 copy stream for 2.5 ms,
 // profiles/r03d_timeline_pinned.txt).
-static hipError_t stage_dma_direct(const Stage &st, uint8_t *dv, size_t b, const uint8_t *pk, const uint8_t *sig,
-                                   const uint8_t *arena, const uint64_t *off, const uint32_t *len, hipStream_t s) {
+static hipError_t stage_dma_direct(const Stage &st, uint8_t *dv, size_t b, const uint8_t *pk, const uint32_t *kidx,
+                                   const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                                   hipStream_t s) {
     const size_t n = st.n;
-    hipError_t e = hipMemcpyAsync(dv + st.o_pk, pk + b * 32, n * 32, hipMemcpyHostToDevice, s);
+    hipError_t e = st.keyed ? hipMemcpyAsync(dv + st.o_kidx, kidx + b, n * 4, hipMemcpyHostToDevice, s)
+                            : hipMemcpyAsync(dv + st.o_pk, pk + b * 32, n * 32, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(dv + st.o_sig, sig + b * 64, n * 64, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(dv + st.o_off, off + b, n * 8, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(dv + st.o_len, len + b, n * 4, hipMemcpyHostToDevice, s);
@@ -856,377 +1050,245 @@ static hipError_t stage_dma_direct(const Stage &st, uint8_t *dv, size_t b, const
     return e;
 }
 
-// Zero-copy form of the small path for tri-chain batches (n <= cvk_get_tri_max(): the notary batches).
-// The records are packed into fine-grained pinned host memory that the fused prep kernel reads over
-// PCIe, and the kernels store the status bytes and one verdict byte per wave (4 bits) into pinned host
-// memory: no DMA in, no copy out.  Measured on the box, notary 4,096 (profiles/r03j_timeline_notary4096.txt),
-// the DMA path paid 19.8 us of H2D + 11.6 us from the DMA's completion to the prep's start + 9.6 us for
-// the verdict copy (a blit kernel after the Straus kernel).
-static int verify_shard_small_zc(Device &d, const Stage &st, size_t b, const uint8_t *pk, const uint8_t *sig,
-                                 const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
-                                 uint8_t *status, WorkerPool *pool, double t_plan, bool gather) {
-    double t[6];
-    t[0] = t_plan;
-    const size_t n = st.n, words = (n + 63) / 64, nnib = words * 16, waves = (n + 3) / 4;
-    Slot &sl = d.slot[0];
-    hipStream_t s = nullptr;
-    CV_TRY(slot_stream(d, 0, &s));
-    CV_TRY(slot_events(sl));
-    d.zc_in.flags = d.zc_out.flags = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
-    CV_TRY(d.zc_in.ensure(st.total));
-    CV_TRY(d.zc_out.ensure(al16(nnib) + al16(n)));
-    CV_TRY(ensure_verify_ws(sl, n));
-    if (!cvk_tri_zc_ok((uint32_t)n, sl.ws_cap)) return CV_E_HIP;   // (cannot happen: checked by the caller)
-    uint8_t *h = d.zc_in.as<uint8_t>();
-    if (gather) CV_TRY(sl.packed.ensure(al16(st.total)));
-    const uint8_t *dv = gather ? sl.packed.as<uint8_t>() : d.zc_in.dev_as<uint8_t>();
-    t[1] = now_s();
-    stage_pack(st, h, b, pk, sig, arena, off, len, pool, [] {});
-    uint8_t *nib = d.zc_out.as<uint8_t>();
-    std::memset(nib + waves, 0, nnib - waves);   // bytes of waves past the batch: no wave stores them
-    t[2] = now_s();
-    auto drain = on_exit([s] { (void)hipStreamSynchronize(s); });   // error paths: no kernel outlives the call
-    CV_TRY(ws_begin(d, sl, s));
-    const hipError_t e = cvk_verify_tri_zc(
-        (uint32_t)n, dv + st.o_pk, dv + st.o_sig, dv + st.o_ar - st.lo, reinterpret_cast<const uint64_t *>(dv + st.o_off),
-        reinterpret_cast<const uint32_t *>(dv + st.o_len), d.zc_out.dev_as<uint8_t>(),
-        status ? d.zc_out.dev_as<uint8_t>() + al16(nnib) : nullptr, sl.ws_tab.as<uint32_t>(), sl.ws_ok.as<uint8_t>(),
-        sl.ws_dig.as<uint32_t>(), sl.ws_cap, s, gather ? d.zc_in.dev : nullptr, gather ? sl.packed.p : nullptr,
-        gather ? al16(st.total) : 0);
-    const hipError_t e2 = ws_end(sl, s);
-    CV_TRY(e);
-    CV_TRY(e2);
-    t[3] = now_s();
-    CV_TRY(hipStreamSynchronize(s));
-    drain.armed = false;
-    t[4] = now_s();
-    for (size_t w = 0; w < words; w++) {
-        uint64_t x = 0;
-        for (int j = 0; j < 16; j++) x |= (uint64_t)(nib[16 * w + j] & 15u) << (4 * j);
-        bitmap[b / 64 + w] = x;
-    }
-    if (status) std::memcpy(status + b, nib + al16(nnib), n);
-    t[5] = now_s();
-    {
-        std::lock_guard<std::mutex> g(g_pipe_stats_mu);
-        for (int k = 0; k < 5; k++) g_small_t[k] += t[k + 1] - t[k];
-        g_small_calls++;
-    }
-    return CV_OK;
+// Staging layout of Merkle transactions [t0, t1) with leaves [l0, l1): off | len | tx_begin slice | arena.
+// The arena part is the leaves' byte range (or the leaves gathered back to back when scattered, as Stage).
+struct MStage {
+    size_t t0 = 0, t1 = 0, l0 = 0, l1 = 0, o_off = 0, o_len = 0, o_txb = 0, o_ar = 0, total = 0;
+    uint64_t lo = 0, hi = 0;
+    bool compact = false;
+};
+static MStage mstage_plan(size_t t0, size_t t1, const uint32_t *txb, const uint64_t *off, const uint32_t *len,
+                          WorkerPool *pool) {
+    MStage st;
+    st.t0 = t0;
+    st.t1 = t1;
+    st.l0 = txb[t0];
+    st.l1 = txb[t1];
+    const size_t nl = st.l1 - st.l0, nt = t1 - t0;
+    const Span sp = nl ? arena_span(st.l0, st.l1, off, len, pool) : Span{0, 0, 0};
+    const uint64_t lo = sp.lo & ~(uint64_t)15;
+    st.compact = nl && sp.hi - lo > 2 * sp.bytes + (1u << 20);
+    st.lo = st.compact ? 0 : (nl ? lo : 0);
+    st.hi = st.compact ? sp.bytes : (nl ? sp.hi : 0);
+    st.o_off = 0;
+    st.o_len = al16(nl * 8);
+    st.o_txb = st.o_len + al16(nl * 4);
+    st.o_ar = st.o_txb + al16((nt + 1) * 4);
+    st.total = st.o_ar + al16(st.hi - st.lo + 16);
+    return st;
 }
-
-// One shard [b, e) of a batch on one device, small form (the notary-sized batches): packed into slot 0's
-// pinned staging, moved by one DMA (two above 1 MB: the first overlaps packing the second part) into
-// one device block, verified, and the bitmap (+ status) come back by one DMA.  b is a multiple of 64,
-// so the shard's bitmap words are whole words of the caller's bitmap.
-static int verify_shard_small(Device &d, size_t b, size_t e, const uint8_t *pk, const uint8_t *sig,
-                              const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
-                              uint8_t *status, int threads) {
-    const size_t n = e - b;
-    WorkerPool *pool = n >= g_small_pool_min ? &d.workers(threads) : nullptr;
-    const double t_plan = now_s();
-    const Stage st = stage_plan(b, e, off, len, pool);
-    if (g_small_zc && cvk_tri_zc_ok((uint32_t)n, (uint32_t)n))
-        return verify_shard_small_zc(d, st, b, pk, sig, arena, off, len, bitmap, status, pool, t_plan,
-                                     g_small_zc == 2 || (g_small_zc == 3 && n >= 2048));
-    const size_t words = (n + 63) / 64;
-    const size_t o_bm = 0, o_st = al16(words * 8), total_out = o_st + al16(n);
-    Slot &sl = d.slot[0];
-    hipStream_t s = nullptr;
-    CV_TRY(slot_stream(d, 0, &s));
-    // the staging of a previous call may still be in a DMA only if that call failed half way (it
-    // drains its queue on every error path below), so this wait is normally free
-    if (sl.h2d_pending) {
-        CV_TRY(hipEventSynchronize(sl.h2d));
-        sl.h2d_pending = false;
-    }
-    CV_TRY(slot_events(sl));
-    CV_TRY(sl.pin_in.ensure(st.total));
-    CV_TRY(d.pin_out.ensure(total_out));
-    CV_TRY(sl.packed.ensure(st.total));
-    CV_TRY(d.bitmap.ensure(total_out));
-    uint8_t *h = sl.pin_in.as<uint8_t>();
-    uint8_t *dv = sl.packed.as<uint8_t>();
-    auto drain = on_exit([s] { (void)hipStreamSynchronize(s); });   // error paths: no DMA outlives the call
-    // Two-stage staging above 1 MB of keys + signatures: they are packed and their DMA is issued
-    // first, so it runs while the offsets, lengths and message bytes are packed (notary 65,536:
-    // 1.29-1.34 -> 1.21-1.25 ms p50); below, one DMA (a second DMA's ~6 us would cost more than it hides).
-    const bool two_stage = st.o_off >= ((size_t)1 << 20);
-    // below g_direct_small_min signatures one packed DMA beats five direct ones even from pinned
-    // arrays (notary 4,096: 0.328 ms p50 packed vs 0.342 direct; 65,536: 1.28 vs 1.10,
-    // profiles/r03h_bench.json)
-    if (n >= g_direct_small_min && stage_direct(st, b, pk, sig, arena, off, len)) {
-        // pinned caller arrays: no packing, the DMAs read them where they are
-        CV_TRY(stage_dma_direct(st, dv, b, pk, sig, arena, off, len, s));
+static void mstage_pack(const MStage &st, uint8_t *h, const uint32_t *txb, const uint8_t *arena, const uint64_t *off,
+                        const uint32_t *len, WorkerPool *pool) {
+    const size_t nl = st.l1 - st.l0, nt = st.t1 - st.t0;
+    uint64_t *hoff = reinterpret_cast<uint64_t *>(h + st.o_off);
+    uint8_t *har = h + st.o_ar;
+    if (st.compact) {
+        par_copy({{h + st.o_len, len + st.l0, nl * 4}, {h + st.o_txb, txb + st.t0, (nt + 1) * 4}}, nullptr);
+        uint64_t pos = 0;
+        for (size_t i = 0; i < nl; i++) {
+            hoff[i] = pos;
+            if (len[st.l0 + i]) std::memcpy(har + pos, arena + off[st.l0 + i], len[st.l0 + i]);
+            pos += len[st.l0 + i];
+        }
     } else {
-        hipError_t e1 = hipSuccess;
-        stage_pack(st, h, b, pk, sig, arena, off, len, pool, [&] {
-            if (two_stage) e1 = hipMemcpyAsync(dv, h, st.o_off, hipMemcpyHostToDevice, s);
-        });
-        CV_TRY(e1);
-        if (two_stage)
-            CV_TRY(hipMemcpyAsync(dv + st.o_off, h + st.o_off, st.total - st.o_off, hipMemcpyHostToDevice, s));
-        else
-            CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, s));
+        par_copy({{h + st.o_off, off + st.l0, nl * 8}, {h + st.o_len, len + st.l0, nl * 4},
+                  {h + st.o_txb, txb + st.t0, (nt + 1) * 4},
+                  {har, st.hi > st.lo ? arena + st.lo : nullptr, (size_t)(st.hi - st.lo)}},
+                 pool);
     }
-    uint8_t *dout = d.bitmap.as<uint8_t>();
-    CV_TRY(launch_verify(d, sl, (uint32_t)n, dv + st.o_pk, dv + st.o_sig, dv + st.o_ar - st.lo,
-                         reinterpret_cast<const uint64_t *>(dv + st.o_off), reinterpret_cast<const uint32_t *>(dv + st.o_len),
-                         reinterpret_cast<uint64_t *>(dout + o_bm), status ? dout + o_st : nullptr, s, nullptr, true));
-    CV_TRY(hipMemcpyAsync(d.pin_out.p, dout, status ? o_st + n : words * 8, hipMemcpyDeviceToHost, s));
-    CV_TRY(hipStreamSynchronize(s));
-    drain.armed = false;
-    std::memcpy(bitmap + b / 64, d.pin_out.as<uint8_t>() + o_bm, words * 8);
-    if (status) std::memcpy(status + b, d.pin_out.as<uint8_t>() + o_st, n);
-    return CV_OK;
+    std::memset(har + (st.hi - st.lo), 0, 16);
+}
+static bool mstage_direct(const MStage &st, const uint32_t *txb, const uint8_t *arena, const uint64_t *off,
+                          const uint32_t *len) {
+    if (st.compact) return false;
+    const size_t nl = st.l1 - st.l0, nt = st.t1 - st.t0;
+    return (nl == 0 || (host_pinned(off + st.l0, nl * 8) && host_pinned(len + st.l0, nl * 4))) &&
+           host_pinned(txb + st.t0, (nt + 1) * 4) && (st.hi == st.lo || host_pinned(arena + st.lo, st.hi - st.lo));
+}
+static hipError_t mstage_dma_direct(const MStage &st, uint8_t *dv, const uint32_t *txb, const uint8_t *arena,
+                                    const uint64_t *off, const uint32_t *len, hipStream_t s) {
+    const size_t nl = st.l1 - st.l0, nt = st.t1 - st.t0;
+    hipError_t e = hipSuccess;
+    if (nl) e = hipMemcpyAsync(dv + st.o_off, off + st.l0, nl * 8, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && nl) e = hipMemcpyAsync(dv + st.o_len, len + st.l0, nl * 4, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(dv + st.o_txb, txb + st.t0, (nt + 1) * 4, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && st.hi > st.lo)
+        e = hipMemcpyAsync(dv + st.o_ar, arena + st.lo, st.hi - st.lo, hipMemcpyHostToDevice, s);
+    return e;
 }
 
-// The pipeline's sub-chunk boundaries of [b, e): [first, C, C, ..., the last two balanced]; every
-// boundary but e is b + a multiple of 64 (whole bitmap words per sub-chunk).
-// With ramp, the sizes after the first double (first, 2 first, 4 first, ...) until they reach C: each
-// sub-chunk's copy then takes about as long as the kernels of the one before it, so the GPU is not left
-// waiting for a big second sub-chunk while a small first one has long finished.
-static std::vector<size_t> pipe_cuts(size_t b, size_t e, size_t first, size_t C, bool ramp = false) {
-    std::vector<size_t> cut{b};
-    if (e <= b) return cut;
-    first = std::max<size_t>(64, first / 64 * 64);
-    C = std::max<size_t>(64, C / 64 * 64);
-    size_t p = b + std::min(e - b, first);
-    cut.push_back(p);
-    size_t step = first;
-    while (p < e) {
-        const size_t rem = e - p;
-        step = ramp ? std::min(C, 2 * step) : C;
-        const size_t m = rem <= step ? rem : rem < 2 * step ? (rem / 2 + 63) / 64 * 64 : step;
-        p += m;
-        cut.push_back(p);
+// ---------------------------------------------------------------- key dedupe
+// Host-side key dedupe of the plain entry points: keys = the distinct key bytes in first-seen order,
+// key_index[i] = its index.  Returns false when the batch does not repeat keys enough for the keyed path to
+// pay (fewer than eight signatures per distinct key: a key's 66 KB of tables cost about 7 plain verifies).
+//   - n > 16,384: a gate first samples 4,096 signatures at pseudo-random positions (a fixed sequence, so a
+//     batch always gets the same decision) and counts repeated keys among them; a batch of c distinct keys
+//     shows about s^2 / 2c repeats in a sample of s, so fewer than 4 s^2 / 2n repeats (an estimated ratio
+//     below four signatures per key) is taken as distinct-keyed without touching the rest.  A performance
+//     guess only: both paths give the same verdicts.
+//   - the dedupe proper runs in slices on the pool, each with its own growing open-addressing table (a
+//     1,024-key pool stays in cache), giving up once any slice has seen more than n / 8 distinct keys;
+//     the slices' key lists are then merged in slice order (first-seen order overall) and the slices'
+//     local indices remapped.
+// Flat tables on the seeded hash of all 32 key bytes (key_hash32), no per-key allocation.
+struct FlatKeys {
+    std::vector<uint32_t> first, id;   // bucket -> representative record, distinct-key index (UINT32_MAX = empty)
+    size_t mask = 0, count = 0;
+    explicit FlatKeys(size_t cap0 = 1024) { reset(cap0); }
+    void reset(size_t cap) {
+        size_t c = 64;
+        while (c < cap) c <<= 1;
+        first.assign(c, UINT32_MAX);
+        id.assign(c, 0);
+        mask = c - 1;
+        count = 0;
     }
-    return cut;
-}
-
-// One shard [b, e) of a large batch, pipelined: sub-chunks (multiples of 64 signatures) go through a ring
-// of kRing device input blocks.  Sub-chunk j's records reach block j % kRing on the device's ONE copy
-// stream — straight from the caller's arrays when they are pinned (stage_direct), else packed by the
-// host threads into pinned staging block j % kRing first — and are verified on slot j % R's stream,
-// which waits for that copy (event) and marks the block free when its kernels are done.  The copy
-// stream waits (on the GPU) for the verify that last read a block before refilling it, so copies run
-// up to kRing sub-chunks ahead of the kernels and never queue behind a running kernel on a compute
-// stream.  One copy queue matters: with copies on every slot stream the runtime ran those of one
-// stream as blit kernels (`__amd_rocclr_copyBuffer`, ~37 GB/s, on the CUs beside the verify kernels)
-// and the C2 host call took 13.8-16 ms for 9.6 ms of kernels (profiles/r03c_timeline_*.txt).  The
-// verdicts come back in ONE copy after the last verify.
-// Copies a finished pipelined call's verdicts into the caller's arrays (waits for them first).
-static int pipe_finish(Device &d, PipeOut &po) {
-    if (!po.pending) return CV_OK;
-    po.pending = false;
-    // host-side join: the call's last launch group on every slot stream, then ONE verdict copy on the
-    // device's output stream (which carries nothing else, so it neither waits behind the next call's
-    // input copies nor holds a compute stream the next call's kernels run on)
-    for (int k = 0; k < kSlots; k++)
-        if (po.slot_used[k]) CV_TRY(hipEventSynchronize(po.slot_done[k]));
-    if (!d.outs) CV_TRY(hipStreamCreateWithFlags(&d.outs, hipStreamNonBlocking));
-    const size_t words = (po.n + 63) / 64;
-    CV_TRY(hipMemcpyAsync(po.hout.p, po.dout.p, po.status ? po.o_st + po.n : words * 8, hipMemcpyDeviceToHost, d.outs));
-    CV_TRY(hipStreamSynchronize(d.outs));
-    std::memcpy(po.bitmap + po.b / 64, po.hout.p, words * 8);
-    if (po.status) std::memcpy(po.status + po.b, po.hout.as<uint8_t>() + po.o_st, po.n);
-    return CV_OK;
-}
-
-// Enqueues the pipelined verify of shard [b, e) on device d with its verdicts going to output slot
-// po (which must not be pending); returns without waiting for the GPU.  The join: the device stream
-// (slot 0's) waits for the other slot streams' last launch groups, copies the verdicts to po's pinned
-// buffer and records po.done.  The ring's in_free / in_ready events stay valid across calls, so the
-// next call's copies and kernels queue right behind this one's (cv_ed25519_verify_batch_async).
-// async: the sub-chunk plan of cv_ed25519_verify_batch_async (g_async_chunk, no ramp — with a call in
-// flight ahead of it the GPU is busy anyway, and bigger launches run closer to the kernels' rate)
-static int pipe_enqueue(Device &d, PipeOut &po, size_t b, size_t e, const uint8_t *pk, const uint8_t *sig,
-                        const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
-                        uint8_t *status, int threads, bool async = false) {
-    const size_t n = e - b;
-    const size_t words = (n + 63) / 64;
-    const size_t o_st = al16(words * 8), total_out = o_st + al16(n);
-    // async sub-chunks: g_async_chunk, up to twice that for big shards (n / 16; same-box sweep:
-    // C2 1M best at 262,144, C5 8M at 524,288, profiles/r03l_async_chunk_sweep.log)
-    const size_t ach = std::max(g_async_chunk, std::min(2 * g_async_chunk, n / 16 / 64 * 64));
-    const std::vector<size_t> cut = async ? pipe_cuts(b, e, ach, ach, false)
-                                          : pipe_cuts(b, e, g_pipe_first, g_pipe_chunk, g_pipe_ramp != 0);
-    const int nsl = g_pipe_slots;
-    hipStream_t ss[kSlots] = {};
-    for (int k = 0; k < nsl; k++) {
-        CV_TRY(slot_stream(d, k, &ss[k]));
-        CV_TRY(slot_events(d.slot[k]));
-    }
-    if (!d.copy) CV_TRY(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
-    for (int q = 0; q < kRing; q++) {
-        if (!d.in_ready[q]) CV_TRY(hipEventCreateWithFlags(&d.in_ready[q], hipEventDisableTiming));
-        if (!d.in_free[q]) CV_TRY(hipEventCreateWithFlags(&d.in_free[q], hipEventDisableTiming));
-    }
-    for (int k = 0; k < nsl; k++)
-        if (!po.slot_done[k]) CV_TRY(hipEventCreateWithFlags(&po.slot_done[k], hipEventDisableTiming));
-    CV_TRY(po.hout.ensure(total_out));
-    CV_TRY(po.dout.ensure(total_out));
-    uint8_t *dout = po.dout.as<uint8_t>();
-    // error paths: drain every queue, forget the ring's state and every pending output of this device
-    auto drain = on_exit([&] {
-        (void)hipStreamSynchronize(d.copy);
-        for (int k = 0; k < nsl; k++) (void)hipStreamSynchronize(ss[k]);
-        for (int q = 0; q < kRing; q++) d.in_used[q] = d.stage_busy[q] = false;
-        for (PipeOut &o : d.out)                  // an earlier call still in flight keeps its verdicts
-            if (&o != &po) (void)pipe_finish(d, o);
-    });
-    WorkerPool *pool = &d.workers(threads);
-    PipeStats ps;
-    bool used[kSlots] = {};
-    for (size_t j = 0; j + 1 < cut.size(); j++) {
-        const size_t c0 = cut[j], c1 = cut[j + 1], m = c1 - c0;
-        const int q = d.ring_next;
-        d.ring_next = (d.ring_next + 1) % kRing;
-        Slot &sl = d.slot[j % nsl];
-        hipStream_t s = ss[j % nsl];
-        used[j % nsl] = true;
-        double t0 = now_s();
-        const Stage st = stage_plan(c0, c1, off, len, pool);
-        const bool direct = stage_direct(st, c0, pk, sig, arena, off, len);
-        double t1 = now_s();
-        ps.plan += t1 - t0;
-        if (st.total > d.inblk[q].cap) {             // growing: the old block may still be read
-            if (d.in_used[q]) CV_TRY(hipEventSynchronize(d.in_free[q]));
-            CV_TRY(d.inblk[q].ensure(st.total));
-        }
-        if (d.in_used[q]) CV_TRY(hipStreamWaitEvent(d.copy, d.in_free[q], 0));
-        uint8_t *dv = d.inblk[q].as<uint8_t>();
-        if (direct) {
-            t0 = now_s();
-            ps.wait += t0 - t1;
-            CV_TRY(stage_dma_direct(st, dv, c0, pk, sig, arena, off, len, d.copy));
-            ps.direct++;
-        } else {
-            // staging block q is free once its previous copy has left it
-            if (d.stage_busy[q]) {
-                CV_TRY(hipEventSynchronize(d.in_ready[q]));
-                d.stage_busy[q] = false;
+    // index of the key pk[32 * i] (inserting it as `fresh` when new); *added = whether it was new
+    uint32_t find_or_add(const uint8_t *pk, uint32_t i, uint32_t fresh, bool *added) {
+        const uint8_t *k = pk + 32 * (size_t)i;
+        size_t bkt = (size_t)key_hash32(k) & mask;
+        for (;;) {
+            const uint32_t f = first[bkt];
+            if (f == UINT32_MAX) {
+                if (2 * (count + 1) > mask + 1) {   // grow: keep the load at or below 1/2
+                    grow(pk);
+                    return find_or_add(pk, i, fresh, added);
+                }
+                first[bkt] = i;
+                id[bkt] = fresh;
+                count++;
+                *added = true;
+                return fresh;
             }
-            CV_TRY(d.instage[q].ensure(st.total));
-            t0 = now_s();
-            ps.wait += t0 - t1;
-            uint8_t *h = d.instage[q].as<uint8_t>();
-            stage_pack(st, h, c0, pk, sig, arena, off, len, pool, [] {});
-            t1 = now_s();
-            ps.pack += t1 - t0;
-            t0 = t1;
-            CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, d.copy));
-            d.stage_busy[q] = true;
+            if (std::memcmp(pk + 32 * (size_t)f, k, 32) == 0) {
+                *added = false;
+                return id[bkt];
+            }
+            bkt = (bkt + 1) & mask;
         }
-        CV_TRY(hipEventRecord(d.in_ready[q], d.copy));
-        CV_TRY(hipStreamWaitEvent(s, d.in_ready[q], 0));
-        const size_t w0 = (c0 - b) / 64;
-        CV_TRY(launch_verify(d, sl, (uint32_t)m, dv + st.o_pk, dv + st.o_sig, dv + st.o_ar - st.lo,
-                             reinterpret_cast<const uint64_t *>(dv + st.o_off),
-                             reinterpret_cast<const uint32_t *>(dv + st.o_len),
-                             reinterpret_cast<uint64_t *>(dout) + w0, status ? dout + o_st + (c0 - b) : nullptr, s,
-                             nullptr, false));
-        CV_TRY(hipEventRecord(d.in_free[q], s));
-        d.in_used[q] = true;
-        ps.enq += now_s() - t0;
-        ps.chunks++;
     }
-    // completion marks per slot stream (pipe_finish joins on the host); no GPU-side join, which would
-    // hold the next call's kernels on that stream until this call had finished
-    for (int k = 0; k < kSlots; k++) {
-        po.slot_used[k] = k < nsl && used[k];
-        if (po.slot_used[k]) CV_TRY(hipEventRecord(po.slot_done[k], ss[k]));
+
+  private:
+    void grow(const uint8_t *pk) {
+        std::vector<uint32_t> f0 = std::move(first), i0 = std::move(id);
+        const size_t c = 2 * (mask + 1);
+        first.assign(c, UINT32_MAX);
+        id.assign(c, 0);
+        mask = c - 1;
+        for (size_t b = 0; b < f0.size(); b++) {
+            if (f0[b] == UINT32_MAX) continue;
+            size_t bkt = (size_t)key_hash32(pk + 32 * (size_t)f0[b]) & mask;
+            while (first[bkt] != UINT32_MAX) bkt = (bkt + 1) & mask;
+            first[bkt] = f0[b];
+            id[bkt] = i0[b];
+        }
     }
-    drain.armed = false;
-    po.pending = true;
-    po.gen++;
-    po.bitmap = bitmap;
-    po.status = status;
-    po.b = b;
-    po.n = n;
-    po.o_st = o_st;
-    {
-        std::lock_guard<std::mutex> g(g_pipe_stats_mu);
-        PipeStats &G = g_pipe_stats;
-        G.plan += ps.plan;
-        G.pack += ps.pack;
-        G.wait += ps.wait;
-        G.enq += ps.enq;
-        G.calls++;
-        G.chunks += ps.chunks;
-        G.direct += ps.direct;
+};
+
+static bool dedupe_gate(size_t n, const uint8_t *pk) {
+    if (n <= 16384) return true;
+    constexpr uint32_t kS = 4096;
+    FlatKeys t(2 * kS);
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    uint32_t rep = 0;
+    std::vector<uint32_t> pos(kS);
+    for (uint32_t j = 0; j < kS; j++) {
+        x = x * 6364136223846793005ull + 1442695040888963407ull;
+        pos[j] = (uint32_t)((x >> 32) * (uint64_t)n >> 32);
     }
-    return CV_OK;
+    std::sort(pos.begin(), pos.end());             // ascending positions: friendlier to the caches
+    uint32_t prev = UINT32_MAX;
+    for (uint32_t j = 0; j < kS; j++) {
+        if (pos[j] == prev) continue;               // the same record twice is not a repeated key
+        prev = pos[j];
+        bool added;
+        t.find_or_add(pk, pos[j], (uint32_t)t.count, &added);
+        rep += added ? 0 : 1;
+    }
+    // keyed worth a full dedupe when s^2 / (2 rep) < n / 4, i.e. rep > 2 s^2 / n
+    return (double)rep > 2.0 * (double)kS * (double)kS / (double)n;
 }
 
-// The device's next free output slot: the older in-flight call is finished first if it still holds it.
-static PipeOut &pipe_out(Device &d, int *index = nullptr) {
-    PipeOut &po = d.out[d.out_next];
-    if (index) *index = d.out_next;
-    d.out_next = (d.out_next + 1) % kOuts;
-    return po;
-}
-
-// One shard [b, e) of a large batch, pipelined (see pipe_enqueue), synchronously: the verdicts are in
-// the caller's arrays on return.
-static int verify_shard_pipe(Device &d, size_t b, size_t e, const uint8_t *pk, const uint8_t *sig,
-                             const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
-                             uint8_t *status, int threads) {
-    PipeOut &po = pipe_out(d);
-    int rc = pipe_finish(d, po);
-    if (rc != CV_OK) return rc;
-    rc = pipe_enqueue(d, po, b, e, pk, sig, arena, off, len, bitmap, status, threads);
-    if (rc != CV_OK) return rc;
-    const double t0 = now_s();
-    rc = pipe_finish(d, po);
-    {
-        std::lock_guard<std::mutex> g(g_pipe_stats_mu);
-        g_pipe_stats.sync += now_s() - t0;
+static bool dedupe_keys(size_t n, const uint8_t *pk, std::vector<uint8_t> &keys, std::vector<uint32_t> &key_index,
+                        WorkerPool *pool, bool gate = true) {
+    if (n < 64 || n > 0xffffffffull) return false;
+    if (gate && !dedupe_gate(n, pk)) return false;
+    const size_t limit = n / 8;                      // most distinct keys the keyed path takes
+    const int nt = pool ? pool->threads() : 1;
+    const size_t nsl = (n >= 65536 && nt > 1) ? (size_t)nt * 2 : 1;
+    const size_t per = (n + nsl - 1) / nsl;
+    key_index.resize(n);
+    std::vector<std::vector<uint32_t>> uniq(nsl);   // per slice: the record of each local key, first-seen order
+    std::atomic<bool> over{false};
+    auto slice = [&](size_t s) {
+        const size_t b = s * per, e = std::min(n, b + per);
+        FlatKeys t(1024);
+        for (size_t i = b; i < e && !over.load(std::memory_order_relaxed); i++) {
+            bool added;
+            key_index[i] = t.find_or_add(pk, (uint32_t)i, (uint32_t)uniq[s].size(), &added);
+            if (added) {
+                uniq[s].push_back((uint32_t)i);
+                if (uniq[s].size() > limit) over.store(true);
+            }
+        }
+    };
+    if (nsl > 1)
+        pool->run(nsl, slice);
+    else
+        slice(0);
+    if (over.load()) return false;
+    // merge the slices' key lists in slice order; remap[s][local] = global index
+    FlatKeys g(4096);
+    std::vector<uint32_t> grec;                      // the representative record of each global key
+    std::vector<std::vector<uint32_t>> remap(nsl);
+    for (size_t s = 0; s < nsl; s++) {
+        remap[s].resize(uniq[s].size());
+        for (size_t u = 0; u < uniq[s].size(); u++) {
+            bool added;
+            remap[s][u] = g.find_or_add(pk, uniq[s][u], (uint32_t)grec.size(), &added);
+            if (added) {
+                grec.push_back(uniq[s][u]);
+                if (grec.size() > limit) return false;
+            }
+        }
     }
-    return rc;
-}
-
-static int verify_shard(Device &d, size_t b, size_t e, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
-                        const uint64_t *off, const uint32_t *len, uint64_t *bitmap, uint8_t *status, int threads) {
-    const size_t n = e - b;
-    if (n == 0) return CV_OK;
-    if (n > 0xffffffffull) return CV_E_TOO_LARGE;
-    CV_TRY(hipSetDevice(d.ordinal));
-    if (n > g_pipe_min) return verify_shard_pipe(d, b, e, pk, sig, arena, off, len, bitmap, status, threads);
-    return verify_shard_small(d, b, e, pk, sig, arena, off, len, bitmap, status, threads);
-}
-
-// Shards [0, n) over the context's devices (contiguous ranges, multiples of 64) and runs fn per shard
-// (fn(device, b, e, packing threads)).
-template <class F> static int for_each_shard(cv_ctx *ctx, size_t n, F fn) {
-    const size_t ndev = ctx->devs.size();
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const int threads = (int)std::max<size_t>(1, std::min<size_t>((size_t)g_pack_threads, hw / ndev));
-    size_t per = (n + ndev - 1) / ndev;
-    per = (per + 63) / 64 * 64;
-    if (ndev == 1 || n <= 64) return fn(ctx->devs[0], 0, n, threads);
-    std::vector<int> rc(ndev, CV_OK);
-    std::vector<std::thread> th;
-    for (size_t k = 0; k < ndev; k++) {
-        const size_t b = std::min(n, k * per), e = std::min(n, b + per);
-        if (b >= e) continue;
-        th.emplace_back([&, k, b, e] { rc[k] = fn(ctx->devs[k], b, e, threads); });
+    if (nsl > 1 || !remap[0].empty()) {
+        auto fix = [&](size_t s) {
+            const size_t b = s * per, e = std::min(n, b + per);
+            const std::vector<uint32_t> &r = remap[s];
+            for (size_t i = b; i < e; i++) key_index[i] = r[key_index[i]];
+        };
+        if (nsl > 1)
+            pool->run(nsl, fix);
+        else
+            fix(0);
     }
-    for (auto &t : th) t.join();
-    for (int r : rc)
-        if (r != CV_OK) return r;
-    return CV_OK;
+    keys.resize(32 * grec.size());
+    for (size_t u = 0; u < grec.size(); u++) std::memcpy(keys.data() + 32 * u, pk + 32 * (size_t)grec[u], 32);
+    return true;
 }
 
-// ---------------------------------------------------------------- keyed verify (per-key comb tables)
+// ---------------------------------------------------------------- keyed: key pool
+// Waits until nothing queued on the device may still read its key pool (before the pool is emptied or
+// reallocated: an asynchronous call's sub-chunks may still be reading the slots being reassigned).
+static hipError_t pool_quiesce(Device &d) {
+    hipError_t e = hipSuccess;
+    for (int k = 0; k < kSlots && e == hipSuccess; k++)
+        if (d.slot[k].stream) e = hipStreamSynchronize(d.slot[k].stream);
+    if (e == hipSuccess && d.kc.last) e = hipEventSynchronize(d.kc.ev);
+    return e;
+}
+
 // Makes the keys k (used[k] != 0, or all when used == nullptr) of keys[0..nk) resident in d's key
 // pool and fills slot_of_key[k]; keyprep launches on s compute the tables of the new ones (at most
-// kKeyprepBatch keys per launch, so the scratch stays bounded).  The caller holds the pool
-// (pool_begin).  Failure leaves an empty pool (capacity 0, no resident keys), never a key mapped to
-// a slot whose tables were not computed or a capacity without its buffers.
+// kKeyprepBatch keys per launch, so the scratch stays bounded) and *prepared says whether any ran.  The
+// caller holds the device lock and the pool (pool_begin).  Failure leaves an empty pool (capacity 0, no
+// resident keys), never a key mapped to a slot whose tables were not computed or a capacity without its
+// buffers.
 static int key_resolve(Device &d, uint32_t cap, size_t nk, const uint8_t *keys, const uint8_t *used,
-                       std::vector<uint32_t> &slot_of_key, hipStream_t s) {
+                       std::vector<uint32_t> &slot_of_key, hipStream_t s, bool *prepared) {
     KeyCache &kc = d.kc;
+    *prepared = false;
     auto fail = [&kc](hipError_t e) {
         kc.map.clear();
         kc.cap = 0;
@@ -1238,7 +1300,7 @@ static int key_resolve(Device &d, uint32_t cap, size_t nk, const uint8_t *keys, 
     const size_t need = std::max<size_t>(cap, nused);
     if (kc.cap < need) {                      // (re)allocate the pool; resident tables are dropped
         if (need > 0xffffffffull / 2) return CV_E_TOO_LARGE;
-        hipError_t e = hipStreamSynchronize(s);
+        hipError_t e = pool_quiesce(d);
         if (e != hipSuccess) return fail(e);
         kc.map.clear();
         kc.cap = 0;
@@ -1248,13 +1310,15 @@ static int key_resolve(Device &d, uint32_t cap, size_t nk, const uint8_t *keys, 
         if ((e = kc.kok.ensure(need)) != hipSuccess) return fail(e);
         kc.cap = (uint32_t)need;
     }
-    if (kc.map.size() + nused > kc.cap) {     // epoch reset: every key of this call gets a fresh slot
+    // epoch reset: every key of this call gets a fresh slot, after the queued readers of the old ones
+    if (kc.map.size() + nused > kc.cap) {
+        const hipError_t e = pool_quiesce(d);
+        if (e != hipSuccess) return fail(e);
         kc.map.clear();
         kc.resets++;
     }
     std::vector<uint8_t> miss_keys;
     std::vector<uint32_t> miss_slots;
-    std::vector<std::array<uint8_t, 32>> miss;     // mapped only once their tables are enqueued
     std::unordered_map<std::array<uint8_t, 32>, uint32_t, KeyHash> fresh;   // this call's new keys
     std::array<uint8_t, 32> key;
     slot_of_key.assign(nk, 0);
@@ -1303,129 +1367,641 @@ static int key_resolve(Device &d, uint32_t cap, size_t nk, const uint8_t *keys, 
         // the pageable copies above read miss_keys / miss_slots asynchronously: keep them alive
         const hipError_t e = hipStreamSynchronize(s);
         if (e != hipSuccess) return fail(e);
+        *prepared = true;
     }
     for (auto &kv : fresh) kc.map.emplace(kv.first, kv.second);
     return CV_OK;
 }
 
-// One shard [b, e) of a keyed host-buffer batch on one device (b a multiple of 64).
-static int verify_shard_keyed(uint32_t cap, Device &d, size_t b, size_t e, size_t nkeys, const uint8_t *keys,
-                              const uint32_t *key_index, const uint8_t *sig, const uint8_t *arena,
-                              const uint64_t *off, const uint32_t *len, uint64_t *bitmap, uint8_t *status) {
-    const size_t n = e - b;
-    if (n == 0) return CV_OK;
-    if (n > 0xffffffffull || nkeys > 0xffffffffull) return CV_E_TOO_LARGE;
-    CV_TRY(hipSetDevice(d.ordinal));
-    std::vector<uint8_t> used(nkeys, 0);
-    uint64_t lo = UINT64_MAX, hi = 0;
-    for (size_t i = b; i < e; i++) {
-        if (key_index[i] >= nkeys) return CV_E_ARGS;
-        used[key_index[i]] = 1;
-        lo = std::min<uint64_t>(lo, off[i]);
-        hi = std::max<uint64_t>(hi, off[i] + len[i]);
-    }
-    if (hi < lo) hi = lo;
-    hipStream_t s = d.stream;
-    Slot &sl = pick_slot(d, s);
+// ---------------------------------------------------------------- verify (host buffers): small paths
+// The caller's record arrays of one host-buffer call.  Keyed calls carry keys[nkeys][32] + key_index[n]
+// instead of per-record keys.
+struct VerifyIn {
+    const uint8_t *pk = nullptr, *sig = nullptr, *arena = nullptr;
+    const uint64_t *off = nullptr;
+    const uint32_t *len = nullptr;
+    const uint8_t *keys = nullptr;       // keyed
+    const uint32_t *key_index = nullptr; // keyed
+    size_t nkeys = 0;
+    const uint8_t *used = nullptr;       // keyed: which of the keys the shard uses (nullptr = all)
+    bool copy_kidx = false;              // keyed: key_index is the call's own host vector (copied to pinned memory)
+    bool auto_keyed = false;             // dedupe pk per shard and take the keyed path
+    uint64_t *bitmap = nullptr;
+    uint8_t *status = nullptr;
+};
+
+// Zero-copy form of the small path for tri-chain batches (the notary batches).  The records are packed into
+// fine-grained pinned host memory that the fused prep kernel reads over PCIe, and the kernels store the
+// status bytes and one verdict byte per wave (4 bits) into pinned host memory: no DMA in, no copy out.
+// Measured on the box, notary 4,096 (profiles/r03j_timeline_notary4096.txt), the DMA path paid 19.8 us of
+// H2D + 11.6 us from the DMA's completion to the prep's start + 9.6 us for the verdict copy.
+static int verify_shard_small_zc(cv_ctx *ctx, Device &d, const Opts &o, const Stage &st, size_t b, const VerifyIn &in,
+                                 WorkerPool *pool, double t_plan, bool gather) {
+    double t[6];
+    t[0] = t_plan;
+    const size_t n = st.n, words = (n + 63) / 64, nnib = words * 16, waves = (n + 3) / 4;
+    Slot &sl = d.slot[0];
+    hipStream_t s = nullptr;
+    CV_TRY(slot_stream(d, 0, &s));
+    CV_TRY(slot_events(sl));
+    d.zc_in.flags = d.zc_out.flags = hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable;
+    CV_TRY(d.zc_in.ensure(st.total));
+    CV_TRY(d.zc_out.ensure(al16(nnib) + al16(n)));
     CV_TRY(ensure_verify_ws(sl, n));
+    if (!cvk_tri_zc_ok(&o.plan, (uint32_t)n, sl.ws_cap)) return CV_E_HIP;   // (cannot happen: checked by the caller)
+    uint8_t *h = d.zc_in.as<uint8_t>();
+    if (gather) CV_TRY(sl.packed.ensure(al16(st.total)));
+    const uint8_t *dv = gather ? sl.packed.as<uint8_t>() : d.zc_in.dev_as<uint8_t>();
+    t[1] = now_s();
+    stage_pack(st, h, b, in.pk, nullptr, in.sig, in.arena, in.off, in.len, pool, [] {});
+    uint8_t *nib = d.zc_out.as<uint8_t>();
+    std::memset(nib + waves, 0, nnib - waves);   // bytes of waves past the batch: no wave stores them
+    t[2] = now_s();
+    auto drain = on_exit([s] { (void)hipStreamSynchronize(s); });   // error paths: no kernel outlives the call
     CV_TRY(ws_begin(d, sl, s));
-    CV_TRY(pool_begin(d.kc, s));
-    auto drain = on_exit([s] { (void)hipStreamSynchronize(s); });   // error paths: no copy outlives the call
-    std::vector<uint32_t> sok;
-    int rc = key_resolve(d, cap, nkeys, keys, used.data(), sok, s);
-    if (rc != CV_OK) return rc;
-    const size_t words = (n + 63) / 64;
-    KeyCache &kc = d.kc;
-    CV_TRY(d.pk.ensure(nkeys * 32));
-    CV_TRY(kc.slot_of_key.ensure(nkeys * 4));
-    CV_TRY(kc.key_index.ensure(n * 4));
-    CV_TRY(d.sig.ensure(n * 64));
-    CV_TRY(d.arena.ensure(hi - lo + 16));
-    CV_TRY(d.off.ensure(n * 8));
-    CV_TRY(d.len.ensure(n * 4));
-    CV_TRY(d.bitmap.ensure(words * 8));
-    CV_TRY(d.status.ensure(n));
-    CV_TRY(hipMemcpyAsync(d.pk.p, keys, nkeys * 32, hipMemcpyHostToDevice, s));
-    CV_TRY(hipMemcpyAsync(kc.slot_of_key.p, sok.data(), nkeys * 4, hipMemcpyHostToDevice, s));
-    CV_TRY(hipMemcpyAsync(kc.key_index.p, key_index + b, n * 4, hipMemcpyHostToDevice, s));
-    CV_TRY(hipMemcpyAsync(d.sig.p, sig + b * 64, n * 64, hipMemcpyHostToDevice, s));
-    if (hi > lo) CV_TRY(hipMemcpyAsync(d.arena.p, arena + lo, hi - lo, hipMemcpyHostToDevice, s));
-    CV_TRY(hipMemcpyAsync(d.off.p, off + b, n * 8, hipMemcpyHostToDevice, s));
-    CV_TRY(hipMemcpyAsync(d.len.p, len + b, n * 4, hipMemcpyHostToDevice, s));
-    CV_TRY(cvk_verify_keyed((uint32_t)n, d.pk.as<uint8_t>(), kc.key_index.as<uint32_t>(), kc.slot_of_key.as<uint32_t>(),
-                            kc.ktab.as<uint32_t>(), kc.kok.as<uint8_t>(), d.sig.as<uint8_t>(),
-                            d.arena.as<uint8_t>() - lo, d.off.as<uint64_t>(), d.len.as<uint32_t>(),
-                            d.bitmap.as<uint64_t>(), status ? d.status.as<uint8_t>() : nullptr, sl.ws_hs.as<uint32_t>(),
-                            sl.ws_R.as<uint32_t>(), sl.ws_ok.as<uint8_t>(), sl.ws_cap, s, nullptr));
-    CV_TRY(ws_end(sl, s));
-    CV_TRY(pool_end(kc, s));
-    CV_TRY(hipMemcpyAsync(bitmap + b / 64, d.bitmap.p, words * 8, hipMemcpyDeviceToHost, s));
-    if (status) CV_TRY(hipMemcpyAsync(status + b, d.status.p, n, hipMemcpyDeviceToHost, s));
+    const hipError_t e = cvk_verify_tri_zc(
+        &o.plan, (uint32_t)n, dv + st.o_pk, dv + st.o_sig, dv + st.o_ar - st.lo,
+        reinterpret_cast<const uint64_t *>(dv + st.o_off), reinterpret_cast<const uint32_t *>(dv + st.o_len),
+        d.zc_out.dev_as<uint8_t>(), in.status ? d.zc_out.dev_as<uint8_t>() + al16(nnib) : nullptr,
+        sl.ws_tab.as<uint32_t>(), sl.ws_ok.as<uint8_t>(), sl.ws_dig.as<uint32_t>(), sl.ws_cap, s,
+        gather ? d.zc_in.dev : nullptr, gather ? sl.packed.p : nullptr, gather ? al16(st.total) : 0);
+    const hipError_t e2 = ws_end(sl, s);
+    CV_TRY(e);
+    CV_TRY(e2);
+    t[3] = now_s();
     CV_TRY(hipStreamSynchronize(s));
     drain.armed = false;
+    t[4] = now_s();
+    for (size_t w = 0; w < words; w++) {
+        uint64_t x = 0;
+        for (int j = 0; j < 16; j++) x |= (uint64_t)(nib[16 * w + j] & 15u) << (4 * j);
+        in.bitmap[b / 64 + w] = x;
+    }
+    if (in.status) std::memcpy(in.status + b, nib + al16(nnib), n);
+    t[5] = now_s();
+    {
+        std::lock_guard<std::mutex> g(ctx->st_mu);
+        for (int k = 0; k < 5; k++) ctx->stats.small[k] += t[k + 1] - t[k];
+        ctx->stats.small_calls++;
+    }
     return CV_OK;
 }
 
-// Host-side key dedupe for the plain entry point: keys[] = distinct key bytes, key_index[i] = its
-// index.  Returns false when the batch does not repeat keys enough for the keyed path to pay (it
-// gives up as soon as more than n/8 distinct keys have been seen).  Flat open addressing on the
-// seeded hash of all 32 key bytes (key_hash32), no per-key allocation.
-static bool dedupe_keys(size_t n, const uint8_t *pk, std::vector<uint8_t> &keys, std::vector<uint32_t> &key_index) {
-    if (n < 64 || n > kAutoKeyedMax) return false;
-    // Cheap early out for batches of (nearly) distinct keys: when the first 256 signatures already
-    // carry more than 192 distinct keys the batch is taken as distinct-keyed without hashing the
-    // rest (a performance guess only: both paths return the same verdicts).
-    if (n > 1024) {
-        constexpr int kS = 256;
-        uint32_t tag[2 * kS];
-        std::fill(tag, tag + 2 * kS, UINT32_MAX);
-        int distinct = 0;
-        for (int i = 0; i < kS; i++) {
-            const uint8_t *k = pk + 32 * (size_t)i;
-            uint32_t bkt = key_hash32(k) & (2 * kS - 1);
-            for (;;) {
-                if (tag[bkt] == UINT32_MAX) {
-                    tag[bkt] = (uint32_t)i;
-                    distinct++;
-                    break;
-                }
-                if (std::memcmp(pk + 32 * (size_t)tag[bkt], k, 32) == 0) break;
-                bkt = (bkt + 1) & (2 * kS - 1);
-            }
-        }
-        if (distinct > 3 * kS / 4) return false;
+// One shard [b, e) of a batch on one device, small form (notary-sized batches): the zero-copy tri-chain form
+// where it applies, else packed into slot 0's pinned staging (or DMAed in place from pinned arrays), moved
+// by one DMA (two above 1 MB: the first overlaps packing the second part) into one device block, verified,
+// and the bitmap (+ status) come back by one DMA.  b is a multiple of 64, so the shard's bitmap words are
+// whole words of the caller's bitmap.
+static int verify_shard_small(cv_ctx *ctx, Device &d, const Opts &o, size_t b, size_t e, const VerifyIn &in,
+                              int threads) {
+    const size_t n = e - b;
+    WorkerPool *pool = n >= 16384 ? &d.workers(threads) : nullptr;
+    const double t_plan = now_s();
+    const Stage st = stage_plan(b, e, in.off, in.len, pool);
+    if (o.small_zc && cvk_tri_zc_ok(&o.plan, (uint32_t)n, (uint32_t)n))
+        return verify_shard_small_zc(ctx, d, o, st, b, in, pool, t_plan,
+                                     o.small_zc == 2 || (o.small_zc == 3 && n >= 2048));
+    const size_t words = (n + 63) / 64;
+    const size_t o_bm = 0, o_st = al16(words * 8), total_out = o_st + al16(n);
+    Slot &sl = d.slot[0];
+    hipStream_t s = nullptr;
+    CV_TRY(slot_stream(d, 0, &s));
+    CV_TRY(slot_events(sl));
+    CV_TRY(sl.pin_in.ensure(st.total));
+    CV_TRY(d.pin_out.ensure(total_out));
+    CV_TRY(sl.packed.ensure(st.total));
+    CV_TRY(d.bitmap.ensure(total_out));
+    uint8_t *h = sl.pin_in.as<uint8_t>();
+    uint8_t *dv = sl.packed.as<uint8_t>();
+    auto drain = on_exit([s] { (void)hipStreamSynchronize(s); });   // error paths: no DMA outlives the call
+    // Two-stage staging above 1 MB of keys + signatures: they are packed and their DMA is issued
+    // first, so it runs while the offsets, lengths and message bytes are packed (notary 65,536:
+    // 1.29-1.34 -> 1.21-1.25 ms p50); below, one DMA (a second DMA's ~6 us would cost more than it hides).
+    const bool two_stage = st.o_off >= ((size_t)1 << 20);
+    // below small_direct_min signatures one packed DMA beats five direct ones even from pinned arrays
+    // (notary 4,096: 0.328 ms p50 packed vs 0.342 direct; 65,536: 1.28 vs 1.10, profiles/r03h_bench.json)
+    if (n >= o.small_direct_min && stage_direct(st, b, in.pk, nullptr, in.sig, in.arena, in.off, in.len)) {
+        CV_TRY(stage_dma_direct(st, dv, b, in.pk, nullptr, in.sig, in.arena, in.off, in.len, s));
+    } else {
+        hipError_t e1 = hipSuccess;
+        stage_pack(st, h, b, in.pk, nullptr, in.sig, in.arena, in.off, in.len, pool, [&] {
+            if (two_stage) e1 = hipMemcpyAsync(dv, h, st.o_off, hipMemcpyHostToDevice, s);
+        });
+        CV_TRY(e1);
+        if (two_stage)
+            CV_TRY(hipMemcpyAsync(dv + st.o_off, h + st.o_off, st.total - st.o_off, hipMemcpyHostToDevice, s));
+        else
+            CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, s));
     }
-    size_t cap = 64;
-    while (cap < 2 * n) cap <<= 1;
-    std::vector<uint32_t> first(cap, UINT32_MAX);   // bucket -> first signature with that key
-    std::vector<uint32_t> uid(cap, 0);              // bucket -> distinct-key index
-    key_index.resize(n);
-    uint32_t nuniq = 0;
-    std::vector<uint32_t> uniq_sig;
-    uniq_sig.reserve(n / 2 + 1);
-    for (size_t i = 0; i < n; i++) {
-        const uint8_t *k = pk + 32 * i;
-        size_t bkt = (size_t)key_hash32(k) & (cap - 1);
-        for (;;) {
-            const uint32_t f = first[bkt];
-            if (f == UINT32_MAX) {
-                first[bkt] = (uint32_t)i;
-                uid[bkt] = nuniq;
-                key_index[i] = nuniq++;
-                uniq_sig.push_back((uint32_t)i);
-                if (8 * (size_t)nuniq > n) return false;   // fewer than eight signatures per key
-                break;
+    uint8_t *dout = d.bitmap.as<uint8_t>();
+    CV_TRY(launch_verify(d, o.plan, sl, (uint32_t)n, dv + st.o_pk, dv + st.o_sig, dv + st.o_ar - st.lo,
+                         reinterpret_cast<const uint64_t *>(dv + st.o_off), reinterpret_cast<const uint32_t *>(dv + st.o_len),
+                         reinterpret_cast<uint64_t *>(dout + o_bm), in.status ? dout + o_st : nullptr, s, nullptr, true));
+    CV_TRY(hipMemcpyAsync(d.pin_out.p, dout, in.status ? o_st + n : words * 8, hipMemcpyDeviceToHost, s));
+    CV_TRY(hipStreamSynchronize(s));
+    drain.armed = false;
+    std::memcpy(in.bitmap + b / 64, d.pin_out.as<uint8_t>() + o_bm, words * 8);
+    if (in.status) std::memcpy(in.status + b, d.pin_out.as<uint8_t>() + o_st, n);
+    return CV_OK;
+}
+
+// ---------------------------------------------------------------- the host pipeline
+// The pipeline's sub-chunk boundaries of [b, e): [first, C, C, ..., the last two balanced]; every boundary
+// but e is b + a multiple of `align`.  With ramp, the sizes after the first double (first, 2 first, ...)
+// until they reach C: each sub-chunk's copy then takes about as long as the kernels of the one before it,
+// so the GPU is not left waiting for a big second sub-chunk while a small first one has long finished.
+static std::vector<size_t> pipe_cuts(size_t b, size_t e, size_t first, size_t C, bool ramp = false, size_t align = 64) {
+    std::vector<size_t> cut{b};
+    if (e <= b) return cut;
+    first = std::max<size_t>(align, first / align * align);
+    C = std::max<size_t>(align, C / align * align);
+    size_t p = b + std::min(e - b, first);
+    cut.push_back(p);
+    size_t step = first;
+    while (p < e) {
+        const size_t rem = e - p;
+        step = ramp ? std::min(C, 2 * step) : C;
+        const size_t m = rem <= step ? rem : rem < 2 * step ? (rem / 2 + align - 1) / align * align : step;
+        p += m;
+        cut.push_back(p);
+    }
+    return cut;
+}
+
+// Copies a finished pipelined call's results into the caller's arrays (waits for them first).  Results of
+// 1 MB and more are copied by the DMA straight into the caller's memory; smaller ones come back through
+// the output's pinned buffer.  The caller holds po.mu.
+static int pipe_finish(Device &d, PipeOut &po) {
+    if (!po.pending) return CV_OK;
+    po.pending = false;
+    CV_TRY(hipSetDevice(d.ordinal));
+    // host-side join: the call's last launch group on every slot stream, then the result copies on the
+    // device's output stream (which carries nothing else, so it neither waits behind the next call's input
+    // copies nor holds a compute stream the next call's kernels run on)
+    for (int k = 0; k < kPipeSlots; k++)
+        if (po.slot_used[k]) CV_TRY(hipEventSynchronize(po.slot_done[k]));
+    constexpr size_t kDirect = 1u << 20;
+    size_t hb = 0;
+    for (int k = 0; k < po.nseg; k++) {
+        const PipeOut::Seg &sg = po.seg[k];
+        if (sg.len >= kDirect)
+            CV_TRY(hipMemcpyAsync(sg.dst, po.dout.as<uint8_t>() + sg.off, sg.len, hipMemcpyDeviceToHost, d.outs));
+        else
+            hb = std::max(hb, sg.off + sg.len);
+    }
+    if (hb) CV_TRY(po.hout.ensure(hb));
+    for (int k = 0; k < po.nseg; k++) {
+        const PipeOut::Seg &sg = po.seg[k];
+        if (sg.len && sg.len < kDirect)
+            CV_TRY(hipMemcpyAsync(po.hout.as<uint8_t>() + sg.off, po.dout.as<uint8_t>() + sg.off, sg.len,
+                                  hipMemcpyDeviceToHost, d.outs));
+    }
+    CV_TRY(hipStreamSynchronize(d.outs));
+    for (int k = 0; k < po.nseg; k++) {
+        const PipeOut::Seg &sg = po.seg[k];
+        if (sg.len && sg.len < kDirect) std::memcpy(sg.dst, po.hout.as<uint8_t>() + sg.off, sg.len);
+    }
+    return CV_OK;
+}
+
+// The device's next output: the older call still holding it is finished first (its results land in its
+// caller's arrays).  Returns it locked.
+static PipeOut &pipe_out(Device &d, int *index, std::unique_lock<std::mutex> &lk, int *rc) {
+    PipeOut &po = d.out[d.out_next];
+    *index = d.out_next;
+    d.out_next = (d.out_next + 1) % kOuts;
+    lk = std::unique_lock<std::mutex>(po.mu);
+    *rc = pipe_finish(d, po);
+    return po;
+}
+
+// The common frame of a pipelined call on one device: the two compute streams, the ring's events and the
+// output's completion events; and the error-path drain.
+struct PipeFrame {
+    Device &d;
+    PipeOut &po;
+    hipStream_t ss[kPipeSlots] = {};
+    bool used[kPipeSlots] = {};
+    double t[5] = {};   // plan, pack, wait, enqueue (seconds)
+    uint64_t chunks = 0, direct = 0;
+    int init() {
+        for (int k = 0; k < kPipeSlots; k++) {
+            CV_TRY(slot_stream(d, k, &ss[k]));
+            CV_TRY(slot_events(d.slot[k]));
+            if (!po.slot_done[k]) CV_TRY(hipEventCreateWithFlags(&po.slot_done[k], hipEventDisableTiming));
+        }
+        for (int q = 0; q < kRing; q++) {
+            if (!d.in_ready[q]) CV_TRY(hipEventCreateWithFlags(&d.in_ready[q], hipEventDisableTiming));
+            if (!d.in_free[q]) CV_TRY(hipEventCreateWithFlags(&d.in_free[q], hipEventDisableTiming));
+        }
+        return CV_OK;
+    }
+    // error paths: drain every queue, forget the ring's state and finish every other pending output of
+    // this device (an earlier call still in flight keeps its results)
+    void drain() {
+        (void)hipStreamSynchronize(d.copy);
+        for (int k = 0; k < kPipeSlots; k++) (void)hipStreamSynchronize(ss[k]);
+        for (int q = 0; q < kRing; q++) d.in_used[q] = d.stage_busy[q] = false;
+        for (PipeOut &o : d.out)
+            if (&o != &po) {
+                std::lock_guard<std::mutex> g(o.mu);
+                (void)pipe_finish(d, o);
             }
-            if (std::memcmp(pk + 32 * (size_t)f, k, 32) == 0) {
-                key_index[i] = uid[bkt];
-                break;
+    }
+    // The next ring block for a stage of `bytes` (waits for a growing block's last reader); the copy
+    // stream waits (on the GPU) for the kernels that last read it.
+    int block(int *q_out, size_t bytes, uint8_t **dv) {
+        const int q = d.ring_next;
+        d.ring_next = (d.ring_next + 1) % kRing;
+        if (bytes > d.inblk[q].cap) {
+            if (d.in_used[q]) CV_TRY(hipEventSynchronize(d.in_free[q]));
+            CV_TRY(d.inblk[q].ensure(bytes));
+        }
+        if (d.in_used[q]) CV_TRY(hipStreamWaitEvent(d.copy, d.in_free[q], 0));
+        *q_out = q;
+        *dv = d.inblk[q].as<uint8_t>();
+        return CV_OK;
+    }
+    // pinned staging block q, free once its previous copy has left it
+    int staging(int q, size_t bytes, uint8_t **h) {
+        if (d.stage_busy[q]) {
+            CV_TRY(hipEventSynchronize(d.in_ready[q]));
+            d.stage_busy[q] = false;
+        }
+        CV_TRY(d.instage[q].ensure(bytes));
+        *h = d.instage[q].as<uint8_t>();
+        return CV_OK;
+    }
+    // after sub-chunk j's copies into block q: compute stream j % 2 waits for them
+    int copied(int q, int j) {
+        CV_TRY(hipEventRecord(d.in_ready[q], d.copy));
+        CV_TRY(hipStreamWaitEvent(ss[j % kPipeSlots], d.in_ready[q], 0));
+        return CV_OK;
+    }
+    // after sub-chunk j's kernels: block q is free once they are done
+    int launched(int q, int j) {
+        CV_TRY(hipEventRecord(d.in_free[q], ss[j % kPipeSlots]));
+        d.in_used[q] = true;
+        used[j % kPipeSlots] = true;
+        chunks++;
+        return CV_OK;
+    }
+    // completion marks per slot stream (pipe_finish joins on the host; no GPU-side join, which would hold
+    // the next call's kernels on that stream until this call had finished)
+    int complete() {
+        for (int k = 0; k < kPipeSlots; k++) {
+            po.slot_used[k] = used[k];
+            if (used[k]) CV_TRY(hipEventRecord(po.slot_done[k], ss[k]));
+        }
+        po.pending = true;
+        po.gen++;
+        return CV_OK;
+    }
+    void account(cv_ctx *ctx) {
+        std::lock_guard<std::mutex> g(ctx->st_mu);
+        Stats &S = ctx->stats;
+        for (int k = 0; k < 4; k++) S.pipe[k] += t[k];
+        S.pipe_calls++;
+        S.pipe_chunks += chunks;
+        S.pipe_direct += direct;
+    }
+};
+
+// Enqueues the pipelined verify of shard [b, e) on device d into output po (held, not pending); returns
+// without waiting for the GPU.  Sub-chunks (multiples of 64 signatures) go through the ring of kRing device
+// input blocks: sub-chunk j's records reach block j % kRing on the device's ONE copy stream — straight from
+// the caller's arrays when they are pinned (stage_direct), else packed by the host threads into pinned
+// staging block j % kRing first — and are verified on slot j % 2's stream, which waits for that copy (event)
+// and marks the block free when its kernels are done.  The copy stream waits (on the GPU) for the kernels
+// that last read a block before refilling it, so copies run up to kRing sub-chunks ahead of the kernels and
+// never queue behind a running kernel on a compute stream.  One copy queue matters: with copies on every
+// slot stream the runtime ran those of one stream as blit kernels (`__amd_rocclr_copyBuffer`, ~37 GB/s, on
+// the CUs beside the verify kernels) and the C2 host call took 13.8-16 ms for 9.6 ms of kernels
+// (profiles/r03c_timeline_*.txt).  Two compute streams: with GPU_MAX_HW_QUEUES = 4 a third shared a
+// hardware queue with the copy stream, whose copies then waited behind its Straus kernel (2.4 ms stalls,
+// profiles/r03e_timeline_pinned_nofill.txt).
+//
+// Keyed shards (explicit keys, or the auto path's dedupe of the shard's keys on the host threads) first
+// resolve their keys against the device's key pool (new keys' tables computed on slot 0's stream, the
+// other stream waits for them), upload the distinct keys and their pool slots once, and stage per
+// sub-chunk key indices instead of keys.
+//
+// async: the sub-chunk plan of the asynchronous entry points (async_chunk, up to twice that for big shards,
+// no ramp — with a call in flight ahead of it the GPU is busy anyway, and bigger launches run closer to the
+// kernels' rate: C2 1M best at 262,144, C5 8M at 524,288, profiles/r03l_async_chunk_sweep.log).
+static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_t b, size_t e, const VerifyIn &in,
+                        int threads, bool async) {
+    const size_t n = e - b;
+    const size_t words = (n + 63) / 64;
+    const size_t o_st = al16(words * 8), total_out = o_st + al16(n);
+    PipeFrame f{d, po};
+    CV_TRY(hipSetDevice(d.ordinal));
+    int rc = f.init();
+    if (rc != CV_OK) return rc;
+    CV_TRY(po.dout.ensure(total_out));
+    uint8_t *dout = po.dout.as<uint8_t>();
+    auto drain = on_exit([&f] { f.drain(); });
+    WorkerPool *pool = &d.workers(threads);
+    const bool keyed = in.keys != nullptr;
+    // ---- keyed: the shard's distinct keys, resident in the pool, uploaded with their slots
+    const uint8_t *keys = in.keys;
+    const size_t nkeys = in.nkeys;
+    const uint32_t *kidx = in.key_index;       // indexed by the caller's record index
+    if (keyed) {
+        double t0 = now_s();
+        if (in.copy_kidx) {                        // the call's own dedupe output: into pinned memory (DMAed in place)
+            CV_TRY(po.kidx.ensure(n * 4));
+            std::memcpy(po.kidx.p, kidx + b, n * 4);
+            kidx = po.kidx.as<uint32_t>() - b;     // so kidx[i] is record i's key, i in [b, e)
+        }
+        for (int k = 0; k < kPipeSlots; k++) CV_TRY(pool_begin(d.kc, f.ss[k]));
+        std::vector<uint32_t> sok;
+        bool prepared = false;
+        rc = key_resolve(d, ctx->key_cap.load(), nkeys, keys, in.used, sok, f.ss[0], &prepared);
+        if (rc != CV_OK) return rc;
+        if (prepared) {                            // the other compute stream waits for the new tables
+            if (!d.kc.kp_ev) CV_TRY(hipEventCreateWithFlags(&d.kc.kp_ev, hipEventDisableTiming));
+            CV_TRY(hipEventRecord(d.kc.kp_ev, f.ss[0]));
+            for (int k = 1; k < kPipeSlots; k++) CV_TRY(hipStreamWaitEvent(f.ss[k], d.kc.kp_ev, 0));
+        }
+        const size_t kb = al16(nkeys * 32) + al16(nkeys * 4);
+        CV_TRY(po.kstage.ensure(kb));
+        CV_TRY(po.kdev.ensure(kb));
+        std::memcpy(po.kstage.p, keys, nkeys * 32);
+        std::memcpy(po.kstage.as<uint8_t>() + al16(nkeys * 32), sok.data(), nkeys * 4);
+        // on the copy stream, ahead of every sub-chunk's records (the sub-chunks' in_ready events cover it)
+        CV_TRY(hipMemcpyAsync(po.kdev.p, po.kstage.p, kb, hipMemcpyHostToDevice, d.copy));
+        f.t[0] += now_s() - t0;
+    }
+    const uint8_t *kdev_keys = po.kdev.as<uint8_t>();
+    const uint32_t *kdev_slot = keyed ? reinterpret_cast<const uint32_t *>(po.kdev.as<uint8_t>() + al16(nkeys * 32)) : nullptr;
+    const size_t ach = std::max(o.async_chunk, std::min(2 * o.async_chunk, n / 16 / 64 * 64));
+    const std::vector<size_t> cut = async ? pipe_cuts(b, e, ach, ach, false) : pipe_cuts(b, e, o.pipe_first, o.pipe_chunk, true);
+    for (size_t j = 0; j + 1 < cut.size(); j++) {
+        const size_t c0 = cut[j], c1 = cut[j + 1], m = c1 - c0;
+        Slot &sl = d.slot[j % kPipeSlots];
+        hipStream_t s = f.ss[j % kPipeSlots];
+        double t0 = now_s();
+        const Stage st = stage_plan(c0, c1, in.off, in.len, pool, keyed);
+        const bool direct = stage_direct(st, c0, in.pk, kidx, in.sig, in.arena, in.off, in.len);
+        double t1 = now_s();
+        f.t[0] += t1 - t0;
+        int q;
+        uint8_t *dv;
+        if ((rc = f.block(&q, st.total, &dv)) != CV_OK) return rc;
+        if (direct) {
+            t0 = now_s();
+            f.t[2] += t0 - t1;
+            CV_TRY(stage_dma_direct(st, dv, c0, in.pk, kidx, in.sig, in.arena, in.off, in.len, d.copy));
+            f.direct++;
+        } else {
+            uint8_t *h;
+            if ((rc = f.staging(q, st.total, &h)) != CV_OK) return rc;
+            t0 = now_s();
+            f.t[2] += t0 - t1;
+            stage_pack(st, h, c0, in.pk, kidx, in.sig, in.arena, in.off, in.len, pool, [] {});
+            t1 = now_s();
+            f.t[1] += t1 - t0;
+            t0 = t1;
+            CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, d.copy));
+            d.stage_busy[q] = true;
+        }
+        if ((rc = f.copied(q, (int)j)) != CV_OK) return rc;
+        const size_t w0 = (c0 - b) / 64;
+        const uint64_t *doff = reinterpret_cast<const uint64_t *>(dv + st.o_off);
+        const uint32_t *dlen = reinterpret_cast<const uint32_t *>(dv + st.o_len);
+        uint64_t *dbm = reinterpret_cast<uint64_t *>(dout) + w0;
+        uint8_t *dst = in.status ? dout + o_st + (c0 - b) : nullptr;
+        if (keyed) {
+            CV_TRY(ensure_verify_ws(sl, m));
+            CV_TRY(ws_begin(d, sl, s));
+            const hipError_t ek = cvk_verify_keyed(&o.plan, (uint32_t)m, kdev_keys, reinterpret_cast<const uint32_t *>(dv + st.o_kidx),
+                                                   kdev_slot, d.kc.ktab.as<uint32_t>(), d.kc.kok.as<uint8_t>(),
+                                                   dv + st.o_sig, dv + st.o_ar - st.lo, doff, dlen, dbm, dst,
+                                                   sl.ws_hs.as<uint32_t>(), sl.ws_R.as<uint32_t>(), sl.ws_ok.as<uint8_t>(),
+                                                   sl.ws_cap, s, nullptr);
+            const hipError_t e2 = ws_end(sl, s);
+            CV_TRY(ek);
+            CV_TRY(e2);
+        } else {
+            CV_TRY(launch_verify(d, o.plan, sl, (uint32_t)m, dv + st.o_pk, dv + st.o_sig, dv + st.o_ar - st.lo, doff, dlen,
+                                 dbm, dst, s, nullptr, false));
+        }
+        if ((rc = f.launched(q, (int)j)) != CV_OK) return rc;
+        f.t[3] += now_s() - t0;
+    }
+    if (keyed) {
+        for (int k = 0; k < kPipeSlots; k++)
+            if (f.used[k]) CV_TRY(pool_end(d.kc, f.ss[k]));   // (the pool's last user: either stream)
+        std::lock_guard<std::mutex> g(ctx->st_mu);
+        ctx->stats.keyed_chunks += f.chunks;
+    }
+    if ((rc = f.complete()) != CV_OK) return rc;
+    drain.armed = false;
+    po.nseg = 0;
+    po.seg[po.nseg++] = {in.bitmap + b / 64, 0, words * 8};
+    if (in.status) po.seg[po.nseg++] = {in.status + b, o_st, n};
+    f.account(ctx);
+    return CV_OK;
+}
+
+// Enqueues the pipelined Merkle ids of transactions [t0, t1) on device d into output po: sub-chunks of about
+// merkle_chunk leaves (whole transactions), each staged (direct DMA from pinned arrays, else packed) into a
+// ring block by the copy stream and hashed on slot j % 2's stream (leaf kernel + tree kernel, leaf digests in
+// the slot's workspace); the ids and statuses go to po's device buffer and come back once.  The leaf bytes
+// dominate (C3: 2 GB per 1M transactions), so the call is bound by the copy and the kernels overlap it.
+struct MerkleIn {
+    const uint8_t *arena;
+    const uint64_t *off;
+    const uint32_t *len;
+    const uint32_t *txb;   // ntx + 1 absolute leaf indices
+    uint8_t *ids, *status;
+};
+static int merkle_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_t t0, size_t t1, const MerkleIn &in,
+                          int threads) {
+    const size_t nt = t1 - t0;
+    const size_t o_st = al16(nt * 32), total_out = o_st + al16(nt);
+    PipeFrame f{d, po};
+    CV_TRY(hipSetDevice(d.ordinal));
+    int rc = f.init();
+    if (rc != CV_OK) return rc;
+    CV_TRY(po.dout.ensure(total_out));
+    uint8_t *dout = po.dout.as<uint8_t>();
+    auto drain = on_exit([&f] { f.drain(); });
+    WorkerPool *pool = &d.workers(threads);
+    // sub-chunk cuts: whole transactions, about merkle_chunk leaves each (at least one transaction)
+    std::vector<size_t> cut{t0};
+    while (cut.back() < t1) {
+        const size_t c = cut.back();
+        const uint64_t want = (uint64_t)in.txb[c] + o.merkle_chunk;
+        size_t nx = (size_t)(std::upper_bound(in.txb + c + 1, in.txb + t1 + 1, (uint32_t)std::min<uint64_t>(want, UINT32_MAX)) - in.txb) - 1;
+        nx = std::max(nx, c + 1);
+        cut.push_back(std::min(nx, t1));
+    }
+    for (size_t j = 0; j + 1 < cut.size(); j++) {
+        const size_t c0 = cut[j], c1 = cut[j + 1];
+        Slot &sl = d.slot[j % kPipeSlots];
+        hipStream_t s = f.ss[j % kPipeSlots];
+        double ta = now_s();
+        const MStage st = mstage_plan(c0, c1, in.txb, in.off, in.len, pool);
+        const bool direct = mstage_direct(st, in.txb, in.arena, in.off, in.len);
+        double tb = now_s();
+        f.t[0] += tb - ta;
+        int q;
+        uint8_t *dv;
+        if ((rc = f.block(&q, st.total, &dv)) != CV_OK) return rc;
+        if (direct) {
+            ta = now_s();
+            f.t[2] += ta - tb;
+            CV_TRY(mstage_dma_direct(st, dv, in.txb, in.arena, in.off, in.len, d.copy));
+            f.direct++;
+        } else {
+            uint8_t *h;
+            if ((rc = f.staging(q, st.total, &h)) != CV_OK) return rc;
+            ta = now_s();
+            f.t[2] += ta - tb;
+            mstage_pack(st, h, in.txb, in.arena, in.off, in.len, pool);
+            tb = now_s();
+            f.t[1] += tb - ta;
+            ta = tb;
+            CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, d.copy));
+            d.stage_busy[q] = true;
+        }
+        if ((rc = f.copied(q, (int)j)) != CV_OK) return rc;
+        const size_t nl = st.l1 - st.l0;
+        CV_TRY(ws_begin(d, sl, s));
+        hipError_t ek = sl.mdig.ensure(nl * 32 + 32);
+        if (ek == hipSuccess)
+            ek = cvk_merkle((uint32_t)(c1 - c0), (uint32_t)nl, (uint32_t)st.l0, dv + st.o_ar - st.lo,
+                            reinterpret_cast<const uint64_t *>(dv + st.o_off), reinterpret_cast<const uint32_t *>(dv + st.o_len),
+                            reinterpret_cast<const uint32_t *>(dv + st.o_txb), sl.mdig.as<uint32_t>(),
+                            dout + (c0 - t0) * 32, dout + o_st + (c0 - t0), s);
+        const hipError_t e2 = ws_end(sl, s);
+        CV_TRY(ek);
+        CV_TRY(e2);
+        if ((rc = f.launched(q, (int)j)) != CV_OK) return rc;
+        f.t[3] += now_s() - ta;
+    }
+    if ((rc = f.complete()) != CV_OK) return rc;
+    drain.armed = false;
+    po.nseg = 0;
+    po.seg[po.nseg++] = {in.ids + t0 * 32, 0, nt * 32};
+    if (in.status) po.seg[po.nseg++] = {in.status + t0, o_st, nt};
+    f.account(ctx);
+    {
+        std::lock_guard<std::mutex> g(ctx->st_mu);
+        ctx->stats.merkle_chunks += cut.size() - 1;
+    }
+    return CV_OK;
+}
+
+// A pipelined call's part on one device, for its ticket: (device index, output index, gen).
+using Part = std::array<uint64_t, 3>;
+
+// One shard of a verify call on device d.  Synchronous calls: small plain shards take the one-DMA (or
+// zero-copy) path, the rest the pipeline and wait for it; asynchronous calls always take the pipeline and
+// record their output in *part.
+static size_t dev_index(cv_ctx *ctx, const Device &d) {
+    for (size_t k = 0; k < ctx->devs.size(); k++)
+        if (ctx->devs[k].get() == &d) return k;
+    return 0;
+}
+
+// One shard of a verify call on device d.  Synchronous calls: small plain shards take the one-DMA (or
+// zero-copy) path, the rest the pipeline and wait for it; asynchronous calls always take the pipeline and
+// record their output in *part.  Auto-keyed shards dedupe their own keys first (on the device's host
+// threads) and fall back to the plain path when they repeat fewer than eight times per key.
+static int verify_shard(cv_ctx *ctx, Device &d, const Opts &o, size_t b, size_t e, const VerifyIn &in0, int threads,
+                        bool async, Part *part) {
+    const size_t n = e - b;
+    if (n == 0) return CV_OK;
+    if (n > 0xffffffffull) return CV_E_TOO_LARGE;
+    CV_TRY(hipSetDevice(d.ordinal));
+    VerifyIn in = in0;
+    std::vector<uint8_t> dkeys, used;
+    std::vector<uint32_t> didx;
+    if (in.auto_keyed) {
+        const double t0 = now_s();
+        in.auto_keyed = false;
+        if (dedupe_keys(n, in.pk + b * 32, dkeys, didx, &d.workers(threads), false)) {
+            in.keys = dkeys.data();
+            in.nkeys = dkeys.size() / 32;
+            in.key_index = didx.data() - b;        // indexed by the caller's record index
+            in.copy_kidx = true;
+        }
+        std::lock_guard<std::mutex> g(ctx->st_mu);
+        ctx->stats.pipe[0] += now_s() - t0;
+    } else if (in.keys) {
+        used.assign(in.nkeys, 0);
+        for (size_t i = b; i < e; i++) {
+            if (in.key_index[i] >= in.nkeys) return CV_E_ARGS;
+            used[in.key_index[i]] = 1;
+        }
+        in.used = used.data();
+    }
+    const bool keyed = in.keys != nullptr;
+    if (!async && !keyed && n <= o.pipe_min) return verify_shard_small(ctx, d, o, b, e, in, threads);
+    int k = 0, rc = CV_OK;
+    std::unique_lock<std::mutex> lk;
+    PipeOut &po = pipe_out(d, &k, lk, &rc);
+    if (rc != CV_OK) return rc;
+    rc = pipe_enqueue(ctx, d, o, po, b, e, in, threads, async);
+    if (rc != CV_OK) return rc;
+    if (keyed) {
+        std::lock_guard<std::mutex> g(ctx->st_mu);
+        ctx->stats.keyed_calls++;
+    }
+    if (async) {
+        *part = {(uint64_t)dev_index(ctx, d), (uint64_t)k, po.gen};
+        return CV_OK;
+    }
+    const double t0 = now_s();
+    rc = pipe_finish(d, po);
+    std::lock_guard<std::mutex> g(ctx->st_mu);
+    ctx->stats.pipe[4] += now_s() - t0;
+    return rc;
+}
+
+// A ticket for the parts of an asynchronous call.  Tickets whose every part is done (its output finished or
+// reused by a later call) are pruned here, so a caller that drops tickets does not grow the map.
+static uint64_t ticket_add(cv_ctx *ctx, std::vector<Part> parts) {
+    std::lock_guard<std::mutex> g(ctx->tk_mu);
+    if (ctx->tickets.size() >= 64) {
+        for (auto it = ctx->tickets.begin(); it != ctx->tickets.end();) {
+            bool live = false;
+            for (const Part &p : it->second) {
+                PipeOut &po = ctx->devs[p[0]]->out[p[1]];
+                std::lock_guard<std::mutex> pg(po.mu);
+                live = live || (po.gen == p[2] && po.pending);
             }
-            bkt = (bkt + 1) & (cap - 1);
+            it = live ? std::next(it) : ctx->tickets.erase(it);
         }
     }
-    keys.resize(32 * (size_t)nuniq);
-    for (uint32_t u = 0; u < nuniq; u++) std::memcpy(keys.data() + 32 * (size_t)u, pk + 32 * (size_t)uniq_sig[u], 32);
-    return true;
+    const uint64_t t = ++ctx->next_ticket;
+    ctx->tickets.emplace(t, std::move(parts));
+    return t;
+}
+
+// Waits for parts (each output's lock only — no device lock, so other threads keep submitting).
+static int parts_wait(cv_ctx *ctx, const std::vector<Part> &parts) {
+    int rc = CV_OK;
+    for (const Part &p : parts) {
+        Device &d = *ctx->devs[p[0]];
+        PipeOut &po = d.out[p[1]];
+        std::lock_guard<std::mutex> g(po.mu);
+        if (po.gen != p[2] || !po.pending) continue;   // already finished (its output was reused)
+        const int r = pipe_finish(d, po);
+        if (r != CV_OK) rc = r;
+    }
+    return rc;
+}
+
+// The keyed decision of the plain entry points: batches the tri-chain latency form takes (n <= tri_max)
+// stay on the plain path whatever their keys — there the per-signature chain is the latency, and the tri
+// chain beats the keyed comb chain (notary batch of 4,096 with 64 signers 0.47 vs 0.34 ms distinct).
+static bool want_keyed(const Opts &o, size_t n, const uint8_t *pk) {
+    if (!o.auto_keyed || n <= o.plan.tri_max) return false;
+    return dedupe_gate(n, pk);
 }
 
 extern "C" {
@@ -1435,7 +2011,9 @@ int cv_diag_dedupe_keys(size_t n, const uint8_t *pk, uint32_t *key_index, size_t
     if (!pk || !key_index || !nkeys) return CV_E_ARGS;
     std::vector<uint8_t> keys;
     std::vector<uint32_t> idx;
-    if (!dedupe_keys(n, pk, keys, idx)) {
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    std::unique_ptr<WorkerPool> pool(n >= 65536 ? new WorkerPool((int)std::min(7u, hw - 1)) : nullptr);
+    if (!dedupe_keys(n, pk, keys, idx, pool.get())) {
         *nkeys = 0;
         return 0;
     }
@@ -1444,29 +2022,45 @@ int cv_diag_dedupe_keys(size_t n, const uint8_t *pk, uint32_t *key_index, size_t
     return 1;
 }
 
+static int verify_call(cv_ctx *ctx, size_t n, VerifyIn in, uint64_t *ticket) {
+    const Opts o = ctx->opts();
+    const bool async = ticket != nullptr;
+    if (!in.keys && want_keyed(o, n, in.pk)) in.auto_keyed = true;
+    std::vector<Part> parts(ctx->devs.size(), Part{UINT64_MAX, 0, 0});
+    const int rc = dispatch(ctx, o, n, 64, [&](Device &d, size_t b, size_t e, int threads) {
+        Part p{UINT64_MAX, 0, 0};
+        const int r = verify_shard(ctx, d, o, b, e, in, threads, async, &p);
+        if (r == CV_OK && async && p[0] != UINT64_MAX) parts[dev_index(ctx, d)] = p;
+        return r;
+    });
+    std::vector<Part> live;
+    for (const Part &p : parts)
+        if (p[0] != UINT64_MAX) live.push_back(p);
+    if (rc != CV_OK) {
+        // a shard failed: the shards that did enqueue are waited for here — nothing may read the caller's
+        // arrays or write its bitmap after an error return
+        (void)parts_wait(ctx, live);
+        return rc;
+    }
+    if (async) *ticket = live.empty() ? 0 : ticket_add(ctx, std::move(live));
+    return CV_OK;
+}
+
 int cv_ed25519_verify_batch(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg_arena,
                             const uint64_t *msg_off, const uint32_t *msg_len, uint64_t *verdict_bitmap,
                             uint8_t *status) {
     if (!ctx) return CV_E_ARGS;
     if (n == 0) return CV_OK;
     if (!pk || !sig || !msg_off || !msg_len || !verdict_bitmap) return CV_E_ARGS;
-    std::lock_guard<std::mutex> g(ctx->mu);
-    std::vector<uint8_t> keys;
-    std::vector<uint32_t> key_index;
-    // Batches the tri-chain latency form takes (n <= 4,096) stay on the plain path whatever their keys:
-    // there the per-signature chain is the latency, and the tri chain (128 doublings spread over four
-    // quads, decodes beside the scalars) beats the keyed comb chain (hash, 60 quad doublings + 96
-    // additions, then the inversion): notary batch of 4,096 with 64 signers 0.47 vs 0.34 ms distinct.
-    if (n > cvk_get_tri_max() && dedupe_keys(n, pk, keys, key_index)) {
-        const size_t nk = keys.size() / 32;
-        return for_each_shard(ctx, n, [&](Device &d, size_t b, size_t e, int) {
-            return verify_shard_keyed(ctx->key_cap, d, b, e, nk, keys.data(), key_index.data(), sig, msg_arena, msg_off,
-                                      msg_len, verdict_bitmap, status);
-        });
-    }
-    return for_each_shard(ctx, n, [&](Device &d, size_t b, size_t e, int threads) {
-        return verify_shard(d, b, e, pk, sig, msg_arena, msg_off, msg_len, verdict_bitmap, status, threads);
-    });
+    VerifyIn in;
+    in.pk = pk;
+    in.sig = sig;
+    in.arena = msg_arena;
+    in.off = msg_off;
+    in.len = msg_len;
+    in.bitmap = verdict_bitmap;
+    in.status = status;
+    return verify_call(ctx, n, in, nullptr);
 }
 
 int cv_ed25519_verify_batch_async(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint8_t *sig,
@@ -1476,62 +2070,29 @@ int cv_ed25519_verify_batch_async(cv_ctx *ctx, size_t n, const uint8_t *pk, cons
     *ticket = 0;
     if (n == 0) return CV_OK;
     if (!pk || !sig || !msg_off || !msg_len || !verdict_bitmap) return CV_E_ARGS;
-    std::lock_guard<std::mutex> g(ctx->mu);
-    std::vector<std::array<uint64_t, 3>> parts(ctx->devs.size(), {UINT64_MAX, 0, 0});
-    const int rc = for_each_shard(ctx, n, [&](Device &d, size_t b, size_t e, int threads) {
-        if (e - b > 0xffffffffull) return CV_E_TOO_LARGE;
-        CV_TRY(hipSetDevice(d.ordinal));
-        int k = 0;
-        PipeOut &po = pipe_out(d, &k);
-        int r = pipe_finish(d, po);               // the slot's previous call (its verdicts land first)
-        if (r == CV_OK)
-            r = pipe_enqueue(d, po, b, e, pk, sig, msg_arena, msg_off, msg_len, verdict_bitmap, status, threads, true);
-        if (r == CV_OK) parts[(size_t)(&d - ctx->devs.data())] = {(uint64_t)(&d - ctx->devs.data()), (uint64_t)k, po.gen};
-        return r;
-    });
-    if (rc != CV_OK) {
-        // a shard failed: the shards that did enqueue are waited for and dropped here — nothing may
-        // read the caller's arrays or write its bitmap after an error return
-        for (const auto &p : parts) {
-            if (p[0] == UINT64_MAX) continue;
-            Device &d = ctx->devs[p[0]];
-            PipeOut &po = d.out[p[1]];
-            (void)hipSetDevice(d.ordinal);
-            for (int k = 0; k < kSlots; k++)
-                if (po.slot_used[k]) (void)hipEventSynchronize(po.slot_done[k]);
-            if (d.copy) (void)hipStreamSynchronize(d.copy);
-            po.pending = false;
-        }
-        return rc;
-    }
-    std::vector<std::array<uint64_t, 3>> live;
-    for (const auto &p : parts)
-        if (p[0] != UINT64_MAX) live.push_back(p);
-    *ticket = ++ctx->next_ticket;
-    ctx->tickets.emplace(*ticket, std::move(live));
-    return CV_OK;
+    VerifyIn in;
+    in.pk = pk;
+    in.sig = sig;
+    in.arena = msg_arena;
+    in.off = msg_off;
+    in.len = msg_len;
+    in.bitmap = verdict_bitmap;
+    in.status = status;
+    return verify_call(ctx, n, in, ticket);
 }
 
 int cv_wait(cv_ctx *ctx, uint64_t ticket) {
     if (!ctx) return CV_E_ARGS;
     if (ticket == 0) return CV_OK;
-    std::lock_guard<std::mutex> g(ctx->mu);
-    auto it = ctx->tickets.find(ticket);
-    if (it == ctx->tickets.end()) return CV_E_ARGS;
-    int rc = CV_OK;
-    for (const auto &p : it->second) {
-        Device &d = ctx->devs[p[0]];
-        PipeOut &po = d.out[p[1]];
-        if (po.gen != p[2] || !po.pending) continue;   // already copied (its slot was reused)
-        if (hipSetDevice(d.ordinal) != hipSuccess) {
-            rc = CV_E_HIP;
-            continue;
-        }
-        const int r = pipe_finish(d, po);
-        if (r != CV_OK) rc = r;
+    std::vector<Part> parts;
+    {
+        std::lock_guard<std::mutex> g(ctx->tk_mu);
+        auto it = ctx->tickets.find(ticket);
+        if (it == ctx->tickets.end()) return CV_E_ARGS;
+        parts = std::move(it->second);
+        ctx->tickets.erase(it);
     }
-    ctx->tickets.erase(it);
-    return rc;
+    return parts_wait(ctx, parts);
 }
 
 int cv_ed25519_verify_batch_keyed(cv_ctx *ctx, size_t n, size_t nkeys, const uint8_t *keys, const uint32_t *key_index,
@@ -1540,29 +2101,39 @@ int cv_ed25519_verify_batch_keyed(cv_ctx *ctx, size_t n, size_t nkeys, const uin
     if (!ctx) return CV_E_ARGS;
     if (n == 0) return CV_OK;
     if (!keys || !key_index || !sig || !msg_off || !msg_len || !verdict_bitmap || nkeys == 0) return CV_E_ARGS;
-    std::lock_guard<std::mutex> g(ctx->mu);
-    return for_each_shard(ctx, n, [&](Device &d, size_t b, size_t e, int) {
-        return verify_shard_keyed(ctx->key_cap, d, b, e, nkeys, keys, key_index, sig, msg_arena, msg_off, msg_len,
-                                  verdict_bitmap, status);
-    });
+    if (nkeys > 0xffffffffull) return CV_E_TOO_LARGE;
+    VerifyIn in;
+    in.sig = sig;
+    in.arena = msg_arena;
+    in.off = msg_off;
+    in.len = msg_len;
+    in.keys = keys;
+    in.key_index = key_index;
+    in.nkeys = nkeys;
+    in.bitmap = verdict_bitmap;
+    in.status = status;
+    return verify_call(ctx, n, in, nullptr);
 }
 
 int cv_key_cache_reserve(cv_ctx *ctx, size_t max_keys) {
     if (!ctx || max_keys == 0 || max_keys > 0x7fffffffull) return CV_E_ARGS;
-    std::lock_guard<std::mutex> g(ctx->mu);
-    ctx->key_cap = (uint32_t)max_keys;
+    ctx->key_cap.store((uint32_t)max_keys);
     return CV_OK;
 }
 
 int cv_key_cache_stats(cv_ctx *ctx, int device, uint64_t *out4) {
     if (!ctx || !out4) return CV_E_ARGS;
-    std::lock_guard<std::mutex> g(ctx->mu);
     Device *d = find_dev(ctx, device);
     if (!d) return CV_E_ARGS;
-    out4[0] = d->kc.map.size();
-    out4[1] = d->kc.cap;
-    out4[2] = d->kc.hits;
-    out4[3] = d->kc.misses;
+    out4[0] = out4[1] = out4[2] = out4[3] = 0;
+    for (auto &dp : ctx->devs) {            // every (virtual) device of that ordinal
+        if (dp->ordinal != device) continue;
+        std::lock_guard<std::mutex> g(dp->mu);
+        out4[0] += dp->kc.map.size();
+        out4[1] += dp->kc.cap;
+        out4[2] += dp->kc.hits;
+        out4[3] += dp->kc.misses;
+    }
     return CV_OK;
 }
 
@@ -1586,6 +2157,7 @@ static int sign_shard(Device &d, size_t b, size_t e, const uint8_t *seed, const 
     CV_TRY(d.pk.ensure(n * 32));
     CV_TRY(d.sig.ensure(n * 64));
     hipStream_t s = d.stream;
+    auto drain = on_exit([s] { (void)hipStreamSynchronize(s); });   // the pageable copies read the caller's arrays
     CV_TRY(hipMemcpyAsync(d.seed.p, seed + b * 32, n * 32, hipMemcpyHostToDevice, s));
     if (hi > lo) CV_TRY(hipMemcpyAsync(d.arena.p, arena + lo, hi - lo, hipMemcpyHostToDevice, s));
     CV_TRY(hipMemcpyAsync(d.off.p, off + b, n * 8, hipMemcpyHostToDevice, s));
@@ -1595,6 +2167,7 @@ static int sign_shard(Device &d, size_t b, size_t e, const uint8_t *seed, const 
     CV_TRY(hipMemcpyAsync(pk + b * 32, d.pk.p, n * 32, hipMemcpyDeviceToHost, s));
     CV_TRY(hipMemcpyAsync(sig + b * 64, d.sig.p, n * 64, hipMemcpyDeviceToHost, s));
     CV_TRY(hipStreamSynchronize(s));
+    drain.armed = false;
     return CV_OK;
 }
 
@@ -1603,16 +2176,18 @@ int cv_ed25519_sign_batch(cv_ctx *ctx, size_t n, const uint8_t *seed, const uint
     if (!ctx) return CV_E_ARGS;
     if (n == 0) return CV_OK;
     if (!seed || !msg_off || !msg_len || !pk_out || !sig_out) return CV_E_ARGS;
-    std::lock_guard<std::mutex> g(ctx->mu);
-    return for_each_shard(ctx, n, [&](Device &d, size_t b, size_t e, int) {
+    const Opts o = ctx->opts();
+    return dispatch(ctx, o, n, 64, [&](Device &d, size_t b, size_t e, int) {
         return sign_shard(d, b, e, seed, msg_arena, msg_off, msg_len, pk_out, sig_out);
     });
 }
 
 // ---------------------------------------------------------------- Merkle (host buffers)
-int cv_merkle_tx_ids_ex(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
-                        const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, uint8_t *ids, uint8_t *tx_status) {
+static int merkle_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
+                       const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, uint8_t *ids, uint8_t *tx_status,
+                       uint64_t *ticket) {
     if (!ctx) return CV_E_ARGS;
+    if (ticket) *ticket = 0;
     if (ntx == 0) return CV_OK;
     if (!tx_leaf_begin || !ids) return CV_E_ARGS;
     const size_t nleaves = tx_leaf_begin[ntx];
@@ -1621,32 +2196,58 @@ int cv_merkle_tx_ids_ex(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, cons
         if (tx_leaf_begin[t + 1] < tx_leaf_begin[t]) return CV_E_ARGS;
     if (nleaves && (!leaf_off || !leaf_len)) return CV_E_ARGS;
     if (ntx > 0xfffffffeull || nleaves > 0xffffffffull) return CV_E_TOO_LARGE;
-    std::lock_guard<std::mutex> g(ctx->mu);
-    Device &d = ctx->devs[0];
-    CV_TRY(hipSetDevice(d.ordinal));
-    uint64_t hi = 0;
-    for (size_t i = 0; i < nleaves; i++) hi = std::max<uint64_t>(hi, leaf_off[i] + leaf_len[i]);
-    CV_TRY(d.arena.ensure(hi + 16));
-    CV_TRY(d.off.ensure(nleaves * 8 + 8));
-    CV_TRY(d.len.ensure(nleaves * 4 + 4));
-    CV_TRY(d.tx_begin.ensure((ntx + 1) * 4));
-    CV_TRY(d.digest.ensure(nleaves * 32 + 32));
-    CV_TRY(d.ids.ensure(ntx * 32));
-    CV_TRY(d.status.ensure(ntx));
-    hipStream_t s = d.stream;
-    if (hi) CV_TRY(hipMemcpyAsync(d.arena.p, leaf_arena, hi, hipMemcpyHostToDevice, s));
-    if (nleaves) {
-        CV_TRY(hipMemcpyAsync(d.off.p, leaf_off, nleaves * 8, hipMemcpyHostToDevice, s));
-        CV_TRY(hipMemcpyAsync(d.len.p, leaf_len, nleaves * 4, hipMemcpyHostToDevice, s));
+    Opts o = ctx->opts();
+    // shards of whole transactions: the leaf work per transaction (Σ blocks) decides, so a batch is cut by
+    // leaves — transaction counts scaled so each device gets ~1/k of the leaves (C3: uniform)
+    o.shard_min = std::max<size_t>(1, o.shard_min / 8);          // ~4,096 signatures' worth of transactions
+    o.spread_min = std::max<size_t>(1, o.spread_min / 8);
+    MerkleIn in{leaf_arena, leaf_off, leaf_len, tx_leaf_begin, ids, tx_status};
+    {
+        std::lock_guard<std::mutex> g(ctx->st_mu);
+        ctx->stats.merkle_calls++;
     }
-    CV_TRY(hipMemcpyAsync(d.tx_begin.p, tx_leaf_begin, (ntx + 1) * 4, hipMemcpyHostToDevice, s));
-    CV_TRY(cvk_merkle((uint32_t)ntx, (uint32_t)nleaves, d.arena.as<uint8_t>(), d.off.as<uint64_t>(),
-                      d.len.as<uint32_t>(), d.tx_begin.as<uint32_t>(), d.digest.as<uint32_t>(), d.ids.as<uint8_t>(),
-                      d.status.as<uint8_t>(), s));
-    CV_TRY(hipMemcpyAsync(ids, d.ids.p, ntx * 32, hipMemcpyDeviceToHost, s));
-    if (tx_status) CV_TRY(hipMemcpyAsync(tx_status, d.status.p, ntx, hipMemcpyDeviceToHost, s));
-    CV_TRY(hipStreamSynchronize(s));
+    std::vector<Part> parts(ctx->devs.size(), Part{UINT64_MAX, 0, 0});
+    const int rc = dispatch(ctx, o, ntx, 1, [&](Device &d, size_t t0, size_t t1, int threads) {
+        if (t1 <= t0) return CV_OK;
+        CV_TRY(hipSetDevice(d.ordinal));
+        int k = 0, r = CV_OK;
+        std::unique_lock<std::mutex> lk;
+        PipeOut &po = pipe_out(d, &k, lk, &r);
+        if (r != CV_OK) return r;
+        r = merkle_enqueue(ctx, d, o, po, t0, t1, in, threads);
+        if (r != CV_OK) return r;
+        if (ticket) {
+            parts[dev_index(ctx, d)] = {(uint64_t)dev_index(ctx, d), (uint64_t)k, po.gen};
+            return CV_OK;
+        }
+        return pipe_finish(d, po);
+    });
+    std::vector<Part> live;
+    for (const Part &p : parts)
+        if (p[0] != UINT64_MAX) live.push_back(p);
+    if (rc != CV_OK) {
+        (void)parts_wait(ctx, live);
+        return rc;
+    }
+    if (ticket) *ticket = live.empty() ? 0 : ticket_add(ctx, std::move(live));
     return CV_OK;
+}
+
+int cv_merkle_tx_ids_ex(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
+                        const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, uint8_t *ids, uint8_t *tx_status) {
+    return merkle_call(ctx, ntx, leaf_arena, leaf_off, leaf_len, tx_leaf_begin, ids, tx_status, nullptr);
+}
+
+int cv_merkle_tx_ids_async(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
+                           const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, uint8_t *ids, uint8_t *tx_status,
+                           uint64_t *ticket) {
+    if (!ticket) return CV_E_ARGS;
+    return merkle_call(ctx, ntx, leaf_arena, leaf_off, leaf_len, tx_leaf_begin, ids, tx_status, ticket);
+}
+
+int cv_merkle_tx_ids(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
+                     const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, uint8_t *ids) {
+    return merkle_call(ctx, ntx, leaf_arena, leaf_off, leaf_len, tx_leaf_begin, ids, nullptr, nullptr);
 }
 
 int cv_partial_merkle_verify(cv_ctx *ctx, size_t ntrees, size_t nnodes, const uint8_t *kind, const uint32_t *left,
@@ -1664,53 +2265,57 @@ int cv_partial_merkle_verify(cv_ctx *ctx, size_t ntrees, size_t nnodes, const ui
         return CV_E_ARGS;
     for (size_t t = 0; t < ntrees; t++)
         if (tree_begin[t + 1] < tree_begin[t] || check_begin[t + 1] < check_begin[t]) return CV_E_ARGS;
-    std::lock_guard<std::mutex> g(ctx->mu);
-    Device &d = ctx->devs[0];
-    CV_TRY(hipSetDevice(d.ordinal));
-    auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
-    const size_t o_kind = 0, o_left = up16(o_kind + nnodes), o_right = up16(o_left + 4 * nnodes);
-    const size_t o_hash = up16(o_right + 4 * nnodes), o_tb = up16(o_hash + 32 * nnodes);
-    const size_t o_root = up16(o_tb + 4 * (ntrees + 1)), o_check = up16(o_root + 32 * ntrees);
-    const size_t o_cb = up16(o_check + 32 * ncheck), o_verdict = up16(o_cb + 4 * (ntrees + 1));
-    const size_t o_status = up16(o_verdict + ntrees), o_dig = up16(o_status + ntrees);
-    const size_t o_flag = up16(o_dig + 32 * nnodes), total = up16(o_flag + nnodes + 1);
-    CV_TRY(d.pmt.ensure(total));
-    uint8_t *base = d.pmt.as<uint8_t>();
-    hipStream_t s = d.stream;
-    if (nnodes) {
-        CV_TRY(hipMemcpyAsync(base + o_kind, kind, nnodes, hipMemcpyHostToDevice, s));
-        CV_TRY(hipMemcpyAsync(base + o_left, left, 4 * nnodes, hipMemcpyHostToDevice, s));
-        CV_TRY(hipMemcpyAsync(base + o_right, right, 4 * nnodes, hipMemcpyHostToDevice, s));
-        CV_TRY(hipMemcpyAsync(base + o_hash, leaf_hash, 32 * nnodes, hipMemcpyHostToDevice, s));
-    }
-    CV_TRY(hipMemcpyAsync(base + o_tb, tree_begin, 4 * (ntrees + 1), hipMemcpyHostToDevice, s));
-    CV_TRY(hipMemcpyAsync(base + o_root, root, 32 * ntrees, hipMemcpyHostToDevice, s));
-    if (ncheck) CV_TRY(hipMemcpyAsync(base + o_check, check, 32 * ncheck, hipMemcpyHostToDevice, s));
-    CV_TRY(hipMemcpyAsync(base + o_cb, check_begin, 4 * (ntrees + 1), hipMemcpyHostToDevice, s));
-    CV_TRY(cvk_pmt_verify((uint32_t)ntrees, base + o_kind, reinterpret_cast<uint32_t *>(base + o_left),
-                          reinterpret_cast<uint32_t *>(base + o_right), base + o_hash,
-                          reinterpret_cast<uint32_t *>(base + o_tb), base + o_root, base + o_check,
-                          reinterpret_cast<uint32_t *>(base + o_cb), reinterpret_cast<uint32_t *>(base + o_dig),
-                          base + o_flag, base + o_verdict, base + o_status, s));
-    CV_TRY(hipMemcpyAsync(verdict, base + o_verdict, ntrees, hipMemcpyDeviceToHost, s));
-    if (status) CV_TRY(hipMemcpyAsync(status, base + o_status, ntrees, hipMemcpyDeviceToHost, s));
-    CV_TRY(hipStreamSynchronize(s));
-    return CV_OK;
-}
-
-int cv_merkle_tx_ids(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
-                     const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, uint8_t *ids) {
-    return cv_merkle_tx_ids_ex(ctx, ntx, leaf_arena, leaf_off, leaf_len, tx_leaf_begin, ids, nullptr);
+    Opts o = ctx->opts();
+    o.shard_min = o.spread_min = SIZE_MAX;   // one device, the least loaded (tear-off batches are small)
+    return dispatch(ctx, o, ntrees, 1, [&](Device &d, size_t, size_t, int) {
+        CV_TRY(hipSetDevice(d.ordinal));
+        auto up16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+        const size_t o_kind = 0, o_left = up16(o_kind + nnodes), o_right = up16(o_left + 4 * nnodes);
+        const size_t o_hash = up16(o_right + 4 * nnodes), o_tb = up16(o_hash + 32 * nnodes);
+        const size_t o_root = up16(o_tb + 4 * (ntrees + 1)), o_check = up16(o_root + 32 * ntrees);
+        const size_t o_cb = up16(o_check + 32 * ncheck), o_verdict = up16(o_cb + 4 * (ntrees + 1));
+        const size_t o_status = up16(o_verdict + ntrees), o_dig = up16(o_status + ntrees);
+        const size_t o_flag = up16(o_dig + 32 * nnodes), total = up16(o_flag + nnodes + 1);
+        CV_TRY(d.pmt.ensure(total));
+        uint8_t *base = d.pmt.as<uint8_t>();
+        hipStream_t s = d.stream;
+        auto drain = on_exit([s] { (void)hipStreamSynchronize(s); });
+        if (nnodes) {
+            CV_TRY(hipMemcpyAsync(base + o_kind, kind, nnodes, hipMemcpyHostToDevice, s));
+            CV_TRY(hipMemcpyAsync(base + o_left, left, 4 * nnodes, hipMemcpyHostToDevice, s));
+            CV_TRY(hipMemcpyAsync(base + o_right, right, 4 * nnodes, hipMemcpyHostToDevice, s));
+            CV_TRY(hipMemcpyAsync(base + o_hash, leaf_hash, 32 * nnodes, hipMemcpyHostToDevice, s));
+        }
+        CV_TRY(hipMemcpyAsync(base + o_tb, tree_begin, 4 * (ntrees + 1), hipMemcpyHostToDevice, s));
+        CV_TRY(hipMemcpyAsync(base + o_root, root, 32 * ntrees, hipMemcpyHostToDevice, s));
+        if (ncheck) CV_TRY(hipMemcpyAsync(base + o_check, check, 32 * ncheck, hipMemcpyHostToDevice, s));
+        CV_TRY(hipMemcpyAsync(base + o_cb, check_begin, 4 * (ntrees + 1), hipMemcpyHostToDevice, s));
+        CV_TRY(cvk_pmt_verify((uint32_t)ntrees, base + o_kind, reinterpret_cast<uint32_t *>(base + o_left),
+                              reinterpret_cast<uint32_t *>(base + o_right), base + o_hash,
+                              reinterpret_cast<uint32_t *>(base + o_tb), base + o_root, base + o_check,
+                              reinterpret_cast<uint32_t *>(base + o_cb), reinterpret_cast<uint32_t *>(base + o_dig),
+                              base + o_flag, base + o_verdict, base + o_status, s));
+        CV_TRY(hipMemcpyAsync(verdict, base + o_verdict, ntrees, hipMemcpyDeviceToHost, s));
+        if (status) CV_TRY(hipMemcpyAsync(status, base + o_status, ntrees, hipMemcpyDeviceToHost, s));
+        CV_TRY(hipStreamSynchronize(s));
+        drain.armed = false;
+        return CV_OK;
+    });
 }
 
 int cv_tx_verdicts(size_t ntx, const uint64_t *bitmap, const uint32_t *tx_sig_begin, uint8_t *tx_ok) {
     if (ntx == 0) return CV_OK;
     if (!bitmap || !tx_sig_begin || !tx_ok) return CV_E_ARGS;
+    // one masked word test per bitmap word the transaction's range touches
     for (size_t t = 0; t < ntx; t++) {
         const uint32_t b = tx_sig_begin[t], e = tx_sig_begin[t + 1];
         if (e < b) return CV_E_ARGS;
         bool ok = e > b;
-        for (uint32_t i = b; i < e && ok; i++) ok = (bitmap[i >> 6] >> (i & 63)) & 1u;
+        for (uint32_t w = b >> 6; ok && e > b && w <= (e - 1) >> 6; w++) {
+            const uint32_t lo = w == (b >> 6) ? (b & 63) : 0, hi = w == ((e - 1) >> 6) ? ((e - 1) & 63) : 63;
+            const uint64_t mask = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & ~((1ull << lo) - 1);
+            ok = (bitmap[w] & mask) == mask;
+        }
         tx_ok[t] = ok ? 1 : 0;
     }
     return CV_OK;
@@ -1725,10 +2330,11 @@ int cv_ed25519_verify_device(cv_ctx *ctx, int device, size_t n, const void *d_pk
     if (n > 0xffffffffull) return CV_E_TOO_LARGE;
     Device *d = find_dev(ctx, device);
     if (!d || !d_pk || !d_sig || !d_arena || !d_off || !d_len || !d_bitmap) return CV_E_ARGS;
-    std::lock_guard<std::mutex> g(ctx->mu);            // enqueue only; ordered on the workspace (ws_begin)
+    const Opts o = ctx->opts();
+    std::lock_guard<std::mutex> g(d->mu);              // enqueue only; ordered on the workspace (ws_begin)
     CV_TRY(hipSetDevice(d->ordinal));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : d->stream;
-    CV_TRY(launch_verify(*d, pick_slot(*d, s), (uint32_t)n, static_cast<const uint8_t *>(d_pk),
+    CV_TRY(launch_verify(*d, o.plan, pick_slot(*d, s), (uint32_t)n, static_cast<const uint8_t *>(d_pk),
                          static_cast<const uint8_t *>(d_sig), static_cast<const uint8_t *>(d_arena),
                          static_cast<const uint64_t *>(d_off), static_cast<const uint32_t *>(d_len),
                          static_cast<uint64_t *>(d_bitmap), static_cast<uint8_t *>(d_status), s, nullptr, true));
@@ -1744,7 +2350,8 @@ int cv_ed25519_verify_device_timed(cv_ctx *ctx, int device, size_t n, const void
     if (n > 0xffffffffull) return CV_E_TOO_LARGE;
     Device *d = find_dev(ctx, device);
     if (!d || !d_pk || !d_sig || !d_arena || !d_off || !d_len || !d_bitmap) return CV_E_ARGS;
-    std::lock_guard<std::mutex> g(ctx->mu);
+    const Opts o = ctx->opts();
+    std::lock_guard<std::mutex> g(d->mu);
     CV_TRY(hipSetDevice(d->ordinal));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : d->stream;
     Slot &sl = pick_slot(*d, s);
@@ -1754,7 +2361,7 @@ int cv_ed25519_verify_device_timed(cv_ctx *ctx, int device, size_t n, const void
     // one workspace chunk at a time (chunk starts are multiples of 64: whole bitmap words)
     for (size_t c0 = 0; c0 < n && e == hipSuccess; c0 += kVerifyChunk) {
         const size_t m = std::min<size_t>(kVerifyChunk, n - c0);
-        e = launch_verify(*d, sl, (uint32_t)m, static_cast<const uint8_t *>(d_pk) + c0 * 32,
+        e = launch_verify(*d, o.plan, sl, (uint32_t)m, static_cast<const uint8_t *>(d_pk) + c0 * 32,
                           static_cast<const uint8_t *>(d_sig) + c0 * 64, static_cast<const uint8_t *>(d_arena),
                           static_cast<const uint64_t *>(d_off) + c0, static_cast<const uint32_t *>(d_len) + c0,
                           static_cast<uint64_t *>(d_bitmap) + c0 / 64, nullptr, s, ev, false);
@@ -1779,7 +2386,8 @@ int cv_ed25519_verify_device_keyed(cv_ctx *ctx, int device, size_t n, size_t nke
     Device *d = find_dev(ctx, device);
     if (!d || nkeys == 0 || !d_keys || !d_key_index || !d_sig || !d_arena || !d_off || !d_len || !d_bitmap)
         return CV_E_ARGS;
-    std::lock_guard<std::mutex> g(ctx->mu);
+    const Opts o = ctx->opts();
+    std::lock_guard<std::mutex> g(d->mu);
     CV_TRY(hipSetDevice(d->ordinal));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : d->stream;
     // the key bytes come to the host (32 B per distinct key) to resolve them against the pool
@@ -1796,7 +2404,8 @@ int cv_ed25519_verify_device_keyed(cv_ctx *ctx, int device, size_t n, size_t nke
     if (e == hipSuccess) e = ws_begin(*d, sl, s);
     if (e == hipSuccess) e = pool_begin(d->kc, s);
     std::vector<uint32_t> sok;
-    int rc = e == hipSuccess ? key_resolve(*d, ctx->key_cap, nkeys, hkeys.data(), nullptr, sok, s) : hip_rc(e);
+    bool prepared = false;
+    int rc = e == hipSuccess ? key_resolve(*d, ctx->key_cap.load(), nkeys, hkeys.data(), nullptr, sok, s, &prepared) : hip_rc(e);
     KeyCache &kc = d->kc;
     if (rc == CV_OK) rc = hip_rc(kc.slot_of_key.ensure(nkeys * 4));
     // slot_of_key goes up through the pool's pinned staging, which the previous keyed call's upload may
@@ -1811,7 +2420,7 @@ int cv_ed25519_verify_device_keyed(cv_ctx *ctx, int device, size_t n, size_t nke
     if (rc == CV_OK) rc = hip_rc(hipEventRecord(kc.pin_ev, s));
     kc.pin_busy = rc == CV_OK;
     if (rc == CV_OK)
-        rc = hip_rc(cvk_verify_keyed((uint32_t)n, static_cast<const uint8_t *>(d_keys),
+        rc = hip_rc(cvk_verify_keyed(&o.plan, (uint32_t)n, static_cast<const uint8_t *>(d_keys),
                                      static_cast<const uint32_t *>(d_key_index), kc.slot_of_key.as<uint32_t>(),
                                      kc.ktab.as<uint32_t>(), kc.kok.as<uint8_t>(), static_cast<const uint8_t *>(d_sig),
                                      static_cast<const uint8_t *>(d_arena), static_cast<const uint64_t *>(d_off),
@@ -1844,6 +2453,7 @@ int cv_ed25519_sign_device(cv_ctx *ctx, int device, size_t n, const void *d_seed
     if (n > 0xffffffffull) return CV_E_TOO_LARGE;
     Device *d = find_dev(ctx, device);
     if (!d || !d_seed || !d_arena || !d_off || !d_len || !d_pk || !d_sig) return CV_E_ARGS;
+    std::lock_guard<std::mutex> g(d->mu);
     CV_TRY(hipSetDevice(d->ordinal));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : d->stream;
     CV_TRY(cvk_sign((uint32_t)n, static_cast<const uint8_t *>(d_seed), static_cast<const uint8_t *>(d_arena),
@@ -1861,9 +2471,10 @@ int cv_merkle_tx_ids_device(cv_ctx *ctx, int device, size_t ntx, size_t nleaves,
     Device *d = find_dev(ctx, device);
     if (!d || !d_tx_leaf_begin || !d_ids || (nleaves && (!d_arena || !d_leaf_off || !d_leaf_len || !d_workspace)))
         return CV_E_ARGS;
+    std::lock_guard<std::mutex> g(d->mu);
     CV_TRY(hipSetDevice(d->ordinal));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : d->stream;
-    CV_TRY(cvk_merkle((uint32_t)ntx, (uint32_t)nleaves, static_cast<const uint8_t *>(d_arena),
+    CV_TRY(cvk_merkle((uint32_t)ntx, (uint32_t)nleaves, 0, static_cast<const uint8_t *>(d_arena),
                       static_cast<const uint64_t *>(d_leaf_off), static_cast<const uint32_t *>(d_leaf_len),
                       static_cast<const uint32_t *>(d_tx_leaf_begin), static_cast<uint32_t *>(d_workspace),
                       static_cast<uint8_t *>(d_ids), static_cast<uint8_t *>(d_tx_status), s));
@@ -1880,7 +2491,7 @@ int cv_synchronize(cv_ctx *ctx, int device) {
 }
 
 // ---------------------------------------------------------------- calibration
-// scoped device scratch and events of the calibration / diagnostic calls (freed on every return path)
+// scoped device scratch and events of the calibration calls (freed on every return path)
 struct ScopedMem {
     void *p = nullptr;
     ~ScopedMem() {
@@ -1905,6 +2516,7 @@ int cv_calibrate(cv_ctx *ctx, int device, double *mad_per_s, double *femul_per_s
     if (!ctx) return CV_E_ARGS;
     Device *d = find_dev(ctx, device);
     if (!d) return CV_E_ARGS;
+    std::lock_guard<std::mutex> g(d->mu);
     CV_TRY(hipSetDevice(d->ordinal));
     hipDeviceProp_t prop;
     CV_TRY(hipGetDeviceProperties(&prop, d->ordinal));
@@ -1939,6 +2551,7 @@ int cv_calibrate_cycles(cv_ctx *ctx, int device, double *out) {
     if (!ctx || !out) return CV_E_ARGS;
     Device *d = find_dev(ctx, device);
     if (!d) return CV_E_ARGS;
+    std::lock_guard<std::mutex> g(d->mu);
     CV_TRY(hipSetDevice(d->ordinal));
     hipDeviceProp_t prop;
     CV_TRY(hipGetDeviceProperties(&prop, d->ordinal));
@@ -1967,48 +2580,6 @@ int cv_calibrate_cycles(cv_ctx *ctx, int device, double *out) {
     out[2] = cyc;
     out[3] = simds;
     out[4] = cyc > 0 ? simds * 2.4e9 * 64.0 / cyc : 0.0;
-    return CV_OK;
-}
-
-// Per-phase shader cycles of the fused prep kernel (diagnostic build of the same code, one chunk):
-// out[k] = mean cycles per wave of phase k (hash, lattice, digits, decode A+R, tables), out[5] =
-// their sum, out[6] = waves measured, out[7] = the SHA-512 part of the hash phase.  The workspace is
-// the device stream's verify workspace slot.
-int cv_diag_prep_phases(cv_ctx *ctx, int device, size_t n, const void *d_pk, const void *d_sig, const void *d_arena,
-                        const void *d_off, const void *d_len, double *out) {
-    if (!ctx || !out || n == 0) return CV_E_ARGS;
-    if (n > kVerifyChunk) return CV_E_TOO_LARGE;
-    Device *d = find_dev(ctx, device);
-    if (!d || !d_pk || !d_sig || !d_arena || !d_off || !d_len) return CV_E_ARGS;
-    std::lock_guard<std::mutex> g(ctx->mu);
-    CV_TRY(hipSetDevice(d->ordinal));
-    Slot &sl = pick_slot(*d, d->stream);
-    CV_TRY(ensure_verify_ws(sl, n));
-    const size_t waves = (n + 63) / 64;
-    ScopedMem st;
-    CV_TRY(hipMalloc(&st.p, waves * 64));
-    CV_TRY(ws_begin(*d, sl, d->stream));
-    hipError_t e = cvk_prep_probe((uint32_t)n, static_cast<const uint8_t *>(d_pk), static_cast<const uint8_t *>(d_sig),
-                                  static_cast<const uint8_t *>(d_arena), static_cast<const uint64_t *>(d_off),
-                                  static_cast<const uint32_t *>(d_len), sl.ws_dig.as<uint32_t>(), sl.ws_tab.as<uint32_t>(),
-                                  sl.ws_cap, static_cast<uint64_t *>(st.p), d->stream);
-    const hipError_t e2 = ws_end(sl, d->stream);
-    if (e == hipSuccess) e = e2;
-    std::vector<uint64_t> h(waves * 8);
-    const hipError_t e3 = hipStreamSynchronize(d->stream);   // also on error: st is freed on return
-    if (e == hipSuccess) e = e3;
-    if (e == hipSuccess) e = hipMemcpy(h.data(), st.p, waves * 64, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) return hip_rc(e);
-    double sum[6] = {0, 0, 0, 0, 0, 0};
-    for (size_t w = 0; w < waves; w++)
-        for (int k = 0; k < 6; k++) sum[k] += (double)h[w * 8 + k];
-    out[5] = 0;
-    for (int k = 0; k < 5; k++) {
-        out[k] = sum[k] / (double)waves;
-        out[5] += out[k];
-    }
-    out[6] = (double)waves;
-    out[7] = sum[5] / (double)waves;
     return CV_OK;
 }
 

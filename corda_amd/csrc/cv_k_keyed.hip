@@ -1,46 +1,7 @@
-// cv_k_full.hip — full-width verify group (prep / straus / finish, the A/B reference schedule) and the keyed
-// per-key comb path (f2).
+// cv_k_keyed.hip — the keyed per-key comb path: key tables, hash + scalar, comb, and the
+// finish kernel (batched inversion, encode, byte compare, bitmap bytes).
 // Shared helpers and every kernel declaration: cv_kcommon.h; launchers: cv_kernels.hip.
 #include "cv_kcommon.h"
-
-template <bool LAT>
-__global__ __launch_bounds__(CV_BLOCK, 2) void cv_prep_kernel(
-    uint32_t n, const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig, const uint8_t *__restrict__ arena,
-    const uint64_t *__restrict__ off, const uint32_t *__restrict__ len, uint32_t *__restrict__ ws_hs,
-    uint32_t *__restrict__ ws_tab, uint8_t *__restrict__ ws_ok, uint8_t *__restrict__ status) {
-    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
-    if (i >= n) return;
-    uint32_t aw[8], rw[8], sw[8];
-    load_words8(aw, pk + (size_t)i * 32);
-    load_words8(rw, sig + (size_t)i * 64);
-    load_words8(sw, sig + (size_t)i * 64 + 32);
-    uint32_t hs[CV_HS_WORDS];
-    const bool ok = cv_verify_prep<LAT>(aw, rw, sw, arena + off[i], len[i], hs, ws_tab + (size_t)i * CV_TAB_WORDS);
-    store_words(ws_hs + (size_t)i * CV_HS_WORDS, hs, CV_HS_WORDS / 4);
-    ws_ok[i] = ok ? 1 : 0;
-    if (status) status[i] = ok ? 0 : 1;
-}
-
-template <int WAVES>
-__global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_straus_kernel(uint32_t n, const uint32_t *__restrict__ ws_hs,
-                                                                    const uint32_t *__restrict__ ws_tab,
-                                                                    uint32_t *__restrict__ ws_R) {
-    __shared__ __attribute__((aligned(16))) uint32_t btab[CV_BTAB_ENTRIES * CV_BTAB_STRIDE];
-    stage_btab(btab);
-    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
-    if (i >= n) return;
-    ge_p2 R;
-    cv_verify_straus(btab, ws_hs + (size_t)i * CV_HS_WORDS, ws_tab + (size_t)i * CV_TAB_WORDS, R);
-    uint32_t rec[CV_R_WORDS];
-    fe_store(rec, R.X);
-    fe_store(rec + 10, R.Y);
-    fe_store(rec + 20, R.Z);
-    rec[30] = rec[31] = 0;
-    store_words(ws_R + (size_t)i * CV_R_WORDS, rec, CV_R_WORDS / 4);
-}
-template __global__ void cv_straus_kernel<2>(uint32_t, const uint32_t *, const uint32_t *, uint32_t *);
-template __global__ void cv_straus_kernel<3>(uint32_t, const uint32_t *, const uint32_t *, uint32_t *);
-template __global__ void cv_straus_kernel<4>(uint32_t, const uint32_t *, const uint32_t *, uint32_t *);
 
 // lane j: signatures [8j, 8j+8) -> bitmap byte j (bytes past n are written as zero)
 template <bool LAT>
@@ -59,44 +20,6 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_finish_kernel(uint32_t n, uint32_
                                 ws_ok + b, cnt);
     }
     bitmap_bytes[j] = (uint8_t)bits;
-}
-
-// ---------------------------------------------------------------- half-size verify (cv_verify.h)
-// hsprep: decode R canonically (r_ok folded into the key-ok byte), k*R table, lattice-reduced
-// (u, v, w) as packed per-window digit words, window-major: ws_dig[win * cap + i].
-template <bool LAT>
-__global__ __launch_bounds__(CV_BLOCK, 2) void cv_hsprep_kernel(uint32_t n, uint32_t cap, const uint8_t *__restrict__ sig,
-                                                                const uint32_t *__restrict__ ws_hs,
-                                                                uint32_t *__restrict__ ws_dig,
-                                                                uint32_t *__restrict__ ws_tabR,
-                                                                uint8_t *__restrict__ ws_ok, int reduce) {
-    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
-    if (i >= n) return;
-    uint32_t rw[8], hs[CV_HS_WORDS];
-    load_words8(rw, sig + (size_t)i * 64);
-    const uint4 *hp = reinterpret_cast<const uint4 *>(ws_hs + (size_t)i * CV_HS_WORDS);
-#pragma unroll
-    for (int q = 0; q < CV_HS_WORDS / 4; q++) {
-        const uint4 x = hp[q];
-        hs[4 * q] = x.x; hs[4 * q + 1] = x.y; hs[4 * q + 2] = x.z; hs[4 * q + 3] = x.w;
-    }
-    const bool r_ok = cv_hs_prep<LAT, true>(rw, hs, ws_dig + i, cap, ws_tabR + (size_t)i * CV_TAB_WORDS, reduce != 0);
-    if (!r_ok) ws_ok[i] = 0;
-}
-
-// ---------------------------------------------------------------- quad (latency) Straus kernels
-// Four lanes per signature (cv_quad.h) for batches too small to fill the chip.  Grid: 4n lanes.
-__global__ __launch_bounds__(CV_BLOCK) void cv_straus_quad_kernel(uint32_t n, const uint32_t *__restrict__ ws_hs,
-                                                                  const uint32_t *__restrict__ ws_tab,
-                                                                  uint32_t *__restrict__ ws_R) {
-    __shared__ __attribute__((aligned(16))) uint32_t btab[CV_BTAB_ENTRIES * CV_BTAB_STRIDE];
-    stage_btab(btab);
-    const uint32_t i = (blockIdx.x * CV_BLOCK + threadIdx.x) >> 2;
-    const int r = threadIdx.x & 3;
-    if (i >= n) return;                       // whole quads leave together
-    fe P;
-    cv_quad_straus(btab, ws_hs + (size_t)i * CV_HS_WORDS, ws_tab + (size_t)i * CV_TAB_WORDS, r, P);
-    if (r < 3) fe_store(ws_R + (size_t)i * CV_R_WORDS + 10 * r, P);
 }
 
 __global__ __launch_bounds__(CV_BLOCK) void cv_comb_quad_kernel(uint32_t n, const uint32_t *__restrict__ ws_hs,
@@ -176,14 +99,7 @@ __global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_comb_kernel(uint32_t n, co
     rec[30] = rec[31] = 0;
     store_words(ws_R + (size_t)i * CV_R_WORDS, rec, CV_R_WORDS / 4);
 }
-template __global__ void cv_comb_kernel<2>(uint32_t, const uint32_t *, const uint32_t *, const uint32_t *,
-                                           const uint32_t *, uint32_t *, const uint32_t *);
 template __global__ void cv_comb_kernel<3>(uint32_t, const uint32_t *, const uint32_t *, const uint32_t *,
                                            const uint32_t *, uint32_t *, const uint32_t *);
-
-template __global__ void cv_prep_kernel<true>( uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_hs, uint32_t *ws_tab, uint8_t *ws_ok, uint8_t *status);
-template __global__ void cv_prep_kernel<false>( uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_hs, uint32_t *ws_tab, uint8_t *ws_ok, uint8_t *status);
 template __global__ void cv_finish_kernel<true>(uint32_t n, uint32_t nbytes, const uint8_t *sig, const uint32_t *ws_R, const uint8_t *ws_ok, uint8_t *bitmap_bytes);
 template __global__ void cv_finish_kernel<false>(uint32_t n, uint32_t nbytes, const uint8_t *sig, const uint32_t *ws_R, const uint8_t *ws_ok, uint8_t *bitmap_bytes);
-template __global__ void cv_hsprep_kernel<true>(uint32_t n, uint32_t cap, const uint8_t *sig, const uint32_t *ws_hs, uint32_t *ws_dig, uint32_t *ws_tabR, uint8_t *ws_ok, int reduce);
-template __global__ void cv_hsprep_kernel<false>(uint32_t n, uint32_t cap, const uint8_t *sig, const uint32_t *ws_hs, uint32_t *ws_dig, uint32_t *ws_tabR, uint8_t *ws_ok, int reduce);

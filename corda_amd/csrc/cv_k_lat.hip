@@ -2,28 +2,6 @@
 // Shared helpers and every kernel declaration: cv_kcommon.h; launchers: cv_kernels.hip.
 #include "cv_kcommon.h"
 
-// Small (latency) batches: 64-thread blocks (one wave each, spread over CUs) and the whole register
-// file for the lone wave — no spills.  A spilling version took 62 us at 256 signatures but 208 us at
-// 4,096 (rocprofv3, profiles/r02_notary_kernels.txt): waves that need scratch queue for scratch slots.
-__global__ __launch_bounds__(64, 1) void cv_scalars_lat_kernel(uint32_t n, uint32_t cap, const uint8_t *__restrict__ pk,
-                                                               const uint8_t *__restrict__ sig,
-                                                               const uint8_t *__restrict__ arena,
-                                                               const uint64_t *__restrict__ off,
-                                                               const uint32_t *__restrict__ len,
-                                                               uint32_t *__restrict__ ws_dig) {
-    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
-    if (i < n) cv_scalars_lane<false, true>(i, cap, pk, sig, arena, off, len, ws_dig);
-}
-
-__global__ __launch_bounds__(64) void cv_points_pair_kernel(uint32_t n, const uint8_t *__restrict__ pk,
-                                                            const uint8_t *__restrict__ sig,
-                                                            uint32_t *__restrict__ ws_tab,
-                                                            uint32_t *__restrict__ ws_tabR,
-                                                            uint8_t *__restrict__ ws_ok,
-                                                            uint8_t *__restrict__ status) {
-    cv_points_pair_lane(blockIdx.x * 64 + threadIdx.x, n, pk, sig, ws_tab, ws_tabR, ws_ok, status);
-}
-
 // Small (latency) batches: the scalars and the point pairs of a signature are independent (both
 // read only the inputs), so one launch runs them side by side on otherwise idle SIMDs — blocks
 // [0, nbp) decode point pairs, blocks [nbp, grid) derive the scalars — and the batch pays
@@ -145,11 +123,9 @@ __global__ __launch_bounds__(256) void cv_gather16_kernel(const uint4 *__restric
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < q; i += stride) dst[i] = src[i];
 }
 
-template __global__ void cv_prep_lat_kernel<true, true>(uint32_t n, uint32_t cap, uint32_t nbp, uint32_t pts4, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
-template __global__ void cv_prep_lat_kernel<false, true>(uint32_t n, uint32_t cap, uint32_t nbp, uint32_t pts4, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
-template __global__ void cv_hs_straus_quad_kernel<false>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);
-template __global__ void cv_hs_straus_quad_kernel<true>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);
-template __global__ void cv_hs_straus_tri_kernel<false>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, uint8_t *nib);
-template __global__ void cv_hs_straus_tri_kernel<true>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, uint8_t *nib);
+// the sequential-carry field forms everywhere (round 3: tri Straus 160 -> 151 us at 4,096 against the ILP
+// forms, quad 216 -> 203 us at 16,384; profiles/r03b_notary_probe_seq_pool.log)
 template __global__ void cv_prep_lat_kernel<true, false>(uint32_t n, uint32_t cap, uint32_t nbp, uint32_t pts4, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
 template __global__ void cv_prep_lat_kernel<false, false>(uint32_t n, uint32_t cap, uint32_t nbp, uint32_t pts4, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
+template __global__ void cv_hs_straus_quad_kernel<true>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);
+template __global__ void cv_hs_straus_tri_kernel<true>(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, uint8_t *nib);

@@ -23,67 +23,8 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_sign_kernel(
 }
 
 // ---------------------------------------------------------------- Merkle tx ids
-// One lane per leaf.  A lane runs as many SHA-256 blocks as its leaf needs and a wave as many as its
-// longest leaf, so each workgroup takes CV_LEAF_SPAN consecutive leaves, orders them by block count
-// (counting sort in LDS: one LDS atomic per leaf, one wave scan) and hashes them in CV_LEAF_SPAN /
-// CV_LEAF_BLOCK passes, lane t of pass p taking the (p * CV_LEAF_BLOCK + t)-th shortest: every wave
-// then holds leaves of similar length while the workgroup's leaves stay one contiguous stretch of
-// the arena.  Digests go to each leaf's own index, so the order is invisible.
-__global__ __launch_bounds__(CV_LEAF_BLOCK) void cv_leaf_hash_kernel(uint32_t nleaves, const uint8_t *__restrict__ arena,
-                                                                     const uint64_t *__restrict__ off,
-                                                                     const uint32_t *__restrict__ len,
-                                                                     uint32_t *__restrict__ leaf_digest) {
-    constexpr uint32_t PASSES = CV_LEAF_SPAN / CV_LEAF_BLOCK;
-    __shared__ uint32_t hist[64], base[64], perm[CV_LEAF_SPAN];
-    const uint32_t t = threadIdx.x, first = blockIdx.x * CV_LEAF_SPAN;
-    const uint32_t nlive = nleaves - first < CV_LEAF_SPAN ? nleaves - first : CV_LEAF_SPAN;
-    if (t < 64) hist[t] = 0;
-    __syncthreads();
-    uint32_t bucket[PASSES], pos[PASSES];
-#pragma unroll
-    for (uint32_t k = 0; k < PASSES; k++) {
-        const uint32_t j = k * CV_LEAF_BLOCK + t;
-        bucket[k] = 0;
-        pos[k] = 0;
-        if (j < nlive) {
-            const uint32_t nb = (len[first + j] + 9u + 63u) / 64u;   // SHA-256 blocks of this leaf
-            bucket[k] = nb < 63u ? nb : 63u;
-            pos[k] = atomicAdd(&hist[bucket[k]], 1u);
-        }
-    }
-    __syncthreads();
-    if (t < 64) {                                                 // exclusive scan, one wave
-        const uint32_t own = hist[t];
-        uint32_t inc = own;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(inc, d, 64);
-            if ((int)t >= d) inc += y;
-        }
-        base[t] = inc - own;
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t k = 0; k < PASSES; k++) {
-        const uint32_t j = k * CV_LEAF_BLOCK + t;
-        if (j < nlive) perm[base[bucket[k]] + pos[k]] = first + j;
-    }
-    __syncthreads();
-#pragma nounroll
-    for (uint32_t k = 0; k < PASSES; k++) {
-        const uint32_t j = k * CV_LEAF_BLOCK + t;
-        if (j >= nlive) break;
-        const uint32_t leaf = perm[j];
-        uint32_t d[8];
-        sha256_bytes(d, arena + off[leaf], len[leaf]);
-        uint4 *o = reinterpret_cast<uint4 *>(leaf_digest + (size_t)leaf * 8);
-        o[0] = make_uint4(d[0], d[1], d[2], d[3]);
-        o[1] = make_uint4(d[4], d[5], d[6], d[7]);
-    }
-}
-
-// Balanced-pair form of the leaf kernel (cvk_set_leaf_mode(1)): the same per-workgroup counting sort,
-// then lane t hashes the t-th shortest AND the t-th longest leaf of the span back to back in one block
+// One lane per leaf PAIR.  Each workgroup takes 2 x CV_LEAF_BLOCK consecutive leaves, orders them by SHA-256
+// block count (counting sort in LDS: one LDS atomic per leaf, one wave scan), then lane t hashes the t-th shortest AND the t-th longest leaf of the span back to back in one block
 // loop (the state restarts between them), so every lane's block count is about the span's mean and
 // a wave no longer runs as long as its longest leaf.  Span = 2 x block.
 __global__ __launch_bounds__(CV_LEAF_BLOCK) void cv_leaf_hash_pair_kernel(uint32_t nleaves, const uint8_t *__restrict__ arena,
@@ -154,14 +95,16 @@ __global__ __launch_bounds__(CV_LEAF_BLOCK) void cv_leaf_hash_pair_kernel(uint32
     }
 }
 
-// one lane per transaction, in place over its leaf digests; ids are written as digest bytes
-__global__ __launch_bounds__(CV_BLOCK) void cv_merkle_tree_kernel(uint32_t ntx, const uint32_t *__restrict__ tx_begin,
+// one lane per transaction, in place over its leaf digests; ids are written as digest bytes.  tx_begin holds
+// absolute leaf indices; leaf_base is the index of leaf_digest[0] (a sub-chunk of a larger batch)
+__global__ __launch_bounds__(CV_BLOCK) void cv_merkle_tree_kernel(uint32_t ntx, uint32_t leaf_base,
+                                                                  const uint32_t *__restrict__ tx_begin,
                                                                   uint32_t *__restrict__ leaf_digest,
                                                                   uint8_t *__restrict__ ids,
                                                                   uint8_t *__restrict__ status) {
     const uint32_t gid = blockIdx.x * CV_BLOCK + threadIdx.x;
     if (gid >= ntx) return;
-    const uint32_t b = tx_begin[gid], e = tx_begin[gid + 1];
+    const uint32_t b = tx_begin[gid] - leaf_base, e = tx_begin[gid + 1] - leaf_base;
     uint32_t root[8];
     const bool ok = cv_merkle_root_inplace(leaf_digest + (size_t)b * 8, e - b, root);
     uint4 *o = reinterpret_cast<uint4 *>(ids + (size_t)gid * 32);
@@ -235,85 +178,6 @@ __global__ __launch_bounds__(CV_BLOCK, 2) void cv_femul_bench_kernel(uint32_t it
 #pragma unroll
         for (int i = 0; i < 10; i++) s ^= x[k].v[i];
     if (s == 0x1234567) out[0] = s;
-}
-
-// ---------------------------------------------------------------- diagnostics: phase cycle probe
-// The fused prep (cv_hs_prep_fused) with s_memtime stamps at its phase boundaries: per wave, lane 0
-// stores the shader-clock cycles of hash | lattice | digit packing | A+R decode | tables into
-// stamps[wave * 8 + k] (vector stores).  Same code and launch shape as the product kernel; each
-// stamp is ordered after the phase's result by a data dependency.  Diagnostic build only.
-__device__ __forceinline__ uint64_t cv_stamp() {
-    uint64_t t;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t));
-    return t;
-}
-#define CV_DEP(x) asm volatile("" ::"v"(x))
-
-__global__ __launch_bounds__(CV_BLOCK, 2) void cv_prep_probe_kernel(
-    uint32_t n, uint32_t cap, const uint8_t *__restrict__ pk, const uint8_t *__restrict__ sig,
-    const uint8_t *__restrict__ arena, const uint64_t *__restrict__ off, const uint32_t *__restrict__ len,
-    uint32_t *__restrict__ ws_dig, uint32_t *__restrict__ ws_tab, uint32_t *__restrict__ ws_tabR,
-    uint64_t *__restrict__ stamps) {
-    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
-    if (i >= n) return;
-    uint32_t aw[8], rw[8], sw[8];
-    load_words8(aw, pk + (size_t)i * 32);
-    load_words8(rw, sig + (size_t)i * 64);
-    load_words8(sw, sig + (size_t)i * 64 + 32);
-    CV_DEP(aw[0]); CV_DEP(rw[0]); CV_DEP(sw[0]);
-    uint64_t t[8];
-    t[0] = cv_stamp();
-    uint32_t hs[CV_HS_WORDS];
-    {   // cv_keyed_hs, split: SHA-512 | the two mod-L scalars
-        uint32_t pre[16], dg[16], hh[8], abyte[8], ss[8];
-        ge_abyte_from_key(abyte, aw);
-#pragma unroll
-        for (int q = 0; q < 8; q++) { pre[q] = rw[q]; pre[8 + q] = abyte[q]; }
-        sha512_pre_msg(dg, pre, 64, arena + off[i], len[i]);
-        CV_DEP(dg[0]); CV_DEP(dg[15]);
-        t[6] = cv_stamp();
-        sc_reduce512(hh, dg);
-        sc_effective_s(ss, sw);
-#pragma unroll
-        for (int q = 0; q < 8; q++) { hs[q] = hh[q]; hs[8 + q] = ss[q]; }
-    }
-    CV_DEP(hs[0]); CV_DEP(hs[15]);
-    t[1] = cv_stamp();
-    uint32_t h[8], s8[8], u[8], v[8], w[8];
-#pragma unroll
-    for (int q = 0; q < 8; q++) { h[q] = hs[q]; s8[q] = hs[8 + q]; }
-    bool v_neg;
-    int nwin;
-    sc_halfsize(u, v, v_neg, nwin, w, h, s8);
-    CV_DEP(u[7]); CV_DEP(v[7]); CV_DEP(w[7]);
-    t[2] = cv_stamp();
-    uint32_t *dig = ws_dig + i;
-#pragma unroll 4
-    for (int win = 0; win < 64; win++) {
-        const int da = -digit16(u, win), dr = v_neg ? -digit16(v, win) : digit16(v, win);
-        const bool bw = (win & 1) == 0 && win < 32;
-        const int dlo = bw ? digit256(w, win >> 1) : 0, dhi = bw ? digit256(w, 16 + (win >> 1)) : 0;
-        dig[(size_t)win * cap] = ((uint32_t)da & 0x1fu) | (((uint32_t)dr & 0x1fu) << 5) |
-                                 (((uint32_t)dlo & 0x1ffu) << 10) | (((uint32_t)dhi & 0x1ffu) << 19);
-    }
-    dig[64 * (size_t)cap] = (uint32_t)nwin;
-    t[3] = cv_stamp();
-    ge_p3 P[2];
-    bool ok[2];
-    ge_decode2_0_1_0<false>(P, ok, aw, rw);
-    CV_DEP(P[0].T.v[0]); CV_DEP(P[1].T.v[0]);
-    t[4] = cv_stamp();
-    ge_p3 nA;
-    ge_p3_neg(nA, P[0]);
-    ge_cached_multiples8(ws_tab + (size_t)i * CV_TAB_WORDS, nA);
-    ge_cached_multiples8(ws_tabR + (size_t)i * CV_TAB_WORDS, P[1]);
-    t[5] = cv_stamp();
-    if ((threadIdx.x & 63u) == 0) {
-        uint64_t *o = stamps + (size_t)(i >> 6) * 8;
-#pragma unroll
-        for (int k = 0; k < 5; k++) o[k] = t[k + 1] - t[k];
-        o[5] = t[6] - t[0];                     // SHA-512 alone (part of phase 0)
-    }
 }
 
 // Cycle-basis calibration: the chip-wide v_mad_u64_u32 bench again, with block 0's lane 0 stamping

@@ -1,10 +1,10 @@
 // cv_kcommon.h — device helpers shared by the kernel translation units and the declarations of every
 // kernel, so the launchers (cv_kernels.hip) and the kernels (cv_k_*.hip) build as separate objects in
 // parallel:
-//   cv_k_hs.hip    half-size throughput group: scalars, points, hs_straus (the C2/C3/C5 hot path)
+//   cv_k_hs.hip    half-size throughput group: scalars, points (cv_k_hss.hip: hs_straus) — the C2/C3/C5 hot path
 //   cv_k_lat.hip   latency forms for notary-sized batches: fused prep, quad and tri-chain Straus
-//   cv_k_full.hip  full-width group (prep / straus / finish), keyed comb path
-//   cv_k_misc.hip  signing, Merkle ids, partial Merkle trees, calibration and probe kernels
+//   cv_k_keyed.hip keyed per-key comb path (key tables, hash, comb, finish)
+//   cv_k_misc.hip  signing, Merkle ids, partial Merkle trees, calibration kernels
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -122,40 +122,25 @@ __device__ __forceinline__ void cv_points_one_lane(uint32_t g, uint32_t n, const
 }
 
 // ---------------------------------------------------------------- kernel declarations
-template <bool LAT> __global__ void cv_prep_kernel( uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_hs, uint32_t *ws_tab, uint8_t *ws_ok, uint8_t *status);
-template <int WAVES> __global__ void cv_straus_kernel(uint32_t n, const uint32_t *ws_hs, const uint32_t *ws_tab, uint32_t *ws_R);
 template <bool LAT> __global__ void cv_finish_kernel(uint32_t n, uint32_t nbytes, const uint8_t *sig, const uint32_t *ws_R, const uint8_t *ws_ok, uint8_t *bitmap_bytes);
-template <bool LAT> __global__ void cv_hsprep_kernel(uint32_t n, uint32_t cap, const uint8_t *sig, const uint32_t *ws_hs, uint32_t *ws_dig, uint32_t *ws_tabR, uint8_t *ws_ok, int reduce);
-__global__ void cv_straus_quad_kernel(uint32_t n, const uint32_t *ws_hs, const uint32_t *ws_tab, uint32_t *ws_R);
 __global__ void cv_comb_quad_kernel(uint32_t n, const uint32_t *ws_hs, const uint32_t *key_index, const uint32_t *slot_of_key, const uint32_t *ktab_pool, uint32_t *ws_R);
 __global__ void cv_keyprep_kernel(uint32_t nk, const uint8_t *keys, const uint32_t *slots, uint32_t *scratch, uint32_t *ktab_pool, uint8_t *kok_pool);
 __global__ void cv_keyed_prep_kernel( uint32_t n, const uint8_t *keys, const uint32_t *key_index, const uint32_t *slot_of_key, const uint8_t *kok_pool, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_hs, uint8_t *ws_ok, uint8_t *status);
 template <int WAVES> __global__ void cv_comb_kernel(uint32_t n, const uint32_t *ws_hs, const uint32_t *key_index, const uint32_t *slot_of_key, const uint32_t *ktab_pool, uint32_t *ws_R, const uint32_t *bw16);
-template <int WAVES> __global__ void cv_hash_kernel(uint32_t n, uint32_t cap, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_hs);
-template <int WAVES> __global__ void cv_lattice_kernel(uint32_t n, uint32_t cap, const uint32_t *ws_hs, uint32_t *ws_dig);
 template <int WAVES> __global__ void cv_scalars_kernel(uint32_t n, uint32_t cap, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig);
-template <bool SUB = false> __global__ void cv_points_kernel(uint32_t n, const uint8_t *pk, const uint8_t *sig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
 template <int WAVES, bool SUB = false> __global__ void cv_points_one_kernel(uint32_t n, const uint8_t *pk, const uint8_t *sig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
 template <int WAVES, bool SUB = false> __global__ void cv_hs_straus_kernel(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);
 __global__ void cv_bw16_init_kernel(uint32_t *tab);
-__global__ void cv_scalars_lat_kernel(uint32_t n, uint32_t cap, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig);
-__global__ void cv_points_pair_kernel(uint32_t n, const uint8_t *pk, const uint8_t *sig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
 template <bool B16, bool LAT = true> __global__ void cv_prep_lat_kernel(uint32_t n, uint32_t cap, uint32_t nbp, uint32_t pts4, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status, uint64_t *bitmap);
 template <bool SEQ> __global__ void cv_hs_straus_quad_kernel(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);
 __global__ void cv_gather16_kernel(const uint4 *src, uint4 *dst, size_t q);
 template <bool SEQ> __global__ void cv_hs_straus_tri_kernel(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, uint8_t *nib);
 __global__ void cv_sign_kernel( uint32_t n, const uint8_t *seed, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint8_t *pk_out, uint8_t *sig_out);
-// leaves per leaf-hash workgroup (sorted by SHA-256 block count inside it)
+// leaves per leaf-hash workgroup (each workgroup sorts 2 x CV_LEAF_BLOCK leaves by SHA-256 block count)
 #define CV_LEAF_BLOCK 256
-#ifndef CV_LEAF_SPAN
-#define CV_LEAF_SPAN 512   // leaves sorted together per workgroup (a multiple of CV_LEAF_BLOCK)
-#endif
-__global__ void cv_leaf_hash_kernel(uint32_t nleaves, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *leaf_digest);
 __global__ void cv_leaf_hash_pair_kernel(uint32_t nleaves, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *leaf_digest);
-__global__ void cv_merkle_tree_kernel(uint32_t ntx, const uint32_t *tx_begin, uint32_t *leaf_digest, uint8_t *ids, uint8_t *status);
+__global__ void cv_merkle_tree_kernel(uint32_t ntx, uint32_t leaf_base, const uint32_t *tx_begin, uint32_t *leaf_digest, uint8_t *ids, uint8_t *status);
 __global__ void cv_pmt_verify_kernel(uint32_t ntrees, const uint8_t *kind, const uint32_t *left, const uint32_t *right, const uint8_t *leaf_hash, const uint32_t *tree_begin, const uint8_t *root, const uint8_t *check, const uint32_t *check_begin, uint32_t *dig, uint8_t *flag, uint8_t *verdict, uint8_t *status);
 __global__ void cv_mad_bench_kernel(uint32_t iters, uint64_t *out);
 __global__ void cv_femul_bench_kernel(uint32_t iters, int32_t *out);
-__global__ void cv_prep_probe_kernel( uint32_t n, uint32_t cap, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint64_t *stamps);
 __global__ void cv_mad_clock_kernel(uint32_t iters, uint64_t *out);
-template <bool SUB> __global__ void cv_prep_tp_kernel(uint32_t n, uint32_t cap, uint32_t nbp, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);

@@ -14,7 +14,7 @@ from typing import Optional, Tuple
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# CV_LIB_PATH: load an alternative build of the same ABI (A/B tooling, tools/ab_lib.sh)
+# CV_LIB_PATH: load an alternative build of the same ABI (A/B tooling)
 LIB_PATH = os.environ.get("CV_LIB_PATH") or os.path.join(HERE, "libcordaverify.so")
 
 CV_OK = 0
@@ -29,20 +29,19 @@ EXPORTED = (
     "cv_ed25519_verify_batch", "cv_merkle_tx_ids", "cv_merkle_tx_ids_ex", "cv_ed25519_sign_batch",
     "cv_tx_verdicts", "cv_ed25519_verify_device", "cv_ed25519_verify_device_timed", "cv_ed25519_sign_device", "cv_merkle_tx_ids_device",
     "cv_synchronize", "cv_calibrate", "cv_ed25519_verify_batch_keyed", "cv_key_cache_reserve", "cv_key_cache_stats",
-    "cv_ed25519_verify_device_keyed", "cv_partial_merkle_verify", "cv_calibrate_cycles", "cv_diag_prep_phases",
+    "cv_ed25519_verify_device_keyed", "cv_partial_merkle_verify", "cv_calibrate_cycles",
     "cv_diag_dedupe_keys", "cv_host_alloc", "cv_host_free", "cv_ed25519_verify_batch_async", "cv_wait",
+    "cv_merkle_tx_ids_async", "cv_set_option", "cv_get_option", "cv_diag_stats",
 )
 
-
-def verify_mode() -> int:
-    """Throughput verify schedule: 1 = half-size scalars (prep | hsprep | hs_straus), 0 = full width
-    (prep | straus | finish)."""
-    lib = load()
-    return int(lib.cvk_get_verify_mode()) if hasattr(lib, "cvk_get_verify_mode") else 0
-
-
-def set_verify_mode(mode: int) -> None:
-    load().cvk_set_verify_mode(int(mode))
+# cv_set_option names (include/cordaverify.h CV_OPT_*)
+OPTIONS = {"tri_max": 1, "quad_max": 2, "drain_split": 3, "drain_split_pct": 4, "pipe_min": 5, "pipe_first": 6,
+           "pipe_chunk": 7, "async_chunk": 8, "host_threads": 9, "small_zero_copy": 10, "small_direct_min": 11,
+           "auto_keyed": 12, "shard_min": 13, "spread_min": 14, "merkle_chunk": 15}
+STATS = {"pipe": (0, ("plan_s", "pack_s", "wait_s", "enqueue_s", "sync_s", "calls", "subchunks", "direct_subchunks")),
+         "small": (1, ("setup_s", "pack_s", "launch_s", "sync_s", "assemble_s", "calls")),
+         "route": (2, ("calls", "routed_whole", "split_calls", "shards", "keyed_shards", "keyed_subchunks",
+                       "merkle_calls", "merkle_subchunks"))}
 
 
 class NativeUnavailable(RuntimeError):
@@ -86,6 +85,16 @@ def load():
         lib.cv_merkle_tx_ids.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp]
         lib.cv_merkle_tx_ids.restype = ctypes.c_int
         lib.cv_merkle_tx_ids_ex.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]
+        lib.cv_merkle_tx_ids_async.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(ctypes.c_uint64)]
+        lib.cv_merkle_tx_ids_async.restype = ctypes.c_int
+        lib.cv_set_option.argtypes = [_vp, ctypes.c_int, ctypes.c_int64]
+        lib.cv_set_option.restype = ctypes.c_int
+        lib.cv_get_option.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
+        lib.cv_get_option.restype = ctypes.c_int
+        lib.cv_diag_stats.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), _sz, ctypes.c_int]
+        lib.cv_diag_stats.restype = ctypes.c_int
+        lib.cvk_set_virtual_devices.argtypes = [ctypes.c_int]
+        lib.cvk_set_virtual_devices.restype = None
         lib.cv_partial_merkle_verify.argtypes = [_vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]
         lib.cv_partial_merkle_verify.restype = ctypes.c_int
         lib.cv_merkle_tx_ids_ex.restype = ctypes.c_int
@@ -100,49 +109,36 @@ def load():
         lib.cv_host_alloc.restype = ctypes.c_int
         lib.cv_host_free.argtypes = [_vp, _vp]
         lib.cv_host_free.restype = None
-        if hasattr(lib, "cvk_msg_end"):
-            lib.cvk_msg_end.argtypes = [_sz, _vp, _vp]
-            lib.cvk_msg_end.restype = ctypes.c_uint64
+        lib.cvk_msg_end.argtypes = [_sz, _vp, _vp]
+        lib.cvk_msg_end.restype = ctypes.c_uint64
         lib.cv_tx_verdicts.argtypes = [_sz, _vp, _vp, _vp]
         lib.cv_tx_verdicts.restype = ctypes.c_int
-        if hasattr(lib, "cvk_set_verify_mode"):                 # internal tuning knobs (not C-ABI)
-            lib.cvk_set_verify_mode.argtypes = [ctypes.c_int]
-            lib.cvk_get_verify_mode.restype = ctypes.c_int
-            if os.environ.get("CV_VERIFY_MODE"):                 # A/B: 0 = full-width group, 1 = half-size
-                lib.cvk_set_verify_mode(int(os.environ["CV_VERIFY_MODE"]))
         lib.cv_ed25519_verify_device.argtypes = [_vp, ctypes.c_int, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
         lib.cv_ed25519_verify_device.restype = ctypes.c_int
-        if hasattr(lib, "cv_ed25519_verify_device_timed"):      # absent only in pre-r01 A/B builds
-            lib.cv_ed25519_verify_device_timed.argtypes = [_vp, ctypes.c_int, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                                           ctypes.POINTER(ctypes.c_float)]
-            lib.cv_ed25519_verify_device_timed.restype = ctypes.c_int
+        lib.cv_ed25519_verify_device_timed.argtypes = [_vp, ctypes.c_int, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                                       ctypes.POINTER(ctypes.c_float)]
+        lib.cv_ed25519_verify_device_timed.restype = ctypes.c_int
         lib.cv_ed25519_sign_device.argtypes = [_vp, ctypes.c_int, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
         lib.cv_ed25519_sign_device.restype = ctypes.c_int
         lib.cv_merkle_tx_ids_device.argtypes = [_vp, ctypes.c_int, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
         lib.cv_merkle_tx_ids_device.restype = ctypes.c_int
         lib.cv_synchronize.argtypes = [_vp, ctypes.c_int]
         lib.cv_synchronize.restype = ctypes.c_int
-        if hasattr(lib, "cv_ed25519_verify_device_keyed"):      # absent only in older A/B builds
-            lib.cv_ed25519_verify_batch_keyed.argtypes = [_vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
-            lib.cv_ed25519_verify_batch_keyed.restype = ctypes.c_int
-            lib.cv_key_cache_reserve.argtypes = [_vp, _sz]
-            lib.cv_key_cache_reserve.restype = ctypes.c_int
-            lib.cv_key_cache_stats.argtypes = [_vp, ctypes.c_int, _vp]
-            lib.cv_key_cache_stats.restype = ctypes.c_int
-            lib.cv_ed25519_verify_device_keyed.argtypes = [_vp, ctypes.c_int, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp,
-                                                           _vp, _vp, _vp, ctypes.POINTER(ctypes.c_float)]
-            lib.cv_ed25519_verify_device_keyed.restype = ctypes.c_int
+        lib.cv_ed25519_verify_batch_keyed.argtypes = [_vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+        lib.cv_ed25519_verify_batch_keyed.restype = ctypes.c_int
+        lib.cv_key_cache_reserve.argtypes = [_vp, _sz]
+        lib.cv_key_cache_reserve.restype = ctypes.c_int
+        lib.cv_key_cache_stats.argtypes = [_vp, ctypes.c_int, _vp]
+        lib.cv_key_cache_stats.restype = ctypes.c_int
+        lib.cv_ed25519_verify_device_keyed.argtypes = [_vp, ctypes.c_int, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp,
+                                                       _vp, _vp, _vp, ctypes.POINTER(ctypes.c_float)]
+        lib.cv_ed25519_verify_device_keyed.restype = ctypes.c_int
         lib.cv_calibrate.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         lib.cv_calibrate.restype = ctypes.c_int
-        if hasattr(lib, "cv_calibrate_cycles"):                 # absent only in pre-r02 A/B builds
-            lib.cv_calibrate_cycles.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
-            lib.cv_calibrate_cycles.restype = ctypes.c_int
-            lib.cv_diag_prep_phases.argtypes = [_vp, ctypes.c_int, _sz, _vp, _vp, _vp, _vp, _vp,
-                                                ctypes.POINTER(ctypes.c_double)]
-            lib.cv_diag_prep_phases.restype = ctypes.c_int
-        if hasattr(lib, "cv_diag_dedupe_keys"):                 # absent only in older A/B builds
-            lib.cv_diag_dedupe_keys.argtypes = [_sz, _vp, _vp, ctypes.POINTER(_sz)]
-            lib.cv_diag_dedupe_keys.restype = ctypes.c_int
+        lib.cv_calibrate_cycles.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+        lib.cv_calibrate_cycles.restype = ctypes.c_int
+        lib.cv_diag_dedupe_keys.argtypes = [_sz, _vp, _vp, ctypes.POINTER(_sz)]
+        lib.cv_diag_dedupe_keys.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -158,9 +154,7 @@ def _u8(a, shape_last=None) -> np.ndarray:
 
 def _msg_end(lib, off: np.ndarray, ln: np.ndarray) -> int:
     """max(off + len) — the arena bytes the records reach (multi-threaded in the library for big n)."""
-    if hasattr(lib, "cvk_msg_end"):
-        return int(lib.cvk_msg_end(off.shape[0], _p(off), _p(ln)))
-    return int((off + ln).max())
+    return int(lib.cvk_msg_end(off.shape[0], _p(off), _p(ln)))
 
 
 def _check(rc: int, what: str):
@@ -171,14 +165,25 @@ def _check(rc: int, what: str):
 class Engine:
     """One context over a set of GPUs (bit d of device_mask = HIP device d; 0 = all).
 
-    Host-buffer methods mirror the JVM drop-in (synchronous); *_device methods take device pointers
-    (ints, e.g. torch.Tensor.data_ptr()) and an optional hipStream_t (int), and return immediately.
+    Host-buffer methods mirror the JVM drop-in (synchronous unless *_async); *_device methods take device
+    pointers (ints, e.g. torch.Tensor.data_ptr()) and an optional hipStream_t (int), and return
+    immediately.  The context is thread-safe: calls from several Python threads run concurrently (ctypes
+    releases the GIL) and the engine routes them over its devices.
+    virtual_devices (test hook): each GPU of the mask appears that many times (independent device slots).
     """
 
-    def __init__(self, device_mask: int = 0):
+    def __init__(self, device_mask: int = 0, virtual_devices: int = 1):
         lib = load()
         h = _vp()
-        rc = lib.cv_open(ctypes.c_uint32(device_mask), ctypes.byref(h))
+        if virtual_devices != 1:
+            with _lock:
+                lib.cvk_set_virtual_devices(virtual_devices)
+                try:
+                    rc = lib.cv_open(ctypes.c_uint32(device_mask), ctypes.byref(h))
+                finally:
+                    lib.cvk_set_virtual_devices(1)
+        else:
+            rc = lib.cv_open(ctypes.c_uint32(device_mask), ctypes.byref(h))
         if rc != CV_OK:
             raise NativeUnavailable(f"cv_open failed: {lib.cv_strerror(rc).decode()} (code {rc})")
         self._lib = lib
@@ -242,9 +247,8 @@ class Engine:
             raise ValueError("message range exceeds the arena")
         bitmap = np.zeros((n + 63) // 64, np.uint64)
         status = np.zeros(n, np.uint8) if want_status else None
-        with self.mu:
-            _check(self._lib.cv_ed25519_verify_batch(self._h, n, _p(pk), _p(sig), _p(arena), _p(off), _p(ln),
-                                                     _p(bitmap), _p(status)), "cv_ed25519_verify_batch")
+        _check(self._lib.cv_ed25519_verify_batch(self._h, n, _p(pk), _p(sig), _p(arena), _p(off), _p(ln),
+                                                 _p(bitmap), _p(status)), "cv_ed25519_verify_batch")
         return bitmap, status
 
     def verify_batch_async(self, pk, sig, arena, off, ln, want_status: bool = True) -> int:
@@ -265,18 +269,22 @@ class Engine:
         bitmap = np.zeros((n + 63) // 64, np.uint64)
         status = np.zeros(n, np.uint8) if want_status else None
         t = ctypes.c_uint64()
+        _check(self._lib.cv_ed25519_verify_batch_async(self._h, n, _p(pk), _p(sig), _p(arena), _p(off), _p(ln),
+                                                       _p(bitmap), _p(status), ctypes.byref(t)),
+               "cv_ed25519_verify_batch_async")
         with self.mu:
-            _check(self._lib.cv_ed25519_verify_batch_async(self._h, n, _p(pk), _p(sig), _p(arena), _p(off), _p(ln),
-                                                           _p(bitmap), _p(status), ctypes.byref(t)),
-                   "cv_ed25519_verify_batch_async")
             self._inflight[t.value] = (bitmap, status, (pk, sig, arena, off, ln))
         return t.value
 
-    def wait(self, ticket: int) -> Tuple[np.ndarray, Optional[np.ndarray]]:
+    def wait(self, ticket: int):
+        """cv_wait: the results of an async call — (bitmap, status) for a verify, (ids, status) for Merkle ids."""
         with self.mu:
-            bitmap, status, _ = self._inflight.pop(ticket, (None, None, None))
-            _check(self._lib.cv_wait(self._h, ctypes.c_uint64(ticket)), "cv_wait")
-        return bitmap, status
+            a, b, keep = self._inflight.get(ticket, (None, None, None))
+        _check(self._lib.cv_wait(self._h, ctypes.c_uint64(ticket)), "cv_wait")
+        with self.mu:
+            self._inflight.pop(ticket, None)
+        del keep
+        return a, b
 
     def verify_batch_keyed(self, keys, key_index, sig, arena, off, ln, want_status: bool = True):
         """keys (nk,32) distinct keys, key_index u32[n] -> (bitmap, status) exactly as verify_batch."""
@@ -296,10 +304,9 @@ class Engine:
             raise ValueError("message range exceeds the arena")
         bitmap = np.zeros((n + 63) // 64, np.uint64)
         status = np.zeros(n, np.uint8) if want_status else None
-        with self.mu:
-            _check(self._lib.cv_ed25519_verify_batch_keyed(self._h, n, nk, _p(keys), _p(key_index), _p(sig), _p(arena),
-                                                           _p(off), _p(ln), _p(bitmap), _p(status)),
-                   "cv_ed25519_verify_batch_keyed")
+        _check(self._lib.cv_ed25519_verify_batch_keyed(self._h, n, nk, _p(keys), _p(key_index), _p(sig), _p(arena),
+                                                       _p(off), _p(ln), _p(bitmap), _p(status)),
+               "cv_ed25519_verify_batch_keyed")
         return bitmap, status
 
     def key_cache_reserve(self, max_keys: int):
@@ -318,12 +325,12 @@ class Engine:
         ln = np.ascontiguousarray(ln, dtype=np.uint32)
         pk = np.zeros((n, 32), np.uint8)
         sig = np.zeros((n, 64), np.uint8)
-        with self.mu:
-            _check(self._lib.cv_ed25519_sign_batch(self._h, n, _p(seeds), _p(arena), _p(off), _p(ln), _p(pk),
-                                                   _p(sig)), "cv_ed25519_sign_batch")
+        _check(self._lib.cv_ed25519_sign_batch(self._h, n, _p(seeds), _p(arena), _p(off), _p(ln), _p(pk),
+                                               _p(sig)), "cv_ed25519_sign_batch")
         return pk, sig
 
-    def merkle_tx_ids(self, arena, leaf_off, leaf_len, tx_leaf_begin) -> Tuple[np.ndarray, np.ndarray]:
+    @staticmethod
+    def _merkle_args(arena, leaf_off, leaf_len, tx_leaf_begin):
         tx_leaf_begin = np.ascontiguousarray(tx_leaf_begin, dtype=np.uint32)
         ntx = tx_leaf_begin.shape[0] - 1
         arena = _u8(arena) if arena is not None and np.asarray(arena).size else np.zeros(16, np.uint8)
@@ -332,12 +339,52 @@ class Engine:
         if leaf_off.size == 0:
             leaf_off = np.zeros(1, np.uint64)
             leaf_len = np.zeros(1, np.uint32)
-        ids = np.zeros((max(ntx, 0), 32), np.uint8)
+        if leaf_off.shape[0] != leaf_len.shape[0] or (ntx > 0 and int(tx_leaf_begin[-1]) > leaf_off.shape[0]):
+            raise ValueError("tx_leaf_begin reaches past the leaf arrays")
+        if ntx > 0 and int(tx_leaf_begin[-1]) and _msg_end(load(), leaf_off[:int(tx_leaf_begin[-1])],
+                                                           leaf_len[:int(tx_leaf_begin[-1])]) > arena.size:
+            raise ValueError("leaf range exceeds the arena")
+        return ntx, arena, leaf_off, leaf_len, tx_leaf_begin
+
+    def merkle_tx_ids(self, arena, leaf_off, leaf_len, tx_leaf_begin, ids=None) -> Tuple[np.ndarray, np.ndarray]:
+        """WireTransaction.id of every transaction -> (ids (ntx,32) u8, status u8[ntx]).  ids: an optional
+        output array (e.g. pinned, host_empty), so the ids are DMAed straight into it."""
+        ntx, arena, leaf_off, leaf_len, tx_leaf_begin = self._merkle_args(arena, leaf_off, leaf_len, tx_leaf_begin)
+        ids = np.zeros((max(ntx, 0), 32), np.uint8) if ids is None else ids
         st = np.zeros(max(ntx, 0), np.uint8)
-        with self.mu:
-            _check(self._lib.cv_merkle_tx_ids_ex(self._h, ntx, _p(arena), _p(leaf_off), _p(leaf_len),
-                                                 _p(tx_leaf_begin), _p(ids), _p(st)), "cv_merkle_tx_ids_ex")
+        _check(self._lib.cv_merkle_tx_ids_ex(self._h, ntx, _p(arena), _p(leaf_off), _p(leaf_len),
+                                             _p(tx_leaf_begin), _p(ids), _p(st)), "cv_merkle_tx_ids_ex")
         return ids, st
+
+    def merkle_tx_ids_async(self, arena, leaf_off, leaf_len, tx_leaf_begin, ids=None) -> int:
+        """cv_merkle_tx_ids_async: enqueue and return a ticket; wait(ticket) -> (ids, status)."""
+        ntx, arena, leaf_off, leaf_len, tx_leaf_begin = self._merkle_args(arena, leaf_off, leaf_len, tx_leaf_begin)
+        ids = np.zeros((max(ntx, 0), 32), np.uint8) if ids is None else ids
+        st = np.zeros(max(ntx, 0), np.uint8)
+        t = ctypes.c_uint64()
+        _check(self._lib.cv_merkle_tx_ids_async(self._h, ntx, _p(arena), _p(leaf_off), _p(leaf_len),
+                                                _p(tx_leaf_begin), _p(ids), _p(st), ctypes.byref(t)),
+               "cv_merkle_tx_ids_async")
+        with self.mu:
+            self._inflight[t.value] = (ids, st, (arena, leaf_off, leaf_len, tx_leaf_begin))
+        return t.value
+
+    # ------------------------------------------------------------ options and diagnostics
+    def set_option(self, name: str, value: int):
+        _check(self._lib.cv_set_option(self._h, OPTIONS[name], int(value)), f"cv_set_option({name})")
+
+    def get_option(self, name: str) -> int:
+        v = ctypes.c_int64()
+        _check(self._lib.cv_get_option(self._h, OPTIONS[name], ctypes.byref(v)), f"cv_get_option({name})")
+        return v.value
+
+    def stats(self, kind: str, reset: bool = False) -> dict:
+        which, names = STATS[kind]
+        out = (ctypes.c_double * len(names))()
+        rc = self._lib.cv_diag_stats(self._h, which, out, len(names), int(reset))
+        if rc < 0:
+            raise CvError(rc, "cv_diag_stats")
+        return dict(zip(names, out))
 
     def partial_merkle_verify(self, kind, left, right, leaf_hash, tree_begin, root, check, check_begin
                               ) -> Tuple[np.ndarray, np.ndarray]:
@@ -359,11 +406,10 @@ class Engine:
         check = pad(check, np.uint8, (1, 32))
         verdict = np.zeros(max(ntrees, 1), np.uint8)
         status = np.zeros(max(ntrees, 1), np.uint8)
-        with self.mu:
-            _check(self._lib.cv_partial_merkle_verify(self._h, ntrees, nnodes, _p(kind), _p(left), _p(right),
-                                                      _p(leaf_hash), _p(tree_begin), _p(root), ncheck, _p(check),
-                                                      _p(check_begin), _p(verdict), _p(status)),
-                   "cv_partial_merkle_verify")
+        _check(self._lib.cv_partial_merkle_verify(self._h, ntrees, nnodes, _p(kind), _p(left), _p(right),
+                                                  _p(leaf_hash), _p(tree_begin), _p(root), ncheck, _p(check),
+                                                  _p(check_begin), _p(verdict), _p(status)),
+               "cv_partial_merkle_verify")
         return verdict[:ntrees], status[:ntrees]
 
     # ------------------------------------------------------------ device-resident API
@@ -374,8 +420,8 @@ class Engine:
 
     def verify_device_timed(self, device: int, n: int, d_pk: int, d_sig: int, d_arena: int, d_off: int, d_len: int,
                             d_bitmap: int, stream: int = 0) -> Tuple[float, float, float]:
-        """Synchronous verify; returns three kernel durations in ms (HIP events): (prep, straus, finish),
-        or (prep, hsprep, hs_straus) in the half-size schedule (verify_mode() == 1)."""
+        """Synchronous verify; returns three kernel durations in ms (HIP events): (scalars, points,
+        hs_straus) for throughput batches, (scalars + point pairs, 0, tri / quad Straus) for latency ones."""
         ms = (ctypes.c_float * 3)()
         _check(self._lib.cv_ed25519_verify_device_timed(self._h, device, n, d_pk, d_sig, d_arena, d_off, d_len,
                                                         d_bitmap, stream or None, ms), "cv_ed25519_verify_device_timed")
@@ -414,15 +460,6 @@ class Engine:
         _check(self._lib.cv_calibrate_cycles(self._h, device, o), "cv_calibrate_cycles")
         return {"mac_per_s": o[0], "clock_ghz": o[1], "cycles_per_wave_instr": o[2], "simds": int(o[3]),
                 "mac_per_s_at_2p4ghz": o[4]}
-
-    def diag_prep_phases(self, device: int, n: int, d_pk: int, d_sig: int, d_arena: int, d_off: int,
-                         d_len: int) -> dict:
-        """Mean shader cycles per wave of each fused-prep phase (cv_diag_prep_phases)."""
-        o = (ctypes.c_double * 8)()
-        _check(self._lib.cv_diag_prep_phases(self._h, device, n, d_pk, d_sig, d_arena, d_off, d_len, o),
-               "cv_diag_prep_phases")
-        return {"hash": o[0], "lattice": o[1], "digits": o[2], "decode": o[3], "tables": o[4], "total": o[5],
-                "waves": int(o[6]), "hash_sha512_part": o[7]}
 
     def synchronize(self, device: int):
         _check(self._lib.cv_synchronize(self._h, device), "cv_synchronize")

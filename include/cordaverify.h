@@ -31,8 +31,10 @@
  * Conventions
  *   - Return codes: CV_OK (0) or a negative CV_E* code; nothing throws, aborts or longjmps across
  *     the ABI.  cv_strerror() gives a static message.
- *   - Host-buffer calls are synchronous; the caller owns every buffer.  A cv_ctx may be used by one
- *     thread at a time (the JVM shim holds one ctx per process behind a mutex).
+ *   - Host-buffer calls are synchronous unless named _async; the caller owns every buffer.  A cv_ctx is
+ *     thread-safe: calls from several threads run concurrently on different devices (each device has
+ *     its own lock and worker thread) and queue on the same one.  A notary's batching threads share one
+ *     context (the JVM shim holds one ctx per process, no mutex around it).
  *   - Record layout (structure-of-arrays): pk[n][32], sig[n][64] (R || S), message i is
  *     msg_arena[msg_off[i] .. msg_off[i] + msg_len[i]).
  *   - verdict_bitmap: ceil(n/64) uint64 words, bit (i % 64) of word (i / 64) = signature i valid.
@@ -40,8 +42,10 @@
  *     bytes are not a valid point: the reference throws IllegalArgumentException when building the
  *     EdDSAPublicKey).  Length errors (sig != 64 B -> SignatureException, key != 32 B) cannot be
  *     expressed in these fixed-width records; the host shim rejects them before the call.
- *   - Multi-GPU: cv_open(mask) with several bits set shards host-buffer batches by contiguous
- *     signature ranges (multiples of 64) over the devices, one host thread + one HIP stream each.
+ *   - Multi-GPU: cv_open(mask) with several bits set routes host-buffer batches over the devices: a batch
+ *     up to CV_OPT_SHARD_MIN records goes whole to the least loaded device, a throughput batch (from
+ *     CV_OPT_SPREAD_MIN) is cut into contiguous ranges (multiples of 64) over all of them, a batch between
+ *     over the devices idle at submission.  No collective: each shard's results land in the caller's arrays.
  */
 #ifndef CORDAVERIFY_H
 #define CORDAVERIFY_H
@@ -83,14 +87,16 @@ int cv_ed25519_verify_batch(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint
                             const uint8_t *msg_arena, const uint64_t *msg_off, const uint32_t *msg_len,
                             uint64_t *verdict_bitmap, uint8_t *status);
 
-/* Asynchronous form of cv_ed25519_verify_batch (same records, same verdicts and status): enqueues the
- * batch on the context's devices and returns a ticket; cv_wait(ticket) returns once verdict_bitmap and
- * status hold the results.  Until then the caller keeps every array of the call alive and unmodified
- * (pinned inputs are read by DMA after this call returns).  Two calls per device may be in flight: a
- * third first completes the oldest (whose cv_wait then returns at once).  A node's batching loop
- * submits batch k+1 before waiting for batch k, so its copies and kernels fill the first one's
- * pipeline ramp and tail.  No host dedupe / keyed path here.  Tickets are waited at most once;
- * cv_close drops results not yet waited for. */
+/* Asynchronous form of cv_ed25519_verify_batch (same records, same verdicts and status, the same
+ * automatic keyed path for batches whose keys repeat): enqueues the batch on the context's devices and
+ * returns a ticket; cv_wait(ticket) returns once verdict_bitmap and status hold the results.  Until then
+ * the caller keeps every array of the call alive and unmodified (pinned inputs are read by DMA after this
+ * call returns).  Four pipelined calls (verify or Merkle) per device may be in flight: a fifth first
+ * completes the oldest (whose cv_wait then returns at once).  A node's batching loop submits batch k+1
+ * before waiting for batch k, so its copies and kernels fill the first one's pipeline ramp and tail.
+ * cv_wait may run on another thread than the submission and does not block submissions.  Tickets are
+ * waited at most once; tickets never waited for are dropped once their results are in; cv_close drops
+ * results not yet waited for. */
 int cv_ed25519_verify_batch_async(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint8_t *sig,
                                   const uint8_t *msg_arena, const uint64_t *msg_off, const uint32_t *msg_len,
                                   uint64_t *verdict_bitmap, uint8_t *status, uint64_t *ticket);
@@ -112,8 +118,8 @@ void cv_host_free(cv_ctx *ctx, void *p);
  * (decoded A and comb multiples k * 2^(64j) * (-A), k = 0..128, 66 KB per key, affine) resident on each
  * device, keyed by the 32 key bytes, so a key is decoded once and each verify needs 56 doublings
  * instead of 252.
- * cv_ed25519_verify_batch takes this path by itself (host-side dedupe) for batches of up to 2^18
- * signatures with at least eight signatures per distinct key. */
+ * cv_ed25519_verify_batch(_async) takes this path by itself (host-side dedupe, any batch size above
+ * CV_OPT_TRI_MAX) for batches with at least eight signatures per distinct key. */
 int cv_ed25519_verify_batch_keyed(cv_ctx *ctx, size_t n, size_t nkeys, const uint8_t *keys, const uint32_t *key_index,
                                   const uint8_t *sig, const uint8_t *msg_arena, const uint64_t *msg_off,
                                   const uint32_t *msg_len, uint64_t *verdict_bitmap, uint8_t *status);
@@ -129,9 +135,19 @@ int cv_key_cache_stats(cv_ctx *ctx, int device, uint64_t *out4);
 int cv_merkle_tx_ids(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
                      const uint32_t *leaf_len, const uint32_t *tx_leaf_begin /* ntx+1 */, uint8_t *ids /* ntx*32 */);
 
-/* as cv_merkle_tx_ids, with per-transaction status (CV_TX_OK / CV_TX_EMPTY) */
+/* as cv_merkle_tx_ids, with per-transaction status (CV_TX_OK / CV_TX_EMPTY).  Transactions are cut into
+ * contiguous ranges over the context's devices (routed as the verify batches), each range's leaves copied
+ * from its own byte window of leaf_arena (offsets need not be sorted; scattered leaves are gathered) and
+ * pipelined through the devices' copy streams in sub-chunks of about CV_OPT_MERKLE_CHUNK leaves; leaf
+ * arrays in pinned memory (cv_host_alloc) are DMAed in place. */
 int cv_merkle_tx_ids_ex(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
                         const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, uint8_t *ids, uint8_t *tx_status);
+
+/* Asynchronous form of cv_merkle_tx_ids_ex (ticket and cv_wait as cv_ed25519_verify_batch_async): a C3 node
+ * step submits the Merkle ids of batch k+1 while the verify of batch k runs, so their copies overlap. */
+int cv_merkle_tx_ids_async(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
+                           const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, uint8_t *ids, uint8_t *tx_status,
+                           uint64_t *ticket);
 
 /* Partial Merkle trees (FilteredTransaction / PartialMerkleTree.verify), one verdict per tree.
  * The shim flattens each PartialTree object in post-order and concatenates the trees: node k has
@@ -222,18 +238,48 @@ int cv_calibrate(cv_ctx *ctx, int device, double *mad_per_s, double *femul_per_s
  * SIMD count, MAC/s ceiling at the 2.4 GHz peak clock for that cycle count}. */
 int cv_calibrate_cycles(cv_ctx *ctx, int device, double *out);
 
-/* Diagnostics (no reference counterpart): shader cycles per wave of each phase of the throughput
- * prep kernel on a device-resident batch (n <= 2^22) — out[8] = {hash, lattice, digits, decode
- * A+R, tables, total, waves, SHA-512 part of hash}.  Writes the device's verify workspace; not thread-safe with verifies
- * on the same device. */
-int cv_diag_prep_phases(cv_ctx *ctx, int device, size_t n, const void *d_pk, const void *d_sig,
-                        const void *d_arena, const void *d_off, const void *d_len, double *out);
+/* ---------------------------------------------------------------- options
+ * Per-context tuning, read at the start of every call (cv_set_option from any thread; a call in progress
+ * keeps the values it started with).  Defaults are the measured best on MI355X; the kernel-form
+ * thresholds also let tests force each form on any batch size.  CV_E_ARGS for an unknown option or a value
+ * out of range. */
+#define CV_OPT_TRI_MAX 1            /* batches up to this many signatures: tri-chain latency kernels (4096; 0 = never) */
+#define CV_OPT_QUAD_MAX 2           /* up to this: quad latency kernels (32768; 0 = never); above: throughput kernels */
+#define CV_OPT_DRAIN_SPLIT 3        /* throughput chunks' drain overlap: 0 off, 1 auto (default), 2 always */
+#define CV_OPT_DRAIN_SPLIT_PCT 4    /* the overlapped tail's share of a split chunk, percent (10) */
+#define CV_OPT_PIPE_MIN 5           /* host batches (per device) above this are pipelined (131072) */
+#define CV_OPT_PIPE_FIRST 6         /* first sub-chunk of a synchronous pipelined call (32768; sizes then double) */
+#define CV_OPT_PIPE_CHUNK 7         /* steady sub-chunk of a synchronous pipelined call (262144) */
+#define CV_OPT_ASYNC_CHUNK 8        /* sub-chunk of the asynchronous calls (262144) */
+#define CV_OPT_HOST_THREADS 9       /* host threads per device packing pageable inputs / deduping keys (8) */
+#define CV_OPT_SMALL_ZERO_COPY 10   /* tri-form host batches: 0 DMA, 1 zero-copy reads, 2 gather kernel, 3 auto (default) */
+#define CV_OPT_SMALL_DIRECT_MIN 11  /* unpipelined batches from pinned inputs DMA them in place from this size (16384) */
+#define CV_OPT_AUTO_KEYED 12        /* host dedupe + keyed path for repeated keys: 1 on (default), 0 off */
+#define CV_OPT_SHARD_MIN 13         /* routing: batches up to this go whole to one device; fewer per shard never (4096) */
+#define CV_OPT_SPREAD_MIN 14        /* routing: batches from this size are cut over all devices (262144) */
+#define CV_OPT_MERKLE_CHUNK 15      /* leaves per Merkle pipeline sub-chunk (262144) */
+#define CV_OPT_COUNT 16
+int cv_set_option(cv_ctx *ctx, int option, int64_t value);
+int cv_get_option(cv_ctx *ctx, int option, int64_t *value);
+
+/* Diagnostics (no reference counterpart): the context's counters since the last reset; returns the number
+ * of values of that kind (fills at most nout of them), or CV_E_ARGS.
+ *   CV_STATS_PIPE  {plan, pack, wait, enqueue, sync seconds of the pipelined host path; calls; sub-chunks;
+ *                   sub-chunks DMAed in place from pinned inputs}
+ *   CV_STATS_SMALL {setup, pack, launch, sync, assemble seconds of the zero-copy notary path; calls}
+ *   CV_STATS_ROUTE {calls, routed whole to one device, cut over several, shards, keyed shards, keyed
+ *                   sub-chunks, Merkle calls, Merkle sub-chunks} */
+#define CV_STATS_PIPE 0
+#define CV_STATS_SMALL 1
+#define CV_STATS_ROUTE 2
+int cv_diag_stats(cv_ctx *ctx, int which, double *out, size_t nout, int reset);
 
 /* Diagnostics: the host-side key dedupe cv_ed25519_verify_batch runs before choosing the keyed path
- * (seeded hash of all 32 key bytes).  Returns 1 and fills key_index[n] / *nkeys when the batch
- * repeats keys enough for the keyed path (64 <= n <= 2^18, at least eight signatures per distinct
- * key; above 1,024 signatures a first 256 carrying more than 192 distinct keys is taken as
- * distinct-keyed without hashing the rest), else 0.  Host only: needs no device and no context. */
+ * (seeded hash of all 32 key bytes).  Returns 1 and fills key_index[n] / *nkeys (distinct keys in
+ * first-seen order) when the batch repeats keys enough for the keyed path (n >= 64, at least eight
+ * signatures per distinct key), else 0.  Above 16,384 signatures a sample of 4,096 at pseudo-random
+ * positions first estimates the repetition (birthday count) and a batch estimated below four signatures
+ * per key is taken as distinct-keyed without hashing the rest.  Host only: needs no device and no context. */
 int cv_diag_dedupe_keys(size_t n, const uint8_t *pk, uint32_t *key_index, size_t *nkeys);
 
 #ifdef __cplusplus

@@ -2,11 +2,12 @@
 // built with AddressSanitizer + UndefinedBehaviorSanitizer (or ThreadSanitizer) and exercised without a
 // GPU.  cv_api.cpp is included whole so its file-local functions are reachable; the kernel launchers it
 // calls (cv_launch.h) are stubs that never run.  Checked here:
-//   dedupe_keys          key dedupe of cv_ed25519_verify_batch (pools, early out, limits)
+//   dedupe_keys          key dedupe of cv_ed25519_verify_batch (pools, gate, slices on a pool, first-seen order)
 //   WorkerPool/par_copy  the packing thread pool and its pinned-staging copies (piece boundaries, empty jobs)
 //   stage_plan/_pack     staging layout of a record range (arena range and compact gather forms)
 //   pipe_cuts            the host pipeline's sub-chunk plan (64-aligned, covering, balanced tail)
-//   for_each_shard       shard ranges over k devices, one thread each
+//   dispatch             routing: shard ranges over k devices, per-device exclusion, concurrent callers
+//   mstage_plan/_pack    Merkle staging of a transaction range (non-monotone offsets, empty txs, compact)
 //   cv_tx_verdicts       per-transaction AND
 // Exit status 0 = every check passed; sanitizer reports abort the run (halt_on_error).
 #include "../../corda_amd/csrc/cv_api.cpp"
@@ -16,23 +17,20 @@
 
 extern "C" {
 // launcher stubs: nothing in this test reaches the device
-hipError_t cvk_verify(uint32_t, const uint8_t *, const uint8_t *, const uint8_t *, const uint64_t *, const uint32_t *,
-                      uint64_t *, uint8_t *, uint32_t *, uint32_t *, uint32_t *, uint8_t *, uint32_t *, uint32_t,
-                      hipStream_t, hipEvent_t *, const CvkSplit *) { return hipErrorNoDevice; }
+hipError_t cvk_verify(const CvkPlan *, uint32_t, const uint8_t *, const uint8_t *, const uint8_t *, const uint64_t *,
+                      const uint32_t *, uint64_t *, uint8_t *, uint32_t *, uint8_t *, uint32_t *, uint32_t, hipStream_t,
+                      hipEvent_t *, const CvkSplit *) { return hipErrorNoDevice; }
 hipError_t cvk_sign(uint32_t, const uint8_t *, const uint8_t *, const uint64_t *, const uint32_t *, uint8_t *, uint8_t *,
                     hipStream_t) { return hipErrorNoDevice; }
 hipError_t cvk_pmt_verify(uint32_t, const uint8_t *, const uint32_t *, const uint32_t *, const uint8_t *, const uint32_t *,
                           const uint8_t *, const uint8_t *, const uint32_t *, uint32_t *, uint8_t *, uint8_t *, uint8_t *,
                           hipStream_t) { return hipErrorNoDevice; }
-hipError_t cvk_merkle(uint32_t, uint32_t, const uint8_t *, const uint64_t *, const uint32_t *, const uint32_t *, uint32_t *,
-                      uint8_t *, uint8_t *, hipStream_t) { return hipErrorNoDevice; }
+hipError_t cvk_merkle(uint32_t, uint32_t, uint32_t, const uint8_t *, const uint64_t *, const uint32_t *, const uint32_t *,
+                      uint32_t *, uint8_t *, uint8_t *, hipStream_t) { return hipErrorNoDevice; }
 hipError_t cvk_calibrate(uint32_t, int, uint32_t, void *, hipStream_t) { return hipErrorNoDevice; }
-hipError_t cvk_prep_probe(uint32_t, const uint8_t *, const uint8_t *, const uint8_t *, const uint64_t *, const uint32_t *,
-                          uint32_t *, uint32_t *, uint32_t, uint64_t *, hipStream_t) { return hipErrorNoDevice; }
 hipError_t cvk_mad_clock(uint32_t, uint32_t, uint64_t *, hipStream_t) { return hipErrorNoDevice; }
-uint32_t cvk_get_tri_max(void) { return 4096; }
-int cvk_tri_zc_ok(uint32_t, uint32_t) { return 0; }
-hipError_t cvk_verify_tri_zc(uint32_t, const uint8_t *, const uint8_t *, const uint8_t *, const uint64_t *,
+int cvk_tri_zc_ok(const CvkPlan *, uint32_t, uint32_t) { return 0; }
+hipError_t cvk_verify_tri_zc(const CvkPlan *, uint32_t, const uint8_t *, const uint8_t *, const uint8_t *, const uint64_t *,
                              const uint32_t *, uint8_t *, uint8_t *, uint32_t *, uint8_t *, uint32_t *, uint32_t,
                              hipStream_t, const void *, void *, size_t) {
     return hipErrorNoDevice;
@@ -41,7 +39,7 @@ hipError_t cvk_prepare(hipStream_t) { return hipErrorNoDevice; }
 hipError_t cvk_keyprep(uint32_t, const uint8_t *, const uint32_t *, uint32_t *, uint32_t *, uint8_t *, hipStream_t) {
     return hipErrorNoDevice;
 }
-hipError_t cvk_verify_keyed(uint32_t, const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *,
+hipError_t cvk_verify_keyed(const CvkPlan *, uint32_t, const uint8_t *, const uint32_t *, const uint32_t *, const uint32_t *,
                             const uint8_t *, const uint8_t *, const uint8_t *, const uint64_t *, const uint32_t *,
                             uint64_t *, uint8_t *, uint32_t *, uint32_t *, uint8_t *, uint32_t, hipStream_t, hipEvent_t *) {
     return hipErrorNoDevice;
@@ -66,27 +64,37 @@ static uint64_t rnd() {
 }
 
 static void test_dedupe() {
-    for (size_t n : {0ul, 1ul, 63ul, 64ul, 65ul, 1000ul, 1025ul, 5000ul, 70000ul, (size_t)kAutoKeyedMax,
-                     (size_t)kAutoKeyedMax + 1}) {
+    for (size_t n : {0ul, 1ul, 63ul, 64ul, 65ul, 1000ul, 1025ul, 5000ul, 70000ul, 300001ul}) {
         for (size_t pool : {1ul, 7ul, 64ul, 300ul, 100000ul}) {
             std::vector<uint8_t> keys_pool(32 * pool);
             for (auto &b : keys_pool) b = (uint8_t)rnd();
             std::vector<uint8_t> pk(32 * std::max<size_t>(n, 1));
             for (size_t i = 0; i < n; i++) std::memcpy(&pk[32 * i], &keys_pool[32 * (rnd() % pool)], 32);
-            std::vector<uint8_t> keys;
-            std::vector<uint32_t> idx;
-            const bool took = dedupe_keys(n, pk.data(), keys, idx);
-            if (n < 64 || n > kAutoKeyedMax) CHECK(!took);
-            if (!took) continue;
-            const size_t nk = keys.size() / 32;
-            CHECK(idx.size() == n);
-            CHECK(8 * nk <= n);
-            for (size_t i = 0; i < n; i++) {
-                CHECK(idx[i] < nk);
-                if (idx[i] < nk) CHECK(std::memcmp(&keys[32 * idx[i]], &pk[32 * i], 32) == 0);
+            for (int threads : {1, 4}) {
+                std::unique_ptr<WorkerPool> wp(threads > 1 ? new WorkerPool(threads - 1) : nullptr);
+                std::vector<uint8_t> keys;
+                std::vector<uint32_t> idx;
+                const bool took = dedupe_keys(n, pk.data(), keys, idx, wp.get());
+                if (n < 64) CHECK(!took);
+                if (n >= 64 && pool * 8 <= n / 2 && pool <= 300) CHECK(took);   // clearly repeated: keyed
+                if (!took) continue;
+                const size_t nk = keys.size() / 32;
+                CHECK(idx.size() == n);
+                CHECK(8 * nk <= n);
+                for (size_t i = 0; i < n; i++) {
+                    CHECK(idx[i] < nk);
+                    if (idx[i] < nk) CHECK(std::memcmp(&keys[32 * idx[i]], &pk[32 * i], 32) == 0);
+                }
+                // distinct keys are distinct, in first-seen order
+                std::vector<uint8_t> seen(nk, 0);
+                uint32_t next = 0;
+                for (size_t i = 0; i < n; i++)
+                    if (idx[i] < nk && !seen[idx[i]]) {
+                        CHECK(idx[i] == next);
+                        seen[idx[i]] = 1;
+                        next++;
+                    }
             }
-            for (size_t a = 0; a + 1 < nk && a < 64; a++)     // distinct keys are distinct
-                CHECK(std::memcmp(&keys[32 * a], &keys[32 * (a + 1)], 32) != 0);
         }
     }
     // keys that differ in one byte only must not collide in the dedupe
@@ -95,8 +103,14 @@ static void test_dedupe() {
     for (size_t i = 0; i < n; i++) pk[32 * i + 31] = (uint8_t)(i / 16);   // 16 per key, 256 keys
     std::vector<uint8_t> keys;
     std::vector<uint32_t> idx;
-    CHECK(dedupe_keys(n, pk.data(), keys, idx));
+    CHECK(dedupe_keys(n, pk.data(), keys, idx, nullptr));
     CHECK(keys.size() / 32 == 256);
+    // the gate: a large distinct-keyed batch is declined, a pooled one accepted
+    std::vector<uint8_t> big(32 * 200000);
+    for (auto &b : big) b = (uint8_t)rnd();
+    CHECK(!dedupe_gate(200000, big.data()));
+    for (size_t i = 0; i < 200000; i++) std::memcpy(&big[32 * i], &big[32 * (rnd() % 1000)], 32);
+    CHECK(dedupe_gate(200000, big.data()));
 }
 
 static void test_pool() {
@@ -162,10 +176,12 @@ static void test_stage(bool scattered, size_t n) {
             WorkerPool pool(2);
             const Stage st = stage_plan(b, e, off.data(), len.data(), (e - b) % 2 ? &pool : nullptr);
             const Stage st1 = stage_plan(b, e, off.data(), len.data());
+            const Stage stk = stage_plan(b, e, off.data(), len.data(), nullptr, true);
+            CHECK(stk.keyed && stk.o_kidx == 0 && stk.o_sig == al16((e - b) * 4) && stk.lo == st.lo && stk.hi == st.hi);
             CHECK(st.lo == st1.lo && st.hi == st1.hi && st.total == st1.total && st.compact == st1.compact);
             if (e - b >= 64) CHECK(st.compact == scattered);
             std::vector<uint8_t> h(st.total + 64, 0xEE);
-            stage_pack(st, h.data(), b, pk.data(), sig.data(), arena.data(), off.data(), len.data(), &pool, [] {});
+            stage_pack(st, h.data(), b, pk.data(), nullptr, sig.data(), arena.data(), off.data(), len.data(), &pool, [] {});
             CHECK(h[st.total] == 0xEE);                                    // nothing past the staging
             CHECK(std::memcmp(h.data() + st.o_pk, &pk[32 * b], 32 * (e - b)) == 0);
             CHECK(std::memcmp(h.data() + st.o_sig, &sig[64 * b], 64 * (e - b)) == 0);
@@ -203,34 +219,105 @@ static void test_pipe_cuts() {
     }
 }
 
-static void test_shards() {
-    for (size_t ndev : {1ul, 2ul, 3ul, 8ul}) {
-        cv_ctx ctx;
-        ctx.devs.resize(ndev);
-        for (size_t k = 0; k < ndev; k++) ctx.devs[k].ordinal = (int)k;
-        for (size_t n : {1ul, 64ul, 65ul, 1000ul, 100003ul}) {
-            std::vector<std::vector<std::pair<size_t, size_t>>> got(ndev);
+// Merkle staging of transactions [t0, t1): leaf offsets not monotone (the arena holds the leaves in reverse
+// order, with gaps), empty transactions, the compact (scattered) form
+static void test_mstage(bool scattered) {
+    const size_t ntx = 700;
+    std::vector<uint32_t> txb(ntx + 1, 0);
+    for (size_t t = 0; t < ntx; t++) txb[t + 1] = txb[t] + (uint32_t)(t % 9 == 0 ? 0 : rnd() % 8);
+    const size_t nl = txb[ntx];
+    std::vector<uint32_t> len(nl);
+    std::vector<uint64_t> off(nl);
+    const size_t arena_size = scattered ? (16u << 20) : nl * 800 + 64;
+    std::vector<uint8_t> arena(arena_size);
+    for (auto &b : arena) b = (uint8_t)rnd();
+    uint64_t pos = arena_size - 8;
+    for (size_t i = 0; i < nl; i++) {
+        len[i] = (uint32_t)(rnd() % 700);
+        if (scattered) {
+            off[i] = rnd() % (arena_size - 701);
+        } else {
+            pos -= len[i] + rnd() % 5;
+            off[i] = pos;                                    // decreasing offsets
+        }
+    }
+    WorkerPool pool(2);
+    for (size_t t0 : {0ul, 1ul, 350ul}) {
+        for (size_t t1 : {t0 + 1, t0 + 9, ntx}) {
+            if (t1 > ntx || t1 <= t0) continue;
+            const MStage st = mstage_plan(t0, t1, txb.data(), off.data(), len.data(), &pool);
+            CHECK(st.l0 == txb[t0] && st.l1 == txb[t1]);
+            std::vector<uint8_t> h(st.total + 64, 0xEE);
+            mstage_pack(st, h.data(), txb.data(), arena.data(), off.data(), len.data(), &pool);
+            CHECK(h[st.total] == 0xEE);
+            const uint64_t *hoff = reinterpret_cast<const uint64_t *>(h.data() + st.o_off);
+            const uint32_t *hlen = reinterpret_cast<const uint32_t *>(h.data() + st.o_len);
+            const uint32_t *htx = reinterpret_cast<const uint32_t *>(h.data() + st.o_txb);
+            for (size_t t = t0; t <= t1; t++) CHECK(htx[t - t0] == txb[t]);
+            for (size_t i = st.l0; i < st.l1; i++) {
+                CHECK(hlen[i - st.l0] == len[i]);
+                const uint64_t rel = hoff[i - st.l0] - st.lo;
+                CHECK(rel + len[i] <= st.hi - st.lo);
+                CHECK(std::memcmp(h.data() + st.o_ar + rel, &arena[off[i]], len[i]) == 0);
+            }
+            if (st.l1 - st.l0 > 64) CHECK(st.compact == scattered);
+        }
+    }
+}
+
+// Routing: shards of every call cover [0, n) exactly (starts at multiples of 64), a device never runs two
+// shards at once (its lock), and the load counts return to zero; threads > 1: concurrent callers
+// (VERDICT r3 item 3 — 4 threads x 200 interleaved calls on a 4-device context, host logic only; under
+// ThreadSanitizer in san_host_tsan).
+static void test_dispatch(size_t ndev, int nthreads, int calls) {
+    cv_ctx ctx;
+    for (size_t k = 0; k < ndev; k++) {
+        ctx.devs.emplace_back(new Device());
+        ctx.devs.back()->ordinal = (int)k;
+    }
+    ctx.opt[CV_OPT_SHARD_MIN].store(1024);
+    ctx.opt[CV_OPT_SPREAD_MIN].store(65536);
+    std::vector<std::atomic<int>> busy(ndev);
+    std::atomic<int> fails{0};
+    auto caller = [&](int t) {
+        uint64_t x = 0x1234567ull + (uint64_t)t * 7919;
+        for (int c = 0; c < calls; c++) {
+            x = x * 6364136223846793005ull + 1442695040888963407ull;
+            static const size_t sizes[] = {1, 64, 100, 1024, 4096, 5000, 9000, 40000, 70001};
+            const size_t n = sizes[(x >> 33) % 9];
             std::mutex mu;
-            const int rc = for_each_shard(&ctx, n, [&](Device &d, size_t b, size_t e, int threads) {
-                std::lock_guard<std::mutex> g(mu);
-                got[(size_t)d.ordinal].push_back({b, e});
+            std::vector<std::pair<size_t, size_t>> got;
+            const Opts o = ctx.opts();
+            const int rc = dispatch(&ctx, o, n, 64, [&](Device &d, size_t b, size_t e, int threads) {
+                const size_t k = dev_index(&ctx, d);
+                if (busy[k].exchange(1) != 0) fails++;          // two shards on one device at once
+                std::this_thread::yield();
+                {
+                    std::lock_guard<std::mutex> g(mu);
+                    got.push_back({b, e});
+                }
+                busy[k].store(0);
                 return threads >= 1 ? CV_OK : CV_E_ARGS;
             });
-            CHECK(rc == CV_OK);
-            std::vector<std::pair<size_t, size_t>> all;
-            for (auto &v : got) all.insert(all.end(), v.begin(), v.end());
-            std::sort(all.begin(), all.end());
+            if (rc != CV_OK) fails++;
+            std::sort(got.begin(), got.end());
             size_t p = 0;
-            for (auto &r : all) {
-                CHECK(r.first == p);
-                CHECK(r.first % 64 == 0);
+            for (auto &r : got) {
+                if (r.first != p || r.first % 64) fails++;
                 p = r.second;
             }
-            CHECK(p == n);
+            if (p != n) fails++;
+            if (n <= 1024 && got.size() != 1) fails++;          // small batches go whole to one device
+            if (n >= 65536 && ndev > 1 && got.size() != ndev) fails++;   // throughput batches spread
         }
-        for (Device &d : ctx.devs) d.stream = nullptr;
-        ctx.devs.clear();
-    }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; t++) th.emplace_back(caller, t);
+    for (auto &t : th) t.join();
+    CHECK(fails.load() == 0);
+    for (auto &d : ctx.devs) CHECK(d->load.load() == 0);
+    for (auto &d : ctx.devs) d->stream = nullptr;
+    ctx.devs.clear();
 }
 
 static void test_tx_verdicts() {
@@ -273,12 +360,15 @@ int main(int argc, char **argv) {
     const bool threads_only = argc > 1 && std::strcmp(argv[1], "--threads") == 0;
     test_pool();
     test_par_copy();
-    test_shards();
+    for (size_t ndev : {1ul, 2ul, 3ul, 8ul}) test_dispatch(ndev, 1, 60);
+    test_dispatch(4, 4, 200);        // 4 threads x 200 interleaved calls, 4 devices
     if (!threads_only) {
         test_dedupe();
         test_stage(false, 3001);
         test_stage(true, 3001);
         test_stage(false, 140001);   // several range-scan slices
+        test_mstage(false);
+        test_mstage(true);
         test_pipe_cuts();
         test_tx_verdicts();
         test_abi_guards();

@@ -96,16 +96,27 @@ def test_dedupe_resists_shared_key_bytes():
     assert dt < 2.0, f"dedupe of 2^18 adversarial keys took {dt:.2f} s"
 
 
-def test_dedupe_prefix_early_out():
-    """Batches above 1024 signatures whose first 256 carry more than 192 distinct keys skip the
-    dedupe (taken as distinct-keyed: a performance guess, the verdicts are the same either way);
-    a batch whose prefix repeats keys is deduped in full; fewer than 8 signatures per distinct key
-    on average is not worth the key tables."""
+def test_dedupe_gate_and_threshold():
+    """The keyed decision (cv_diag_dedupe_keys = the host dedupe cv_ed25519_verify_batch runs): at most 16,384
+    signatures are deduped in full; above, a birthday count over 4,096 pseudo-random positions skips batches
+    estimated below four signatures per key (a performance guess: the verdicts are the same either way).
+    The full dedupe then takes the keyed path at eight or more signatures per distinct key, whatever the
+    order of the records (a distinct-looking prefix included)."""
     rng = np.random.default_rng(9)
     keys = rng.integers(0, 256, (300, 32), dtype=np.uint8)
     pk = np.concatenate([keys] * 8)                          # 2400 sigs, 8 per key, prefix distinct
-    assert native.dedupe_keys(pk) is None
-    pk2 = np.repeat(keys, 8, axis=0)                        # same multiset, prefix repeats
-    idx, nk = native.dedupe_keys(pk2)
-    assert nk == 300 and np.array_equal(idx, np.repeat(np.arange(300), 8))
+    idx, nk = native.dedupe_keys(pk)
+    assert nk == 300 and np.array_equal(idx, np.tile(np.arange(300), 8))
     assert native.dedupe_keys(np.repeat(keys, 7, axis=0)) is None   # 7 per key: plain path
+    # 2^20 signatures over a 1,024-key pool (the SURVEY §8(d) C2 variant), in random order
+    pool = rng.integers(0, 256, (1024, 32), dtype=np.uint8)
+    order = rng.integers(0, 1024, 1 << 20)
+    idx, nk = native.dedupe_keys(pool[order])
+    first = np.unique(order, return_index=True)[1]
+    assert nk == 1024 and np.array_equal(pool[order][first[np.argsort(first)]][idx], pool[order])
+    # 2^20 distinct keys: the gate declines without the full dedupe
+    import time
+    big = rng.integers(0, 256, (1 << 20, 32), dtype=np.uint8)
+    t = time.perf_counter()
+    assert native.dedupe_keys(big) is None
+    assert time.perf_counter() - t < 0.5

@@ -134,13 +134,7 @@ def test_c5_shard_8m(engine):
 
 
 def _virtual_engine(k):
-    lib = native.load()
-    lib.cvk_set_virtual_devices.argtypes = [ctypes.c_int]
-    lib.cvk_set_virtual_devices(k)
-    try:
-        return native.Engine(1)
-    finally:
-        lib.cvk_set_virtual_devices(1)
+    return native.Engine(1, virtual_devices=k)
 
 
 @pytest.mark.parametrize("k", [2, 3, 8])

@@ -149,17 +149,7 @@ def test_key_pool_batch(engine, oracle_c):
         assert 0 < int(ref.sum()) < n
 
 
-@pytest.fixture(params=[0, 1], ids=["sorted_passes", "balanced_pairs"])
-def leaf_mode(request):
-    """Both leaf-hash kernels (cvk_set_leaf_mode): length-sorted passes and balanced pairs."""
-    lib = native.load()
-    lib.cvk_set_leaf_mode.argtypes = [ctypes.c_int]
-    lib.cvk_set_leaf_mode(request.param)
-    yield request.param
-    lib.cvk_set_leaf_mode(1)              # the default
-
-
-def test_merkle_golden(engine, merkle_cases, leaf_mode):
+def test_merkle_golden(engine, merkle_cases):
     m = merkle_cases
     ids, st = engine.merkle_tx_ids(m["arena"], m["leaf_off"], m["leaf_len"], m["tx_leaf_begin"])
     assert np.array_equal(st, m["status"])
@@ -167,7 +157,7 @@ def test_merkle_golden(engine, merkle_cases, leaf_mode):
     assert ids[0].tobytes().hex().upper() == "F6D8FB3720114F8D040D64F633B0D9178EB09A55AA7D62FAE1A070D1BF561051"
 
 
-def test_merkle_sha256_multiblock_kat(engine, leaf_mode):
+def test_merkle_sha256_multiblock_kat(engine):
     """One-leaf tx over the 71,644-byte prospectus jar: id = SHA-256(jar) = decd0986... (SellerFlow.kt:23)."""
     here = os.path.dirname(os.path.abspath(__file__))
     data = np.fromfile(os.path.join(here, "golden", "bank-of-london-cp.jar.bin"), np.uint8)
@@ -176,7 +166,7 @@ def test_merkle_sha256_multiblock_kat(engine, leaf_mode):
     assert ids[0].tobytes().hex() == "decd098666b9657314870e192ced0c3519c2c9d395507a238338f8d003929de9"
 
 
-def test_merkle_random_vs_oracle(engine, oracle_c, leaf_mode):
+def test_merkle_random_vs_oracle(engine, oracle_c):
     rng = np.random.default_rng(3)
     ntx = 3000
     counts = rng.integers(0, 12, ntx)
@@ -303,19 +293,29 @@ def test_keyed_device_baseline_size(engine):
     assert np.array_equal(native.bitmap_to_bools(bm.cpu().numpy().view(np.uint64), n), expect)
 
 
-# ---------------------------------------------------------------- both Straus forms at every size
-@pytest.mark.parametrize("quad_max,tri_max", [(0, 0), (1 << 30, 0), (1 << 30, 1 << 30)])
+# ---------------------------------------------------------------- every kernel form at every size
+class _opts:
+    """Per-context options (cv_set_option) set for the block and restored after it."""
+
+    def __init__(self, engine, **kw):
+        self.e, self.kw = engine, kw
+
+    def __enter__(self):
+        self.old = {k: self.e.get_option(k) for k in self.kw}
+        for k, v in self.kw.items():
+            self.e.set_option(k, v)
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            self.e.set_option(k, v)
+
+
+@pytest.mark.parametrize("quad_max,tri_max", [(0, 0), (1 << 22, 0), (1 << 22, 1 << 20)])
 def test_lane_quad_and_tri_forms_agree(engine, corpus, oracle_c, quad_max, tri_max):
     """Small batches normally run the 16-lanes-per-signature (tri-chain) or 4-lanes-per-signature
-    (quad) Straus; force each form in turn (internal switches cvk_set_quad_max / cvk_set_tri_max)
-    over the golden corpus, keyed and plain, and a random batch."""
-    import ctypes
-    lib = native.load()
-    lib.cvk_set_quad_max.argtypes = [ctypes.c_uint32]
-    lib.cvk_set_quad_max(quad_max)
-    lib.cvk_set_tri_max.argtypes = [ctypes.c_int]
-    lib.cvk_set_tri_max(tri_max)
-    try:
+    (quad) Straus; force each form in turn (per-context options CV_OPT_QUAD_MAX / CV_OPT_TRI_MAX: (0, 0) =
+    the throughput kernels at every size) over the golden corpus, keyed and plain, and a random batch."""
+    with _opts(engine, quad_max=quad_max, tri_max=tri_max):
         bitmap, status = engine.verify_batch(corpus["pk"], corpus["sig"], corpus["arena"], corpus["off"], corpus["len"])
         assert np.array_equal(_bits(bitmap, len(corpus["pk"])), corpus["verdict"].astype(bool))
         assert np.array_equal(status, corpus["status"])
@@ -335,60 +335,41 @@ def test_lane_quad_and_tri_forms_agree(engine, corpus, oracle_c, quad_max, tri_m
         bitmap, _ = engine.verify_batch(pk, sig, arena, off, ln)
         ref, _ = oracle_c.verify_batch(pk, sig, arena, off, ln, nthreads=8)
         assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
-    finally:
-        lib.cvk_set_quad_max(32768)
-        lib.cvk_set_tri_max(4096)
 
 
-@pytest.mark.parametrize("lat_seq", [0, 7])
 @pytest.mark.parametrize("n", [4096, 9001])
-def test_latency_field_forms_agree(engine, corpus, oracle_c, lat_seq, n):
-    """The latency kernels' two field forms (cvk_set_lat_seq: 0 = ILP forms everywhere, 7 = the
-    sequential-carry forms in the tri and quad Straus AND the fused prep's decodes): the golden corpus
-    tiled to n records (n = 4,096: tri chain, 9,001: quad) gives the pinned verdicts and statuses, and
-    a corrupted random batch of n the C oracle's."""
-    import ctypes
-    lib = native.load()
-    lib.cvk_set_lat_seq.argtypes = [ctypes.c_int]
-    lib.cvk_set_lat_seq(lat_seq)
-    try:
-        rng = np.random.default_rng(n + lat_seq)
-        sel = rng.integers(0, len(corpus["pk"]), n)
-        bitmap, status = engine.verify_batch(corpus["pk"][sel], corpus["sig"][sel], corpus["arena"],
-                                             corpus["off"][sel], corpus["len"][sel])
-        assert np.array_equal(_bits(bitmap, n), corpus["verdict"][sel].astype(bool))
-        assert np.array_equal(status, corpus["status"][sel])
-        seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
-        arena = rng.integers(0, 256, n * 32 + 16, dtype=np.uint8)
-        off = np.arange(n, dtype=np.uint64) * 32
-        ln = np.full(n, 32, np.uint32)
-        pk, sig = engine.sign_batch(seeds, arena, off, ln)
-        sig[1::5, 35] ^= 4
-        pk[2::7, 3] ^= 0x40
-        bitmap, status = engine.verify_batch(pk, sig, arena, off, ln)
-        ref, rst = oracle_c.verify_batch(pk, sig, arena, off, ln, nthreads=8)
-        assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
-        assert np.array_equal(status, rst)
-    finally:
-        lib.cvk_set_lat_seq(7)
+def test_latency_forms_corpus_and_oracle(engine, corpus, oracle_c, n):
+    """The latency kernels at their default sizes (n = 4,096: tri chain, 9,001: quad): the golden corpus
+    tiled to n records gives the pinned verdicts and statuses, and a corrupted random batch of n the C
+    oracle's."""
+    rng = np.random.default_rng(n + 7)
+    sel = rng.integers(0, len(corpus["pk"]), n)
+    bitmap, status = engine.verify_batch(corpus["pk"][sel], corpus["sig"][sel], corpus["arena"],
+                                         corpus["off"][sel], corpus["len"][sel])
+    assert np.array_equal(_bits(bitmap, n), corpus["verdict"][sel].astype(bool))
+    assert np.array_equal(status, corpus["status"][sel])
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    arena = rng.integers(0, 256, n * 32 + 16, dtype=np.uint8)
+    off = np.arange(n, dtype=np.uint64) * 32
+    ln = np.full(n, 32, np.uint32)
+    pk, sig = engine.sign_batch(seeds, arena, off, ln)
+    sig[1::5, 35] ^= 4
+    pk[2::7, 3] ^= 0x40
+    bitmap, status = engine.verify_batch(pk, sig, arena, off, ln)
+    ref, rst = oracle_c.verify_batch(pk, sig, arena, off, ln, nthreads=8)
+    assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
+    assert np.array_equal(status, rst)
 
 
-# ---------------------------------------------------------------- both throughput schedules
-@pytest.mark.parametrize("mode", [0, 1])
-def test_full_width_and_half_size_schedules_agree(engine, corpus, oracle_c, mode):
-    """The lane-form throughput path in each schedule (internal switch cvk_set_verify_mode: 0 = full
-    width prep/straus/finish, 1 = half-size scalars prep/hsprep/hs_straus with the wave-ballot
-    verdicts) over the golden corpus, ragged tails, and a corrupted random batch vs the C oracle."""
-    import ctypes
-    lib = native.load()
-    lib.cvk_set_quad_max.argtypes = [ctypes.c_uint32]
-    lib.cvk_set_quad_max(0)
-    native.set_verify_mode(mode)
-    try:
+def test_throughput_form_small_and_ragged(engine, corpus, oracle_c):
+    """The throughput kernels (scalars -> lane-pair points -> hs_straus with wave-ballot verdicts) forced onto
+    small and ragged batches (CV_OPT_QUAD_MAX = 0): the golden corpus, ragged tails, and corrupted random
+    batches (R, S, key, S >= 2^255, variable-length messages) against the C oracle."""
+    with _opts(engine, quad_max=0):
         bitmap, status = engine.verify_batch(corpus["pk"], corpus["sig"], corpus["arena"], corpus["off"], corpus["len"])
         assert np.array_equal(_bits(bitmap, len(corpus["pk"])), corpus["verdict"].astype(bool))
         assert np.array_equal(status, corpus["status"])
-        for n in (1, 63, 65, 257, 699):
+        for n in (1, 63, 65, 257, 699, 1001):
             sel = np.arange(n) % len(corpus["pk"])
             bitmap, status = engine.verify_batch(corpus["pk"][sel], corpus["sig"][sel], corpus["arena"],
                                                  corpus["off"][sel], corpus["len"][sel])
@@ -407,28 +388,22 @@ def test_full_width_and_half_size_schedules_agree(engine, corpus, oracle_c, mode
         sig[3::13, 63] |= 0x80                          # S >= 2^255
         sig[4::17, 40] ^= 0x01                          # S corrupted
         pk[5::19, 7] ^= 0x20                            # key corrupted
+        pk[6::23, 5] ^= 0x10                            # key corrupted (often not a point)
         bitmap, status = engine.verify_batch(pk, sig, arena, off, lens)
         ref, rst = oracle_c.verify_batch(pk, sig, arena, off, lens, nthreads=8)
         assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
         assert np.array_equal(status, rst)
         assert 0.4 < ref.mean() < 0.9
-    finally:
-        native.set_verify_mode(1)
-        lib.cvk_set_quad_max(32768)
 
 
-@pytest.mark.parametrize("mode,n", [(0, 200_003), (1, 200_003), (2, 200_003), (3, 200_003),
-                                    (3, (1 << 22) + 200_003), (1, (1 << 22) + 200_003)])
+@pytest.mark.parametrize("mode,n", [(0, 200_003), (1, 200_003), (2, 200_003), (1, (1 << 22) + 200_003),
+                                    (2, (1 << 22) + 200_003)])
 def test_split_launch_plans_agree(engine, corpus, mode, n):
-    """The two-stream sub-chunk plan (internal switch cvk_set_split_mode: 0 off, 1 concurrent, 2 tail
-    after head prep, 3 auto) over the golden corpus tiled to a ragged n through the device API — at
-    2^22 + 200,003 the batch is two workspace chunks and only the second one's last round is
-    near-empty: every verdict and key-status byte follows its record, bits past n stay clear."""
-    import ctypes
+    """The drain-overlap sub-chunk plan (CV_OPT_DRAIN_SPLIT: 0 off, 1 auto, 2 always with a 25 % tail) over
+    the golden corpus tiled to a ragged n through the device API — at 2^22 + 200,003 the batch is two
+    workspace chunks and only the second one's last round is near-empty: every verdict and key-status byte
+    follows its record, bits past n stay clear."""
     import torch
-    lib = native.load()
-    lib.cvk_set_split_mode.argtypes = [ctypes.c_int]
-    lib.cvk_set_split_pct.argtypes = [ctypes.c_int]
     rng = np.random.default_rng(7)
     idx = rng.integers(0, len(corpus["pk"]), n)
     dev = "cuda:0"
@@ -437,17 +412,12 @@ def test_split_launch_plans_agree(engine, corpus, mode, n):
     arena = torch.from_numpy(np.concatenate([corpus["arena"], np.zeros(64, np.uint8)])).to(dev)
     off = torch.from_numpy(corpus["off"][idx].astype(np.uint64).view(np.int64)).to(dev)
     ln = torch.from_numpy(corpus["len"][idx].astype(np.uint32).view(np.int32)).to(dev)
-    try:
-        lib.cvk_set_split_mode(mode)
-        lib.cvk_set_split_pct(10 if mode == 3 else 25)
+    with _opts(engine, drain_split=mode, drain_split_pct=10 if mode == 1 else 25):
         bm = torch.full(((n + 63) // 64,), -1, dtype=torch.int64, device=dev)
         st = torch.full((n,), 7, dtype=torch.uint8, device=dev)
         engine.verify_device(0, n, pk.data_ptr(), sig.data_ptr(), arena.data_ptr(), off.data_ptr(), ln.data_ptr(),
                              bm.data_ptr(), st.data_ptr())
         engine.synchronize(0)
-    finally:
-        lib.cvk_set_split_mode(3)
-        lib.cvk_set_split_pct(10)
     bits = bm.cpu().numpy().view(np.uint64)
     assert np.array_equal(_bits(bits, n), corpus["verdict"][idx].astype(bool))
     assert np.array_equal(st.cpu().numpy(), corpus["status"][idx])
@@ -456,8 +426,8 @@ def test_split_launch_plans_agree(engine, corpus, mode, n):
 
 def test_host_buffer_api_split_size_exact_pattern(engine):
     """Host-buffer C-ABI (cv_ed25519_verify_batch: H2D, verify, D2H) at a size whose last Straus
-    round is near-empty (200,003 distinct-key signatures over 300-byte messages, so the drain-overlap
-    plan runs): honest signatures accepted, every 16th (one S bit flipped) rejected, key status clear."""
+    round is near-empty (200,003 distinct-key signatures over 300-byte messages): honest signatures
+    accepted, every 16th (one S bit flipped) rejected, key status clear."""
     from corda_amd import workload
     n = 200_003
     b = workload.make_batch(engine, 0, n, 300, seed=123)
@@ -467,76 +437,3 @@ def test_host_buffer_api_split_size_exact_pattern(engine):
     assert np.array_equal(_bits(bitmap, n), expect)
     assert int(status.sum()) == 0
     assert int(bitmap[-1]) >> (n % 64) == 0
-
-
-# ---------------------------------------------------------------- the points kernel forms
-@pytest.mark.parametrize("points_mode", [0, 2, 3])
-def test_points_kernel_forms_agree(engine, corpus, oracle_c, points_mode):
-    """The throughput points phase in each form (internal switch cvk_set_points_mode: 0 = one lane
-    decodes A and R interleaved, 2 / 3 = a lane pair per signature at 2 / 3 waves per SIMD) over the
-    golden corpus (every key / R class, statuses) and a corrupted random batch vs the C oracle."""
-    import ctypes
-    lib = native.load()
-    lib.cvk_set_quad_max.argtypes = [ctypes.c_uint32]
-    lib.cvk_set_points_mode.argtypes = [ctypes.c_int]
-    lib.cvk_set_quad_max(0)
-    lib.cvk_set_points_mode(points_mode)
-    try:
-        for n in (len(corpus["pk"]), 1001):
-            sel = np.arange(n) % len(corpus["pk"])
-            bitmap, status = engine.verify_batch(corpus["pk"][sel], corpus["sig"][sel], corpus["arena"],
-                                                 corpus["off"][sel], corpus["len"][sel])
-            assert np.array_equal(_bits(bitmap, n), corpus["verdict"][sel].astype(bool))
-            assert np.array_equal(status, corpus["status"][sel])
-        rng = np.random.default_rng(43 + points_mode)
-        n = 5000
-        seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
-        arena = rng.integers(0, 256, n * 32 + 16, dtype=np.uint8)
-        off = np.arange(n, dtype=np.uint64) * 32
-        ln = np.full(n, 32, np.uint32)
-        pk, sig = engine.sign_batch(seeds, arena, off, ln)
-        sig[1::7, rng.integers(0, 32)] ^= 0x08          # R corrupted
-        pk[2::9, 5] ^= 0x10                             # key corrupted (often not a point)
-        bitmap, status = engine.verify_batch(pk, sig, arena, off, ln)
-        ref, rst = oracle_c.verify_batch(pk, sig, arena, off, ln, nthreads=8)
-        assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
-        assert np.array_equal(status, rst)
-    finally:
-        lib.cvk_set_points_mode(3)
-        lib.cvk_set_quad_max(32768)
-
-
-# ---------------------------------------------------------------- prep launch variants (knobs)
-@pytest.mark.parametrize("knob,value", [("cvk_set_prep_tp", 1), ("cvk_set_scalars_waves", 2)])
-def test_prep_variants_agree(engine, corpus, oracle_c, knob, value):
-    """The non-default throughput prep launches — scalars and point pairs fused into one launch
-    (cv_prep_tp_kernel), the scalars kernel at 2 waves/SIMD — give the default's verdicts: golden
-    corpus (every class, statuses) and a corrupted random batch vs the C oracle."""
-    import ctypes
-    lib = native.load()
-    lib.cvk_set_quad_max.argtypes = [ctypes.c_uint32]
-    getattr(lib, knob).argtypes = [ctypes.c_int]
-    lib.cvk_set_quad_max(0)
-    getattr(lib, knob)(value)
-    try:
-        sel = np.arange(2 * len(corpus["pk"]) + 37) % len(corpus["pk"])
-        bitmap, status = engine.verify_batch(corpus["pk"][sel], corpus["sig"][sel], corpus["arena"],
-                                             corpus["off"][sel], corpus["len"][sel])
-        assert np.array_equal(_bits(bitmap, len(sel)), corpus["verdict"][sel].astype(bool))
-        assert np.array_equal(status, corpus["status"][sel])
-        rng = np.random.default_rng(47)
-        n = 3000
-        seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
-        arena = rng.integers(0, 256, n * 32 + 16, dtype=np.uint8)
-        off = np.arange(n, dtype=np.uint64) * 32
-        ln = np.full(n, 32, np.uint32)
-        pk, sig = engine.sign_batch(seeds, arena, off, ln)
-        sig[3::11, 40] ^= 0x02                           # S corrupted
-        pk[4::13, 9] ^= 0x20                             # key corrupted
-        bitmap, status = engine.verify_batch(pk, sig, arena, off, ln)
-        ref, rst = oracle_c.verify_batch(pk, sig, arena, off, ln, nthreads=8)
-        assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
-        assert np.array_equal(status, rst)
-    finally:
-        getattr(lib, knob)(0 if knob == "cvk_set_prep_tp" else 3)
-        lib.cvk_set_quad_max(32768)

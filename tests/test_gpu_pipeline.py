@@ -18,17 +18,26 @@ from corda_amd import native, workload
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
-PIPE_DEFAULT = (131072, 32768, 262144, 8)
 
 
 def _bits(bitmap, n):
     return native.bitmap_to_bools(np.asarray(bitmap, dtype=np.uint64), n)
 
 
-def _set_pipe(min_n, first, chunk, threads):
-    lib = native.load()
-    lib.cvk_set_pipe.argtypes = [ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int]
-    lib.cvk_set_pipe(min_n, first, chunk, threads)
+class _opts:
+    """Per-context options (cv_set_option) set for the block and restored after it."""
+
+    def __init__(self, engine, **kw):
+        self.e, self.kw = engine, kw
+
+    def __enter__(self):
+        self.old = {k: self.e.get_option(k) for k in self.kw}
+        for k, v in self.kw.items():
+            self.e.set_option(k, v)
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            self.e.set_option(k, v)
 
 
 def _bad_key_records(corpus):
@@ -73,12 +82,9 @@ def test_host_pipeline_small_subchunks_golden(engine, corpus, first, chunk):
     rng = np.random.default_rng(first + chunk)
     n = 9001
     sel = rng.integers(0, len(corpus["pk"]), n)
-    try:
-        _set_pipe(512, first, chunk, 3)
+    with _opts(engine, pipe_min=512, pipe_first=first, pipe_chunk=chunk, host_threads=3, auto_keyed=0):
         bitmap, status = engine.verify_batch(corpus["pk"][sel], corpus["sig"][sel], corpus["arena"],
                                              corpus["off"][sel], corpus["len"][sel])
-    finally:
-        _set_pipe(*PIPE_DEFAULT)
     assert np.array_equal(_bits(bitmap, n), corpus["verdict"][sel].astype(bool))
     assert np.array_equal(status, corpus["status"][sel])
     assert int(bitmap[-1]) >> (n % 64) == 0
@@ -108,11 +114,8 @@ def test_host_pipeline_scattered_arena(engine, corpus, oracle_c):
     bitmap, status = engine.verify_batch(pk, sig, arena, offs, lens)
     assert np.array_equal(_bits(bitmap, n), ref.astype(bool))
     assert np.array_equal(status, rst)
-    try:                                             # the same batch on the small (one-DMA) path
-        _set_pipe(1 << 30, 0, 0, 0)
+    with _opts(engine, pipe_min=1 << 30):            # the same batch on the small (one-DMA) path
         b2, s2 = engine.verify_batch(pk, sig, arena, offs, lens)
-    finally:
-        _set_pipe(*PIPE_DEFAULT)
     assert np.array_equal(b2, bitmap) and np.array_equal(s2, status)
 
 
@@ -208,10 +211,7 @@ def test_host_pipeline_pinned_inputs_direct_dma(engine, corpus):
     """Inputs in pinned host memory (cv_host_alloc): the pipelined path DMAs every sub-chunk straight
     out of the caller's arrays (no packing) — same verdicts and status as the pageable call on a
     ragged 600,037-signature batch with corrupted S / R bytes and golden not-a-point keys, and the
-    direct path was really taken (cvk_pipe_direct_chunks)."""
-    lib = native.load()
-    lib.cvk_pipe_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    lib.cvk_pipe_direct_chunks.restype = ctypes.c_double
+    direct path was really taken (cv_diag_stats CV_STATS_PIPE)."""
     n = 600_037
     b = workload.make_batch(engine, 0, n, 300, seed=4242)
     expect = workload.corrupt_fraction(b, 16)
@@ -228,9 +228,9 @@ def test_host_pipeline_pinned_inputs_direct_dma(engine, corpus):
     exp[kidx] = False
     page_bm, page_st = engine.verify_batch(pk, sig, arena, off, ln)
     pinned = [engine.host_copy(x) for x in (pk, sig, arena, off, ln)]
-    lib.cvk_pipe_stats(None, 1)
+    engine.stats("pipe", reset=True)
     pin_bm, pin_st = engine.verify_batch(*pinned)
-    assert lib.cvk_pipe_direct_chunks() > 0, "pinned inputs did not take the direct-DMA path"
+    assert engine.stats("pipe")["direct_subchunks"] > 0, "pinned inputs did not take the direct-DMA path"
     assert np.array_equal(_bits(pin_bm, n), exp)
     assert np.array_equal(pin_bm, page_bm) and np.array_equal(pin_st, page_st)
     assert int(pin_st.sum()) == kidx.size
@@ -244,13 +244,8 @@ def test_host_small_pinned_inputs_golden(engine, corpus, n):
     sel = rng.integers(0, len(corpus["pk"]), n)
     arr = [engine.host_copy(x) for x in (corpus["pk"][sel], corpus["sig"][sel], corpus["arena"],
                                          corpus["off"][sel], corpus["len"][sel])]
-    lib = native.load()
-    lib.cvk_set_direct_small_min.argtypes = [ctypes.c_int]
-    lib.cvk_set_direct_small_min(1)                  # the direct DMAs at every size (default: >= 16,384)
-    try:
+    with _opts(engine, small_direct_min=1, small_zero_copy=0):   # the direct DMAs at every size
         bitmap, status = engine.verify_batch(*arr)
-    finally:
-        lib.cvk_set_direct_small_min(16384)
     assert np.array_equal(_bits(bitmap, n), corpus["verdict"][sel].astype(bool))
     assert np.array_equal(status, corpus["status"][sel])
     assert int(bitmap[-1]) >> (n % 64) == 0 if n % 64 else True
@@ -265,17 +260,12 @@ def test_host_small_zero_copy_golden(engine, corpus, n):
     rng = np.random.default_rng(1000 + n)
     sel = rng.integers(0, len(corpus["pk"]), n)
     arr = (corpus["pk"][sel], corpus["sig"][sel], corpus["arena"], corpus["off"][sel], corpus["len"][sel])
-    lib = native.load()
-    lib.cvk_set_small_zc.argtypes = [ctypes.c_int]
     out = {}
-    try:
-        for zc in (0, 1, 2):
-            lib.cvk_set_small_zc(zc)
+    for zc in (0, 1, 2):
+        with _opts(engine, small_zero_copy=zc):
             out[zc] = engine.verify_batch(*arr)
             out[zc, "pinned"] = engine.verify_batch(*[engine.host_copy(x) for x in arr])
             out[zc, "nostatus"] = engine.verify_batch(*arr, want_status=False)
-    finally:
-        lib.cvk_set_small_zc(3)
     exp = corpus["verdict"][sel].astype(bool)
     for k, (bitmap, status) in out.items():
         assert np.array_equal(_bits(bitmap, n), exp), k
@@ -287,10 +277,9 @@ def test_host_small_zero_copy_golden(engine, corpus, n):
 
 def test_async_calls_in_flight_match_sync(engine, corpus, oracle_c):
     """cv_ed25519_verify_batch_async: three batches in flight (pageable 300,007 with corrupted S bytes,
-    pinned 262,145 with corrupted R bytes and golden not-a-point keys, a 4,096 golden tile) — more than
-    the two output slots per device, so the third submission completes the first — waited out of
-    order: each equals its synchronous cv_ed25519_verify_batch (verdicts and status), and the pinned
-    and golden ones their expected patterns."""
+    pinned 262,145 with corrupted R bytes and golden not-a-point keys, a 4,096 golden tile) — waited
+    out of order: each equals its synchronous cv_ed25519_verify_batch (verdicts and status), and the
+    pinned and golden ones their expected patterns."""
     n1, n2, n3 = 300_007, 262_145, 4096
     b1 = workload.make_batch(engine, 0, n1, 300, seed=71)
     e1 = workload.corrupt_fraction(b1, 13).cpu().numpy()

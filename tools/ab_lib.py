@@ -27,18 +27,10 @@ def main():
     ap.add_argument("--keyed", type=int, default=0, help="key pool size: time the keyed device path")
     args = ap.parse_args()
     eng = native.Engine(1)
-    lib = native.load()
-    if os.environ.get("CV_COMB_WAVES") and hasattr(lib, "cvk_set_comb_waves"):
-        lib.cvk_set_comb_waves.argtypes = [ctypes.c_int]
-        lib.cvk_set_comb_waves(int(os.environ["CV_COMB_WAVES"]))
-    if os.environ.get("CV_QUAD_MAX"):
-        lib.cvk_set_quad_max.argtypes = [ctypes.c_uint32]
-        lib.cvk_set_quad_max(int(os.environ["CV_QUAD_MAX"]))
-    # CV_KNOBS="cvk_set_hs_waves=2,cvk_set_prep_lat=1": any internal int setter of the library
-    for kv in filter(None, os.environ.get("CV_KNOBS", "").split(",")):
+    # CV_OPTS="quad_max=0,drain_split=2": per-context options (cv_set_option) for this run
+    for kv in filter(None, os.environ.get("CV_OPTS", "").split(",")):
         k, v = kv.split("=")
-        getattr(lib, k).argtypes = [ctypes.c_int]
-        getattr(lib, k)(int(v))
+        eng.set_option(k, int(v))
     if args.keyed:
         return keyed(eng, args)
     stream = torch.cuda.Stream(0)

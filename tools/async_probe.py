@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Rate of host-buffer calls with two in flight (cv_ed25519_verify_batch_async / cv_wait) against the
 synchronous call, on a C2- or C5-shaped batch from pinned or pageable buffers, for a list of async
-sub-chunk sizes (cvk_set_async_chunk).  One JSON line per setting.
+sub-chunk sizes (CV_OPT_ASYNC_CHUNK).  One JSON line per setting.
 
     python tools/async_probe.py --shape c2 --chunks 262144,524288,1048576 --calls 8
 """
@@ -25,8 +25,6 @@ def main():
     a = ap.parse_args()
     import torch  # noqa: F401
     from corda_amd import native, workload
-    lib = native.load()
-    lib.cvk_set_async_chunk.argtypes = [ctypes.c_int]
     eng = native.Engine(1)
     n, ml = (1_000_000, 300) if a.shape == "c2" else (8_000_000, 32)
     b = workload.make_batch(eng, 0, n, ml, seed=11)
@@ -41,7 +39,7 @@ def main():
         sync_ms = (time.perf_counter() - t) / a.calls * 1e3
         assert native.bitmap_to_bools(bm, n).all()
         for ch in (int(x) for x in a.chunks.split(",")):
-            lib.cvk_set_async_chunk(ch)
+            eng.set_option("async_chunk", ch)
             eng.wait(eng.verify_batch_async(*arrs, want_status=False))
             t = time.perf_counter()
             pend = []

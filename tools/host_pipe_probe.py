@@ -30,10 +30,12 @@ def main():
     ap.add_argument("--n5", type=int, default=8_000_000)
     ap.add_argument("--reps", type=int, default=4)
     a = ap.parse_args()
-    lib = native.load()
-    lib.cvk_set_pipe.argtypes = [ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int]
-    lib.cvk_pipe_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
     eng = native.Engine(1)
+
+    def set_pipe(first, chunk, threads):
+        eng.set_option("pipe_first", first)
+        eng.set_option("pipe_chunk", chunk)
+        eng.set_option("host_threads", threads)
     dev = torch.device("cuda", 0)
     for name, n, ml in (("c2", a.n2, 300), ("c5", a.n5, 32)):
         b = workload.make_batch(eng, 0, n, ml, seed=11)
@@ -64,16 +66,16 @@ def main():
             print(json.dumps({"h2d_pinned_gb_per_s": (256 << 20) / e0.elapsed_time(e1) / 1e6}), flush=True)
         del h, dd
         for first, chunk, th in SETTINGS + SETTINGS[:1]:
-            lib.cvk_set_pipe(131072, first, chunk, th)
+            set_pipe(first, chunk, th)
             eng.verify_batch(pk, sig, arena, off, ln, want_status=False)
+            eng.stats("pipe", reset=True)
             ts = []
             for _ in range(a.reps):
                 t = time.perf_counter()
                 bm, _ = eng.verify_batch(pk, sig, arena, off, ln, want_status=False)
                 ts.append(time.perf_counter() - t)
             assert native.bitmap_to_bools(bm, n).all()
-            st = (ctypes.c_double * 7)()
-            lib.cvk_pipe_stats(st, 1)
+            st = list(eng.stats("pipe", reset=True).values())
             calls = max(st[5], 1)
             print(json.dumps({"shape": name, "first": first, "chunk": chunk, "threads": th,
                               "ms_med": float(np.median(ts) * 1e3), "ms_min": float(np.min(ts) * 1e3),
@@ -83,7 +85,7 @@ def main():
         # the same call from pinned inputs (cv_host_alloc): sub-chunks DMAed in place, no packing
         pinned = [eng.host_copy(x) for x in (pk, sig, arena, off, ln)]
         for first, chunk in ((65536, 262144), (131072, 524288), (32768, 131072)):
-            lib.cvk_set_pipe(131072, first, chunk, 8)
+            set_pipe(first, chunk, 8)
             eng.verify_batch(*pinned, want_status=False)
             ts = []
             for _ in range(a.reps):
@@ -99,7 +101,7 @@ def main():
         _ = np.concatenate([pk.reshape(-1), sig.reshape(-1), arena])
         print(json.dumps({"shape": name, "host_numpy_concat_gb_per_s": (pk.nbytes + sig.nbytes + arena.nbytes) /
                           (time.perf_counter() - t) / 1e9}), flush=True)
-        lib.cvk_set_pipe(131072, 65536, 262144, 8)
+        set_pipe(32768, 262144, 8)
     eng.close()
 
 

@@ -52,8 +52,6 @@ def main():
     ap.add_argument("--first", type=int, default=0)
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--threads", type=int, default=0)
-    ap.add_argument("--slots", type=int, default=0)
-    ap.add_argument("--ramp", type=int, default=-1)
     ap.add_argument("--n", type=int, default=0, help="signatures (overrides the shape's)")
     a = ap.parse_args()
     if a.summarize:
@@ -62,14 +60,10 @@ def main():
     import torch  # noqa: F401
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from corda_amd import native, workload
-    lib = native.load()
-    lib.cvk_set_pipe.argtypes = [ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int]
-    lib.cvk_set_pipe(0, a.first, a.chunk, a.threads)
-    if a.slots:
-        lib.cvk_set_pipe_slots(a.slots)
-    if a.ramp >= 0:
-        lib.cvk_set_pipe_ramp(a.ramp)
     eng = native.Engine(1)
+    for k, v in (("pipe_first", a.first), ("pipe_chunk", a.chunk), ("host_threads", a.threads)):
+        if v:
+            eng.set_option(k, v)
     n, ml = (1_000_000, 300) if a.shape == "c2" else (8_000_000, 32)
     if a.n:
         n = a.n

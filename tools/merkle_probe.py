@@ -24,14 +24,9 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--sort-leaves", action="store_true")
     ap.add_argument("--tag", default=os.environ.get("CV_LIB_PATH", "default"))
-    ap.add_argument("--leaf-mode", type=int, default=-1, help="cvk_set_leaf_mode (0 sorted passes, 1 pairs)")
+    ap.add_argument("--leaf-mode", type=int, default=-1, help="(ignored: one leaf kernel since round 4)")
     args = ap.parse_args()
     eng = native.Engine(1)
-    if args.leaf_mode >= 0:
-        import ctypes
-        lib = native.load()
-        lib.cvk_set_leaf_mode.argtypes = [ctypes.c_int]
-        lib.cvk_set_leaf_mode(args.leaf_mode)
     tb = workload.make_tx_batch(eng, 0, args.ntx, signers=1)
     off, ln = tb.leaf_off, tb.leaf_len
     if args.sort_leaves:

@@ -41,28 +41,24 @@ def main():
     ap.add_argument("--reps", type=int, default=100)
     ap.add_argument("--sizes", default="256,4096,65536")
     ap.add_argument("--variants", default="base:",
-                    help="';'-free list 'NAME:SETTER=A/B,SETTER=C ...' separated by spaces; rounds interleave them")
+                    help="space-separated 'NAME:OPTION=V,OPTION=V' (cv_set_option names, e.g. small:small_zero_copy=1); "
+                         "rounds interleave them")
     ap.add_argument("--rounds", type=int, default=1)
     args = ap.parse_args()
-    import ctypes
-    lib = native.load()
+    # variants: "name:option=value,option=value ..." (per-context options, cv_set_option names)
     variants = []
     for v in args.variants.split():
         name, _, body = v.partition(":")
-        variants.append((name, [(k, tuple(int(x) for x in a.split("/"))) for k, a in
-                                (kv.split("=") for kv in filter(None, body.split(",")))]))
+        variants.append((name, [(k, int(a)) for k, a in (kv.split("=") for kv in filter(None, body.split(",")))]))
     used = {k for _, sets in variants for k, _ in sets}
-    argt = {"cvk_set_pipe": [ctypes.c_size_t] * 3 + [ctypes.c_int]}
-    reset = {"cvk_set_pipe": (131072, 32768, 262144, 8), "cvk_set_small_pool_min": (16384,), "cvk_set_small_zc": (3,), "cvk_set_lat_points_quad": (1,), "cvk_set_lat_seq": (7,), "cvk_set_tri_max": (4096,), "cvk_set_prep_lat_fused": (1,)}
 
     def apply(sets):
         for k in used:
-            getattr(lib, k).argtypes = argt.get(k, [ctypes.c_int] * len(reset[k]))
-            getattr(lib, k)(*reset[k])
+            eng.set_option(k, defaults[k])
         for k, a in sets:
-            getattr(lib, k).argtypes = argt.get(k, [ctypes.c_int] * len(a))
-            getattr(lib, k)(*a)
+            eng.set_option(k, a)
     eng = native.Engine(1)
+    defaults = {k: eng.get_option(k) for k in used}
     adv = adversarial_pool()
     dev = torch.device("cuda", 0)
     s = torch.cuda.Stream(dev)
@@ -71,13 +67,11 @@ def main():
         for rnd in range(args.rounds):
             for vname, sets in variants:
                 apply(sets)
-                st = (ctypes.c_double * 6)()
-                lib.cvk_small_stats.argtypes = [ctypes.c_void_p, ctypes.c_int]
-                lib.cvk_small_stats(None, 1)
+                eng.stats("small", reset=True)
                 host = p50(lambda: eng.verify_batch(pk, sig, arena, off, ln, want_status=False), args.reps)
-                lib.cvk_small_stats(st, 1)
-                zc_us = {k: round(st[i] / max(st[5], 1) * 1e6, 1) for i, k in
-                         enumerate(("plan_setup", "pack", "launch", "sync", "assemble"))} if st[5] else None
+                st = eng.stats("small", reset=True)
+                zc_us = {k: round(st[k + "_s"] / max(st["calls"], 1) * 1e6, 1) for k in
+                         ("setup", "pack", "launch", "sync", "assemble")} if st["calls"] else None
                 bm_h, _ = eng.verify_batch(pk, sig, arena, off, ln, want_status=False)
                 assert np.array_equal(native.bitmap_to_bools(bm_h, n), expect)
                 d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in
