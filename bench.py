@@ -210,19 +210,25 @@ def host_c3_rate(eng, local, sh, ntx: int, steps: int, device_value: float, pcie
     for b in bufs:
         b[-16:] = 0
 
+    blocked = {"merkle_ms": 0.0, "verify_ms": 0.0}
+
     def run(k_steps):
         ok_all = True
         tm = eng.merkle_tx_ids_async(arena, leaf_off, leaf_len, tx_begin, ids=bufs[0][:ntx * 32].reshape(ntx, 32))
         tv_prev = None
         for k in range(k_steps):
+            t0 = time.perf_counter()
             ids, st = eng.wait(tm)
+            blocked["merkle_ms"] += (time.perf_counter() - t0) * 1e3
             tv = eng.verify_batch_async(pk, sig, bufs[k % 3], msg_off, msg_len, want_status=False)
             if k + 1 < k_steps:
                 nb = bufs[(k + 1) % 3]
                 tm = eng.merkle_tx_ids_async(arena, leaf_off, leaf_len, tx_begin, ids=nb[:ntx * 32].reshape(ntx, 32))
             id_ok = (ids.view(np.uint64).reshape(ntx, 4) == claimed).all(axis=1) & (st == 0)
             if tv_prev is not None:
+                t0 = time.perf_counter()
                 bm, _ = eng.wait(tv_prev[0])
+                blocked["verify_ms"] += (time.perf_counter() - t0) * 1e3
                 ok_all &= bool((native.tx_verdicts(bm, sig_begin).astype(bool) & tv_prev[1]).all())
             tv_prev = (tv, id_ok)
         bm, _ = eng.wait(tv_prev[0])
@@ -230,6 +236,7 @@ def host_c3_rate(eng, local, sh, ntx: int, steps: int, device_value: float, pcie
         return ok_all
 
     assert run(2), "host C3 step rejected an honest transaction"        # warm: staging / device blocks
+    blocked.update(merkle_ms=0.0, verify_ms=0.0)
     t = time.perf_counter()
     ok = run(steps)
     dt = time.perf_counter() - t
@@ -239,6 +246,7 @@ def host_c3_rate(eng, local, sh, ntx: int, steps: int, device_value: float, pcie
     return {"value": v, "unit": "verifies/s", "tx_ids_per_s": ntx * steps / dt, "ms_per_step": dt / steps * 1e3,
             "steps": steps, "ratio_to_device_value": v / device_value, "device_value": device_value,
             "input_bytes_per_step": in_bytes, "pcie_floor_ms_per_step": in_bytes / (pcie_gbs * 1e9) * 1e3,
+            "host_blocked_ms_per_step": {k: v / steps for k, v in blocked.items()},
             "path": "cv_merkle_tx_ids_async (leaves) + cv_ed25519_verify_batch_async (sigs over the returned ids) "
                     "+ cv_tx_verdicts and the id check, pinned host buffers, Merkle k+1 submitted behind verify k"}
 

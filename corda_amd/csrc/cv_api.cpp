@@ -151,7 +151,12 @@ struct Slot {
 };
 constexpr int kSlots = 4;
 constexpr int kPipeSlots = 2;   // compute slots the pipeline deals its sub-chunks over (see pipe_enqueue)
-constexpr int kRing = 6;        // input blocks of the host pipeline (more than slots: copies run ahead of kernels)
+// input blocks of the host pipeline on the device: copies run up to kRing sub-chunks ahead of the kernels, so
+// a call's copies are all queued early and a Merkle call submitted behind a verify call copies its leaves
+// while that verify's kernels run (round 4: with 6 blocks the verify's copies were paced by its kernels and
+// the Merkle copies queued behind them, host C3 0.67x of the device rate)
+constexpr int kRing = 16;
+constexpr int kStage = 6;       // pinned host staging blocks (pageable inputs are packed into them)
 constexpr int kOuts = 4;        // pipelined host calls in flight per device (async verify + Merkle calls)
 
 // The output of one pipelined host call on one device: its results on the device (dout), the pinned
@@ -312,17 +317,21 @@ struct Device {
     std::unique_ptr<WorkerPool> pool;    // host packing threads (created on the first large host batch)
     // The host pipeline's input ring: sub-chunk j's records go into device block j % kRing by the ONE copy
     // stream (so every H2D copy runs on one DMA queue, never as a blit kernel beside the verify kernels),
-    // packed first into pinned staging block j % kRing when the caller's arrays are pageable.  in_ready[q]:
-    // after block q's copies (copy stream); in_free[q]: after the kernels that read it (its slot stream).
+    // packed first into the next pinned staging block when the caller's arrays are pageable.  in_ready[q]:
+    // after block q's copies (copy stream); in_free[q]: after the kernels that read it (its slot stream);
+    // stage_ev[k]: after the copy out of staging block k.
     hipStream_t copy = nullptr;
     hipStream_t outs = nullptr;          // the pipeline's result copies (pipe_finish)
     PipeOut out[kOuts];
     int out_next = 0;
     DevBuf inblk[kRing];
-    PinBuf instage[kRing];
     hipEvent_t in_ready[kRing] = {}, in_free[kRing] = {};
-    bool in_used[kRing] = {}, stage_busy[kRing] = {};
+    bool in_used[kRing] = {};
     int ring_next = 0;
+    PinBuf instage[kStage];
+    hipEvent_t stage_ev[kStage] = {};
+    bool stage_busy[kStage] = {};
+    int stage_next = 0;
     WorkerPool &workers(int threads) {
         if (!pool || pool->threads() != threads) {
             pool.reset();
@@ -751,9 +760,12 @@ void cv_close(cv_ctx *ctx) {
         if (d.outs) (void)hipStreamDestroy(d.outs);
         for (int q = 0; q < kRing; q++) {
             d.inblk[q].release();
-            d.instage[q].release();
             for (hipEvent_t v : {d.in_ready[q], d.in_free[q]})
                 if (v) (void)hipEventDestroy(v);
+        }
+        for (int k = 0; k < kStage; k++) {
+            d.instage[k].release();
+            if (d.stage_ev[k]) (void)hipEventDestroy(d.stage_ev[k]);
         }
         if (d.copy) (void)hipStreamDestroy(d.copy);
         d.kc.pin.release();
@@ -1594,6 +1606,8 @@ struct PipeFrame {
             if (!d.in_ready[q]) CV_TRY(hipEventCreateWithFlags(&d.in_ready[q], hipEventDisableTiming));
             if (!d.in_free[q]) CV_TRY(hipEventCreateWithFlags(&d.in_free[q], hipEventDisableTiming));
         }
+        for (int k = 0; k < kStage; k++)
+            if (!d.stage_ev[k]) CV_TRY(hipEventCreateWithFlags(&d.stage_ev[k], hipEventDisableTiming));
         return CV_OK;
     }
     // error paths: drain every queue, forget the ring's state and finish every other pending output of
@@ -1601,7 +1615,8 @@ struct PipeFrame {
     void drain() {
         (void)hipStreamSynchronize(d.copy);
         for (int k = 0; k < kPipeSlots; k++) (void)hipStreamSynchronize(ss[k]);
-        for (int q = 0; q < kRing; q++) d.in_used[q] = d.stage_busy[q] = false;
+        for (int q = 0; q < kRing; q++) d.in_used[q] = false;
+        for (int k = 0; k < kStage; k++) d.stage_busy[k] = false;
         for (PipeOut &o : d.out)
             if (&o != &po) {
                 std::lock_guard<std::mutex> g(o.mu);
@@ -1622,14 +1637,23 @@ struct PipeFrame {
         *dv = d.inblk[q].as<uint8_t>();
         return CV_OK;
     }
-    // pinned staging block q, free once its previous copy has left it
-    int staging(int q, size_t bytes, uint8_t **h) {
-        if (d.stage_busy[q]) {
-            CV_TRY(hipEventSynchronize(d.in_ready[q]));
-            d.stage_busy[q] = false;
+    // the next pinned staging block, free once its previous copy has left it
+    int staging(int *k_out, size_t bytes, uint8_t **h) {
+        const int k = d.stage_next;
+        d.stage_next = (d.stage_next + 1) % kStage;
+        if (d.stage_busy[k]) {
+            CV_TRY(hipEventSynchronize(d.stage_ev[k]));
+            d.stage_busy[k] = false;
         }
-        CV_TRY(d.instage[q].ensure(bytes));
-        *h = d.instage[q].as<uint8_t>();
+        CV_TRY(d.instage[k].ensure(bytes));
+        *h = d.instage[k].as<uint8_t>();
+        *k_out = k;
+        return CV_OK;
+    }
+    // the copy out of staging block k was enqueued
+    int staged(int k) {
+        CV_TRY(hipEventRecord(d.stage_ev[k], d.copy));
+        d.stage_busy[k] = true;
         return CV_OK;
     }
     // after sub-chunk j's copies into block q: compute stream j % 2 waits for them
@@ -1756,7 +1780,8 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
             f.direct++;
         } else {
             uint8_t *h;
-            if ((rc = f.staging(q, st.total, &h)) != CV_OK) return rc;
+            int sk;
+            if ((rc = f.staging(&sk, st.total, &h)) != CV_OK) return rc;
             t0 = now_s();
             f.t[2] += t0 - t1;
             stage_pack(st, h, c0, in.pk, kidx, in.sig, in.arena, in.off, in.len, pool, [] {});
@@ -1764,7 +1789,7 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
             f.t[1] += t1 - t0;
             t0 = t1;
             CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, d.copy));
-            d.stage_busy[q] = true;
+            if ((rc = f.staged(sk)) != CV_OK) return rc;
         }
         if ((rc = f.copied(q, (int)j)) != CV_OK) return rc;
         const size_t w0 = (c0 - b) / 64;
@@ -1857,7 +1882,8 @@ static int merkle_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, si
             f.direct++;
         } else {
             uint8_t *h;
-            if ((rc = f.staging(q, st.total, &h)) != CV_OK) return rc;
+            int sk;
+            if ((rc = f.staging(&sk, st.total, &h)) != CV_OK) return rc;
             ta = now_s();
             f.t[2] += ta - tb;
             mstage_pack(st, h, in.txb, in.arena, in.off, in.len, pool);
@@ -1865,7 +1891,7 @@ static int merkle_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, si
             f.t[1] += tb - ta;
             ta = tb;
             CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, d.copy));
-            d.stage_busy[q] = true;
+            if ((rc = f.staged(sk)) != CV_OK) return rc;
         }
         if ((rc = f.copied(q, (int)j)) != CV_OK) return rc;
         const size_t nl = st.l1 - st.l0;
