@@ -1863,6 +1863,17 @@ static int merkle_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, si
         nx = std::max(nx, c + 1);
         cut.push_back(std::min(nx, t1));
     }
+    // the slots' leaf-digest workspaces, sized once for the call's largest sub-chunk: a buffer that grows is
+    // freed, so the slot's queued kernels (the previous call's) are waited for first
+    size_t max_nl = 0;
+    for (size_t j = 0; j + 1 < cut.size(); j++) max_nl = std::max<size_t>(max_nl, in.txb[cut[j + 1]] - in.txb[cut[j]]);
+    for (int k = 0; k < kPipeSlots; k++) {
+        Slot &sl = d.slot[k];
+        if (max_nl * 32 + 32 > sl.mdig.cap) {
+            if (sl.last && sl.ev) CV_TRY(hipEventSynchronize(sl.ev));
+            CV_TRY(sl.mdig.ensure(max_nl * 32 + 32));
+        }
+    }
     for (size_t j = 0; j + 1 < cut.size(); j++) {
         const size_t c0 = cut[j], c1 = cut[j + 1];
         Slot &sl = d.slot[j % kPipeSlots];
@@ -1896,9 +1907,7 @@ static int merkle_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, si
         if ((rc = f.copied(q, (int)j)) != CV_OK) return rc;
         const size_t nl = st.l1 - st.l0;
         CV_TRY(ws_begin(d, sl, s));
-        hipError_t ek = sl.mdig.ensure(nl * 32 + 32);
-        if (ek == hipSuccess)
-            ek = cvk_merkle((uint32_t)(c1 - c0), (uint32_t)nl, (uint32_t)st.l0, dv + st.o_ar - st.lo,
+        const hipError_t ek = cvk_merkle((uint32_t)(c1 - c0), (uint32_t)nl, (uint32_t)st.l0, dv + st.o_ar - st.lo,
                             reinterpret_cast<const uint64_t *>(dv + st.o_off), reinterpret_cast<const uint32_t *>(dv + st.o_len),
                             reinterpret_cast<const uint32_t *>(dv + st.o_txb), sl.mdig.as<uint32_t>(),
                             dout + (c0 - t0) * 32, dout + o_st + (c0 - t0), s);
@@ -2433,6 +2442,8 @@ int cv_ed25519_verify_device_keyed(cv_ctx *ctx, int device, size_t n, size_t nke
     bool prepared = false;
     int rc = e == hipSuccess ? key_resolve(*d, ctx->key_cap.load(), nkeys, hkeys.data(), nullptr, sok, s, &prepared) : hip_rc(e);
     KeyCache &kc = d->kc;
+    // a slot_of_key that grows is freed: the previous keyed call still queued on the pool reads it
+    if (rc == CV_OK && nkeys * 4 > kc.slot_of_key.cap) rc = hip_rc(pool_quiesce(*d));
     if (rc == CV_OK) rc = hip_rc(kc.slot_of_key.ensure(nkeys * 4));
     // slot_of_key goes up through the pool's pinned staging, which the previous keyed call's upload may
     // still be reading: that call's pool event (after its verify) has passed once its upload has

@@ -53,6 +53,9 @@ def main():
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--n", type=int, default=0, help="signatures (overrides the shape's)")
+    ap.add_argument("--key-pool", type=int, default=0, help="signers from a pool of this many keys (keyed path)")
+    ap.add_argument("--async-calls", type=int, default=0, help="after the timed calls: this many async calls, "
+                                                               "two in flight (the summary's last window)")
     a = ap.parse_args()
     if a.summarize:
         summarize(a.summarize)
@@ -67,7 +70,7 @@ def main():
     n, ml = (1_000_000, 300) if a.shape == "c2" else (8_000_000, 32)
     if a.n:
         n = a.n
-    b = workload.make_batch(eng, 0, n, ml, seed=11)
+    b = workload.make_batch(eng, 0, n, ml, seed=11, key_pool=a.key_pool or None)
     arrs = b.to_host()
     del b
     if a.pinned:
@@ -78,6 +81,18 @@ def main():
         bm, _ = eng.verify_batch(*arrs, want_status=False)
         print(f"call {k}: {(time.perf_counter() - t) * 1e3:.2f} ms", flush=True)
     assert native.bitmap_to_bools(bm, n).all()
+    if a.async_calls:
+        time.sleep(0.01)
+        t = time.perf_counter()
+        pend = []
+        for _ in range(a.async_calls):
+            pend.append(eng.verify_batch_async(*arrs, want_status=False))
+            if len(pend) == 2:
+                bm, _ = eng.wait(pend.pop(0))
+        for tk in pend:
+            bm, _ = eng.wait(tk)
+        print(f"async: {(time.perf_counter() - t) / a.async_calls * 1e3:.2f} ms per call", flush=True)
+        assert native.bitmap_to_bools(bm, n).all()
     eng.close()
 
 
