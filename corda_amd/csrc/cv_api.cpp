@@ -1930,6 +1930,52 @@ static int merkle_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, si
     return CV_OK;
 }
 
+// One shard of a small synchronous Merkle call (a resolve chain's or a notary batch's transactions, staging below
+// kMerkleSmall bytes): packed into slot 0's pinned staging (or DMAed in place from pinned arrays), one DMA, the
+// two kernels, one result copy and one synchronisation — the pipeline's per-call frame (ring events, output
+// join, result stream) costs more than it hides at this size.
+constexpr size_t kMerkleSmall = 24u << 20;
+static int merkle_shard_small(Device &d, const MStage &st, const MerkleIn &in, WorkerPool *pool) {
+    const size_t nt = st.t1 - st.t0, nl = st.l1 - st.l0;
+    const size_t o_st = al16(nt * 32), total_out = o_st + al16(nt);
+    Slot &sl = d.slot[0];
+    hipStream_t s = nullptr;
+    CV_TRY(slot_stream(d, 0, &s));
+    CV_TRY(slot_events(sl));
+    CV_TRY(sl.pin_in.ensure(st.total));
+    CV_TRY(sl.packed.ensure(st.total));
+    CV_TRY(d.pin_out.ensure(total_out));
+    CV_TRY(d.ids.ensure(total_out));
+    if (nl * 32 + 32 > sl.mdig.cap) {
+        if (sl.last && sl.ev) CV_TRY(hipEventSynchronize(sl.ev));
+        CV_TRY(sl.mdig.ensure(nl * 32 + 32));
+    }
+    uint8_t *dv = sl.packed.as<uint8_t>();
+    auto drain = on_exit([s] { (void)hipStreamSynchronize(s); });   // error paths: no DMA outlives the call
+    if (st.total >= (1u << 20) && mstage_direct(st, in.txb, in.arena, in.off, in.len)) {
+        CV_TRY(mstage_dma_direct(st, dv, in.txb, in.arena, in.off, in.len, s));
+    } else {
+        mstage_pack(st, sl.pin_in.as<uint8_t>(), in.txb, in.arena, in.off, in.len, pool);
+        CV_TRY(hipMemcpyAsync(dv, sl.pin_in.p, st.total, hipMemcpyHostToDevice, s));
+    }
+    uint8_t *dout = d.ids.as<uint8_t>();
+    CV_TRY(ws_begin(d, sl, s));
+    const hipError_t ek = cvk_merkle((uint32_t)nt, (uint32_t)nl, (uint32_t)st.l0, dv + st.o_ar - st.lo,
+                                     reinterpret_cast<const uint64_t *>(dv + st.o_off),
+                                     reinterpret_cast<const uint32_t *>(dv + st.o_len),
+                                     reinterpret_cast<const uint32_t *>(dv + st.o_txb), sl.mdig.as<uint32_t>(), dout,
+                                     dout + o_st, s);
+    const hipError_t e2 = ws_end(sl, s);
+    CV_TRY(ek);
+    CV_TRY(e2);
+    CV_TRY(hipMemcpyAsync(d.pin_out.p, dout, in.status ? o_st + nt : nt * 32, hipMemcpyDeviceToHost, s));
+    CV_TRY(hipStreamSynchronize(s));
+    drain.armed = false;
+    std::memcpy(in.ids + st.t0 * 32, d.pin_out.p, nt * 32);
+    if (in.status) std::memcpy(in.status + st.t0, d.pin_out.as<uint8_t>() + o_st, nt);
+    return CV_OK;
+}
+
 // A pipelined call's part on one device, for its ticket: (device index, output index, gen).
 using Part = std::array<uint64_t, 3>;
 
@@ -2245,6 +2291,11 @@ static int merkle_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const
     const int rc = dispatch(ctx, o, ntx, 1, [&](Device &d, size_t t0, size_t t1, int threads) {
         if (t1 <= t0) return CV_OK;
         CV_TRY(hipSetDevice(d.ordinal));
+        if (!ticket) {                                // small synchronous shards: one DMA, no pipeline frame
+            WorkerPool *pool = &d.workers(threads);
+            const MStage st = mstage_plan(t0, t1, tx_leaf_begin, leaf_off, leaf_len, pool);
+            if (st.total <= kMerkleSmall) return merkle_shard_small(d, st, in, pool);
+        }
         int k = 0, r = CV_OK;
         std::unique_lock<std::mutex> lk;
         PipeOut &po = pipe_out(d, &k, lk, &r);

@@ -71,12 +71,16 @@ def test_merkle_host_sharded_pipelined_vs_oracle(engine, oracle_c, scattered):
             ids, st = e.merkle_tx_ids(arena, off, lens, begin)
             assert np.array_equal(ids, ref_ids) and np.array_equal(st, ref_st), f"k={k}"
             r = e.stats("route")
-            assert r["merkle_calls"] == 1 and r["merkle_subchunks"] >= 6 and r["shards"] == k, r
+            assert r["merkle_calls"] == 1 and r["shards"] == k, r
+            if k == 1:                                             # 75 MB of leaves: the pipelined form
+                assert r["merkle_subchunks"] >= 6, r
             out = e.host_empty((30_000, 32))
             ids_p, st_p = e.merkle_tx_ids(*pinned, ids=out)           # direct DMA in, ids DMAed into pinned memory
             assert np.array_equal(ids_p, ref_ids) and np.array_equal(st_p, ref_st)
-            t1 = e.merkle_tx_ids_async(arena, off, lens, begin)
+            e.stats("route", reset=True)
+            t1 = e.merkle_tx_ids_async(arena, off, lens, begin)      # async calls always pipeline
             t2 = e.merkle_tx_ids_async(*pinned)
+            assert e.stats("route")["merkle_subchunks"] >= 12
             a2, s2 = e.wait(t2)
             a1, s1 = e.wait(t1)
             assert np.array_equal(a1, ref_ids) and np.array_equal(s1, ref_st)
