@@ -167,8 +167,9 @@ struct PipeOut {
     std::mutex mu;
     DevBuf dout;
     PinBuf hout;
-    hipEvent_t slot_done[kPipeSlots] = {};   // after this call's last launch group on each slot stream
-    bool slot_used[kPipeSlots] = {};
+    // after this call's last launch group on each slot stream, and (Merkle calls) on the copy stream
+    hipEvent_t slot_done[kPipeSlots + 1] = {};
+    bool slot_used[kPipeSlots + 1] = {};
     bool pending = false;
     uint64_t gen = 0;
     struct Seg {
@@ -1550,7 +1551,7 @@ static int pipe_finish(Device &d, PipeOut &po) {
     // host-side join: the call's last launch group on every slot stream, then the result copies on the
     // device's output stream (which carries nothing else, so it neither waits behind the next call's input
     // copies nor holds a compute stream the next call's kernels run on)
-    for (int k = 0; k < kPipeSlots; k++)
+    for (int k = 0; k <= kPipeSlots; k++)
         if (po.slot_used[k]) CV_TRY(hipEventSynchronize(po.slot_done[k]));
     constexpr size_t kDirect = 1u << 20;
     size_t hb = 0;
@@ -1593,15 +1594,16 @@ struct PipeFrame {
     Device &d;
     PipeOut &po;
     hipStream_t ss[kPipeSlots] = {};
-    bool used[kPipeSlots] = {};
+    bool used[kPipeSlots + 1] = {};   // + the copy stream (Merkle kernels)
     double t[5] = {};   // plan, pack, wait, enqueue (seconds)
     uint64_t chunks = 0, direct = 0;
     int init() {
         for (int k = 0; k < kPipeSlots; k++) {
             CV_TRY(slot_stream(d, k, &ss[k]));
             CV_TRY(slot_events(d.slot[k]));
-            if (!po.slot_done[k]) CV_TRY(hipEventCreateWithFlags(&po.slot_done[k], hipEventDisableTiming));
         }
+        for (int k = 0; k <= kPipeSlots; k++)
+            if (!po.slot_done[k]) CV_TRY(hipEventCreateWithFlags(&po.slot_done[k], hipEventDisableTiming));
         for (int q = 0; q < kRing; q++) {
             if (!d.in_ready[q]) CV_TRY(hipEventCreateWithFlags(&d.in_ready[q], hipEventDisableTiming));
             if (!d.in_free[q]) CV_TRY(hipEventCreateWithFlags(&d.in_free[q], hipEventDisableTiming));
@@ -1673,9 +1675,9 @@ struct PipeFrame {
     // completion marks per slot stream (pipe_finish joins on the host; no GPU-side join, which would hold
     // the next call's kernels on that stream until this call had finished)
     int complete() {
-        for (int k = 0; k < kPipeSlots; k++) {
+        for (int k = 0; k <= kPipeSlots; k++) {
             po.slot_used[k] = used[k];
-            if (used[k]) CV_TRY(hipEventRecord(po.slot_done[k], ss[k]));
+            if (used[k]) CV_TRY(hipEventRecord(po.slot_done[k], k < kPipeSlots ? ss[k] : d.copy));
         }
         po.pending = true;
         po.gen++;
@@ -1854,30 +1856,58 @@ static int merkle_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, si
     uint8_t *dout = po.dout.as<uint8_t>();
     auto drain = on_exit([&f] { f.drain(); });
     WorkerPool *pool = &d.workers(threads);
-    // sub-chunk cuts: whole transactions, about merkle_chunk leaves each (at least one transaction)
+    // sub-chunk cuts: whole transactions, about merkle_chunk leaves each (at least one transaction), and at most
+    // ~12 per shard, so one call's copies fit the ring ahead of its kernels
+    const size_t nl_all = in.txb[t1] - in.txb[t0];
+    const size_t per = std::max<size_t>(o.merkle_chunk, (nl_all + kRing - 5) / (kRing - 4));
     std::vector<size_t> cut{t0};
     while (cut.back() < t1) {
         const size_t c = cut.back();
-        const uint64_t want = (uint64_t)in.txb[c] + o.merkle_chunk;
+        const uint64_t want = (uint64_t)in.txb[c] + per;
         size_t nx = (size_t)(std::upper_bound(in.txb + c + 1, in.txb + t1 + 1, (uint32_t)std::min<uint64_t>(want, UINT32_MAX)) - in.txb) - 1;
         nx = std::max(nx, c + 1);
         cut.push_back(std::min(nx, t1));
     }
-    // the slots' leaf-digest workspaces, sized once for the call's largest sub-chunk: a buffer that grows is
-    // freed, so the slot's queued kernels (the previous call's) are waited for first
+    // The kernels run on the copy stream itself, behind the call's copies: on a compute stream they would queue
+    // behind the verify kernels already there (a C3 node submits the Merkle ids of batch k+1 behind the verify
+    // of batch k, which keeps both compute streams busy for ~75 ms: host C3 0.76x of the device rate), on the
+    // copy stream they wait only for their leaves and take CU slots between the verify's waves.  The copies of
+    // up to kRing - 2 sub-chunks go first, then their kernels (a copy stream stalled behind a kernel that waits
+    // for CU slots moves nothing), so a call's copies run back to back.  One leaf-digest buffer serves them all
+    // (the kernels run one after another); it grows after the copy stream's queued kernels.
     size_t max_nl = 0;
     for (size_t j = 0; j + 1 < cut.size(); j++) max_nl = std::max<size_t>(max_nl, in.txb[cut[j + 1]] - in.txb[cut[j]]);
-    for (int k = 0; k < kPipeSlots; k++) {
-        Slot &sl = d.slot[k];
-        if (max_nl * 32 + 32 > sl.mdig.cap) {
-            if (sl.last && sl.ev) CV_TRY(hipEventSynchronize(sl.ev));
-            CV_TRY(sl.mdig.ensure(max_nl * 32 + 32));
-        }
+    if (max_nl * 32 + 32 > d.digest.cap) {
+        CV_TRY(hipStreamSynchronize(d.copy));
+        CV_TRY(d.digest.ensure(max_nl * 32 + 32));
     }
+    struct Pending {
+        MStage st;
+        int q;
+        uint8_t *dv;
+    };
+    std::vector<Pending> pend;
+    auto flush = [&]() -> int {
+        const double ta = now_s();
+        for (const Pending &p : pend) {
+            const MStage &st = p.st;
+            const size_t nl = st.l1 - st.l0;
+            CV_TRY(cvk_merkle((uint32_t)(st.t1 - st.t0), (uint32_t)nl, (uint32_t)st.l0, p.dv + st.o_ar - st.lo,
+                              reinterpret_cast<const uint64_t *>(p.dv + st.o_off),
+                              reinterpret_cast<const uint32_t *>(p.dv + st.o_len),
+                              reinterpret_cast<const uint32_t *>(p.dv + st.o_txb), d.digest.as<uint32_t>(),
+                              dout + (st.t0 - t0) * 32, dout + o_st + (st.t0 - t0), d.copy));
+            CV_TRY(hipEventRecord(d.in_free[p.q], d.copy));
+            d.in_used[p.q] = true;
+            f.chunks++;
+        }
+        pend.clear();
+        f.used[kPipeSlots] = true;
+        f.t[3] += now_s() - ta;
+        return CV_OK;
+    };
     for (size_t j = 0; j + 1 < cut.size(); j++) {
         const size_t c0 = cut[j], c1 = cut[j + 1];
-        Slot &sl = d.slot[j % kPipeSlots];
-        hipStream_t s = f.ss[j % kPipeSlots];
         double ta = now_s();
         const MStage st = mstage_plan(c0, c1, in.txb, in.off, in.len, pool);
         const bool direct = mstage_direct(st, in.txb, in.arena, in.off, in.len);
@@ -1904,19 +1934,11 @@ static int merkle_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, si
             CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, d.copy));
             if ((rc = f.staged(sk)) != CV_OK) return rc;
         }
-        if ((rc = f.copied(q, (int)j)) != CV_OK) return rc;
-        const size_t nl = st.l1 - st.l0;
-        CV_TRY(ws_begin(d, sl, s));
-        const hipError_t ek = cvk_merkle((uint32_t)(c1 - c0), (uint32_t)nl, (uint32_t)st.l0, dv + st.o_ar - st.lo,
-                            reinterpret_cast<const uint64_t *>(dv + st.o_off), reinterpret_cast<const uint32_t *>(dv + st.o_len),
-                            reinterpret_cast<const uint32_t *>(dv + st.o_txb), sl.mdig.as<uint32_t>(),
-                            dout + (c0 - t0) * 32, dout + o_st + (c0 - t0), s);
-        const hipError_t e2 = ws_end(sl, s);
-        CV_TRY(ek);
-        CV_TRY(e2);
-        if ((rc = f.launched(q, (int)j)) != CV_OK) return rc;
         f.t[3] += now_s() - ta;
+        pend.push_back({st, q, dv});
+        if (pend.size() + 2 >= (size_t)kRing && (rc = flush()) != CV_OK) return rc;
     }
+    if ((rc = flush()) != CV_OK) return rc;
     if ((rc = f.complete()) != CV_OK) return rc;
     drain.armed = false;
     po.nseg = 0;
@@ -1926,6 +1948,7 @@ static int merkle_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, si
     {
         std::lock_guard<std::mutex> g(ctx->st_mu);
         ctx->stats.merkle_chunks += cut.size() - 1;
+        ctx->stats.pipe_chunks -= f.chunks;   // counted as Merkle sub-chunks only
     }
     return CV_OK;
 }

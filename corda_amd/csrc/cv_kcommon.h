@@ -113,16 +113,12 @@ __device__ __forceinline__ void cv_points_one_lane(uint32_t g, uint32_t n, const
     const bool is_r = (g & 1u) != 0;
     uint32_t w[8];
     load_words8(w, is_r ? sig + (size_t)i * 64 : pk + (size_t)i * 32);
-    // decode, verdict bytes, then the table: the output pointers are dead before the table's peak register
-    // pressure, and the table loop re-reads 1P from its stored entry — no spill at 3 waves per SIMD
-    ge_p3 P;
-    const bool ok = cv_hs_point_decode<false>(w, is_r, P);
+    const bool ok = cv_hs_point_one<false>(w, is_r, (is_r ? ws_tabR : ws_tab) + (size_t)i * CV_TAB_WORDS);
     const bool r_ok = __shfl_xor((int)ok, 1) != 0;
     if (!is_r) {
         ws_ok[i] = (ok && r_ok) ? 1 : 0;
         if (status) status[i] = ok ? 0 : 1;
     }
-    ge_cached_multiples8((is_r ? ws_tabR : ws_tab) + (size_t)i * CV_TAB_WORDS, P);
 }
 
 // ---------------------------------------------------------------- kernel declarations

@@ -133,12 +133,6 @@ __host__ __device__ __forceinline__ void ge_cached_multiples8(uint32_t *tab, con
     ge_cached_store(tab + 80, c);
 #pragma unroll 1
     for (int k = 3; k <= 8; k++) {
-#ifdef __HIP_DEVICE_COMPILE__
-        // 1P is re-read from the entry just stored (cache-resident) instead of held across the loop: 40
-        // fewer live VGPRs in the throughput points kernel (no spill at 3 waves per SIMD)
-        asm volatile("" ::: "memory");
-        ge_cached_load(c1, tab + 40);
-#endif
         ge_add(t, P, c1);
         ge_p1p1_to_p3(P, t);
         ge_p3_to_cached(c, P);
@@ -939,23 +933,15 @@ __host__ __device__ __forceinline__ bool cv_hs_points(const uint32_t aw[8], cons
 // points, one encoding per lane (latency form: a lane pair per signature runs the two decodes side by
 // side): is_r = false decodes the key A into k*(-A), true decodes R (canonical) into k*R.  Both lanes
 // run the same instructions.  Returns the lane's decode verdict (key_ok or r_ok).
-// The decode half of cv_hs_point_one: P = the key's -A (is_r false) or R (is_r true, canonical encodings only);
-// an invalid point becomes the identity (its verdict is forced false by ok).
-template <bool LAT = false>
-__host__ __device__ __forceinline__ bool cv_hs_point_decode(const uint32_t w[8], bool is_r, ge_p3 &P) {
-    ge_p3 nP;
+template <bool LAT = true>
+__host__ __device__ __forceinline__ bool cv_hs_point_one(const uint32_t w[8], bool is_r, uint32_t *tab,
+                                                         int half = -1) {
+    ge_p3 P, nP;
     bool ok = ge_decode_0_1_0<LAT>(P, w);
     ok = ok && (!is_r || cv_r_canonical(w));
     if (!ok) ge_p3_identity(P);
     ge_p3_neg(nP, P);
     if (!is_r) P = nP;
-    return ok;
-}
-template <bool LAT = true>
-__host__ __device__ __forceinline__ bool cv_hs_point_one(const uint32_t w[8], bool is_r, uint32_t *tab,
-                                                         int half = -1) {
-    ge_p3 P;
-    const bool ok = cv_hs_point_decode<LAT>(w, is_r, P);
     if (half < 0)
         ge_cached_multiples8(tab, P);
     else
