@@ -329,6 +329,7 @@ struct Device {
     hipEvent_t in_ready[kRing] = {}, in_free[kRing] = {};
     bool in_used[kRing] = {};
     int ring_next = 0;
+    size_t ring_max = 0;                 // the largest ring block (blocks grow to it)
     PinBuf instage[kStage];
     hipEvent_t stage_ev[kStage] = {};
     bool stage_busy[kStage] = {};
@@ -1627,12 +1628,17 @@ struct PipeFrame {
     }
     // The next ring block for a stage of `bytes` (waits for a growing block's last reader); the copy
     // stream waits (on the GPU) for the kernels that last read it.
+    // A block grows straight to the largest block of the ring (at least 1.25x the request): freeing device
+    // memory waits for the whole device, so a ring whose blocks grew one request at a time stalled every
+    // call whose sub-chunk sizes differed from the last ones (a synchronous call's ramp, then async calls).
     int block(int *q_out, size_t bytes, uint8_t **dv) {
         const int q = d.ring_next;
         d.ring_next = (d.ring_next + 1) % kRing;
         if (bytes > d.inblk[q].cap) {
             if (d.in_used[q]) CV_TRY(hipEventSynchronize(d.in_free[q]));
-            CV_TRY(d.inblk[q].ensure(bytes));
+            d.ring_max = std::max(d.ring_max, bytes + bytes / 4);
+            CV_TRY(d.inblk[q].ensure(d.ring_max));
+            d.ring_max = std::max(d.ring_max, d.inblk[q].cap);
         }
         if (d.in_used[q]) CV_TRY(hipStreamWaitEvent(d.copy, d.in_free[q], 0));
         *q_out = q;
