@@ -122,10 +122,13 @@ struct KeyCache {
     uint32_t cap = 0;
     std::unordered_map<std::array<uint8_t, 32>, uint32_t, KeyHash> map;
     uint64_t hits = 0, misses = 0, resets = 0;
-    // the last stream that used the pool, and an event after that use (pool_begin / pool_end)
+    // the last stream that used the pool and an event after that use (pool_end: what an epoch reset waits
+    // for), and the stream of the last table WRITE (keyprep) with an event after it (key_resolve): a reader on
+    // another stream waits only for that (pool_begin) — readers do not wait for readers
     hipStream_t last = nullptr;
     hipEvent_t ev = nullptr;
-    hipEvent_t kp_ev = nullptr;    // after the last keyprep launch (the pipeline's other slot streams wait on it)
+    hipStream_t wlast = nullptr;
+    hipEvent_t wev = nullptr;
     // the device-API keyed call's slot_of_key: device copy, pinned staging, event after its upload
     DevBuf slot_of_key;
     PinBuf pin;
@@ -498,7 +501,8 @@ hipError_t ws_end(Slot &sl, hipStream_t s) {
 hipError_t pool_begin(KeyCache &kc, hipStream_t s) {
     hipError_t e = hipSuccess;
     if (!kc.ev && (e = hipEventCreateWithFlags(&kc.ev, hipEventDisableTiming)) != hipSuccess) return e;
-    if (kc.last && kc.last != s) e = hipStreamWaitEvent(s, kc.ev, 0);
+    if (!kc.wev && (e = hipEventCreateWithFlags(&kc.wev, hipEventDisableTiming)) != hipSuccess) return e;
+    if (kc.wlast && kc.wlast != s) e = hipStreamWaitEvent(s, kc.wev, 0);
     return e;
 }
 hipError_t pool_end(KeyCache &kc, hipStream_t s) {
@@ -771,7 +775,7 @@ void cv_close(cv_ctx *ctx) {
         }
         if (d.copy) (void)hipStreamDestroy(d.copy);
         d.kc.pin.release();
-        for (hipEvent_t v : {d.kc.ev, d.kc.pin_ev, d.kc.kp_ev})
+        for (hipEvent_t v : {d.kc.ev, d.kc.pin_ev, d.kc.wev})
             if (v) (void)hipEventDestroy(v);
         if (d.stream) (void)hipStreamDestroy(d.stream);
         d.pool.reset();
@@ -1379,8 +1383,10 @@ static int key_resolve(Device &d, uint32_t cap, size_t nk, const uint8_t *keys, 
     }
     if (m) {
         // the pageable copies above read miss_keys / miss_slots asynchronously: keep them alive
-        const hipError_t e = hipStreamSynchronize(s);
+        hipError_t e = hipStreamSynchronize(s);
+        if (e == hipSuccess) e = hipEventRecord(kc.wev, s);
         if (e != hipSuccess) return fail(e);
+        kc.wlast = s;
         *prepared = true;
     }
     for (auto &kv : fresh) kc.map.emplace(kv.first, kv.second);
@@ -1751,11 +1757,8 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
         bool prepared = false;
         rc = key_resolve(d, ctx->key_cap.load(), nkeys, keys, in.used, sok, f.ss[0], &prepared);
         if (rc != CV_OK) return rc;
-        if (prepared) {                            // the other compute stream waits for the new tables
-            if (!d.kc.kp_ev) CV_TRY(hipEventCreateWithFlags(&d.kc.kp_ev, hipEventDisableTiming));
-            CV_TRY(hipEventRecord(d.kc.kp_ev, f.ss[0]));
-            for (int k = 1; k < kPipeSlots; k++) CV_TRY(hipStreamWaitEvent(f.ss[k], d.kc.kp_ev, 0));
-        }
+        if (prepared)                              // the other compute stream waits for the new tables
+            for (int k = 1; k < kPipeSlots; k++) CV_TRY(pool_begin(d.kc, f.ss[k]));
         const size_t kb = al16(nkeys * 32) + al16(nkeys * 4);
         CV_TRY(po.kstage.ensure(kb));
         CV_TRY(po.kdev.ensure(kb));
@@ -2518,6 +2521,9 @@ int cv_ed25519_verify_device_keyed(cv_ctx *ctx, int device, size_t n, size_t nke
     if (e == hipSuccess && phase_ms) e = hipEventRecord(ev[0], s);
     if (e == hipSuccess) e = ws_begin(*d, sl, s);
     if (e == hipSuccess) e = pool_begin(d->kc, s);
+    // device-API keyed calls also wait for the pool's previous user on another stream (their streams are the
+    // caller's: an epoch reset can only wait for the last of them, so they stay a chain)
+    if (e == hipSuccess && d->kc.last && d->kc.last != s) e = hipStreamWaitEvent(s, d->kc.ev, 0);
     std::vector<uint32_t> sok;
     bool prepared = false;
     int rc = e == hipSuccess ? key_resolve(*d, ctx->key_cap.load(), nkeys, hkeys.data(), nullptr, sok, s, &prepared) : hip_rc(e);
