@@ -291,6 +291,11 @@ CV_HD void digits65536_pairs(uint32_t out[8], const uint32_t n[8]) {
 // steps (relative error ~2^-52, against the IEEE division's ~15-instruction scale/fma/fixup sequence);
 // every use tolerates it — the Lehmer loop re-checks each quotient (0 <= remainder < divisor, else it
 // stops early and the exact loop continues), the exact loop scales its estimate by 1 - 2^-44
+// Host builds (the test harness): a nonzero cv_rcp_emulation replaces the exact division by the device's
+// sequence — an initial reciprocal with that relative error (v_rcp_f64's estimate; tests use errors up to
+// 2^-12, far worse) refined by the same two Newton steps — so the CPU tests run the quotients the GPU runs.
+// (A host variable: device code never reads it.)
+inline double cv_rcp_emulation = 0.0;
 CV_HD double cv_qdiv(double a, double b) {
 #ifdef __HIP_DEVICE_COMPILE__
     double r = __builtin_amdgcn_rcp(b);
@@ -298,6 +303,12 @@ CV_HD double cv_qdiv(double a, double b) {
     r = fma(fma(-b, r, 1.0), r, r);
     return a * r;
 #else
+    if (cv_rcp_emulation != 0.0) {
+        double r = (1.0 / b) * (1.0 + cv_rcp_emulation);
+        r = fma(fma(-b, r, 1.0), r, r);
+        r = fma(fma(-b, r, 1.0), r, r);
+        return a * r;
+    }
     return a / b;
 #endif
 }
@@ -314,6 +325,14 @@ CV_HD double cv_sw5_abs_double(const uint32_t t[5]) {
 #pragma unroll
     for (int i = 4; i >= 0; i--) d = d * 4294967296.0 + (double)(neg ? ~t[i] : t[i]);
     return neg ? d + 1.0 : d;
+}
+// The exact loop's quotient (r0 >= r1 >= 2^128): an estimate never above floor(r0 / r1) — the doubles carry
+// < 2^-49 relative error (word conversions 2^-53 each, the reciprocal and product a few ulp), scaled down by
+// 1 - 2^-44 — clamped to [1, 2^32 - 1]; an underestimate leaves r0 - q r1 >= r1 for the next step.
+CV_HD uint32_t cv_exact_quotient(const uint32_t r0[8], const uint32_t r1[8]) {
+    double q = cv_qdiv(cv_words_to_double(r0), cv_words_to_double(r1)) * (1.0 - 0x1p-44);
+    q = q < 1.0 ? 1.0 : (q > 4294967295.0 ? 4294967295.0 : q);
+    return (uint32_t)q;
 }
 // a -= q * b (8 words, no underflow by construction)
 CV_HD void cv_submul8(uint32_t a[8], const uint32_t b[8], uint32_t q) {
@@ -460,10 +479,7 @@ __host__ __device__ __forceinline__ bool sc_halfsize(uint32_t u[8], uint32_t v[8
             break;
         }
         CV_STAT(g_exact++;)
-        // quotient estimate, never above floor(r0 / r1): the doubles carry < 2^-49 relative error
-        double q = cv_qdiv(cv_words_to_double(r0), cv_words_to_double(r1)) * (1.0 - 0x1p-44);
-        q = q < 1.0 ? 1.0 : (q > 4294967295.0 ? 4294967295.0 : q);
-        const uint32_t qi = (uint32_t)q;
+        const uint32_t qi = cv_exact_quotient(r0, r1);
         cv_submul8(r0, r1, qi);
         cv_submul5(t0, t1, qi);
     }

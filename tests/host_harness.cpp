@@ -280,6 +280,21 @@ int cvh_halfsize(const uint8_t *h, const uint8_t *s, uint8_t *out, int *v_neg, i
     return ok ? 1 : 0;
 }
 
+// The device's reciprocal sequence in cv_qdiv on the host (0 = exact division), for the lattice tests.
+void cvh_set_rcp_emulation(double rel_err) { cv_rcp_emulation = rel_err; }
+
+// One quotient step of sc_halfsize's exact loop on (r0, r1) given as 32 LE bytes each (r0 >= r1 >= 2^128):
+// returns q and r0 - q r1 in out (32 B).
+uint32_t cvh_exact_step(const uint8_t *r0b, const uint8_t *r1b, uint8_t *out) {
+    uint32_t r0[8], r1[8];
+    words_from_bytes(r0, r0b, 8);
+    words_from_bytes(r1, r1b, 8);
+    const uint32_t q = cv_exact_quotient(r0, r1);
+    cv_submul8(r0, r1, q);
+    bytes_from_words(out, r0, 8);
+    return q;
+}
+
 // PartialMerkleTree.verify of tree t of a flat batch (cv_pmt_verify); returns status, *verdict.
 int cvh_pmt_verify(uint32_t b, uint32_t e, const uint8_t *kind, const uint32_t *left, const uint32_t *right,
                    const uint8_t *leaf_hash, const uint8_t *root, const uint8_t *check, uint32_t cb, uint32_t ce,

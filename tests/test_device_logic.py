@@ -277,9 +277,49 @@ def test_verify_batch_logic_chunks(host_harness, corpus, manifest):
         assert np.array_equal(status, corpus["status"][order])
 
 
-def test_halfsize_lattice_properties(host_harness):
+@pytest.fixture(params=[0.0, 2.0 ** -26, -(2.0 ** -26), 2.0 ** -12, -(2.0 ** -12)],
+                ids=["exact_div", "rcp+2^-26", "rcp-2^-26", "rcp+2^-12", "rcp-2^-12"])
+def rcp(host_harness, request):
+    """the device computes the lattice quotients with v_rcp_f64 + two Newton steps (cv_qdiv), the
+    host build with an exact division; these runs emulate the device sequence on the host from initial
+    reciprocals far worse than the hardware's (relative error 2^-26 and 2^-12, both signs)."""
+    host_harness.cvh_set_rcp_emulation.argtypes = [ctypes.c_double]
+    host_harness.cvh_set_rcp_emulation(request.param)
+    yield request.param
+    host_harness.cvh_set_rcp_emulation(0.0)
+
+
+def test_exact_loop_quotients_just_below_integers(host_harness, rcp):
+    """The exact loop's quotient step (cv_exact_quotient + cv_submul8) on r0 = k r1 - d with d tiny (the true
+    quotient just below the integer k, where a rounded-up estimate would underflow the remainder), r0 = k r1
+    exactly, and random pairs: q <= floor(r0 / r1) always (the remainder never wraps), and q is at most one
+    short of it for quotients below 2^32."""
+    H = host_harness
+    H.cvh_exact_step.restype = ctypes.c_uint32
+    rng = random.Random(99 + int(rcp * 2 ** 30))
+    cases = []
+    for _ in range(4000):
+        r1 = rng.randrange(2 ** 128, 2 ** rng.randrange(129, 225))
+        k = rng.choice([1, 2, 3, rng.randrange(2, 2 ** 32), 2 ** 32 - 1, 2 ** rng.randrange(1, 32)])
+        for d in (0, 1, 2, rng.randrange(1, 2 ** 20), -1, -rng.randrange(1, 2 ** 20)):
+            r0 = k * r1 - d
+            if r1 <= r0 < 2 ** 256:
+                cases.append((r0, r1))
+    for r0, r1 in cases:
+        out = _out(32)
+        q = H.cvh_exact_step(_b(r0.to_bytes(32, "little")), _b(r1.to_bytes(32, "little")), out)
+        rem = int.from_bytes(bytes(out), "little")
+        true_q = r0 // r1
+        assert 1 <= q <= true_q, (r0, r1, q, true_q)
+        assert rem == r0 - q * r1
+        if true_q < 2 ** 32:
+            assert true_q - q <= 1 and rem < 2 * r1
+
+
+def test_halfsize_lattice_properties(host_harness, rcp):
     """sc_halfsize: u = v h (mod 8L), v odd, w = -v s (mod L), |u|, |v| < 16^nwin; the fallback
-    (h, 1) only when no short odd-v vector exists.  Random h, s plus edge scalars."""
+    (h, 1) only when no short odd-v vector exists.  Random h, s plus edge scalars; with the exact division
+    and with the device's reciprocal sequence emulated (rcp)."""
     H = host_harness
     rng = random.Random(7)
     cases = [(0, 0), (1, 5), (L - 1, L - 1), (2**128 - 1, 3), (2**128, 1), (2**252, 7), (8, 9)]
