@@ -1637,12 +1637,15 @@ struct PipeFrame {
     // A block grows straight to the largest block of the ring (at least 1.25x the request): freeing device
     // memory waits for the whole device, so a ring whose blocks grew one request at a time stalled every
     // call whose sub-chunk sizes differed from the last ones (a synchronous call's ramp, then async calls).
-    int block(int *q_out, size_t bytes, uint8_t **dv) {
+    // hint: the call's largest sub-chunk at this one's bytes per record, so a ramp's first small sub-chunks
+    // do not size blocks that its later big ones must grow again.
+    int block(int *q_out, size_t bytes, uint8_t **dv, size_t hint = 0) {
         const int q = d.ring_next;
         d.ring_next = (d.ring_next + 1) % kRing;
         if (bytes > d.inblk[q].cap) {
             if (d.in_used[q]) CV_TRY(hipEventSynchronize(d.in_free[q]));
-            d.ring_max = std::max(d.ring_max, bytes + bytes / 4);
+            const size_t want = std::max(bytes, hint);
+            d.ring_max = std::max(d.ring_max, want + want / 4);
             CV_TRY(d.inblk[q].ensure(d.ring_max));
             d.ring_max = std::max(d.ring_max, d.inblk[q].cap);
         }
@@ -1772,6 +1775,8 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
     const uint32_t *kdev_slot = keyed ? reinterpret_cast<const uint32_t *>(po.kdev.as<uint8_t>() + al16(nkeys * 32)) : nullptr;
     const size_t ach = std::max(o.async_chunk, std::min(2 * o.async_chunk, n / 16 / 64 * 64));
     const std::vector<size_t> cut = async ? pipe_cuts(b, e, ach, ach, false) : pipe_cuts(b, e, o.pipe_first, o.pipe_chunk, true);
+    size_t max_m = 1;
+    for (size_t j = 0; j + 1 < cut.size(); j++) max_m = std::max(max_m, cut[j + 1] - cut[j]);
     for (size_t j = 0; j + 1 < cut.size(); j++) {
         const size_t c0 = cut[j], c1 = cut[j + 1], m = c1 - c0;
         Slot &sl = d.slot[j % kPipeSlots];
@@ -1783,7 +1788,7 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
         f.t[0] += t1 - t0;
         int q;
         uint8_t *dv;
-        if ((rc = f.block(&q, st.total, &dv)) != CV_OK) return rc;
+        if ((rc = f.block(&q, st.total, &dv, (size_t)((double)st.total / (double)m * (double)max_m))) != CV_OK) return rc;
         if (direct) {
             t0 = now_s();
             f.t[2] += t0 - t1;

@@ -77,9 +77,13 @@ def main():
         arrs = tuple(eng.host_copy(x) for x in arrs)
     for k in range(a.calls):
         time.sleep(0.01)                      # a gap between calls (the summary takes the last one)
+        eng.stats("pipe", reset=True)
         t = time.perf_counter()
         bm, _ = eng.verify_batch(*arrs, want_status=False)
-        print(f"call {k}: {(time.perf_counter() - t) * 1e3:.2f} ms", flush=True)
+        dt = (time.perf_counter() - t) * 1e3
+        st = eng.stats("pipe", reset=True)
+        print(f"call {k}: {dt:.2f} ms  host ms: " + " ".join(f"{n[:-2]}={v * 1e3:.2f}" for n, v in st.items()
+                                                            if n.endswith("_s")), flush=True)
     assert native.bitmap_to_bools(bm, n).all()
     if a.async_calls:
         time.sleep(0.01)
