@@ -1991,6 +1991,21 @@ static int merkle_shard_small(Device &d, const MStage &st, const MerkleIn &in, W
     auto drain = on_exit([s] { (void)hipStreamSynchronize(s); });   // error paths: no DMA outlives the call
     if (st.total >= (1u << 20) && mstage_direct(st, in.txb, in.arena, in.off, in.len)) {
         CV_TRY(mstage_dma_direct(st, dv, in.txb, in.arena, in.off, in.len, s));
+    } else if (!st.compact && st.hi - st.lo >= (4u << 20)) {
+        // a contiguous leaf range of 4 MB and more: the records first, then the leaf bytes in 2 MB pieces, each
+        // piece's DMA issued as soon as it is packed (the copies overlap the packing)
+        uint8_t *h = sl.pin_in.as<uint8_t>();
+        const size_t nl = st.l1 - st.l0, nt = st.t1 - st.t0;
+        par_copy({{h + st.o_off, in.off + st.l0, nl * 8}, {h + st.o_len, in.len + st.l0, nl * 4},
+                  {h + st.o_txb, in.txb + st.t0, (nt + 1) * 4}}, nullptr);
+        CV_TRY(hipMemcpyAsync(dv, h, st.o_ar, hipMemcpyHostToDevice, s));
+        const size_t span = st.hi - st.lo;
+        constexpr size_t kPiece = 2u << 20;
+        for (size_t p0 = 0; p0 < span; p0 += kPiece) {
+            const size_t m = std::min(kPiece, span - p0);
+            par_copy({{h + st.o_ar + p0, in.arena + st.lo + p0, m}}, pool);
+            CV_TRY(hipMemcpyAsync(dv + st.o_ar + p0, h + st.o_ar + p0, m, hipMemcpyHostToDevice, s));
+        }
     } else {
         mstage_pack(st, sl.pin_in.as<uint8_t>(), in.txb, in.arena, in.off, in.len, pool);
         CV_TRY(hipMemcpyAsync(dv, sl.pin_in.p, st.total, hipMemcpyHostToDevice, s));
