@@ -80,7 +80,7 @@ __device__ __forceinline__ void cv_points_pair_lane(uint32_t g, uint32_t n, cons
     }
 }
 
-// points of the latency prep with FOUR lanes per signature (cvk_set_lat_points_quad): lanes 4i + {0, 1}
+// points of the latency prep with FOUR lanes per signature (cv_prep_lat_kernel<true, ...>, the tri form): lanes 4i + {0, 1}
 // decode A / R and build entries 0, 1, 3, 5, 7 of their table, lanes 4i + {2, 3} decode the same points
 // (the redundant decode costs no time: the lanes are idle otherwise) and build entries 2, 4, 6, 8 —
 // each lane's chain is the decode + 1 doubling + 3 additions instead of + 1 + 6
