@@ -102,14 +102,38 @@ CV_HD void fe_carry(fe &h, const fe &f) {
     for (int i = 0; i < 10; i++) h.v[i] = t[i];
 }
 
+// Carry of the even limbs only: even limbs < 2^26, odd limbs grow by at most 2^6.  Half the instructions
+// of fe_carry; enough for a multiplication's g operand whose limbs are a few units (19 g_j < 2^32 for odd
+// limbs up to 6.7 units and even limbs up to 3.3) when fe_check_mul_in's column rule holds.
+CV_HD void fe_carry_even(fe &h) {
+#pragma unroll
+    for (int i = 0; i < 10; i += 2) {
+        h.v[i + 1] += h.v[i] >> 26;
+        h.v[i] &= 0x3ffffffu;
+    }
+}
+
 CV_HD uint64_t mu64(uint32_t a, uint32_t b) { return (uint64_t)a * (uint64_t)b; }
 
+// The operand rules of fe_mul, checked exactly on the host build: 2 f_i (odd i) and 19 g_j fit 32 bits,
+// and every column sum (x2 for odd x odd limbs, x19 past 2^255) stays below 2^63.9, which leaves room
+// for the sequential carry-in (< 2^40).  The documented bounds (f <= 8, g <= 3.3 units) satisfy them;
+// so do the refined ones some formulas use (g's odd limbs up to 6.7 units with a smaller f or even g).
 CV_HD void fe_check_mul_in(const fe &f, const fe &g) {
 #if CV_CHECKING
     for (int i = 0; i < 10; i++) {
-        CV_ASSERT((uint64_t)f.v[i] <= (uint64_t)8 << CV_W(i), "fe_mul: f limb > 8M");
+        CV_ASSERT((uint64_t)f.v[i] * 2 < ((uint64_t)1 << 32), "fe_mul: 2*f overflows");
         CV_ASSERT(i == 0 || (uint64_t)g.v[i] * 19 < ((uint64_t)1 << 32), "fe_mul: 19*g overflows");
-        CV_ASSERT((uint64_t)g.v[i] * 10 < ((uint64_t)33 << CV_W(i)), "fe_mul: g limb > 3.3M");
+    }
+    for (int k = 0; k < 10; k++) {
+        unsigned __int128 sum = 0;
+        for (int i = 0; i < 10; i++) {
+            const int j = (k - i + 10) % 10;
+            const uint64_t a = ((i & 1) && (j & 1)) ? 2ull * f.v[i] : f.v[i];
+            const uint64_t b = i + j >= 10 ? 19ull * g.v[j] : g.v[j];
+            sum += (unsigned __int128)a * b;
+        }
+        CV_ASSERT(sum < ((unsigned __int128)15 << 60), "fe_mul: column sum >= 2^63.9");
     }
 #else
     (void)f; (void)g;

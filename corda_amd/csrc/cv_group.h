@@ -65,15 +65,15 @@ CV_HD void ge_p3_to_cached(ge_cached &r, const ge_p3 &p) {
 // r = 2p: 4 squarings.  p1p1 = (E, H', G, F') with E = 2XY, H' = X^2+Y^2, G = Y^2-X^2,
 // F' = 2Z^2-G: the negated (E, -H, G, -F) form of HWCD's doubling, which names the same point.
 CV_HD void ge_p2_dbl(ge_p1p1 &r, const ge_p2 &p) {
-    fe a, hs, sq[4];
+    fe a, sq[4];
     fe_add(a, p.X, p.Y);
     const fe in[4] = {p.X, p.Y, p.Z, a};
     fe_sq_n<4, 0x4>(sq, in);      // X^2, Y^2, 2 Z^2, (X+Y)^2
     const fe &xx = sq[0], &yy = sq[1], &zz2 = sq[2], &aa = sq[3];
-    fe_add(hs, yy, xx);
-    fe_carry(r.Y, hs);            // H' (tight: it is subtracted below with a 2p bias)
+    fe_add(r.Y, yy, xx);          // H' <= 2.02 (an f operand: not carried)
     fe_sub<2>(r.Z, yy, xx);       // G  <= 3.01
-    fe_sub<2>(r.X, aa, r.Y);      // E  <= 3.01
+    fe_sub<3>(r.X, aa, r.Y);      // E  <= 4.01, a g operand: its even limbs carried (<= 1.0, odd <= 4.01)
+    fe_carry_even(r.X);
     fe_sub<4>(r.T, zz2, r.Z);     // F' <= 5.01
 }
 CV_HD void ge_p3_dbl(ge_p1p1 &r, const ge_p3 &p) {

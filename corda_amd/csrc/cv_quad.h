@@ -21,59 +21,81 @@ template <int CTRL> __device__ __forceinline__ void fe_qp(fe &h, const fe &f) {
     for (int i = 0; i < 10; i++) h.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)f.v[i], CTRL, 0xF, 0xF, true);
 }
 
-// the second half of both formulas: R1 = (H, G, F, E) on lanes 0..3 (tight) ->
-// own coordinate of (X, Y, Z, T) = (E F, G H, F G, E H)
+// the second half of both formulas: R1 = (F, H, G, E) on lanes 0..3 (even limbs carried, fe_carry_even) ->
+// own coordinate of (X, Y, Z, T) = (E F, G H, F G, E H): each lane multiplies its own value by the one
+// the quad_perm (3, 2, 0, 1) brings (one move per limb; the own operand needs none)
 template <bool SEQ = false>
 __device__ __forceinline__ void quad_finish_products(fe &P, const fe &R1) {
-    fe op1, op2;
-    fe_qp<CV_QP(3, 1, 2, 3)>(op1, R1);   // E, G, F, E
-    fe_qp<CV_QP(2, 0, 1, 0)>(op2, R1);   // F, H, G, H
-    fe_mul_q<SEQ>(P, op1, op2);
+    fe op2;
+    fe_qp<CV_QP(3, 2, 0, 1)>(op2, R1);   // E, G, F, H
+    fe_mul_q<SEQ>(P, R1, op2);
 }
 
-// P <- 2P.  P: own coordinate of an extended point (T is not read).
+// One limb moved inside the quad.  Written so that every moved value feeds only VOP2 operations (add,
+// and, xor) with VGPR operands: LLVM's DPP combiner then folds the move into each of them (v_add_u32_dpp,
+// v_xor_b32_dpp, ...) and no v_mov_b32_dpp is issued.  Lane-dependent signs use the identity
+// (x XOR m) + (m AND (k p_i + 1)) = k p_i - x on the lanes where m is all ones, x on the others — two
+// instructions instead of a subtraction on every lane plus a select.
+template <int CTRL> __device__ __forceinline__ uint32_t qpv(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, true);
+}
+// all ones on the lanes where c holds.  Opaque to the optimiser: seen as a select, x AND mask became a
+// v_cndmask (VOP3), which takes no DPP operand, and the move stayed.
+__device__ __forceinline__ uint32_t lane_mask(bool c) {
+    uint32_t m = c ? ~0u : 0u;
+    asm volatile("" : "+v"(m));
+    return m;
+}
+
+// P <- 2P.  P: own coordinate of an extended point (T is not read).  Squares on lanes 0..3: C = 2 Z^2,
+// A = X^2, B = Y^2, S = (X + Y)^2; then lane 0 F' = C - G = C + A - B, lane 1 H' = A + B, lane 2 G = B - A,
+// lane 3 E = S - H' (the negated-(F, H) doubling: (E F', G H', F' G, E H') is 2P).
 template <bool SEQ = false>
 __device__ __forceinline__ void quad_dbl(fe &P, int r) {
-    fe w, x, u, sq;
-    fe_qp<CV_QP(0, 1, 2, 1)>(w, P);      // X, Y, Z, Y
-    fe_qp<CV_QP(0, 0, 0, 0)>(x, P);      // X everywhere
+    const uint32_t m3 = lane_mask(r == 3);
+    const uint32_t ma = lane_mask(r != 1), na = lane_mask(r >= 2);     // A: +, 0, -, -
+    const uint32_t mb = lane_mask(r != 2), nb = lane_mask(r == 0 || r == 3);   // B: -, +, 0, -
+    fe u, sq, R1;
+    // lane 0 Z, lane 1 X, lane 2 Y, lane 3 X + Y (<= 2.02)
 #pragma unroll
-    for (int i = 0; i < 10; i++) u.v[i] = w.v[i] + (r == 3 ? x.v[i] : 0u);   // lane 3: X + Y (<= 2.02)
-    fe_sq_q<SEQ>(sq, u, r == 2);         // A = X^2, B = Y^2, C = 2 Z^2, S = (X + Y)^2   (tight)
-    fe a, b, hp, g, t, d, R1;
-    fe_qp<CV_QP(0, 0, 0, 0)>(a, sq);
-    fe_qp<CV_QP(1, 1, 1, 1)>(b, sq);
-    fe_add(hp, a, b);                    // H' = A + B          <= 2.02
-    fe_sub<2>(g, b, a);                  // G  = B - A          <= 3.01
-    fe_sel(t, g, hp, r == 0 || r == 3);
-    fe_sub<4>(d, sq, t);                 // lane 2: F' = C - G, lane 3: E = S - H'   (<= 6.03)
-    fe_sel(R1, t, d, r >= 2);
-    fe_carry(R1, R1);
-    quad_finish_products<SEQ>(P, R1);    // (E F', G H', F' G, E H') — the negated-(F, H) doubling, same point
+    for (int i = 0; i < 10; i++) u.v[i] = qpv<CV_QP(2, 0, 1, 1)>(P.v[i]) + (qpv<CV_QP(0, 0, 0, 0)>(P.v[i]) & m3);
+    fe_sq_q<SEQ>(sq, u, r == 0);         // C, A, B, S (tight)
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        // own + (+-A or 0) + (+-B or 0), each negation x -> (x XOR ~0) + kp_i + 1:
+        // F' = C + A + 2p - B (<= 4.02), H' = A + B (<= 2.02), G = B + 2p - A (<= 3.01), E = S + 4p - A - B (<= 5.01)
+        const uint32_t ta = (qpv<CV_QP(1, 1, 1, 1)>(sq.v[i]) & ma) ^ na;
+        const uint32_t tb = (qpv<CV_QP(2, 2, 2, 2)>(sq.v[i]) & mb) ^ nb;
+        const uint32_t k = r == 1 ? 0u : r == 3 ? 2u * (cv_kp(2, i) + 1u) : cv_kp(2, i) + 1u;
+        R1.v[i] = sq.v[i] + ta + tb + k;
+    }
+    fe_carry_even(R1);
+    quad_finish_products<SEQ>(P, R1);
 }
 
 // P <- P + Q, q = this lane's coordinate of Q in cached form (Y+X, Y-X, Z, 2dT); for an affine
-// "precomp" Q (y+x, y-x, 1, 2dxy) lane 2 passes the constant 1.
+// "precomp" Q (y+x, y-x, 1, 2dxy) lane 2 passes the constant 1.  Products on lanes 0..3: a = (Y1+X1)(Y2+X2),
+// b = (Y1-X1)(Y2-X2), dd = Z1 Z2, c = T1 2d T2; then lane 0 F = 2dd - c, lane 1 H = a + b, lane 2 G = 2dd + c,
+// lane 3 E = a - b.
 template <bool SEQ = false>
 __device__ __forceinline__ void quad_add(fe &P, const fe &q, int r) {
-    fe y, x, s, d, L, m;
-    fe_qp<CV_QP(1, 1, 2, 3)>(y, P);      // Y, Y, Z, T
-    fe_qp<CV_QP(0, 0, 2, 3)>(x, P);      // X, X, Z, T
-    fe_add(s, y, x);                     // lane 0: Y + X      <= 2.02
-    fe_sub<2>(d, y, x);                  // lane 1: Y - X      <= 3.01
-    fe_sel(L, y, d, r == 1);
-    fe_sel(L, L, s, r == 0);             // lanes 2, 3: Z, T
-    fe_mul_q<SEQ>(m, L, q);              // a, b, dd = Z1 Z2, c = T1 2d T2
-    fe o1, o2, sum, diff, R1;
-    fe_qp<CV_QP(0, 2, 2, 0)>(o1, m);     // a, dd, dd, a
-    const uint32_t sh = (r == 1 || r == 2) ? 1u : 0u;
+    const uint32_t m01 = lane_mask(r < 2), m1 = lane_mask(r == 1);
+    const uint32_t m02 = lane_mask(r == 0 || r == 2), n03 = lane_mask(r == 0 || r == 3);
+    fe L, m, R1;
+    // lane 0 Y + X (<= 2.02), lane 1 Y + 2p - X (<= 3.01), lanes 2, 3 their own Z, T
 #pragma unroll
-    for (int i = 0; i < 10; i++) o1.v[i] <<= sh;   // 2 dd on lanes 1, 2 (<= 2.02)
-    fe_qp<CV_QP(1, 3, 3, 1)>(o2, m);     // b, c, c, b
-    fe_add(sum, o1, o2);                 // lane 0: H = a + b, lane 1: G = 2dd + c
-    fe_sub<2>(diff, o1, o2);             // lane 2: F = 2dd - c, lane 3: E = a - b
-    fe_sel(R1, diff, sum, r < 2);
-    fe_carry(R1, R1);
+    for (int i = 0; i < 10; i++)
+        L.v[i] = qpv<CV_QP(1, 1, 2, 3)>(P.v[i]) + ((qpv<CV_QP(0, 0, 0, 0)>(P.v[i]) & m01) ^ m1) +
+                 (m1 & (cv_kp(2, i) + 1u));
+    fe_mul_q<SEQ>(m, L, q);              // a, b, dd, c
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        // x = dd, a, dd, a (doubled on lanes 0, 2);  y = c, b, c, b (negated on lanes 0, 3)
+        const uint32_t x = qpv<CV_QP(2, 0, 2, 0)>(m.v[i]) + (qpv<CV_QP(2, 0, 2, 0)>(m.v[i]) & m02);
+        // F = 2dd + 2p - c (<= 4.02), H = a + b, G = 2dd + c (<= 3.03), E = a + 2p - b (<= 3.01)
+        R1.v[i] = x + (qpv<CV_QP(3, 1, 3, 1)>(m.v[i]) ^ n03) + (n03 & (cv_kp(2, i) + 1u));
+    }
+    fe_carry_even(R1);
     quad_finish_products<SEQ>(P, R1);
 }
 
