@@ -68,9 +68,8 @@ __device__ __forceinline__ bool cv_quad_hs_straus(const uint32_t *blo, const uin
 // this lane's coordinate of d * P, cached form, from either table format: the per-signature cached
 // tables (precomp = false: 40 words per entry, entry k = k P, entry 0 = identity) or the CV_BCOMB affine rows
 // (precomp = true: stride CV_BTAB_STRIDE, row k = k P, row 0 = identity; Z = 1).  Same instructions
-// on every lane (only addresses and selects differ), so the four quads never diverge.  In two parts, so a
-// window's entry can be loaded one window ahead (quad_any_load) and fixed up when it is added (quad_any_fix).
-__device__ __forceinline__ void quad_any_load(fe &q, const uint32_t *tab, bool precomp, int a, int r) {
+// on every lane (only addresses and selects differ), so the four quads never diverge.
+__device__ __forceinline__ void quad_any_coord(fe &q, const uint32_t *tab, bool precomp, int a, int r) {
     const int m = a < 0 ? -a : a;
     const bool neg = a < 0;
     const int c = (r < 2 && neg) ? 1 - r : r;            // -(Y+X, Y-X, Z, T2d) = (Y-X, Y+X, Z, -T2d)
@@ -84,17 +83,11 @@ __device__ __forceinline__ void quad_any_load(fe &q, const uint32_t *tab, bool p
         q.v[2 * j] = v.x;
         q.v[2 * j + 1] = v.y;
     }
-}
-__device__ __forceinline__ void quad_any_fix(fe &q, bool precomp, int a, int r) {
     fe nq, one;
     fe_neg(nq, q);
-    fe_sel(q, q, nq, a < 0 && r == 3);
+    fe_sel(q, q, nq, neg && r == 3);
     fe_one(one);
     fe_sel(q, q, one, precomp && r == 2);
-}
-__device__ __forceinline__ void quad_any_coord(fe &q, const uint32_t *tab, bool precomp, int a, int r) {
-    quad_any_load(q, tab, precomp, a, r);
-    quad_any_fix(q, precomp, a, r);
 }
 
 // this lane's coordinate of a full extended point in cached form (Y+X, Y-X, Z, 2dT), from each
@@ -121,32 +114,26 @@ template <int CTRL> __device__ __forceinline__ void fe_dpp_row(fe &h, const fe &
 
 // E = [v]R + [u]A + [w]B by four chains (quad c of the 16-lane group, coordinate r); returns E == O
 // on every lane.  tab / precomp / field: this quad's table and digit field (5 bits at `field`).
+// (Loading each window's entry one window ahead, behind the four doublings, measured 2-4 us SLOWER at 256,
+// 1,024, 2,048 and 4,096 signatures on one box and 2.7 us faster at 4,096 on another: not kept,
+// tools/microbench/lat_parts.hip, profiles/r04_tri_quad_formulas.log.)
 template <bool SEQ = false>
 __device__ __forceinline__ bool cv_tri_hs_straus(const uint32_t *dig, size_t stride, const uint32_t *tab, bool precomp,
                                                  int field, int nw, int r) {
     fe P, q;
     fe_zero(P);
     if (r == 1 || r == 2) P.v[0] = 1;                    // identity (0, 1, 1, 0)
-    // software-pipelined: window win's table entry is loaded during window win + 1 (behind its four
-    // doublings), and the digit word two windows ahead
-    int dg = cv_sfield(dig[(size_t)(nw - 1) * stride], field, 5);
-    quad_any_load(q, tab, precomp, dg, r);
-    uint32_t dw_next = dig[(size_t)(nw - 2) * stride];   // nw >= 32
 #pragma unroll 1
     for (int win = nw - 1; win >= 0; win--) {
+        const uint32_t dw = dig[(size_t)win * stride];
         if (win != nw - 1) {
             quad_dbl<SEQ>(P, r);
             quad_dbl<SEQ>(P, r);
             quad_dbl<SEQ>(P, r);
             quad_dbl<SEQ>(P, r);
         }
-        quad_any_fix(q, precomp, dg, r);
+        quad_any_coord(q, tab, precomp, cv_sfield(dw, field, 5), r);
         quad_add<SEQ>(P, q, r);
-        if (win > 0) {
-            dg = cv_sfield(dw_next, field, 5);
-            quad_any_load(q, tab, precomp, dg, r);
-            dw_next = dig[(size_t)(win >= 2 ? win - 2 : 0) * stride];
-        }
     }
     // every quad adds the quad 4 lanes away, then the quad 8 lanes away (row rotations): each quad
     // ends with the sum of all four chains

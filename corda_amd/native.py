@@ -143,8 +143,19 @@ def load():
         return lib
 
 
+_C0 = ctypes.c_char * 0
+
+
 def _p(a: Optional[np.ndarray]):
-    return None if a is None else a.ctypes.data_as(_vp)
+    """The array's data pointer as an int (c_void_p arguments).  Through the buffer protocol: ~0.4 us per
+    pointer against ~3 us for ndarray.ctypes.data_as, which a notary-sized call pays seven times; arrays the
+    buffer protocol refuses (read-only, non-contiguous) take the ctypes attribute."""
+    if a is None:
+        return None
+    try:
+        return ctypes.addressof(_C0.from_buffer(a))
+    except (TypeError, ValueError, BufferError):
+        return a.ctypes.data
 
 
 def _u8(a, shape_last=None) -> np.ndarray:

@@ -77,6 +77,45 @@ __global__ __launch_bounds__(64, 1) void k_points(uint32_t n, const uint8_t *pk,
     cv_points_quad_lane<false>(blockIdx.x * 64 + threadIdx.x, n, pk, sig, tab, tabR, ok, status);
 }
 
+// one lane per signature, the prep's parts back to back with s_memrealtime stamps (100 MHz): SHA-512 + mod L
+// + effective S | lattice (sc_halfsize) | window digit words | decode of A | its odd-multiple table
+__global__ __launch_bounds__(64, 1) void k_clk(uint32_t n, uint32_t cap, const uint8_t *pk, const uint8_t *sig,
+                                               const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                                               uint32_t *dig, uint32_t *tab, uint64_t *stamps) {
+    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= n) return;
+    uint64_t t[6];
+    uint32_t aw[8], rw[8], sw[8], hs[CV_HS_WORDS];
+    load_words8(aw, pk + (size_t)i * 32);
+    load_words8(rw, sig + (size_t)i * 64);
+    load_words8(sw, sig + (size_t)i * 64 + 32);
+    t[0] = __builtin_amdgcn_s_memrealtime();
+    cv_keyed_hs(aw, rw, sw, arena + off[i], len[i], hs);
+    asm volatile("" ::"v"(hs[0]), "v"(hs[15]));
+    t[1] = __builtin_amdgcn_s_memrealtime();
+    uint32_t u[8], v[8], w[8];
+    bool v_neg;
+    int nwin;
+    sc_halfsize(u, v, v_neg, nwin, w, hs, hs + 8);
+    asm volatile("" ::"v"(u[0]), "v"(v[0]), "v"(w[0]));
+    t[2] = __builtin_amdgcn_s_memrealtime();
+#pragma unroll 4
+    for (int win = 0; win < 64; win++) {
+        const int da = -digit16(u, win), dr = v_neg ? -digit16(v, win) : digit16(v, win);
+        const int dlo = win < 32 ? digit16(w, win) : 0, dhi = win < 32 ? digit16(w, 32 + win) : 0;
+        dig[(size_t)win * cap + i] = ((uint32_t)da & 0x1fu) | (((uint32_t)dr & 0x1fu) << 5) |
+                                     (((uint32_t)dlo & 0x1fu) << 10) | (((uint32_t)dhi & 0x1fu) << 15);
+    }
+    t[3] = __builtin_amdgcn_s_memrealtime();
+    ge_p3 P;
+    const bool ok = ge_decode_0_1_0<false>(P, aw);
+    asm volatile("" ::"v"(P.X.v[0]), "v"(P.T.v[9]));
+    t[4] = __builtin_amdgcn_s_memrealtime();
+    ge_cached_multiples8_half(tab + (size_t)i * CV_TAB_WORDS, P, ok);
+    t[5] = __builtin_amdgcn_s_memrealtime();
+    for (int k = 0; k < 5; k++) stamps[(size_t)i * 5 + k] = t[k + 1] - t[k];
+}
+
 template <typename F> static float time_ms(F launch, int reps) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
@@ -155,6 +194,22 @@ int main(int argc, char **argv) {
             cv_hs_straus_tri_kernel<true><<<(16 * n + CV_BLOCK - 1) / CV_BLOCK, CV_BLOCK>>>(n, cap, d_dig, d_tab, d_tabR,
                                                                                          d_ok, d_bm, nullptr);
         }, reps);
+        uint64_t *d_st;
+        CK(hipMalloc(&d_st, 8 * 5 * (size_t)n));
+        k_clk<<<g1, 64>>>(n, cap, d_pk, d_sig, d_msg, d_off, d_len, d_dig, d_tab, d_st);
+        CK(hipDeviceSynchronize());
+        std::vector<uint64_t> st(5 * (size_t)n);
+        CK(hipMemcpy(st.data(), d_st, 8 * st.size(), hipMemcpyDeviceToHost));
+        CK(hipFree(d_st));
+        double part[5];
+        for (int k = 0; k < 5; k++) {
+            std::vector<uint64_t> col(n);
+            for (uint32_t i = 0; i < n; i++) col[i] = st[5 * (size_t)i + k];
+            std::sort(col.begin(), col.end());
+            part[k] = col[n / 2] * 0.01;   // 100 MHz ticks -> us
+        }
+        std::printf("{\"n\": %u, \"lane_us_median\": {\"hash\": %.1f, \"halfsize\": %.1f, \"digits\": %.1f, "
+                    "\"decode\": %.1f, \"table_half\": %.1f}}\n", n, part[0], part[1], part[2], part[3], part[4]);
         std::vector<uint64_t> bm((n + 63) / 64);
         CK(hipMemcpy(bm.data(), d_bm, 8 * bm.size(), hipMemcpyDeviceToHost));
         uint32_t acc = 0;
