@@ -1848,9 +1848,9 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
 
 // Enqueues the pipelined Merkle ids of transactions [t0, t1) on device d into output po: sub-chunks of about
 // merkle_chunk leaves (whole transactions), each staged (direct DMA from pinned arrays, else packed) into a
-// ring block by the copy stream and hashed on slot j % 2's stream (leaf kernel + tree kernel, leaf digests in
-// the slot's workspace); the ids and statuses go to po's device buffer and come back once.  The leaf bytes
-// dominate (C3: 2 GB per 1M transactions), so the call is bound by the copy and the kernels overlap it.
+// ring block by the copy stream and hashed on the copy stream itself behind its copies (leaf kernel + tree
+// kernel, leaf digests in the device's digest buffer); the ids and statuses go to po's device buffer and come
+// back once.  The leaf bytes dominate (C3: 2 GB per 1M transactions), so the call is bound by the copy.
 struct MerkleIn {
     const uint8_t *arena;
     const uint64_t *off;

@@ -888,6 +888,44 @@ __host__ __device__ __forceinline__ void cv_hs_scalars(const uint32_t hs[CV_HS_W
         // select per digit); same-box A/B: throughput scalars 0.88 -> 0.82 ms per 10^6
 #pragma unroll
         for (int win = 0; win < 64; win++) dig[(size_t)win * stride] = window_word(win);
+    } else if constexpr (B16) {
+        // the tri form's lone wave: a rolled loop over the eight 32-bit words (straight-line code for all 64
+        // windows was slower — a lone wave waits on its instruction fetches), eight windows per word with
+        // constant shifts: digit = sign-extended nibble + the bit below it (digit16's recoding); the arrays
+        // shift down one word per iteration so every index is a constant.  ~1.3 k instructions for the 64
+        // words instead of ~6 k with digit16's word selects (in-lane 17.7 us, tools/microbench/lat_parts.hip).
+        uint32_t pu = 0, pv = 0, pl = 0, ph = w[3] >> 31;     // the bit below each array's current word
+        const uint32_t vneg = v_neg ? ~0u : 0u;
+#pragma unroll 1
+        for (int j = 0; j < 8; j++) {
+            const uint32_t xu = u[0], xv = v[0], xl = j < 4 ? w[0] : 0u, xh = j < 4 ? w[4] : 0u;
+#pragma unroll
+            for (int t = 0; t < 8; t++) {
+                auto dgt = [&](uint32_t x, uint32_t prev) -> int {
+                    const int nib = (int)(x << (28 - 4 * t)) >> 28;                    // sign-extended nibble
+                    return nib + (int)(t ? (x >> (4 * t - 1)) & 1u : prev);
+                };
+                const int du = dgt(xu, pu), dv = dgt(xv, pv), dl = dgt(xl, pl), dh = dgt(xh, ph);
+                const uint32_t da = (uint32_t)(-du), dr = ((uint32_t)dv ^ vneg) - vneg;   // -u digit, +-v digit
+                dig[(size_t)(8 * j + t) * stride] = (da & 0x1fu) | ((dr & 0x1fu) << 5) | (((uint32_t)dl & 0x1fu) << 10) |
+                                                    (((uint32_t)dh & 0x1fu) << 15);
+            }
+            pu = xu >> 31;
+            pv = xv >> 31;
+            pl = j < 3 ? xl >> 31 : 0u;                       // w's halves end at window 32: no carry-in past it
+            ph = j < 3 ? xh >> 31 : 0u;
+#pragma unroll
+            for (int k = 0; k < 7; k++) {
+                u[k] = u[k + 1];
+                v[k] = v[k + 1];
+            }
+            u[7] = v[7] = 0;
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                w[k] = w[k + 1];
+                w[4 + k] = w[5 + k];
+            }
+        }
     } else {
         // the tri form's lone-wave prep: the unrolled code was slower (0.089 -> 0.095 ms at 4,096)
 #pragma unroll 4

@@ -213,6 +213,29 @@ void cvh_digits65536(const uint8_t *s, uint32_t *out8) {
     std::memcpy(w, s, 32);
     digits65536_pairs(out8, w);
 }
+// The tri form's window words (cv_hs_scalars<true, false>: rolled constant-shift digit recoding) against the
+// definition — window word = -u digit | (+-v digit) << 5 | w-low digit << 10 | w-high digit << 15 (5 bits
+// each, digit16's recoding, w's halves split at 2^128), plus the window count at word 64.  Returns the
+// number of differing words of the 65.
+int cvh_tri_digit_words_mismatch(const uint8_t *h32, const uint8_t *s32) {
+    uint32_t h[8], s[8], hs[CV_HS_WORDS], dig[65], u[8], v[8], w[8];
+    words_from_bytes(h, h32, 8);
+    words_from_bytes(s, s32, 8);
+    for (int i = 0; i < 8; i++) { hs[i] = h[i]; hs[8 + i] = s[i]; }
+    cv_hs_scalars<true, false>(hs, dig, 1);
+    bool v_neg;
+    int nwin;
+    sc_halfsize(u, v, v_neg, nwin, w, h, s);
+    int bad = dig[64] != (uint32_t)nwin;
+    for (int win = 0; win < 64; win++) {
+        const int da = -digit16(u, win), dr = v_neg ? -digit16(v, win) : digit16(v, win);
+        const int dlo = win < 32 ? digit16(w, win) : 0, dhi = win < 32 ? digit16(w, 32 + win) : 0;
+        const uint32_t want = ((uint32_t)da & 0x1fu) | (((uint32_t)dr & 0x1fu) << 5) | (((uint32_t)dlo & 0x1fu) << 10) |
+                              (((uint32_t)dhi & 0x1fu) << 15);
+        bad += dig[win] != want;
+    }
+    return bad;
+}
 int cvh_digit256(const uint8_t *s, int k) {
     uint32_t w[8];
     words_from_bytes(w, s, 8);
@@ -318,6 +341,7 @@ int cvh_verify_hs_fused(const uint8_t *pk, const uint8_t *sig, const uint8_t *ms
     return ok ? 1 : 0;
 }
 
+static int table_compare(const uint32_t *full, const uint32_t *split);
 // The latency prep's split odd-multiple table (two lanes per point, ge_cached_multiples8_half) against
 // the one-lane table, for the point a 32-byte encoding decodes to (as key: k*(-A); as R: k*R; the
 // identity when it does not decode).  Returns the number of differing words of the 9-entry table.
@@ -329,9 +353,13 @@ int cvh_table_split_mismatch(const uint8_t *enc32, int is_r) {
     const bool ok1 = cv_hs_point_one<false>(w, is_r != 0, full);
     const bool ok2 = cv_hs_point_one<false>(w, is_r != 0, split, 0);
     const bool ok3 = cv_hs_point_one<false>(w, is_r != 0, split, 1);
-    int bad = (ok1 != ok2 || ok1 != ok3) ? 1000 : 0;
-    // the same point in each entry (projective: the split halves reach 4P, 6P, 8P by additions, so
-    // their Z differs from the one-lane doublings'): (Y+X)/Z, (Y-X)/Z, 2dT/Z agree
+    return ((ok1 != ok2 || ok1 != ok3) ? 1000 : 0) + table_compare(full, split);
+}
+
+// the same point in each entry (projective: the split tables reach 4P, 6P, 8P by additions, so their Z
+// differs from the one-lane doublings'): (Y+X)/Z, (Y-X)/Z, 2dT/Z agree, and Z != 0
+static int table_compare(const uint32_t *full, const uint32_t *split) {
+    int bad = 0;
     for (int k = 0; k < 9; k++) {
         ge_cached a, b;
         ge_cached_load(a, full + 40 * k);

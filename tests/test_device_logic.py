@@ -403,6 +403,21 @@ def test_slide_replay_structured(host_harness):
         assert H.cvh_slide_drops(_b(sb)) == int(E.slide_drops_carry(sb)), hex(s)
 
 
+def test_tri_digit_words(host_harness, rcp):
+    """The tri form's 64 window words from the rolled constant-shift recoding equal the digit16 definition
+    (and word 64 the window count) for random (h, s), the degenerate lattices that fall back to (h, 1) with
+    64 windows, and scalars whose nibbles sit at the recoding's edges (all ones, alternating, top bits)."""
+    H = host_harness
+    H.cvh_tri_digit_words_mismatch.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    rng = random.Random(2024)
+    L = 2**252 + 27742317777372353535851937790883648493
+    hs = [0, 1, 2**128, 2**252, L - 1, 2**253 - 1, int("8" * 63, 16) % L, int("7" * 63, 16) % L]
+    hs += [rng.randrange(L) for _ in range(2000)]
+    for i, h in enumerate(hs):
+        s = rng.randrange(L) if i % 3 else (L - 1 - i)
+        assert H.cvh_tri_digit_words_mismatch(h.to_bytes(32, "little"), s.to_bytes(32, "little")) == 0, (hex(h), hex(s))
+
+
 def test_split_odd_multiple_tables(host_harness, corpus):
     """The latency prep's four-lanes-per-signature form builds each point's 9-entry table k*P in two
     halves (entries 0,1,3,5,7 and 2,4,6,8, the same instruction stream on both lanes): every entry of
@@ -416,3 +431,4 @@ def test_split_odd_multiple_tables(host_harness, corpus):
     encs += [(rng.integers(0, 256, 32, dtype=np.uint8).tobytes(), int(k & 1)) for k in range(200)]
     bad = [(e.hex(), r) for e, r in encs if host_harness.cvh_table_split_mismatch(e, r) != 0]
     assert not bad, bad[:5]
+
