@@ -1774,7 +1774,12 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
     const uint8_t *kdev_keys = po.kdev.as<uint8_t>();
     const uint32_t *kdev_slot = keyed ? reinterpret_cast<const uint32_t *>(po.kdev.as<uint8_t>() + al16(nkeys * 32)) : nullptr;
     const size_t ach = std::max(o.async_chunk, std::min(2 * o.async_chunk, n / 16 / 64 * 64));
-    const std::vector<size_t> cut = async ? pipe_cuts(b, e, ach, ach, false) : pipe_cuts(b, e, o.pipe_first, o.pipe_chunk, true);
+    // synchronous calls: about 16 sub-chunks after the ramp, between 2 x pipe_first and pipe_chunk.  A 1M C2 call
+    // (tools/sync_pipe_sweep.py, two rounds on one box): 262,144-record sub-chunks 13.0-13.3 ms, 98,304 12.0,
+    // 65,536 11.6, 49,152 12.9, 32,768 13.3; an 8M C5 call is compute-bound and keeps 262,144 (74 ms).
+    // (keyed calls keep pipe_chunk: each of their sub-chunks carries more fixed work)
+    const size_t sch = keyed ? o.pipe_chunk : std::min(o.pipe_chunk, std::max(2 * o.pipe_first, (n / 16 + 63) / 64 * 64));
+    const std::vector<size_t> cut = async ? pipe_cuts(b, e, ach, ach, false) : pipe_cuts(b, e, o.pipe_first, sch, true);
     size_t max_m = 1;
     for (size_t j = 0; j + 1 < cut.size(); j++) max_m = std::max(max_m, cut[j + 1] - cut[j]);
     for (size_t j = 0; j + 1 < cut.size(); j++) {
