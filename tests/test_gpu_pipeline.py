@@ -74,6 +74,27 @@ def test_host_pipeline_large_exact_pattern(engine, corpus):
     assert int(bitmap[-1]) >> (n % 64) == 0
 
 
+@pytest.mark.parametrize("n", [131_137, 600_001])
+def test_host_pipeline_sync_subchunk_plan_exact(engine, n):
+    """Synchronous calls cut their batch in about n / 16 records per sub-chunk after the ramp (at least 2 x
+    pipe_first, at most pipe_chunk): sizes just above the pipeline threshold and mid-way to a C2 batch, from
+    pinned buffers (direct DMA) and pageable ones (packed), every 13th S corrupted and every 101st R byte:
+    every verdict exact, bits past n clear."""
+    b = workload.make_batch(engine, 0, n, 300, seed=n)
+    expect = workload.corrupt_fraction(b, 13)
+    idx = torch.arange(7, n, 101, device=DEV)
+    b.sig[idx, 5] ^= 0x08
+    expect[idx] = False
+    arrs = b.to_host()
+    del b
+    exp = expect.cpu().numpy()
+    for form, a in (("pageable", arrs), ("pinned", tuple(engine.host_copy(x) for x in arrs))):
+        bitmap, _ = engine.verify_batch(*a, want_status=False)
+        got = _bits(bitmap, n)
+        assert np.array_equal(got, exp), f"{form}: {int((got != exp).sum())} verdicts differ"
+        assert int(bitmap[-1]) >> (n % 64) == 0
+
+
 @pytest.mark.parametrize("first,chunk", [(64, 64 * 17), (64 * 5, 64 * 3), (1024, 4096)])
 def test_host_pipeline_small_subchunks_golden(engine, corpus, first, chunk):
     """The pipeline forced onto tiny sub-chunks (first / steady sizes, so one batch has hundreds of
