@@ -145,33 +145,6 @@ __device__ __forceinline__ void quad_precomp_coord(fe &q, const uint32_t *tab, i
     }
 }
 
-// Quad version of cv_verify_straus: R' = [h](-A) + [s]B; lanes 0..2 return X, Y, Z.
-__device__ __forceinline__ void cv_quad_straus(const uint32_t *btab, const uint32_t *hs, const uint32_t *tab, int r,
-                                               fe &P) {
-    uint32_t h[8], s[8];
-#pragma unroll
-    for (int q = 0; q < 8; q++) { h[q] = hs[q]; s[q] = hs[8 + q]; }
-    fe_zero(P);
-    if (r == 1 || r == 2) P.v[0] = 1;          // identity (0, 1, 1, 0)
-#pragma unroll 1
-    for (int w = 63; w >= 0; w--) {
-        if (w != 63) {
-            quad_dbl(P, r);
-            quad_dbl(P, r);
-            quad_dbl(P, r);
-            quad_dbl(P, r);
-        }
-        fe q;
-        quad_cached_coord(q, tab, digit16(h, w), r);
-        quad_add(P, q, r);
-        if ((w & 1) == 0) {
-            // B table rows: k*B for k = 0..128 (row 0 = identity), stride CV_BTAB_STRIDE
-            quad_precomp_coord(q, btab, CV_BTAB_STRIDE, digit256(s, w >> 1), r, true);
-            quad_add(P, q, r);
-        }
-    }
-}
-
 // Quad version of cv_comb_straus (keyed path, reference schedule): affine key rows (entry k =
 // k * 2^(64 j)(-A), entry 0 the identity), radix-16 digits of h, radix-256 CV_BCOMB rows for s.
 __device__ __forceinline__ void cv_quad_comb(const uint32_t *bcomb, const uint32_t *hs, const uint32_t *ktab, int r,

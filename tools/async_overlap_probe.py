@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--calls", type=int, default=12)
     ap.add_argument("--busy", default="0,1,3,6")
     ap.add_argument("--sleep", type=int, default=0, help="sleep instead of spinning")
+    ap.add_argument("--depth", type=int, default=2, help="calls in flight (the engine keeps up to 4 per device)")
     a = ap.parse_args()
     eng = native.Engine(1)
     b = workload.make_batch(eng, 0, 1_000_000, 300, seed=11, key_pool=a.key_pool or None)
@@ -40,11 +41,11 @@ def main():
                     t1 = time.perf_counter() + busy / 1e3
                     while time.perf_counter() < t1:
                         pass
-            if len(pend) == 2:
+            if len(pend) == a.depth:
                 eng.wait(pend.pop(0))
         for tk in pend:
             eng.wait(tk)
-        print(f"key_pool {a.key_pool} busy {busy} ms{' (sleep)' if a.sleep else ''}: "
+        print(f"key_pool {a.key_pool} depth {a.depth} busy {busy} ms{' (sleep)' if a.sleep else ''}: "
               f"{(time.perf_counter() - t) / a.calls * 1e3:.2f} ms per call", flush=True)
     eng.close()
 

@@ -26,6 +26,7 @@ def main():
                                           "first64k:pipe_first=65536,pipe_chunk=524288 nosplit:drain_split=0")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--pageable", type=int, default=0, help="pageable numpy inputs (host threads pack them)")
     a = ap.parse_args()
     eng = native.Engine(1)
     variants = []
@@ -38,7 +39,7 @@ def main():
     dev = torch.device("cuda", 0)
     bm_d = torch.zeros((a.n + 63) // 64, dtype=torch.int64, device=dev)
     s = torch.cuda.Stream(dev)
-    pinned = [eng.host_copy(x) for x in b.to_host()]
+    pinned = list(b.to_host()) if a.pageable else [eng.host_copy(x) for x in b.to_host()]
     for rnd in range(a.rounds):
         for name, sets in variants:
             for k in used:
@@ -60,7 +61,7 @@ def main():
             s.synchronize()
             dev_ms = (time.perf_counter() - t) / 3 * 1e3
             med = float(np.median(ts) * 1e3)
-            print(json.dumps({"n": a.n, "msg": a.msg, "round": rnd, "setting": name, "sync_pinned_ms": round(med, 3),
+            print(json.dumps({"n": a.n, "msg": a.msg, "pageable": a.pageable, "round": rnd, "setting": name, "sync_pinned_ms": round(med, 3),
                               "device_ms": round(dev_ms, 3), "ratio": round(dev_ms / med, 4)}), flush=True)
     eng.close()
 
