@@ -748,10 +748,10 @@ def main():
     # Steps are independent batches (a node's concurrent verify calls): step k goes on streams[k % S],
     # each stream with its own bitmap; the engine gives each stream its own workspace slot, so step k+1's
     # prep runs while step k's last Straus round drains.  Every step is a full verify of all n signatures.
-    # (round 3: with HIP's default four hardware queues one vs two streams flipped from box to box with
-    # the queues the streams landed on, profiles/r03n_stream_ab.log, r03o_stream_ab_q4.log; with eight
-    # (set above) two streams won on every run, 8.86-9.04 vs 9.18-9.23 ms per call on one box,
-    # profiles/r03p_bench_q8_streams.log.  The other form is reported beside the value.)
+    # (round 3: with HIP's default four hardware queues one vs two streams flipped from box to box with the
+    # queues the streams landed on, profiles/r03n_stream_ab.log, r03o_stream_ab_q4.log; round 4: two streams
+    # at four vs eight queues within 2 %, profiles/r04_queue_ab.log, so the bench keeps HIP's default and
+    # records it.  The other form is reported beside the value.)
     streams = [stream] + [torch.cuda.Stream(dev) for _ in range(max(2, args.streams) - 1)]
     nstreams = max(1, args.streams)
     bitmaps = [torch.zeros(words, dtype=torch.int64, device=dev) for _ in streams]
