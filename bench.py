@@ -252,6 +252,83 @@ def host_c3_rate(eng, local, sh, ntx: int, steps: int, device_value: float, pcie
                     "+ cv_tx_verdicts and the id check, pinned host buffers, Merkle k+1 submitted behind verify k"}
 
 
+def host_c3_fused_rate(eng, local, sh, ntx: int, steps: int, device_value: float, pcie_gbs: float, sync: bool = False):
+    """C3 through the fused drop-in entry point (cv_verify_transactions_async: SignedTransaction.verifySignatures'
+    id + signature checks for the batch in one call): per step the leaves, keys and signatures of 1M transactions
+    from pinned host buffers; the ids stay on the device as the verify's messages; per transaction tx_ok AND id ==
+    claimed.  Two calls in flight (a node's loop submits batch k+1 before it takes the verdicts of batch k).
+    sync: the synchronous call, one step at a time."""
+    signers = 8
+    tb = workload.make_tx_batch(eng, local, ntx, signers, seed=20261016, stream=sh)
+    n = ntx * signers
+    pin = lambda t: eng.host_copy(t.cpu().numpy())  # noqa: E731
+    arena, leaf_off = pin(tb.leaf_arena), eng.host_copy(tb.leaf_off.cpu().numpy().astype(np.uint64))
+    leaf_len, tx_begin = eng.host_copy(tb.leaf_len.cpu().numpy().astype(np.uint32)), \
+        eng.host_copy(tb.tx_begin.cpu().numpy().astype(np.uint32))
+    claimed = tb.ids.cpu().numpy().view(np.uint64).reshape(ntx, 4)
+    pk, sig = pin(tb.sigs.pk), pin(tb.sigs.sig)
+    leaf_bytes = int(tb.leaf_len.to(torch.int64).sum())
+    del tb
+    torch.cuda.empty_cache()
+    sig_begin = eng.host_copy(np.arange(0, n + 1, signers, dtype=np.uint32))
+    bufs = [eng.host_empty((ntx, 32)) for _ in range(3)]
+    args = (arena, leaf_off, leaf_len, tx_begin, pk, sig, sig_begin)
+    blocked = {"wait_ms": 0.0}
+
+    fails = []
+
+    def check(ok, ids):
+        idok = (ids.view(np.uint64).reshape(ntx, 4) == claimed).all(axis=1)
+        good = bool(ok.all() and idok.all())
+        if not good:
+            bad = np.nonzero(ok == 0)[0]
+            # the same host arrays through the separate verify over the claimed ids: bad inputs or a bad call?
+            bm, _ = eng.verify_batch(pk, sig, np.concatenate([claimed.view(np.uint8).reshape(-1), np.zeros(16, np.uint8)]),
+                                     (np.arange(n, dtype=np.uint64) // signers) * 32, np.full(n, 32, np.uint32),
+                                     want_status=False)
+            sep = np.nonzero(~native.bitmap_to_bools(bm, n))[0]
+            fails.append({"rejected": int(bad.size), "ids_wrong": int((~idok).sum()), "first": bad[:8].tolist(),
+                          "last": bad[-3:].tolist(), "separate_bad_sigs": int(sep.size), "separate_first": sep[:4].tolist(),
+                          "separate_last": sep[-3:].tolist()})
+        return good
+
+    def run(k_steps):
+        ok_all = True
+        if sync:
+            for k in range(k_steps):
+                ok, ids, _, _ = eng.verify_transactions(*args, ids=bufs[k % 3], want_status=False)
+                ok_all &= check(ok, ids)
+            return ok_all
+        prev = None
+        for k in range(k_steps):
+            t = eng.verify_transactions_async(*args, ids=bufs[k % 3], want_status=False)
+            if prev is not None:
+                t0 = time.perf_counter()
+                ok, rest = eng.wait(prev)
+                blocked["wait_ms"] += (time.perf_counter() - t0) * 1e3
+                ok_all &= check(ok, rest[0])
+            prev = t
+        ok, rest = eng.wait(prev)
+        return ok_all & check(ok, rest[0])
+
+    assert run(2), f"fused C3 step rejected an honest transaction: {fails}"   # warm: staging / device blocks
+    blocked["wait_ms"] = 0.0
+    t = time.perf_counter()
+    ok = run(steps)
+    dt = time.perf_counter() - t
+    assert ok, f"fused C3 step rejected an honest transaction: {fails}"
+    in_bytes = leaf_bytes + ntx * 6 * 12 + 2 * (ntx + 1) * 4 + n * (32 + 64)
+    v = n * steps / dt
+    return {"value": v, "unit": "verifies/s", "tx_ids_per_s": ntx * steps / dt, "ms_per_step": dt / steps * 1e3,
+            "steps": steps, "ratio_to_device_value": v / device_value, "device_value": device_value,
+            "input_bytes_per_step": in_bytes, "pcie_floor_ms_per_step": in_bytes / (pcie_gbs * 1e9) * 1e3,
+            "host_blocked_ms_per_step": {k: v / steps for k, v in blocked.items()},
+            "path": ("cv_verify_transactions (synchronous)" if sync else
+                     "cv_verify_transactions_async, two in flight") +
+                    ": leaves + keys + signatures from pinned host buffers, ids kept on the device as the messages, "
+                    "tx_ok AND id == claimed"}
+
+
 def host_keyed_rate(eng, local, sh, n: int, msg_len: int, steps: int, device_value: float, pcie_gbs: float):
     """The keyed path through host buffers: C2 with a 1,024-key pool handed to
     cv_ed25519_verify_batch(_async) as plain records — the engine dedupes the keys itself (host threads,
@@ -854,6 +931,7 @@ def main():
             D_["c3"] = c3_line(eng, local, rank, world, sh, dev, 1_000_000, 3, 1, mad_rate)
             if not args.no_host:
                 D_["host_api"]["c3"] = host_c3_rate(eng, local, sh, 1_000_000, 4, D_["c3"]["value"], pcie)
+                D_["host_api"]["c3_fused"] = host_c3_fused_rate(eng, local, sh, 1_000_000, 4, D_["c3"]["value"], pcie)
             D_["c5_shard"] = c5_line(eng, local, rank, sh, dev, 8_000_000, 3, mad_rate, host_api=not args.no_host)
             if D_["c5_shard"].get("host_api") and "host_api" in D_:
                 D_["host_api"]["c5"] = D_["c5_shard"].pop("host_api")
@@ -905,7 +983,7 @@ def main():
         if "host_api" in D_:
             H = D_["host_api"]
             h = {"pcie_h2d_gb_per_s": r3(pcie)}
-            for k in ("c2", "c5", "c3", "keyed"):
+            for k in ("c2", "c5", "c3", "c3_fused", "keyed"):
                 if k in H:
                     h[k] = {"value": r3(H[k]["value"]), "ratio": r3(H[k]["ratio_to_device_value"]),
                             "ms_per_step": r3(H[k]["ms_per_step"])}

@@ -179,12 +179,13 @@ struct PipeOut {
         void *dst;
         size_t off, len;
     };
-    Seg seg[2] = {};
+    Seg seg[4] = {};
     int nseg = 0;
     // keyed calls: the call's distinct keys and their pool slots on the device (kdev: keys | slot_of_key,
     // uploaded through kstage), the auto path's key_index (pinned, DMAed per sub-chunk)
     DevBuf kdev;
     PinBuf kstage, kidx;
+    PinBuf tstage;   // transaction calls: the shard's signature boundaries when the caller's are pageable
 };
 
 // A fixed set of host threads for index-parallel jobs (the host-buffer path's packing, range scans and key
@@ -337,6 +338,8 @@ struct Device {
     hipEvent_t stage_ev[kStage] = {};
     bool stage_busy[kStage] = {};
     int stage_next = 0;
+    // transaction calls: after each Merkle launch group (the signature groups wait for it), + one join event
+    std::vector<hipEvent_t> mev;
     WorkerPool &workers(int threads) {
         if (!pool || pool->threads() != threads) {
             pool.reset();
@@ -760,6 +763,7 @@ void cv_close(cv_ctx *ctx) {
             o.kdev.release();
             o.kstage.release();
             o.kidx.release();
+            o.tstage.release();
             for (hipEvent_t v : o.slot_done)
                 if (v) (void)hipEventDestroy(v);
         }
@@ -773,6 +777,8 @@ void cv_close(cv_ctx *ctx) {
             d.instage[k].release();
             if (d.stage_ev[k]) (void)hipEventDestroy(d.stage_ev[k]);
         }
+        for (hipEvent_t v : d.mev) (void)hipEventDestroy(v);
+        d.mev.clear();
         if (d.copy) (void)hipStreamDestroy(d.copy);
         d.kc.pin.release();
         for (hipEvent_t v : {d.kc.ev, d.kc.pin_ev, d.kc.wev})
@@ -2033,6 +2039,211 @@ static int merkle_shard_small(Device &d, const MStage &st, const MerkleIn &in, W
     return CV_OK;
 }
 
+// ---------------------------------------------------------------- transactions (verifySignatures)
+// The fused form of SignedTransaction.verifySignatures over a batch: each transaction's id (WireTransaction.id)
+// and whether every one of its signatures verifies over that id.  The ids are computed into the output's device
+// buffer and read there as the signatures' messages: no id round trip through the host and no message upload,
+// so a verify never waits for the host to hand it the ids of a Merkle call (the separate calls left the verify
+// kernels idle ~6 ms per C3 step, DESIGN.md "Next" item 5).
+//
+// One shard = transactions [t0, t1) and their signatures [s0, s1) on device d.  Sub-chunks of whole transactions
+// (about merkle_chunk leaves, ramped: a quarter, a half, then full) and of signatures (multiples of 64 from s0,
+// sized as pipe_enqueue's) share the input ring and the copy stream; the launch groups alternate over the two
+// compute streams.  A Merkle group (leaf + tree kernels on the slot's digest workspace) records mev[J]; the
+// signature groups it makes available — those whose transactions all lie in sub-chunks 0..J — follow it, each
+// waiting for its own copy and for the mev of every Merkle group its transactions lie in (a group may start
+// inside sub-chunk J - 1, whose kernels can still be queued on the other stream), then writing its message
+// references (cvk_tx_sig_refs: id offsets within the shard) and verifying.  Last, the per-transaction verdicts (cvk_tx_verdicts) on the stream of the
+// last group, after the other stream's last group.
+// dout: ids | Merkle status | tx_ok | signature status | verdict bitmap | message offsets | lengths | boundaries
+struct TxIn {
+    MerkleIn m;             // the leaves; m.ids and m.status may be null
+    const uint8_t *pk, *sig;
+    const uint32_t *tsb;    // ntx + 1 signature boundaries
+    uint8_t *sig_status;    // may be null
+    uint8_t *tx_ok;
+};
+static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_t t0, size_t t1, const TxIn &in,
+                       int threads, bool async) {
+    const MerkleIn &mi = in.m;
+    const size_t nt = t1 - t0, s0 = in.tsb[t0], s1 = in.tsb[t1], ns = s1 - s0;
+    const size_t words = (ns + 63) / 64;
+    const size_t o_mst = al16(nt * 32), o_ok = o_mst + al16(nt), o_sst = o_ok + al16(nt);
+    const size_t o_bm = o_sst + (in.sig_status ? al16(ns) : 0), o_off = o_bm + al16(words * 8);
+    const size_t o_len = o_off + al16(ns * 8), o_tsb = o_len + al16(ns * 4), total_out = o_tsb + al16((nt + 1) * 4);
+    PipeFrame f{d, po};
+    CV_TRY(hipSetDevice(d.ordinal));
+    int rc = f.init();
+    if (rc != CV_OK) return rc;
+    CV_TRY(po.dout.ensure(total_out));
+    uint8_t *dout = po.dout.as<uint8_t>();
+    const uint32_t *dtsb = reinterpret_cast<const uint32_t *>(dout + o_tsb);
+    uint64_t *doff = reinterpret_cast<uint64_t *>(dout + o_off);
+    uint32_t *dlen = reinterpret_cast<uint32_t *>(dout + o_len);
+    uint64_t *dbm = reinterpret_cast<uint64_t *>(dout + o_bm);
+    auto drain = on_exit([&f] { f.drain(); });
+    WorkerPool *pool = &d.workers(threads);
+    // the shard's signature boundaries go first on the copy stream, so every group's copy event covers them
+    {
+        const double ta = now_s();
+        const uint32_t *src = in.tsb + t0;
+        if (!host_pinned(src, (nt + 1) * 4)) {   // (po was finished by pipe_out: no DMA still reads tstage)
+            CV_TRY(po.tstage.ensure((nt + 1) * 4));
+            std::memcpy(po.tstage.p, src, (nt + 1) * 4);
+            src = po.tstage.as<uint32_t>();
+        }
+        CV_TRY(hipMemcpyAsync(dout + o_tsb, src, (nt + 1) * 4, hipMemcpyHostToDevice, d.copy));
+        f.t[0] += now_s() - ta;
+    }
+    // Merkle sub-chunks: whole transactions, ramped up to `per` leaves (at least one transaction each)
+    const size_t nl_all = mi.txb[t1] - mi.txb[t0];
+    const size_t per = std::max<size_t>(o.merkle_chunk, (nl_all + 11) / 12);
+    std::vector<size_t> mcut{t0};
+    for (size_t want = std::max<size_t>(1, per / 4); mcut.back() < t1; want = std::min(per, 2 * want)) {
+        const size_t c = mcut.back();
+        const uint64_t target = (uint64_t)mi.txb[c] + want;
+        size_t nx = (size_t)(std::upper_bound(mi.txb + c + 1, mi.txb + t1 + 1,
+                                              (uint32_t)std::min<uint64_t>(target, UINT32_MAX)) - mi.txb) - 1;
+        mcut.push_back(std::min(std::max(nx, c + 1), t1));
+    }
+    const size_t nm = mcut.size() - 1;
+    size_t max_nl = 0;
+    for (size_t j = 0; j < nm; j++) max_nl = std::max<size_t>(max_nl, mi.txb[mcut[j + 1]] - mi.txb[mcut[j]]);
+    for (int k = 0; k < kPipeSlots; k++) {   // the two slots' leaf-digest workspaces
+        Slot &sl = d.slot[k];
+        if (max_nl * 32 + 32 > sl.mdig.cap) {
+            if (sl.last && sl.ev) CV_TRY(hipEventSynchronize(sl.ev));
+            CV_TRY(hipStreamSynchronize(f.ss[k]));
+            CV_TRY(sl.mdig.ensure(max_nl * 32 + 32));
+        }
+    }
+    while (d.mev.size() < nm + 1) {
+        hipEvent_t v = nullptr;
+        CV_TRY(hipEventCreateWithFlags(&v, hipEventDisableTiming));
+        d.mev.push_back(v);
+    }
+    // signature sub-chunks: as pipe_enqueue's plan for ns records; at least vmin unless the shard ends there
+    const size_t vch = async ? std::max(o.async_chunk, std::min(2 * o.async_chunk, ns / 16 / 64 * 64))
+                             : std::min(o.pipe_chunk, std::max(2 * o.pipe_first, (ns / 16 + 63) / 64 * 64));
+    const size_t vmin = std::min(vch, std::max<size_t>(o.pipe_first, 4096));
+    int g = 0;           // launch groups so far (group g runs on compute stream g % 2)
+    size_t p = s0;       // the next signature to stage
+    for (size_t J = 0; J < nm; J++) {
+        // ---- Merkle group J
+        double ta = now_s();
+        const MStage st = mstage_plan(mcut[J], mcut[J + 1], mi.txb, mi.off, mi.len, pool);
+        const bool direct = mstage_direct(st, mi.txb, mi.arena, mi.off, mi.len);
+        double tb = now_s();
+        f.t[0] += tb - ta;
+        int q;
+        uint8_t *dv;
+        if ((rc = f.block(&q, st.total, &dv)) != CV_OK) return rc;
+        if (direct) {
+            ta = now_s();
+            f.t[2] += ta - tb;
+            CV_TRY(mstage_dma_direct(st, dv, mi.txb, mi.arena, mi.off, mi.len, d.copy));
+            f.direct++;
+        } else {
+            uint8_t *h;
+            int sk;
+            if ((rc = f.staging(&sk, st.total, &h)) != CV_OK) return rc;
+            ta = now_s();
+            f.t[2] += ta - tb;
+            mstage_pack(st, h, mi.txb, mi.arena, mi.off, mi.len, pool);
+            tb = now_s();
+            f.t[1] += tb - ta;
+            ta = tb;
+            CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, d.copy));
+            if ((rc = f.staged(sk)) != CV_OK) return rc;
+        }
+        if ((rc = f.copied(q, g)) != CV_OK) return rc;
+        {
+            Slot &sl = d.slot[g % kPipeSlots];
+            hipStream_t s = f.ss[g % kPipeSlots];
+            CV_TRY(ws_begin(d, sl, s));
+            const hipError_t ek = cvk_merkle((uint32_t)(st.t1 - st.t0), (uint32_t)(st.l1 - st.l0), (uint32_t)st.l0,
+                                             dv + st.o_ar - st.lo, reinterpret_cast<const uint64_t *>(dv + st.o_off),
+                                             reinterpret_cast<const uint32_t *>(dv + st.o_len),
+                                             reinterpret_cast<const uint32_t *>(dv + st.o_txb), sl.mdig.as<uint32_t>(),
+                                             dout + (st.t0 - t0) * 32, dout + o_mst + (st.t0 - t0), s);
+            const hipError_t e2 = ws_end(sl, s);
+            CV_TRY(ek);
+            CV_TRY(e2);
+            CV_TRY(hipEventRecord(d.mev[J], s));
+        }
+        if ((rc = f.launched(q, g++)) != CV_OK) return rc;
+        f.t[3] += now_s() - ta;
+        // ---- the signature groups whose transactions' ids are now all enqueued
+        const bool last = J + 1 == nm;
+        const size_t avail = last ? s1 : s0 + (in.tsb[mcut[J + 1]] - s0) / 64 * 64;
+        while (p < avail) {
+            const size_t m = std::min(vch, avail - p);
+            if (!last && m < vmin) break;
+            ta = now_s();
+            const size_t o_sig = al16(m * 32), bytes = o_sig + al16(m * 64);
+            if ((rc = f.block(&q, bytes, &dv, al16(vch * 32) + al16(vch * 64))) != CV_OK) return rc;
+            if (host_pinned(in.pk + p * 32, m * 32) && host_pinned(in.sig + p * 64, m * 64)) {
+                tb = now_s();
+                f.t[2] += tb - ta;
+                CV_TRY(hipMemcpyAsync(dv, in.pk + p * 32, m * 32, hipMemcpyHostToDevice, d.copy));
+                CV_TRY(hipMemcpyAsync(dv + o_sig, in.sig + p * 64, m * 64, hipMemcpyHostToDevice, d.copy));
+                f.direct++;
+            } else {
+                uint8_t *h;
+                int sk;
+                if ((rc = f.staging(&sk, bytes, &h)) != CV_OK) return rc;
+                tb = now_s();
+                f.t[2] += tb - ta;
+                par_copy({{h, in.pk + p * 32, m * 32}, {h + o_sig, in.sig + p * 64, m * 64}}, pool);
+                ta = now_s();
+                f.t[1] += ta - tb;
+                tb = ta;
+                CV_TRY(hipMemcpyAsync(dv, h, bytes, hipMemcpyHostToDevice, d.copy));
+                if ((rc = f.staged(sk)) != CV_OK) return rc;
+            }
+            if ((rc = f.copied(q, g)) != CV_OK) return rc;
+            Slot &sl = d.slot[g % kPipeSlots];
+            hipStream_t s = f.ss[g % kPipeSlots];
+            // every Merkle group holding one of its transactions: the first one's (the largest t with tsb[t] <= p)
+            // through J — a group on the other stream may not have run yet
+            const size_t tf = (size_t)(std::upper_bound(in.tsb + t0, in.tsb + t1 + 1, (uint32_t)p) - in.tsb) - 1;
+            const size_t jf = (size_t)(std::upper_bound(mcut.begin(), mcut.end(), tf) - mcut.begin()) - 1;
+            for (size_t j = jf; j <= J; j++) CV_TRY(hipStreamWaitEvent(s, d.mev[j], 0));
+            const size_t c0 = p - s0;
+            CV_TRY(cvk_tx_sig_refs((uint32_t)m, (uint32_t)c0, (uint32_t)nt, (uint32_t)s0, dtsb, doff, dlen, s));
+            CV_TRY(launch_verify(d, o.plan, sl, (uint32_t)m, dv, dv + o_sig, dout, doff + c0, dlen + c0, dbm + c0 / 64,
+                                 in.sig_status ? dout + o_sst + c0 : nullptr, s, nullptr, false));
+            if ((rc = f.launched(q, g++)) != CV_OK) return rc;
+            f.t[3] += now_s() - tb;
+            p += m;
+        }
+    }
+    // ---- per-transaction verdicts, behind both streams' last groups
+    {
+        const int kl = (g - 1) % kPipeSlots;
+        hipStream_t s = f.ss[kl];
+        for (int k = 0; k < kPipeSlots; k++)
+            if (k != kl && f.used[k]) {
+                CV_TRY(hipEventRecord(d.mev[nm], f.ss[k]));
+                CV_TRY(hipStreamWaitEvent(s, d.mev[nm], 0));
+            }
+        CV_TRY(cvk_tx_verdicts((uint32_t)nt, (uint32_t)s0, dtsb, dout + o_mst, dbm, dout + o_ok, s));
+    }
+    if ((rc = f.complete()) != CV_OK) return rc;
+    drain.armed = false;
+    po.nseg = 0;
+    po.seg[po.nseg++] = {in.tx_ok + t0, o_ok, nt};
+    if (mi.ids) po.seg[po.nseg++] = {mi.ids + t0 * 32, 0, nt * 32};
+    if (mi.status) po.seg[po.nseg++] = {mi.status + t0, o_mst, nt};
+    if (in.sig_status && ns) po.seg[po.nseg++] = {in.sig_status + s0, o_sst, ns};
+    f.account(ctx);
+    {
+        std::lock_guard<std::mutex> g2(ctx->st_mu);
+        ctx->stats.merkle_chunks += nm;
+    }
+    return CV_OK;
+}
+
 // A pipelined call's part on one device, for its ticket: (device index, output index, gen).
 using Part = std::array<uint64_t, 3>;
 
@@ -2391,6 +2602,78 @@ int cv_merkle_tx_ids_async(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, c
 int cv_merkle_tx_ids(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
                      const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, uint8_t *ids) {
     return merkle_call(ctx, ntx, leaf_arena, leaf_off, leaf_len, tx_leaf_begin, ids, nullptr, nullptr);
+}
+
+static int txs_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
+                    const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, const uint8_t *pk, const uint8_t *sig,
+                    const uint32_t *tx_sig_begin, uint8_t *ids, uint8_t *tx_status, uint8_t *sig_status, uint8_t *tx_ok,
+                    uint64_t *ticket) {
+    if (!ctx) return CV_E_ARGS;
+    if (ticket) *ticket = 0;
+    if (ntx == 0) return CV_OK;
+    if (!tx_leaf_begin || !tx_sig_begin || !tx_ok) return CV_E_ARGS;
+    if (tx_leaf_begin[0] != 0 || tx_sig_begin[0] != 0) return CV_E_ARGS;
+    for (size_t t = 0; t < ntx; t++)
+        if (tx_leaf_begin[t + 1] < tx_leaf_begin[t] || tx_sig_begin[t + 1] < tx_sig_begin[t]) return CV_E_ARGS;
+    const size_t nleaves = tx_leaf_begin[ntx], nsig = tx_sig_begin[ntx];
+    if (nleaves && (!leaf_off || !leaf_len)) return CV_E_ARGS;
+    if (nsig && (!pk || !sig)) return CV_E_ARGS;
+    if (ntx > 0xfffffffeull) return CV_E_TOO_LARGE;
+    Opts o = ctx->opts();
+    // shards of whole transactions, scaled as merkle_call's (~4,096 signatures' worth at C3's 8 per transaction)
+    o.shard_min = std::max<size_t>(1, o.shard_min / 8);
+    o.spread_min = std::max<size_t>(1, o.spread_min / 8);
+    TxIn in{{leaf_arena, leaf_off, leaf_len, tx_leaf_begin, ids, tx_status}, pk, sig, tx_sig_begin, sig_status, tx_ok};
+    {
+        std::lock_guard<std::mutex> g(ctx->st_mu);
+        ctx->stats.merkle_calls++;
+    }
+    std::vector<Part> parts(ctx->devs.size(), Part{UINT64_MAX, 0, 0});
+    const int rc = dispatch(ctx, o, ntx, 1, [&](Device &d, size_t t0, size_t t1, int threads) {
+        if (t1 <= t0) return CV_OK;
+        CV_TRY(hipSetDevice(d.ordinal));
+        int k = 0, r = CV_OK;
+        std::unique_lock<std::mutex> lk;
+        PipeOut &po = pipe_out(d, &k, lk, &r);
+        if (r != CV_OK) return r;
+        r = txs_enqueue(ctx, d, o, po, t0, t1, in, threads, ticket != nullptr);
+        if (r != CV_OK) return r;
+        if (ticket) {
+            parts[dev_index(ctx, d)] = {(uint64_t)dev_index(ctx, d), (uint64_t)k, po.gen};
+            return CV_OK;
+        }
+        const double ts = now_s();
+        r = pipe_finish(d, po);
+        std::lock_guard<std::mutex> g(ctx->st_mu);
+        ctx->stats.pipe[4] += now_s() - ts;
+        return r;
+    });
+    std::vector<Part> live;
+    for (const Part &p : parts)
+        if (p[0] != UINT64_MAX) live.push_back(p);
+    if (rc != CV_OK) {
+        (void)parts_wait(ctx, live);
+        return rc;
+    }
+    if (ticket) *ticket = live.empty() ? 0 : ticket_add(ctx, std::move(live));
+    return CV_OK;
+}
+
+int cv_verify_transactions(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
+                           const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, const uint8_t *pk, const uint8_t *sig,
+                           const uint32_t *tx_sig_begin, uint8_t *ids, uint8_t *tx_status, uint8_t *sig_status,
+                           uint8_t *tx_ok) {
+    return txs_call(ctx, ntx, leaf_arena, leaf_off, leaf_len, tx_leaf_begin, pk, sig, tx_sig_begin, ids, tx_status,
+                    sig_status, tx_ok, nullptr);
+}
+
+int cv_verify_transactions_async(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
+                                 const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, const uint8_t *pk,
+                                 const uint8_t *sig, const uint32_t *tx_sig_begin, uint8_t *ids, uint8_t *tx_status,
+                                 uint8_t *sig_status, uint8_t *tx_ok, uint64_t *ticket) {
+    if (!ticket) return CV_E_ARGS;
+    return txs_call(ctx, ntx, leaf_arena, leaf_off, leaf_len, tx_leaf_begin, pk, sig, tx_sig_begin, ids, tx_status,
+                    sig_status, tx_ok, ticket);
 }
 
 int cv_partial_merkle_verify(cv_ctx *ctx, size_t ntrees, size_t nnodes, const uint8_t *kind, const uint32_t *left,

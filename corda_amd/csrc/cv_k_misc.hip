@@ -113,6 +113,45 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_merkle_tree_kernel(uint32_t ntx, 
     if (status) status[gid] = ok ? 0 : 1;
 }
 
+// ---------------------------------------------------------------- transactions (cv_verify_transactions)
+// Message references of signatures [c0, c0 + m) of a shard whose transactions' ids sit back to back on the
+// device: signature s0 + c0 + i belongs to the transaction t with tsb[t] <= s0 + c0 + i < tsb[t + 1] (the
+// largest such t, so empty transactions are passed over), and its message is that id, 32 bytes at t * 32.
+// tsb: the shard's nt + 1 absolute signature boundaries (tsb[0] = s0).
+__global__ __launch_bounds__(CV_BLOCK) void cv_tx_sig_refs_kernel(uint32_t m, uint32_t c0, uint32_t nt, uint32_t s0,
+                                                                  const uint32_t *__restrict__ tsb,
+                                                                  uint64_t *__restrict__ off, uint32_t *__restrict__ len) {
+    const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t g = s0 + c0 + i;
+    uint32_t lo = 0, hi = nt;   // tsb[lo] <= g < tsb[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (tsb[mid] <= g) lo = mid;
+        else hi = mid;
+    }
+    off[c0 + i] = (uint64_t)lo * 32;
+    len[c0 + i] = 32;
+}
+
+// verifySignatures' verdict per transaction: its id was computed (at least one leaf) and it has at least one
+// signature, all valid.  bitmap: the shard's verdicts, bit j = signature s0 + j.
+__global__ __launch_bounds__(CV_BLOCK) void cv_tx_verdict_kernel(uint32_t nt, uint32_t s0, const uint32_t *__restrict__ tsb,
+                                                                 const uint8_t *__restrict__ mstatus,
+                                                                 const uint64_t *__restrict__ bitmap,
+                                                                 uint8_t *__restrict__ tx_ok) {
+    const uint32_t t = blockIdx.x * CV_BLOCK + threadIdx.x;
+    if (t >= nt) return;
+    const uint32_t b = tsb[t] - s0, e = tsb[t + 1] - s0;
+    bool ok = mstatus[t] == 0 && e > b;
+    for (uint32_t w = b >> 6; ok && w <= (e - 1) >> 6; w++) {
+        const uint32_t lo = w == (b >> 6) ? (b & 63) : 0, hi = w == ((e - 1) >> 6) ? ((e - 1) & 63) : 63;
+        const uint64_t mask = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & ~((1ull << lo) - 1);
+        ok = (bitmap[w] & mask) == mask;
+    }
+    tx_ok[t] = ok ? 1 : 0;
+}
+
 // ---------------------------------------------------------------- partial Merkle trees (f3)
 // one lane per tree (FilteredTransaction.verify / PartialMerkleTree.verify, cv_verify.h)
 __global__ __launch_bounds__(CV_BLOCK) void cv_pmt_verify_kernel(uint32_t ntrees, const uint8_t *__restrict__ kind,

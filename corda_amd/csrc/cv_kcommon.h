@@ -140,6 +140,8 @@ __global__ void cv_sign_kernel( uint32_t n, const uint8_t *seed, const uint8_t *
 #define CV_LEAF_BLOCK 256
 __global__ void cv_leaf_hash_pair_kernel(uint32_t nleaves, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *leaf_digest);
 __global__ void cv_merkle_tree_kernel(uint32_t ntx, uint32_t leaf_base, const uint32_t *tx_begin, uint32_t *leaf_digest, uint8_t *ids, uint8_t *status);
+__global__ void cv_tx_sig_refs_kernel(uint32_t m, uint32_t c0, uint32_t nt, uint32_t s0, const uint32_t *tsb, uint64_t *off, uint32_t *len);
+__global__ void cv_tx_verdict_kernel(uint32_t nt, uint32_t s0, const uint32_t *tsb, const uint8_t *mstatus, const uint64_t *bitmap, uint8_t *tx_ok);
 __global__ void cv_pmt_verify_kernel(uint32_t ntrees, const uint8_t *kind, const uint32_t *left, const uint32_t *right, const uint8_t *leaf_hash, const uint32_t *tree_begin, const uint8_t *root, const uint8_t *check, const uint32_t *check_begin, uint32_t *dig, uint8_t *flag, uint8_t *verdict, uint8_t *status);
 __global__ void cv_mad_bench_kernel(uint32_t iters, uint64_t *out);
 __global__ void cv_femul_bench_kernel(uint32_t iters, int32_t *out);

@@ -286,6 +286,22 @@ hipError_t cvk_merkle(uint32_t ntx, uint32_t nleaves, uint32_t leaf_base, const 
     return hipGetLastError();
 }
 
+hipError_t cvk_tx_sig_refs(uint32_t m, uint32_t c0, uint32_t nt, uint32_t s0, const uint32_t *tsb, uint64_t *off,
+                           uint32_t *len, hipStream_t stream) {
+    if (m == 0) return hipSuccess;
+    hipLaunchKernelGGL(cv_tx_sig_refs_kernel, dim3((m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, stream, m, c0, nt,
+                       s0, tsb, off, len);
+    return hipGetLastError();
+}
+
+hipError_t cvk_tx_verdicts(uint32_t nt, uint32_t s0, const uint32_t *tsb, const uint8_t *mstatus, const uint64_t *bitmap,
+                           uint8_t *tx_ok, hipStream_t stream) {
+    if (nt == 0) return hipSuccess;
+    hipLaunchKernelGGL(cv_tx_verdict_kernel, dim3((nt + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0, stream, nt, s0, tsb,
+                       mstatus, bitmap, tx_ok);
+    return hipGetLastError();
+}
+
 hipError_t cvk_mad_clock(uint32_t iters, uint32_t blocks, uint64_t *out, hipStream_t stream) {
     hipLaunchKernelGGL(cv_mad_clock_kernel, dim3(blocks), dim3(CV_BLOCK), 0, stream, iters, out);
     return hipGetLastError();

@@ -42,6 +42,13 @@ hipError_t cvk_pmt_verify(uint32_t ntrees, const uint8_t *kind, const uint32_t *
 hipError_t cvk_merkle(uint32_t ntx, uint32_t nleaves, uint32_t leaf_base, const uint8_t *arena, const uint64_t *leaf_off,
                       const uint32_t *leaf_len, const uint32_t *tx_begin, uint32_t *leaf_digest, uint8_t *ids,
                       uint8_t *status, hipStream_t stream);
+// cv_verify_transactions: message references (off = 32 x the signature's transaction within the shard, len = 32)
+// of shard-local signatures [c0, c0 + m); per-transaction verdicts from the shard's Merkle statuses and
+// verdict bitmap.  tsb: the shard's nt + 1 absolute signature boundaries, tsb[0] = s0.
+hipError_t cvk_tx_sig_refs(uint32_t m, uint32_t c0, uint32_t nt, uint32_t s0, const uint32_t *tsb, uint64_t *off,
+                           uint32_t *len, hipStream_t stream);
+hipError_t cvk_tx_verdicts(uint32_t nt, uint32_t s0, const uint32_t *tsb, const uint8_t *mstatus, const uint64_t *bitmap,
+                           uint8_t *tx_ok, hipStream_t stream);
 hipError_t cvk_calibrate(uint32_t iters, int which, uint32_t blocks, void *scratch, hipStream_t stream);
 hipError_t cvk_mad_clock(uint32_t iters, uint32_t blocks, uint64_t *out, hipStream_t stream);
 // Does a batch of n take the tri-chain form under this plan, in one chunk of a workspace of ws_cap?

@@ -32,6 +32,7 @@ EXPORTED = (
     "cv_ed25519_verify_device_keyed", "cv_partial_merkle_verify", "cv_calibrate_cycles",
     "cv_diag_dedupe_keys", "cv_host_alloc", "cv_host_free", "cv_ed25519_verify_batch_async", "cv_wait",
     "cv_merkle_tx_ids_async", "cv_set_option", "cv_get_option", "cv_diag_stats",
+    "cv_verify_transactions", "cv_verify_transactions_async",
 )
 
 # cv_set_option names (include/cordaverify.h CV_OPT_*)
@@ -87,6 +88,10 @@ def load():
         lib.cv_merkle_tx_ids_ex.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]
         lib.cv_merkle_tx_ids_async.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(ctypes.c_uint64)]
         lib.cv_merkle_tx_ids_async.restype = ctypes.c_int
+        lib.cv_verify_transactions.argtypes = [_vp, _sz] + [_vp] * 11
+        lib.cv_verify_transactions.restype = ctypes.c_int
+        lib.cv_verify_transactions_async.argtypes = [_vp, _sz] + [_vp] * 11 + [ctypes.POINTER(ctypes.c_uint64)]
+        lib.cv_verify_transactions_async.restype = ctypes.c_int
         lib.cv_set_option.argtypes = [_vp, ctypes.c_int, ctypes.c_int64]
         lib.cv_set_option.restype = ctypes.c_int
         lib.cv_get_option.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
@@ -378,6 +383,49 @@ class Engine:
                "cv_merkle_tx_ids_async")
         with self.mu:
             self._inflight[t.value] = (ids, st, (arena, leaf_off, leaf_len, tx_leaf_begin))
+        return t.value
+
+    def _tx_args(self, arena, leaf_off, leaf_len, tx_leaf_begin, pk, sig, tx_sig_begin, ids, want_status,
+                 want_sig_status):
+        ntx, arena, leaf_off, leaf_len, tx_leaf_begin = self._merkle_args(arena, leaf_off, leaf_len, tx_leaf_begin)
+        tx_sig_begin = np.ascontiguousarray(tx_sig_begin, dtype=np.uint32)
+        if tx_sig_begin.shape[0] != ntx + 1:
+            raise ValueError("tx_sig_begin must have ntx + 1 entries")
+        pk = _u8(pk)
+        sig = _u8(sig)
+        nsig = int(tx_sig_begin[-1]) if ntx > 0 else 0
+        if pk.size < nsig * 32 or sig.size < nsig * 64:
+            raise ValueError("tx_sig_begin reaches past pk / sig")
+        if pk.size == 0:
+            pk, sig = np.zeros(32, np.uint8), np.zeros(64, np.uint8)
+        ntx = max(ntx, 0)
+        ids = np.zeros((ntx, 32), np.uint8) if ids is None else ids
+        st = np.zeros(ntx, np.uint8) if want_status else None
+        sst = np.zeros(nsig, np.uint8) if want_sig_status else None
+        ok = np.zeros(ntx, np.uint8)
+        args = (ntx, _p(arena), _p(leaf_off), _p(leaf_len), _p(tx_leaf_begin), _p(pk), _p(sig), _p(tx_sig_begin),
+                _p(ids), _p(st), _p(sst), _p(ok))
+        return args, (ok, ids, st, sst), (arena, leaf_off, leaf_len, tx_leaf_begin, pk, sig, tx_sig_begin)
+
+    def verify_transactions(self, arena, leaf_off, leaf_len, tx_leaf_begin, pk, sig, tx_sig_begin, ids=None,
+                            want_status: bool = True, want_sig_status: bool = False):
+        """cv_verify_transactions (SignedTransaction.verifySignatures' id + signature checks for a batch) ->
+        (tx_ok u8[ntx], ids (ntx,32) u8, tx_status u8[ntx] or None, sig_status u8[nsig] or None)."""
+        args, out, _keep = self._tx_args(arena, leaf_off, leaf_len, tx_leaf_begin, pk, sig, tx_sig_begin, ids,
+                                         want_status, want_sig_status)
+        _check(self._lib.cv_verify_transactions(self._h, *args), "cv_verify_transactions")
+        return out
+
+    def verify_transactions_async(self, arena, leaf_off, leaf_len, tx_leaf_begin, pk, sig, tx_sig_begin, ids=None,
+                                  want_status: bool = True, want_sig_status: bool = False) -> int:
+        """cv_verify_transactions_async: enqueue and return a ticket; wait(ticket) -> (tx_ok, (ids, tx_status,
+        sig_status))."""
+        args, out, keep = self._tx_args(arena, leaf_off, leaf_len, tx_leaf_begin, pk, sig, tx_sig_begin, ids,
+                                        want_status, want_sig_status)
+        t = ctypes.c_uint64()
+        _check(self._lib.cv_verify_transactions_async(self._h, *args, ctypes.byref(t)), "cv_verify_transactions_async")
+        with self.mu:
+            self._inflight[t.value] = (out[0], out[1:], keep)
         return t.value
 
     # ------------------------------------------------------------ options and diagnostics

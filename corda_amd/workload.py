@@ -154,6 +154,10 @@ def make_tx_batch(engine: native.Engine, device: int, ntx: int, signers: int = 8
     pk = torch.empty((n, 32), dtype=torch.uint8, device=dev)
     sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
     id_arena = torch.cat([ids.reshape(-1), torch.zeros(16, dtype=torch.uint8, device=dev)])
+    # the key seeds and id arena above are written on torch's stream; with stream = 0 the signing runs on the
+    # engine's own stream, which does not wait for them (it read half-written seeds: ~45,000 of 1M transactions
+    # signed with garbage keys when the GPU was busy)
+    torch.cuda.synchronize(dev)
     engine.sign_device(device, n, key_seeds.data_ptr(), id_arena.data_ptr(), off.data_ptr(), ln.data_ptr(),
                        pk.data_ptr(), sig.data_ptr(), stream)
     engine.synchronize(device)

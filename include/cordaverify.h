@@ -23,6 +23,8 @@
  *                                 generate synthetic workloads, not on the validation path)
  *   cv_tx_verdicts            per-transaction AND of signature verdicts (the "all sigs valid" half of
  *                                 SignedTransaction.verifySignatures, SignedTransaction.kt:58-72)
+ *   cv_verify_transactions    N x  SignedTransaction.verifySignatures' id + signature checks in one call
+ *                                 (SignedTransaction.kt:59-71, 83-87; WireTransaction.kt:45-52)
  *   cv_partial_merkle_verify  N x  PartialMerkleTree.verify(merkleRootHash, hashesToCheck)
  *                                 core/src/main/kotlin/net/corda/core/crypto/PartialMerkleTree.kt:117-144
  *                             behind FilteredTransaction.verify (MerkleTransaction.kt:170-178; the
@@ -177,6 +179,28 @@ int cv_ed25519_sign_batch(cv_ctx *ctx, size_t n, const uint8_t *seed /* n*32 */,
 /* tx_ok[t] = AND of verdict bits [tx_sig_begin[t], tx_sig_begin[t+1]); a transaction with no
  * signatures is not ok (SignedTransaction requires sigs.isNotEmpty(), SignedTransaction.kt:27-29). */
 int cv_tx_verdicts(size_t ntx, const uint64_t *verdict_bitmap, const uint32_t *tx_sig_begin, uint8_t *tx_ok);
+
+/* SignedTransaction.verifySignatures over a batch in one call (SignedTransaction.kt:59-71, 83-87 with
+ * WireTransaction.id, WireTransaction.kt:45-52): the ids of ntx transactions (leaves as cv_merkle_tx_ids_ex) and
+ * the verify of their signatures over those ids, the ids staying on the device as the messages.  The signatures
+ * of transaction t are records [tx_sig_begin[t], tx_sig_begin[t+1]) of pk[][32] / sig[][64].
+ *   tx_ok[t]      = 1 iff the transaction has at least one leaf, at least one signature, and every signature
+ *                   verifies over its id (cv_merkle_tx_ids_ex + cv_ed25519_verify_batch over the ids +
+ *                   cv_tx_verdicts, result for result).  The caller still compares ids with the claimed
+ *                   SignedTransaction.id (line 70): where they differ the reference rejects the transaction
+ *                   too — by that check, or by a signature over the claimed id — so the overall verdict
+ *                   is the same.
+ *   ids[ntx][32], tx_status[ntx] (CV_TX_OK / CV_TX_EMPTY), sig_status[nsig] (CV_SIG_*): optional (NULL).
+ * Transactions are cut into contiguous ranges over the devices as cv_merkle_tx_ids_ex's; pinned inputs are
+ * DMAed in place.  _async: ticket and cv_wait as cv_ed25519_verify_batch_async. */
+int cv_verify_transactions(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
+                           const uint32_t *leaf_len, const uint32_t *tx_leaf_begin /* ntx+1 */, const uint8_t *pk,
+                           const uint8_t *sig, const uint32_t *tx_sig_begin /* ntx+1 */, uint8_t *ids,
+                           uint8_t *tx_status, uint8_t *sig_status, uint8_t *tx_ok /* ntx */);
+int cv_verify_transactions_async(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
+                                 const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, const uint8_t *pk,
+                                 const uint8_t *sig, const uint32_t *tx_sig_begin, uint8_t *ids, uint8_t *tx_status,
+                                 uint8_t *sig_status, uint8_t *tx_ok, uint64_t *ticket);
 
 /* ---------------------------------------------------------------- device-resident API
  * All pointers are device pointers on HIP device `device` (which must be in the context); work is

@@ -27,6 +27,12 @@ hipError_t cvk_pmt_verify(uint32_t, const uint8_t *, const uint32_t *, const uin
                           hipStream_t) { return hipErrorNoDevice; }
 hipError_t cvk_merkle(uint32_t, uint32_t, uint32_t, const uint8_t *, const uint64_t *, const uint32_t *, const uint32_t *,
                       uint32_t *, uint8_t *, uint8_t *, hipStream_t) { return hipErrorNoDevice; }
+hipError_t cvk_tx_sig_refs(uint32_t, uint32_t, uint32_t, uint32_t, const uint32_t *, uint64_t *, uint32_t *, hipStream_t) {
+    return hipErrorNoDevice;
+}
+hipError_t cvk_tx_verdicts(uint32_t, uint32_t, const uint32_t *, const uint8_t *, const uint64_t *, uint8_t *, hipStream_t) {
+    return hipErrorNoDevice;
+}
 hipError_t cvk_calibrate(uint32_t, int, uint32_t, void *, hipStream_t) { return hipErrorNoDevice; }
 hipError_t cvk_mad_clock(uint32_t, uint32_t, uint64_t *, hipStream_t) { return hipErrorNoDevice; }
 int cvk_tri_zc_ok(const CvkPlan *, uint32_t, uint32_t) { return 0; }

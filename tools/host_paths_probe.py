@@ -6,6 +6,7 @@
             engine's host phases (cv_diag_stats CV_STATS_PIPE: plan incl. key dedupe, pack, wait, enqueue, sync)
   c3        the host C3 step of bench.py (1M txs x 8 signers): per-step wall time, time blocked on the Merkle
             ids and on the verdicts
+  c3f       the same step through the fused cv_verify_transactions(_async), async then synchronous
 
     python tools/host_paths_probe.py [--what resolve,keyed,c3] [--reps N]
 """
@@ -100,6 +101,20 @@ def c3(eng, reps):
     print(json.dumps({"what": "c3", **r, "pipe_stats": st}), flush=True)
 
 
+def c3f(eng, reps):
+    import bench  # noqa: E402
+    pcie = bench.pcie_h2d_probe(torch.device("cuda", 0))
+    for sync in (False, True) * int(os.environ.get("C3F_ROUNDS", "1")):
+        eng.stats("pipe", reset=True)
+        try:
+            r = bench.host_c3_fused_rate(eng, 0, 0, 1_000_000, reps, 1.0, pcie, sync=sync)
+        except AssertionError as e:
+            print(json.dumps({"what": "c3_fused", "sync": sync, "error": str(e)}), flush=True)
+            continue
+        r.pop("ratio_to_device_value", None)
+        print(json.dumps({"what": "c3_fused", "sync": sync, **r, "pipe_stats": eng.stats("pipe")}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="resolve,keyed,c3")
@@ -107,7 +122,7 @@ def main():
     a = ap.parse_args()
     eng = native.Engine(1)
     for w in a.what.split(","):
-        {"resolve": resolve, "keyed": keyed, "c3": c3}[w](eng, a.reps if w != "c3" else 4)
+        {"resolve": resolve, "keyed": keyed, "c3": c3, "c3f": c3f}[w](eng, a.reps if w not in ("c3", "c3f") else 4)
     eng.close()
 
 
