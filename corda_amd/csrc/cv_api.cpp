@@ -2050,9 +2050,9 @@ static int merkle_shard_small(Device &d, const MStage &st, const MerkleIn &in, W
 // (about merkle_chunk leaves, ramped: a quarter, a half, then full) and of signatures (multiples of 64 from s0,
 // sized as pipe_enqueue's) share the input ring and the copy stream; the launch groups alternate over the two
 // compute streams.  A Merkle group (leaf + tree kernels on the slot's digest workspace) records mev[J]; the
-// signature groups it makes available — those whose transactions all lie in sub-chunks 0..J — follow it, each
+// signature groups whose transactions all lie in sub-chunks 0..J are issued after Merkle group J + 1, each
 // waiting for its own copy and for the mev of every Merkle group its transactions lie in (a group may start
-// inside sub-chunk J - 1, whose kernels can still be queued on the other stream), then writing its message
+// inside an earlier sub-chunk, whose kernels can still be queued on the other stream), then writing its message
 // references (cvk_tx_sig_refs: id offsets within the shard) and verifying.  Last, the per-transaction verdicts (cvk_tx_verdicts) on the stream of the
 // last group, after the other stream's last group.
 // dout: ids | Merkle status | tx_ok | signature status | verdict bitmap | message offsets | lengths | boundaries
@@ -2128,8 +2128,59 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
     const size_t vmin = std::min(vch, std::max<size_t>(o.pipe_first, 4096));
     int g = 0;           // launch groups so far (group g runs on compute stream g % 2)
     size_t p = s0;       // the next signature to stage
+    // the signature groups whose transactions all lie in Merkle sub-chunks 0..jc (to the shard's end if last)
+    auto emit_sigs = [&](size_t jc, bool last) -> int {
+        const size_t avail = last ? s1 : s0 + (in.tsb[mcut[jc + 1]] - s0) / 64 * 64;
+        while (p < avail) {
+            const size_t m = std::min(vch, avail - p);
+            if (!last && m < vmin) break;
+            double ta = now_s();
+            const size_t o_sig = al16(m * 32), bytes = o_sig + al16(m * 64);
+            int q;
+            uint8_t *dv;
+            int r = f.block(&q, bytes, &dv, al16(vch * 32) + al16(vch * 64));
+            if (r != CV_OK) return r;
+            double tb;
+            if (host_pinned(in.pk + p * 32, m * 32) && host_pinned(in.sig + p * 64, m * 64)) {
+                tb = now_s();
+                f.t[2] += tb - ta;
+                CV_TRY(hipMemcpyAsync(dv, in.pk + p * 32, m * 32, hipMemcpyHostToDevice, d.copy));
+                CV_TRY(hipMemcpyAsync(dv + o_sig, in.sig + p * 64, m * 64, hipMemcpyHostToDevice, d.copy));
+                f.direct++;
+            } else {
+                uint8_t *h;
+                int sk;
+                if ((r = f.staging(&sk, bytes, &h)) != CV_OK) return r;
+                tb = now_s();
+                f.t[2] += tb - ta;
+                par_copy({{h, in.pk + p * 32, m * 32}, {h + o_sig, in.sig + p * 64, m * 64}}, pool);
+                ta = now_s();
+                f.t[1] += ta - tb;
+                tb = ta;
+                CV_TRY(hipMemcpyAsync(dv, h, bytes, hipMemcpyHostToDevice, d.copy));
+                if ((r = f.staged(sk)) != CV_OK) return r;
+            }
+            if ((r = f.copied(q, g)) != CV_OK) return r;
+            Slot &sl = d.slot[g % kPipeSlots];
+            hipStream_t s = f.ss[g % kPipeSlots];
+            // every Merkle group holding one of its transactions: the first one's (the largest t with tsb[t] <= p)
+            // through jc — a group on the other stream may not have run yet
+            const size_t tf = (size_t)(std::upper_bound(in.tsb + t0, in.tsb + t1 + 1, (uint32_t)p) - in.tsb) - 1;
+            const size_t jf = (size_t)(std::upper_bound(mcut.begin(), mcut.end(), tf) - mcut.begin()) - 1;
+            for (size_t j = jf; j <= jc; j++) CV_TRY(hipStreamWaitEvent(s, d.mev[j], 0));
+            const size_t c0 = p - s0;
+            CV_TRY(cvk_tx_sig_refs((uint32_t)m, (uint32_t)c0, (uint32_t)nt, (uint32_t)s0, dtsb, doff, dlen, s));
+            CV_TRY(launch_verify(d, o.plan, sl, (uint32_t)m, dv, dv + o_sig, dout, doff + c0, dlen + c0, dbm + c0 / 64,
+                                 in.sig_status ? dout + o_sst + c0 : nullptr, s, nullptr, false));
+            if ((r = f.launched(q, g++)) != CV_OK) return r;
+            f.t[3] += now_s() - tb;
+            p += m;
+        }
+        return CV_OK;
+    };
+    // Merkle group J goes one step ahead of the signature groups of sub-chunk J - 1, so on its stream it queues
+    // behind older signature groups only and has usually run by the time the groups that read its ids start
     for (size_t J = 0; J < nm; J++) {
-        // ---- Merkle group J
         double ta = now_s();
         const MStage st = mstage_plan(mcut[J], mcut[J + 1], mi.txb, mi.off, mi.len, pool);
         const bool direct = mstage_direct(st, mi.txb, mi.arena, mi.off, mi.len);
@@ -2137,7 +2188,9 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
         f.t[0] += tb - ta;
         int q;
         uint8_t *dv;
-        if ((rc = f.block(&q, st.total, &dv)) != CV_OK) return rc;
+        if ((rc = f.block(&q, st.total, &dv, (size_t)((double)st.total / (double)std::max<size_t>(1, st.l1 - st.l0) *
+                                                      (double)max_nl))) != CV_OK)
+            return rc;
         if (direct) {
             ta = now_s();
             f.t[2] += ta - tb;
@@ -2173,51 +2226,9 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
         }
         if ((rc = f.launched(q, g++)) != CV_OK) return rc;
         f.t[3] += now_s() - ta;
-        // ---- the signature groups whose transactions' ids are now all enqueued
-        const bool last = J + 1 == nm;
-        const size_t avail = last ? s1 : s0 + (in.tsb[mcut[J + 1]] - s0) / 64 * 64;
-        while (p < avail) {
-            const size_t m = std::min(vch, avail - p);
-            if (!last && m < vmin) break;
-            ta = now_s();
-            const size_t o_sig = al16(m * 32), bytes = o_sig + al16(m * 64);
-            if ((rc = f.block(&q, bytes, &dv, al16(vch * 32) + al16(vch * 64))) != CV_OK) return rc;
-            if (host_pinned(in.pk + p * 32, m * 32) && host_pinned(in.sig + p * 64, m * 64)) {
-                tb = now_s();
-                f.t[2] += tb - ta;
-                CV_TRY(hipMemcpyAsync(dv, in.pk + p * 32, m * 32, hipMemcpyHostToDevice, d.copy));
-                CV_TRY(hipMemcpyAsync(dv + o_sig, in.sig + p * 64, m * 64, hipMemcpyHostToDevice, d.copy));
-                f.direct++;
-            } else {
-                uint8_t *h;
-                int sk;
-                if ((rc = f.staging(&sk, bytes, &h)) != CV_OK) return rc;
-                tb = now_s();
-                f.t[2] += tb - ta;
-                par_copy({{h, in.pk + p * 32, m * 32}, {h + o_sig, in.sig + p * 64, m * 64}}, pool);
-                ta = now_s();
-                f.t[1] += ta - tb;
-                tb = ta;
-                CV_TRY(hipMemcpyAsync(dv, h, bytes, hipMemcpyHostToDevice, d.copy));
-                if ((rc = f.staged(sk)) != CV_OK) return rc;
-            }
-            if ((rc = f.copied(q, g)) != CV_OK) return rc;
-            Slot &sl = d.slot[g % kPipeSlots];
-            hipStream_t s = f.ss[g % kPipeSlots];
-            // every Merkle group holding one of its transactions: the first one's (the largest t with tsb[t] <= p)
-            // through J — a group on the other stream may not have run yet
-            const size_t tf = (size_t)(std::upper_bound(in.tsb + t0, in.tsb + t1 + 1, (uint32_t)p) - in.tsb) - 1;
-            const size_t jf = (size_t)(std::upper_bound(mcut.begin(), mcut.end(), tf) - mcut.begin()) - 1;
-            for (size_t j = jf; j <= J; j++) CV_TRY(hipStreamWaitEvent(s, d.mev[j], 0));
-            const size_t c0 = p - s0;
-            CV_TRY(cvk_tx_sig_refs((uint32_t)m, (uint32_t)c0, (uint32_t)nt, (uint32_t)s0, dtsb, doff, dlen, s));
-            CV_TRY(launch_verify(d, o.plan, sl, (uint32_t)m, dv, dv + o_sig, dout, doff + c0, dlen + c0, dbm + c0 / 64,
-                                 in.sig_status ? dout + o_sst + c0 : nullptr, s, nullptr, false));
-            if ((rc = f.launched(q, g++)) != CV_OK) return rc;
-            f.t[3] += now_s() - tb;
-            p += m;
-        }
+        if (J > 0 && (rc = emit_sigs(J - 1, false)) != CV_OK) return rc;
     }
+    if ((rc = emit_sigs(nm - 1, true)) != CV_OK) return rc;
     // ---- per-transaction verdicts, behind both streams' last groups
     {
         const int kl = (g - 1) % kPipeSlots;

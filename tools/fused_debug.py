@@ -8,6 +8,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -96,6 +97,7 @@ def main():
             kw = dict(want_sig_status=bool(fl["sst"]), want_status=bool(fl["st"]))
             for rep in range(a.reps):
                 idb = eng.host_empty((ntx, 32)) if fl["pin"] else None
+                t_call = time.perf_counter()
                 if form == "sync":
                     ok, ids, st, sst = eng.verify_transactions(*args, ids=idb, **kw)
                 else:
@@ -103,11 +105,12 @@ def main():
                     t2 = eng.verify_transactions_async(*args, ids=idb, **kw)
                     eng.wait(t1)
                     ok, (ids, st, sst) = eng.wait(t2)
+                ms = (time.perf_counter() - t_call) * 1e3
                 st = np.zeros(1) if st is None else st
                 sst = np.zeros(1) if sst is None else sst
                 bad = np.nonzero(ok == 0)[0]
                 idbad = np.nonzero((ids != claimed).any(axis=1))[0]
-                print(json.dumps({"setting": name, "form": form, "outs": ov, "rep": rep, "rejected": int(bad.size),
+                print(json.dumps({"setting": name, "form": form, "outs": ov, "rep": rep, "ms": round(ms, 2), "rejected": int(bad.size),
                                   "ids_wrong": int(idbad.size), "status_nonzero": int((st != 0).sum()),
                                   "sig_status_nonzero": int((sst != 0).sum()),
                                   "first_rejected": bad[:12].tolist(), "first_ids_wrong": idbad[:12].tolist(),
