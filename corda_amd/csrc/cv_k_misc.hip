@@ -123,14 +123,7 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_tx_sig_refs_kernel(uint32_t m, ui
                                                                   uint64_t *__restrict__ off, uint32_t *__restrict__ len) {
     const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
     if (i >= m) return;
-    const uint32_t g = s0 + c0 + i;
-    uint32_t lo = 0, hi = nt;   // tsb[lo] <= g < tsb[hi]
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (tsb[mid] <= g) lo = mid;
-        else hi = mid;
-    }
-    off[c0 + i] = (uint64_t)lo * 32;
+    off[c0 + i] = (uint64_t)cv_tx_of_sig(s0 + c0 + i, nt, tsb) * 32;
     len[c0 + i] = 32;
 }
 
@@ -142,14 +135,7 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_tx_verdict_kernel(uint32_t nt, ui
                                                                  uint8_t *__restrict__ tx_ok) {
     const uint32_t t = blockIdx.x * CV_BLOCK + threadIdx.x;
     if (t >= nt) return;
-    const uint32_t b = tsb[t] - s0, e = tsb[t + 1] - s0;
-    bool ok = mstatus[t] == 0 && e > b;
-    for (uint32_t w = b >> 6; ok && w <= (e - 1) >> 6; w++) {
-        const uint32_t lo = w == (b >> 6) ? (b & 63) : 0, hi = w == ((e - 1) >> 6) ? ((e - 1) & 63) : 63;
-        const uint64_t mask = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & ~((1ull << lo) - 1);
-        ok = (bitmap[w] & mask) == mask;
-    }
-    tx_ok[t] = ok ? 1 : 0;
+    tx_ok[t] = mstatus[t] == 0 && cv_tx_all_valid(tsb[t] - s0, tsb[t + 1] - s0, bitmap) ? 1 : 0;
 }
 
 // ---------------------------------------------------------------- partial Merkle trees (f3)

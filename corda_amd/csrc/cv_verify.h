@@ -1020,3 +1020,28 @@ __host__ __device__ __forceinline__ bool cv_verify_one_hs_fused(const uint32_t *
     const bool eq = cv_hs_straus(bcomb, bcomb + 2 * CV_BTAB_ENTRIES * CV_BTAB_STRIDE, dig, 1, tab, tabR, nw);
     return ok && eq;
 }
+
+// ---------------------------------------------------------------- transactions (cv_verify_transactions)
+// The transaction signature g belongs to: the largest t < nt with tsb[t] <= g (tsb[0] <= g < tsb[nt]), so
+// transactions without signatures are passed over.  tsb: nt + 1 non-decreasing boundaries.
+__host__ __device__ __forceinline__ uint32_t cv_tx_of_sig(uint32_t g, uint32_t nt, const uint32_t *tsb) {
+    uint32_t lo = 0, hi = nt;   // tsb[lo] <= g < tsb[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (tsb[mid] <= g) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// Signatures [b, e) all valid in a verdict bitmap (bit j of word j / 64), and at least one of them: the "all
+// signatures valid" half of verifySignatures (SignedTransaction.kt:83-87; a transaction has sigs, :28).
+__host__ __device__ __forceinline__ bool cv_tx_all_valid(uint32_t b, uint32_t e, const uint64_t *bitmap) {
+    bool ok = e > b;
+    for (uint32_t w = b >> 6; ok && w <= (e - 1) >> 6; w++) {
+        const uint32_t lo = w == (b >> 6) ? (b & 63) : 0, hi = w == ((e - 1) >> 6) ? ((e - 1) & 63) : 63;
+        const uint64_t mask = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & ~((1ull << lo) - 1);
+        ok = (bitmap[w] & mask) == mask;
+    }
+    return ok;
+}

@@ -256,6 +256,9 @@ void cvh_sha256(const uint8_t *msg, uint32_t n, uint8_t *out) {
     }
 }
 // Merkle root over leaf digests (bytes, cnt x 32); returns 0 for empty
+uint32_t cvh_tx_of_sig(uint32_t g, uint32_t nt, const uint32_t *tsb) { return cv_tx_of_sig(g, nt, tsb); }
+int cvh_tx_all_valid(uint32_t b, uint32_t e, const uint64_t *bitmap) { return cv_tx_all_valid(b, e, bitmap) ? 1 : 0; }
+
 int cvh_merkle_root(const uint8_t *leaves, uint32_t cnt, uint8_t *out) {
     uint32_t *lvl = new uint32_t[8 * (cnt ? cnt : 1)];
     for (uint32_t i = 0; i < 8 * cnt; i++) {

@@ -432,3 +432,36 @@ def test_split_odd_multiple_tables(host_harness, corpus):
     bad = [(e.hex(), r) for e, r in encs if host_harness.cvh_table_split_mismatch(e, r) != 0]
     assert not bad, bad[:5]
 
+
+
+def test_tx_sig_refs_and_verdicts(host_harness):
+    """cv_verify_transactions' per-lane logic (cv_tx_of_sig, cv_tx_all_valid in cv_verify.h, the bodies of
+    cv_tx_sig_refs_kernel / cv_tx_verdict_kernel): on ragged signature lists with runs of empty transactions,
+    every signature maps to the transaction whose range holds it (numpy searchsorted), and a transaction's
+    verdict is "at least one signature, all bits set" — equal to the host ABI's cv_tx_verdicts."""
+    from corda_amd import native
+    h = host_harness
+    u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
+    u64p = np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS")
+    h.cvh_tx_of_sig.argtypes = [ctypes.c_uint32, ctypes.c_uint32, u32p]
+    h.cvh_tx_of_sig.restype = ctypes.c_uint32
+    h.cvh_tx_all_valid.argtypes = [ctypes.c_uint32, ctypes.c_uint32, u64p]
+    rng = np.random.default_rng(81)
+    for nt, maxs in ((1, 5), (7, 3), (300, 70), (2000, 9)):
+        counts = rng.integers(0, maxs + 1, nt)
+        counts[rng.random(nt) < 0.3] = 0                         # runs of transactions without signatures
+        counts[-1] = max(counts[-1], 1)
+        tsb = np.zeros(nt + 1, np.uint32)
+        tsb[1:] = np.cumsum(counts)
+        ns = int(tsb[-1])
+        want = np.searchsorted(tsb, np.arange(ns), side="right") - 1
+        got = np.array([h.cvh_tx_of_sig(g, nt, tsb) for g in range(ns)])
+        assert np.array_equal(got, want), nt
+        bits = rng.random(ns) < 0.98
+        words = np.zeros((ns + 63) // 64, np.uint64)
+        for j in np.nonzero(bits)[0]:
+            words[j // 64] |= np.uint64(1) << np.uint64(j % 64)
+        ok = np.array([h.cvh_tx_all_valid(int(tsb[t]), int(tsb[t + 1]), words) for t in range(nt)], np.uint8)
+        ref = np.array([int(counts[t] > 0 and bits[tsb[t]:tsb[t + 1]].all()) for t in range(nt)], np.uint8)
+        assert np.array_equal(ok, ref) and 0 < ref.sum()
+        assert np.array_equal(ok, native.tx_verdicts(words, tsb))
