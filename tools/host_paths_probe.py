@@ -7,6 +7,7 @@
   c3        the host C3 step of bench.py (1M txs x 8 signers): per-step wall time, time blocked on the Merkle
             ids and on the verdicts
   c3f       the same step through the fused cv_verify_transactions(_async), async then synchronous
+  txsmall   notary-sized transaction batches (32 and 512 txs x 8 signers): fused call vs the separate calls, p50
 
     python tools/host_paths_probe.py [--what resolve,keyed,c3] [--reps N]
 """
@@ -101,6 +102,40 @@ def c3(eng, reps):
     print(json.dumps({"what": "c3", **r, "pipe_stats": st}), flush=True)
 
 
+def txsmall(eng, reps):
+    """A notary-sized batch of transactions (512 x 8 signers = 4,096 signatures, C3-shaped leaves) through the
+    fused call against the separate Merkle + verify + cv_tx_verdicts calls: p50 per batch."""
+    for ntx in (32, 512):
+        signers = 8
+        tb = workload.make_tx_batch(eng, 0, ntx, signers, seed=777 + ntx)
+        arena = tb.leaf_arena.cpu().numpy().copy()
+        leaf_off = tb.leaf_off.cpu().numpy().astype(np.uint64)
+        leaf_len = tb.leaf_len.cpu().numpy().astype(np.uint32)
+        tx_begin = tb.tx_begin.cpu().numpy().astype(np.uint32)
+        claimed = tb.ids.cpu().numpy()
+        pk, sig, _, _, _ = tb.sigs.to_host()
+        n = ntx * signers
+        sig_begin = np.arange(0, n + 1, signers, dtype=np.uint32)
+        msg_off = (np.arange(n, dtype=np.uint64) // signers) * 32
+        msg_len = np.full(n, 32, np.uint32)
+
+        def separate():
+            ids, st = eng.merkle_tx_ids(arena, leaf_off, leaf_len, tx_begin)
+            bm, _ = eng.verify_batch(pk, sig, np.concatenate([ids.reshape(-1), np.zeros(16, np.uint8)]), msg_off,
+                                     msg_len, want_status=False)
+            return native.tx_verdicts(bm, sig_begin).astype(bool) & (st == 0)
+
+        def fused():
+            ok, ids, _, _ = eng.verify_transactions(arena, leaf_off, leaf_len, tx_begin, pk, sig, sig_begin,
+                                                    want_status=False)
+            return ok.astype(bool)
+
+        assert separate().all() and fused().all() and (eng.merkle_tx_ids(arena, leaf_off, leaf_len, tx_begin)[0]
+                                                        == claimed).all()
+        print(json.dumps({"what": "txsmall", "txs": ntx, "sigs": n, "separate_p50_ms": p50(separate, reps),
+                          "fused_p50_ms": p50(fused, reps)}), flush=True)
+
+
 def c3f(eng, reps):
     import bench  # noqa: E402
     pcie = bench.pcie_h2d_probe(torch.device("cuda", 0))
@@ -122,7 +157,7 @@ def main():
     a = ap.parse_args()
     eng = native.Engine(1)
     for w in a.what.split(","):
-        {"resolve": resolve, "keyed": keyed, "c3": c3, "c3f": c3f}[w](eng, a.reps if w not in ("c3", "c3f") else 4)
+        {"resolve": resolve, "keyed": keyed, "c3": c3, "c3f": c3f, "txsmall": txsmall}[w](eng, a.reps if w not in ("c3", "c3f") else 4)
     eng.close()
 
 
