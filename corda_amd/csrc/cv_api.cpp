@@ -2615,6 +2615,71 @@ int cv_merkle_tx_ids(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const u
     return merkle_call(ctx, ntx, leaf_arena, leaf_off, leaf_len, tx_leaf_begin, ids, nullptr, nullptr);
 }
 
+// One shard of a small synchronous transaction call (a notary's or a resolve chain's batch: staging up to
+// kMerkleSmall bytes): leaves, keys, signatures and boundaries packed into slot 0's pinned staging (one DMA),
+// then on one stream the Merkle kernels, the message references, the verify (a tri-chain or quad batch at
+// notary sizes) and the per-transaction verdicts, and one result copy — the pipeline's per-call frame costs more
+// than it hides at this size (fused 0.41 / 0.47 ms against 0.34 / 0.44 for the separate calls at 32 / 512
+// transactions x 8 signers through the frame, profiles/r04m_txsmall.log).
+static int txs_shard_small(Device &d, const Opts &o, const MStage &st, const TxIn &in, WorkerPool *pool) {
+    const MerkleIn &mi = in.m;
+    const size_t t0 = st.t0, nt = st.t1 - st.t0, nl = st.l1 - st.l0;
+    const size_t s0 = in.tsb[t0], ns = in.tsb[st.t1] - s0, words = (ns + 63) / 64;
+    // staging: the Merkle stage | pk | sig | boundaries
+    const size_t o_pk = al16(st.total), o_sig = o_pk + al16(ns * 32), o_tsb = o_sig + al16(ns * 64);
+    const size_t total = o_tsb + al16((nt + 1) * 4);
+    // device results: ids | Merkle status | tx_ok | signature status (copied back as one block) | bitmap | off | len
+    const size_t o_mst = al16(nt * 32), o_ok = o_mst + al16(nt), o_sst = o_ok + al16(nt);
+    const size_t back = o_sst + (in.sig_status ? ns : 0), o_bm = al16(o_sst + ns), o_off = o_bm + al16(words * 8);
+    const size_t o_len = o_off + al16(ns * 8), total_out = o_len + al16(ns * 4);
+    Slot &sl = d.slot[0];
+    hipStream_t s = nullptr;
+    CV_TRY(slot_stream(d, 0, &s));
+    CV_TRY(slot_events(sl));
+    CV_TRY(sl.pin_in.ensure(total));
+    CV_TRY(sl.packed.ensure(total));
+    CV_TRY(d.pin_out.ensure(al16(back)));
+    CV_TRY(d.ids.ensure(total_out));
+    if (nl * 32 + 32 > sl.mdig.cap) {
+        if (sl.last && sl.ev) CV_TRY(hipEventSynchronize(sl.ev));
+        CV_TRY(sl.mdig.ensure(nl * 32 + 32));
+    }
+    uint8_t *h = sl.pin_in.as<uint8_t>(), *dv = sl.packed.as<uint8_t>(), *dout = d.ids.as<uint8_t>();
+    auto drain = on_exit([s] { (void)hipStreamSynchronize(s); });   // error paths: no DMA outlives the call
+    mstage_pack(st, h, mi.txb, mi.arena, mi.off, mi.len, pool);
+    par_copy({{h + o_pk, in.pk + s0 * 32, ns * 32}, {h + o_sig, in.sig + s0 * 64, ns * 64},
+              {h + o_tsb, in.tsb + t0, (nt + 1) * 4}}, pool);
+    CV_TRY(hipMemcpyAsync(dv, h, total, hipMemcpyHostToDevice, s));
+    const uint32_t *dtsb = reinterpret_cast<const uint32_t *>(dv + o_tsb);
+    uint64_t *doff = reinterpret_cast<uint64_t *>(dout + o_off);
+    uint32_t *dlen = reinterpret_cast<uint32_t *>(dout + o_len);
+    uint64_t *dbm = reinterpret_cast<uint64_t *>(dout + o_bm);
+    CV_TRY(ws_begin(d, sl, s));
+    const hipError_t ek = cvk_merkle((uint32_t)nt, (uint32_t)nl, (uint32_t)st.l0, dv + st.o_ar - st.lo,
+                                     reinterpret_cast<const uint64_t *>(dv + st.o_off),
+                                     reinterpret_cast<const uint32_t *>(dv + st.o_len),
+                                     reinterpret_cast<const uint32_t *>(dv + st.o_txb), sl.mdig.as<uint32_t>(), dout,
+                                     dout + o_mst, s);
+    const hipError_t e2 = ws_end(sl, s);
+    CV_TRY(ek);
+    CV_TRY(e2);
+    if (ns) {
+        CV_TRY(cvk_tx_sig_refs((uint32_t)ns, 0, (uint32_t)nt, (uint32_t)s0, dtsb, doff, dlen, s));
+        CV_TRY(launch_verify(d, o.plan, sl, (uint32_t)ns, dv + o_pk, dv + o_sig, dout, doff, dlen, dbm,
+                             in.sig_status ? dout + o_sst : nullptr, s, nullptr, false));
+    }
+    CV_TRY(cvk_tx_verdicts((uint32_t)nt, (uint32_t)s0, dtsb, dout + o_mst, dbm, dout + o_ok, s));
+    CV_TRY(hipMemcpyAsync(d.pin_out.p, dout, back, hipMemcpyDeviceToHost, s));
+    CV_TRY(hipStreamSynchronize(s));
+    drain.armed = false;
+    const uint8_t *r = d.pin_out.as<uint8_t>();
+    std::memcpy(in.tx_ok + t0, r + o_ok, nt);
+    if (mi.ids) std::memcpy(mi.ids + t0 * 32, r, nt * 32);
+    if (mi.status) std::memcpy(mi.status + t0, r + o_mst, nt);
+    if (in.sig_status && ns) std::memcpy(in.sig_status + s0, r + o_sst, ns);
+    return CV_OK;
+}
+
 static int txs_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
                     const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, const uint8_t *pk, const uint8_t *sig,
                     const uint32_t *tx_sig_begin, uint8_t *ids, uint8_t *tx_status, uint8_t *sig_status, uint8_t *tx_ok,
@@ -2643,6 +2708,12 @@ static int txs_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const ui
     const int rc = dispatch(ctx, o, ntx, 1, [&](Device &d, size_t t0, size_t t1, int threads) {
         if (t1 <= t0) return CV_OK;
         CV_TRY(hipSetDevice(d.ordinal));
+        if (!ticket) {                                // small synchronous shards: one DMA, one stream
+            WorkerPool *pool = &d.workers(threads);
+            const MStage st = mstage_plan(t0, t1, tx_leaf_begin, leaf_off, leaf_len, pool);
+            const size_t ns = tx_sig_begin[t1] - tx_sig_begin[t0];
+            if (st.total + ns * 96 <= kMerkleSmall) return txs_shard_small(d, o, st, in, pool);
+        }
         int k = 0, r = CV_OK;
         std::unique_lock<std::mutex> lk;
         PipeOut &po = pipe_out(d, &k, lk, &r);

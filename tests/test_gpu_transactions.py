@@ -71,10 +71,11 @@ def _check(out, ref, what):
 
 
 def test_verify_transactions_vs_oracle(engine, oracle_c, corpus):
-    """4,000 ragged transactions (~38,000 signatures) on contexts of 1 and 3 (virtual) devices, with small
-    Merkle and signature sub-chunks (many launch groups per shard, signature groups that start mid-transaction),
-    pageable and pinned inputs, synchronous and two async calls in flight: ids, Merkle statuses, signature
-    statuses and per-transaction verdicts all equal the oracle's — and the separate entry points'."""
+    """4,000 ragged transactions (~38,000 signatures) on contexts of 1 and 3 (virtual) devices: synchronous calls
+    (the small one-stream form at this size) from pageable and pinned inputs, and two async calls in flight (the
+    pipeline, with small Merkle and signature sub-chunks: many launch groups per shard, signature groups that
+    start mid-transaction): ids, Merkle statuses, signature statuses and per-transaction verdicts all equal the
+    oracle's — and the separate entry points'."""
     leaves, sigs, ref, msgs = _tx_case(engine, oracle_c, corpus, 31, 4000)
     ntx = leaves[3].shape[0] - 1
     # the separate calls give the same results (the fused call's definition)
@@ -93,14 +94,16 @@ def test_verify_transactions_vs_oracle(engine, oracle_c, corpus):
             e.set_option("async_chunk", 2048)
             e.set_option("shard_min", 64)
             e.stats("route", reset=True)
-            out = e.verify_transactions(*leaves, *sigs, want_sig_status=True)
+            out = e.verify_transactions(*leaves, *sigs, want_sig_status=True)     # small shards: one-stream form
             _check(out, ref, f"k={k} pageable")
             r = e.stats("route")
-            assert r["shards"] == k and r["merkle_subchunks"] >= 2 * k, r
+            assert r["shards"] == k and r["merkle_subchunks"] == 0, r
             out = e.verify_transactions(*pinned_l, *pinned_s, ids=e.host_empty((ntx, 32)), want_sig_status=True)
             _check(out, ref, f"k={k} pinned")
-            t1 = e.verify_transactions_async(*leaves, *sigs, want_sig_status=True)
+            e.stats("route", reset=True)
+            t1 = e.verify_transactions_async(*leaves, *sigs, want_sig_status=True)   # async: the pipeline
             t2 = e.verify_transactions_async(*pinned_l, *pinned_s, want_sig_status=True)
+            assert e.stats("route")["merkle_subchunks"] >= 4 * k
             for t in (t2, t1):
                 ok, rest = e.wait(t)
                 _check((ok, *rest), ref, f"k={k} async")
