@@ -2097,7 +2097,10 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
     }
     // Merkle sub-chunks: whole transactions, ramped up to `per` leaves (at least one transaction each)
     const size_t nl_all = mi.txb[t1] - mi.txb[t0];
-    const size_t per = std::max<size_t>(o.merkle_chunk, (nl_all + 11) / 12);
+    // about six full Merkle sub-chunks per shard (C3: 1M leaves, ~360 MB each): twelve were 3-4 % slower per
+    // call (85.3-86.3 against 82.5-82.6 ms, profiles/r04o_fused_merkle_chunk.log) — fewer Merkle groups to
+    // interleave with the signature groups' kernels
+    const size_t per = std::max<size_t>(o.merkle_chunk, (nl_all + 5) / 6);
     std::vector<size_t> mcut{t0};
     for (size_t want = std::max<size_t>(1, per / 4); mcut.back() < t1; want = std::min(per, 2 * want)) {
         const size_t c = mcut.back();
