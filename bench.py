@@ -5,17 +5,27 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+`--gpus N` with N > 1 and no launcher environment (WORLD_SIZE unset): the process starts N fresh ranks of
+itself (corda_amd/launch.py: RANK / LOCAL_RANK / WORLD_SIZE set, before any GPU call, no exec) and exits
+with their status; with fewer than N visible GPUs it exits 2 and names the count.  A WORLD_SIZE that
+differs from --gpus is an error too, so a line never reports a GPU count other than the one asked for.
+
 A "step" = one verify pass over the whole per-GPU batch (inputs resident in HBM; the engine's
 production launch plan), plus — for N > 1 —
 the RCCL all-gather of the verdict bitmaps that feeds the notary commit step.  Weak scaling: every
 rank verifies its own N_PER_GPU signatures.  value = all signatures verified by all ranks / the max
-over ranks of the timed region.
+over ranks of the timed region.  N > 1 adds two sub-lines (BASELINE.json configs[4]):
+  c5           8M signatures over 32-byte ids per rank (64M at N = 8), RCCL all-gather of the bitmaps
+               inside every timed step, the gathered bitmap checked all-ones
+  c_abi_multi  the JVM node's form: ONE process, cv_open(0) over every visible GPU, the N x 8M C5 batch
+               from pinned host buffers through cv_ed25519_verify_batch (routed over the devices by the
+               engine, no collective), against the same call on one device
 
 Default workload (N=1): BASELINE config C2 — 1,000,000 single-signer Ed25519 signatures over
 300-byte messages, distinct key per signature, generated on the GPU by the engine's signer.
 
 Extra fields on the JSON line:
-  roofline      VALU-issue roofline of the dominant kernel (cv_hs_straus_kernel: 141,660 32x32->64
+  roofline      VALU-issue roofline of the dominant kernel (cv_hs_straus_kernel: 130,460 32x32->64
                 MACs per verify, DESIGN.md "Half-size scalars") against the measured v_mad_u64_u32
                 peak of this GPU, kernel time from HIP events on whole-chunk launches of the same
                 batch; "group" = the whole launch group against its own MAC count
@@ -757,6 +767,155 @@ def c5_line(eng, local, rank, sh, dev, n, steps, mad_rate, host_api: bool = True
             "roofline": straus_roofline(eng, local, n, float(ph[2]), float(ph.sum()), mad_rate)}
 
 
+def timed_steps(step, steps: int, world: int, sync):
+    """The contract's timed region: barrier + sync, K steps, sync + barrier; returns (seconds, last step's
+    result).  sync() waits for this rank's device (a no-op in the CPU plumbing mode)."""
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    out = None
+    for k in range(steps):
+        out = step(k)
+    sync()
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0, out
+
+
+def max_over_ranks(vals, device) -> list:
+    """Element-wise max of per-rank floats (the slowest rank's timed region is the job's)."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return [float(v) for v in vals]
+    tt = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=device)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return [float(x) for x in tt.cpu()]
+
+
+def c5_multi_line(eng, local, rank, world, sh, dev, n: int, steps: int) -> dict:
+    """C5 over the ranks (BASELINE.json configs[4]): each rank verifies its own n signatures over 32-byte ids
+    (device-resident) and every timed step ends with the RCCL all-gather of the verdict bitmaps into the
+    replicated global bitmap the commit step reads; weak scaling, value = world * n * steps / max time."""
+    assert n % 64 == 0, "per-rank shard must be whole bitmap words"
+    b = workload.make_batch(eng, local, n, 32, seed=5 + 7919 * rank, stream=sh)
+    bm = torch.zeros(n // 64, dtype=torch.int64, device=dev)
+    a = (b.pk.data_ptr(), b.sig.data_ptr(), b.arena.data_ptr(), b.off.data_ptr(), b.len.data_ptr(), bm.data_ptr())
+
+    def step(k):
+        eng.verify_device(local, n, *a, 0, sh)
+        return D.gather_bitmap(bm, world * n)             # on the current (= sh) stream, behind the verify
+
+    step(0)                                               # warm: workspace chunks, RCCL channels
+    el, gathered = timed_steps(step, steps, world, lambda: torch.cuda.synchronize(dev))
+    ok = bool((gathered == -1).all()) and torch.equal(gathered.view(world, -1)[rank], bm)
+    (el, bad) = max_over_ranks([el, 0.0 if ok else 1.0], dev)
+    assert bad == 0.0, "C5 multi-GPU: a gathered verdict bitmap is not all-ones"
+    del b
+    torch.cuda.empty_cache()
+    return {"workload": f"C5: {n} sigs per GPU x {world} GPUs = {world * n} over 32-byte tx ids, RCCL all-gather "
+                        "of the verdict bitmaps in every step",
+            "value": world * n * steps / el, "unit": "verifies/s", "ms_per_step": el / steps * 1e3, "steps": steps,
+            "sigs_total": world * n, "gathered_bitmap_words": world * n // 64, "gathered_all_ones": True}
+
+
+def c_abi_multi_line(eng, local, sh, dev, n_per_dev: int, steps: int) -> dict:
+    """The JVM node's multi-GPU form: ONE process, one context over every visible GPU
+    (cv_open(0)), the whole C5 batch of n_per_dev x devices signatures from pinned host buffers through the
+    synchronous cv_ed25519_verify_batch — the engine cuts it into 64-aligned ranges over the devices, each
+    shard's bitmap words copied straight into the caller's bitmap, no collective (cv_api.cpp dispatch) — and
+    the same call with two in flight (the async form a batching node uses).  Baseline beside it: the first
+    n_per_dev records through a one-device context (this rank's GPU), so value / (devices x single) is the
+    C-ABI path's scaling efficiency."""
+    multi = native.Engine(0)
+    ndev = multi.device_count
+    N = ndev * n_per_dev
+    pk, sig = multi.host_empty((N, 32)), multi.host_empty((N, 64))
+    arena = multi.host_empty(N * 32 + 16)
+    arena[-16:] = 0
+    for j in range(ndev):                                 # generated on this rank's GPU, DMAed into pinned memory
+        b = workload.make_batch(eng, local, n_per_dev, 32, seed=900 + j, stream=sh)
+        lo, hi = j * n_per_dev, (j + 1) * n_per_dev
+        torch.from_numpy(pk[lo:hi]).copy_(b.pk)
+        torch.from_numpy(sig[lo:hi]).copy_(b.sig)
+        torch.from_numpy(arena[lo * 32:hi * 32]).copy_(b.arena[:n_per_dev * 32])
+        del b
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+    off = multi.host_copy(np.arange(N, dtype=np.uint64) * 32)
+    ln = multi.host_copy(np.full(N, 32, np.uint32))
+    full = native.bitmap_to_bools
+
+    def sync_calls(e, n, k):
+        bm = None
+        t = time.perf_counter()
+        for _ in range(k):
+            bm, _ = e.verify_batch(pk[:n], sig[:n], arena, off[:n], ln[:n], want_status=False)
+        dt = time.perf_counter() - t
+        assert full(bm, n).all(), "C-ABI multi-device call rejected an honest signature"
+        return dt
+
+    def async_calls(e, n, k):
+        pend, bm = [], None
+        t = time.perf_counter()
+        for _ in range(k):
+            pend.append(e.verify_batch_async(pk[:n], sig[:n], arena, off[:n], ln[:n], want_status=False))
+            if len(pend) == 2:
+                bm, _ = e.wait(pend.pop(0))
+        for tk in pend:
+            bm, _ = e.wait(tk)
+        dt = time.perf_counter() - t
+        assert full(bm, n).all(), "C-ABI multi-device async call rejected an honest signature"
+        return dt
+
+    multi.stats("route", reset=True)
+    sync_calls(multi, N, 1)                               # warm: every device's workspace and input ring
+    route = multi.stats("route")
+    dt = sync_calls(multi, N, steps)
+    dta = async_calls(multi, N, steps + 1)
+    sync_calls(eng, n_per_dev, 1)
+    dt1 = sync_calls(eng, n_per_dev, steps)
+    dta1 = async_calls(eng, n_per_dev, steps + 1)
+    multi.close()
+    del pk, sig, arena, off, ln
+    v, va = N * steps / dt, N * (steps + 1) / dta
+    v1, va1 = n_per_dev * steps / dt1, n_per_dev * (steps + 1) / dta1
+    return {"workload": f"C5 through the C-ABI: {N} sigs ({n_per_dev} x {ndev} devices) over 32-byte ids, pinned "
+                        "host buffers, one process, cv_open(0)",
+            "devices": ndev, "value": v, "unit": "verifies/s", "ms_per_call": dt / steps * 1e3, "steps": steps,
+            "async_value": va, "async_ms_per_call": dta / (steps + 1) * 1e3,
+            "single_device_value": v1, "single_device_async_value": va1,
+            "efficiency_vs_devices_x_single": v / (ndev * v1), "async_efficiency_vs_devices_x_single": va / (ndev * va1),
+            "shards_per_call": route["shards"], "path": "cv_ed25519_verify_batch (sync) and _async two in flight, "
+                                                        "engine-routed over the context's devices"}
+
+
+def plumbing_main(args, world: int, rank: int):
+    """CPU check of the N > 1 machinery (tests/test_bench_launch.py): the self-launch, the gloo process group,
+    the timed region's barriers, the bitmap all-gather and the max over ranks, with NO verification — each
+    rank's "verify" fills its shard bitmap with ones.  The printed line says so and is never a measurement."""
+    dist.init_process_group("gloo")
+    n = args.n or 64 * 1000
+    assert n % 64 == 0
+    bm = torch.zeros(n // 64, dtype=torch.int64)
+
+    def step(k):
+        bm.fill_(-1)                                      # stand-in for this rank's verify kernel
+        return D.gather_bitmap(bm, world * n)
+
+    step(0)
+    el, gathered = timed_steps(step, args.steps, world, lambda: None)
+    (el,) = max_over_ranks([el], "cpu")
+    if rank == 0:
+        print(json.dumps({"metric": "PLUMBING CHECK (launcher + gloo all-gather + timing; no verification)",
+                          "value": None, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": el / args.steps * 1e3, "gathered_words": int(gathered.numel()),
+                          "gathered_all_ones": bool((gathered == -1).all()),
+                          "rank_env": {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE",
+                                                                       "MASTER_ADDR")}}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -776,13 +935,39 @@ def main():
     ap.add_argument("--streams", type=int, default=2,
                     help="device streams the K timed steps are dealt over (each its own workspace slot); the "
                          "line also reports the other form (1 <-> 2 streams) beside it")
+    ap.add_argument("--c5-per-gpu", type=int, default=8_000_000,
+                    help="N > 1: signatures per GPU of the c5 and c_abi_multi sub-lines (BASELINE configs[4]: 8M)")
+    ap.add_argument("--c-abi-multi", action="store_true",
+                    help="also run the c_abi_multi sub-line at N = 1 (it always runs at N > 1)")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="CPU check of the N > 1 launcher / gloo all-gather / timing, no GPU and NO verification "
+                         "(tests/test_bench_launch.py); its line is never a measurement")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: start the ranks ourselves (no GPU call has been made in this process)
+        from corda_amd import launch
+        sys.exit(launch.spawn(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                              require_gpus=not args.plumbing))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"bench.py: --gpus {args.gpus} but the launcher's WORLD_SIZE is {world}; refusing to report a line "
+            f"for a GPU count other than the one asked for")
+        sys.exit(2)
+    if args.plumbing:
+        plumbing_main(args, world, rank)
+        return
+    if world > 1 and torch.cuda.device_count() < world:
+        log(f"bench.py: {world} ranks but only {torch.cuda.device_count()} GPU(s) visible")
+        sys.exit(2)
+    cpu_group = None
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # ranks that wait for rank 0's one-rank legs (c_abi_multi, notary, ...) block on the CPU, not in an
+        # RCCL kernel on their GPU (the c_abi_multi leg uses every GPU of the node)
+        cpu_group = dist.new_group(backend="gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     n = args.n or (1_000_000 if args.config == "c2" else 8_000_000)
@@ -848,17 +1033,8 @@ def main():
         return bm
 
     def timed(ns):
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        out = None
-        for k in range(args.steps):
-            out = step(k, ns)                                 # N>1: RCCL all-gather into the commit step
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        return time.perf_counter() - t0, out
+        # N>1: every step ends with the RCCL all-gather into the commit step
+        return timed_steps(lambda k: step(k, ns), args.steps, world, lambda: torch.cuda.synchronize(dev))
 
     for k in range(args.warmup):
         step(k)
@@ -888,13 +1064,21 @@ def main():
     assert torch.equal(bitmap, full), "verify rejected an honest signature"
     ph = np.mean(np.array(phases), axis=0)
     kern_ms, straus_ms = float(ph.sum()), float(ph[2])
+    multi = {}
     if world > 1:
-        tt = torch.tensor([elapsed, kern_ms, straus_ms, other_elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms, straus_ms, other_elapsed = float(tt[0]), float(tt[1]), float(tt[2]), float(tt[3])
+        elapsed, kern_ms, straus_ms, other_elapsed = max_over_ranks([elapsed, kern_ms, straus_ms, other_elapsed], dev)
         assert torch.equal(gathered.view(world, words)[rank], bitmap)
         assert bool((gathered == -1).all()), "a rank rejected an honest signature"
     value = world * n * args.steps / elapsed
+    if world > 1 and not args.no_sub:
+        del batch
+        torch.cuda.empty_cache()
+        multi["c5"] = c5_multi_line(eng, local, rank, world, sh, dev, args.c5_per_gpu, 3)
+    if (world > 1 or args.c_abi_multi) and not args.no_host:
+        if rank == 0:
+            multi["c_abi_multi"] = c_abi_multi_line(eng, local, sh, dev, args.c5_per_gpu, 3)
+        if world > 1:
+            dist.barrier(group=cpu_group)
 
     if rank == 0:
         mad_rate, femul_rate = eng.calibrate(local)
@@ -1008,6 +1192,16 @@ def main():
                             "hs_straus_frac": r3(c["roofline"]["frac"])}
         if "c5_shard" in D_:
             result["c5_shard"] = {"value": r3(D_["c5_shard"]["value"]), "hs_straus_frac": r3(D_["c5_shard"]["roofline"]["frac"])}
+        D_.update(multi)
+        if "c5" in multi:
+            m = multi["c5"]
+            result["c5"] = {"value": r3(m["value"]), "ms_per_step": r3(m["ms_per_step"]), "sigs_total": m["sigs_total"],
+                            "gathered_all_ones": m["gathered_all_ones"]}
+        if "c_abi_multi" in multi:
+            m = multi["c_abi_multi"]
+            result["c_abi_multi"] = {k: (r3(m[k]) if isinstance(m[k], float) else m[k]) for k in
+                                     ("devices", "value", "ms_per_call", "async_value", "single_device_value",
+                                      "efficiency_vs_devices_x_single", "async_efficiency_vs_devices_x_single")}
         if "keyed" in D_:
             result["keyed"] = {"value": r3(D_["keyed"]["value"]), "comb_ms": r3(D_["keyed"]["phase_ms"]["comb"])}
         if "notary" in D_:
@@ -1030,7 +1224,7 @@ def main():
             log(f"could not write {detail}: {ex}")
         print(json.dumps(result), flush=True)
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=cpu_group)
         dist.destroy_process_group()
     eng.close()
 

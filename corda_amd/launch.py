@@ -1,0 +1,90 @@
+"""One process per GPU: start N ranks of a command on this node and wait for them.
+
+`bench.py --gpus N` (N > 1) started without a torch.distributed launcher lands here: it starts N fresh
+child processes of itself with RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_ADDR /
+MASTER_PORT set — the environment `python -m torch.distributed.run --nnodes=1 --nproc-per-node N` gives
+its workers — and returns the first non-zero exit status (0 when every rank succeeded).  The parent
+makes no GPU call and never execs: the children are new processes (shard by signature,
+one process per GPU).  When a rank fails, the others are stopped (their exact pids, never a pattern), so a
+broken rank cannot leave the rest waiting in a collective.
+"""
+from __future__ import annotations
+
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+from typing import List, Optional, Sequence
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def visible_gpus() -> int:
+    """GPUs this process could give its ranks.  torch.cuda.device_count() reads the device list without
+    initialising a HIP context on this image, so the launcher stays GPU-free."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def rank_env(rank: int, world: int, port: int, base: Optional[dict] = None) -> dict:
+    env = dict(os.environ if base is None else base)
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    return env
+
+
+def spawn(world: int, cmd: Sequence[str], require_gpus: bool = True, poll_s: float = 0.2,
+          timeout_s: Optional[float] = None) -> int:
+    """Run `cmd` as `world` ranks; returns 0 or the first failing rank's exit status (a rank killed by
+    a signal reports 128 + signal).  require_gpus: refuse (status 2) when fewer GPUs are visible than
+    ranks, naming the count — a rank without its own GPU would otherwise share or fail on device 0."""
+    if world < 1:
+        print(f"launch: world size {world} < 1", file=sys.stderr, flush=True)
+        return 2
+    if require_gpus:
+        have = visible_gpus()
+        if have < world:
+            print(f"launch: {world} ranks requested (one per GPU) but only {have} GPU(s) are visible; "
+                  f"refusing to run so no line is reported for the wrong GPU count", file=sys.stderr, flush=True)
+            return 2
+    port = free_port()
+    procs: List[subprocess.Popen] = []
+    for r in range(world):
+        procs.append(subprocess.Popen(list(cmd), env=rank_env(r, world, port)))
+    t0 = time.monotonic()
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0] if bad[0] > 0 else 128 - bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            if timeout_s is not None and time.monotonic() - t0 > timeout_s:
+                print(f"launch: ranks still running after {timeout_s:.0f} s", file=sys.stderr, flush=True)
+                rc = 124
+                break
+            time.sleep(poll_s)
+    finally:
+        live = [p for p in procs if p.poll() is None]
+        for p in live:
+            p.send_signal(signal.SIGTERM)
+        for p in live:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    if rc:
+        print(f"launch: a rank failed with status {rc}; the other ranks were stopped", file=sys.stderr, flush=True)
+    return rc

@@ -1,0 +1,80 @@
+"""bench.py --gpus N: the self-launch of one rank per GPU (corda_amd/launch.py) and the N > 1 timing /
+all-gather machinery, on CPU (gloo).  VERDICT r4 "next round" item 1: `--gpus N` must run N ranks or fail
+non-zero, and never print a line whose n_gpus differs from N."""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+from corda_amd import launch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(REPO, "bench.py")
+
+
+def _env(**kw):
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    e.update({k: str(v) for k, v in kw.items()})
+    return e
+
+
+def _run(args, env=None, timeout=240):
+    return subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True, timeout=timeout,
+                          env=env or _env(), cwd=REPO)
+
+
+def _line(out: str) -> dict:
+    lines = [x for x in out.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_self_launch_gathers_over_ranks(world):
+    """--gpus N without a launcher starts N ranks (RANK / LOCAL_RANK / WORLD_SIZE set by the parent), every
+    timed step all-gathers the ranks' bitmaps, and rank 0's single line reports n_gpus = N."""
+    r = _run(["--gpus", str(world), "--plumbing", "--steps", "3", "--warmup", "1", "--n", "6400"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == world and d["value"] is None and "no verification" in d["metric"].lower()
+    assert d["gathered_words"] == world * 100 and d["gathered_all_ones"]
+    assert d["rank_env"]["WORLD_SIZE"] == str(world) and d["rank_env"]["RANK"] == "0"
+    assert d["rank_env"]["MASTER_ADDR"] == "127.0.0.1"
+
+
+def test_gpus_more_than_visible_fails_nonzero():
+    """--gpus 2 with fewer than two visible GPUs (this container has none, the GPU box one) exits 2 and names
+    the count instead of printing a one-GPU line."""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("two or more GPUs visible")
+    r = _run(["--gpus", "2", "--steps", "1", "--warmup", "0"], timeout=120)
+    assert r.returncode == 2, (r.stdout, r.stderr[-2000:])
+    assert "GPU(s) are visible" in r.stderr
+    assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
+
+
+def test_world_size_mismatch_refused():
+    """A launcher environment whose WORLD_SIZE differs from --gpus is refused (exit 2), before any GPU call."""
+    r = _run(["--gpus", "2", "--plumbing", "--steps", "1"], env=_env(WORLD_SIZE=1, RANK=0, LOCAL_RANK=0))
+    assert r.returncode == 2 and "WORLD_SIZE is 1" in r.stderr
+
+
+def test_launcher_propagates_failure_and_stops_the_rest():
+    """One failing rank: spawn returns its status and stops the ranks still running (here one that would
+    sleep for a minute) instead of waiting for them."""
+    code = ("import os, sys, time\n"
+            "r = int(os.environ['RANK'])\n"
+            "assert os.environ['WORLD_SIZE'] == '2' and os.environ['LOCAL_RANK'] == str(r)\n"
+            "time.sleep(60) if r == 0 else sys.exit(5)\n")
+    t = time.monotonic()
+    rc = launch.spawn(2, [sys.executable, "-c", code], require_gpus=False)
+    assert rc == 5 and time.monotonic() - t < 40
+
+
+def test_launcher_all_ranks_ok():
+    code = "import os, sys; sys.exit(0 if os.environ['MASTER_ADDR'] == '127.0.0.1' else 1)"
+    assert launch.spawn(3, [sys.executable, "-c", code], require_gpus=False) == 0
