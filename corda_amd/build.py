@@ -18,14 +18,17 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcordaverify.so")
 OBJDIR = os.path.join(HERE, "_obj")
+MAPFILE = os.path.join(CSRC, "cordaverify.map")   # export list: the header's cv_* entry points only
 ARCH = os.environ.get("CV_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # kernel translation units (cv_kcommon.h) compile in parallel; cv_kernels.hip holds the launchers
 SOURCES = ["cv_k_hs.hip", "cv_k_hss.hip", "cv_k_lat.hip", "cv_k_keyed.hip", "cv_k_misc.hip", "cv_kernels.hip",
            "cv_api.cpp"]
+# host symbols hidden: the library exports only the cv_* entry points include/cordaverify.h declares
+# (cv_api.cpp gives the header's declarations default visibility); the cvk_* launchers stay internal
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
-          "-Wno-unused-variable"]
+          "-Wno-unused-variable", "-Xarch_host", "-fvisibility=hidden"]
 # kernels: LLVM's max-ILP machine scheduler (A/B on one MI355X, 3 alternating rounds: C2 1M verify
 # 11.34 -> 11.15 ms median; the iterative-ILP strategy was 5 % slower) — DESIGN.md "Kernels"
 KERNEL_FLAGS = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
@@ -35,7 +38,7 @@ SRC_FLAGS = {"cv_k_hss.hip": os.environ["CV_HSS_FLAGS"].split() if os.environ.ge
 
 def _deps():
     return (glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(REPO, "include", "*.h")) +
-            [os.path.abspath(__file__)])
+            [os.path.abspath(__file__), MAPFILE])
 
 
 def _stale(target: str, inputs) -> bool:
@@ -77,7 +80,8 @@ def build(verbose: bool = False, force: bool = False) -> str:
             if verbose and r.stderr.strip():
                 sys.stderr.write(r.stderr)
     if force or _stale(LIB, objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + ["-lpthread"]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + ["-lpthread",
+                                                                                 f"-Wl,--version-script={MAPFILE}"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

@@ -13,6 +13,7 @@
 #include <chrono>
 #include <deque>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <random>
@@ -20,7 +21,11 @@
 #include <unordered_map>
 #include <vector>
 
+// The library is built with hidden host symbols (corda_amd/build.py: -fvisibility=hidden); only the
+// entry points the header declares are exported.
+#pragma GCC visibility push(default)
 #include "../../include/cordaverify.h"
+#pragma GCC visibility pop
 #include "cv_launch.h"
 
 namespace {
@@ -186,6 +191,14 @@ struct PipeOut {
     DevBuf kdev;
     PinBuf kstage, kidx;
     PinBuf tstage;   // transaction calls: the shard's signature boundaries when the caller's are pageable
+    // calls on this output whose finish failed: (gen, error), kept after the output is reused so a cv_wait on
+    // such a call still returns its error (bounded: the last 64 failures)
+    std::deque<std::pair<uint64_t, int>> failed;
+    int result_of(uint64_t g) const {
+        for (const auto &f : failed)
+            if (f.first == g) return f.second;
+        return CV_OK;
+    }
 };
 
 // A fixed set of host threads for index-parallel jobs (the host-buffer path's packing, range scans and key
@@ -561,6 +574,7 @@ struct cv_ctx {
     std::mutex tk_mu;
     uint64_t next_ticket = 0;
     std::unordered_map<uint64_t, std::vector<std::array<uint64_t, 3>>> tickets;
+    std::map<uint64_t, int> tickets_done;   // finished tickets pruned from `tickets`, with their result
     std::mutex st_mu;
     Stats stats;
     cv_ctx() {
@@ -603,16 +617,9 @@ const char *cv_strerror(int code) {
     }
 }
 
-// Test hook (internal, not in the header): every device of the next cv_open appears k times in the
-// context — k independent Device slots (own lock, worker, stream, buffers, workspace, key pool) on one
-// GPU — so the multi-device host path (routing, shards, per-device dedupe and key pools) runs and is
-// tested on a one-GPU box.  0 / 1 = off.
-static std::atomic<int> g_virtual_devices{1};
-void cvk_set_virtual_devices(int k) { g_virtual_devices.store((k >= 1 && k <= 16) ? k : 1); }
-
-// max(off[i] + len[i]) over n records (0 for n = 0): the arena bytes a batch reaches, for the Python
-// mirror's bounds check; slices of 2^20 records on up to 8 threads.
-uint64_t cvk_msg_end(size_t n, const uint64_t *off, const uint32_t *len) {
+// max(off[i] + len[i]) over n records (0 for n = 0): the arena bytes a batch reaches (the shims' bounds
+// check); slices of 2^20 records on up to 8 threads.
+uint64_t cv_msg_extent(size_t n, const uint64_t *off, const uint32_t *len) {
     if (!n || !off || !len) return 0;
     constexpr size_t kSlice = 1u << 20;
     const size_t ns = (n + kSlice - 1) / kSlice;
@@ -691,14 +698,19 @@ int cv_diag_stats(cv_ctx *ctx, int which, double *out, size_t nout, int reset) {
     return (int)nv;
 }
 
-int cv_open(uint32_t device_mask, cv_ctx **out) {
-    if (!out) return CV_E_ARGS;
+int cv_open(uint32_t device_mask, cv_ctx **out) { return cv_open_ex(device_mask, 1, out); }
+
+// slots_per_device > 1: each GPU of the mask appears that many times in THIS context — independent Device slots
+// (own lock, worker, streams, buffers, workspace, key pool) on one GPU — so the multi-device host path
+// (routing, shards, per-device dedupe and key pools) runs and is tested on a one-GPU box.
+int cv_open_ex(uint32_t device_mask, int slots_per_device, cv_ctx **out) {
+    if (!out || slots_per_device < 1 || slots_per_device > 16) return CV_E_ARGS;
     *out = nullptr;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return CV_E_NO_DEVICE;
     cv_ctx *ctx = new (std::nothrow) cv_ctx();
     if (!ctx) return CV_E_OOM;
-    const int virt = g_virtual_devices.load();
+    const int virt = slots_per_device;
     for (int d = 0; d < count && d < 32; d++) {
         if (device_mask && !(device_mask & (1u << d))) continue;
         for (int v = 0; v < virt; v++) {
@@ -1557,9 +1569,7 @@ static std::vector<size_t> pipe_cuts(size_t b, size_t e, size_t first, size_t C,
 // Copies a finished pipelined call's results into the caller's arrays (waits for them first).  Results of
 // 1 MB and more are copied by the DMA straight into the caller's memory; smaller ones come back through
 // the output's pinned buffer.  The caller holds po.mu.
-static int pipe_finish(Device &d, PipeOut &po) {
-    if (!po.pending) return CV_OK;
-    po.pending = false;
+static int pipe_copy_back(Device &d, PipeOut &po) {
     CV_TRY(hipSetDevice(d.ordinal));
     // host-side join: the call's last launch group on every slot stream, then the result copies on the
     // device's output stream (which carries nothing else, so it neither waits behind the next call's input
@@ -1590,14 +1600,28 @@ static int pipe_finish(Device &d, PipeOut &po) {
     return CV_OK;
 }
 
+// Finishes the call pending on po (if any) and returns its result; a failure is also recorded under the call's
+// gen, so whoever finishes it — its own cv_wait, a later call reusing the output, an error path's drain — the
+// call's waiter gets the error.  The caller holds po.mu.
+static int pipe_finish(Device &d, PipeOut &po) {
+    if (!po.pending) return CV_OK;
+    po.pending = false;
+    const int rc = pipe_copy_back(d, po);
+    if (rc != CV_OK) {
+        po.failed.emplace_back(po.gen, rc);
+        if (po.failed.size() > 64) po.failed.pop_front();
+    }
+    return rc;
+}
+
 // The device's next output: the older call still holding it is finished first (its results land in its
-// caller's arrays).  Returns it locked.
-static PipeOut &pipe_out(Device &d, int *index, std::unique_lock<std::mutex> &lk, int *rc) {
+// caller's arrays; an error is kept for that call's cv_wait, not handed to the new caller).  Returns it locked.
+static PipeOut &pipe_out(Device &d, int *index, std::unique_lock<std::mutex> &lk) {
     PipeOut &po = d.out[d.out_next];
     *index = d.out_next;
     d.out_next = (d.out_next + 1) % kOuts;
     lk = std::unique_lock<std::mutex>(po.mu);
-    *rc = pipe_finish(d, po);
+    (void)pipe_finish(d, po);
     return po;
 }
 
@@ -2304,11 +2328,10 @@ static int verify_shard(cv_ctx *ctx, Device &d, const Opts &o, size_t b, size_t 
     }
     const bool keyed = in.keys != nullptr;
     if (!async && !keyed && n <= o.pipe_min) return verify_shard_small(ctx, d, o, b, e, in, threads);
-    int k = 0, rc = CV_OK;
+    int k = 0;
     std::unique_lock<std::mutex> lk;
-    PipeOut &po = pipe_out(d, &k, lk, &rc);
-    if (rc != CV_OK) return rc;
-    rc = pipe_enqueue(ctx, d, o, po, b, e, in, threads, async);
+    PipeOut &po = pipe_out(d, &k, lk);
+    int rc = pipe_enqueue(ctx, d, o, po, b, e, in, threads, async);
     if (rc != CV_OK) return rc;
     if (keyed) {
         std::lock_guard<std::mutex> g(ctx->st_mu);
@@ -2325,36 +2348,48 @@ static int verify_shard(cv_ctx *ctx, Device &d, const Opts &o, size_t b, size_t 
     return rc;
 }
 
-// A ticket for the parts of an asynchronous call.  Tickets whose every part is done (its output finished or
-// reused by a later call) are pruned here, so a caller that drops tickets does not grow the map.
+// A ticket for the parts of an asynchronous call.  Once 64 tickets are outstanding, those whose every part is
+// done (its output finished, or reused by a later call) move to the finished list with their result, so a
+// caller that drops tickets does not grow the live map and a late cv_wait still gets the call's status; the
+// finished list keeps the last kTicketsDone results.
+constexpr size_t kTicketsDone = 4096;
 static uint64_t ticket_add(cv_ctx *ctx, std::vector<Part> parts) {
     std::lock_guard<std::mutex> g(ctx->tk_mu);
     if (ctx->tickets.size() >= 64) {
         for (auto it = ctx->tickets.begin(); it != ctx->tickets.end();) {
             bool live = false;
+            int rc = CV_OK;
             for (const Part &p : it->second) {
                 PipeOut &po = ctx->devs[p[0]]->out[p[1]];
                 std::lock_guard<std::mutex> pg(po.mu);
                 live = live || (po.gen == p[2] && po.pending);
+                const int r = po.result_of(p[2]);
+                if (r != CV_OK) rc = r;
             }
-            it = live ? std::next(it) : ctx->tickets.erase(it);
+            if (live) {
+                ++it;
+                continue;
+            }
+            ctx->tickets_done.emplace(it->first, rc);
+            it = ctx->tickets.erase(it);
         }
+        while (ctx->tickets_done.size() > kTicketsDone) ctx->tickets_done.erase(ctx->tickets_done.begin());
     }
     const uint64_t t = ++ctx->next_ticket;
     ctx->tickets.emplace(t, std::move(parts));
     return t;
 }
 
-// Waits for parts (each output's lock only — no device lock, so other threads keep submitting).
+// Waits for parts (each output's lock only — no device lock, so other threads keep submitting) and returns
+// the first error of any part, also of parts an earlier call's reuse of their output already finished.
 static int parts_wait(cv_ctx *ctx, const std::vector<Part> &parts) {
     int rc = CV_OK;
     for (const Part &p : parts) {
         Device &d = *ctx->devs[p[0]];
         PipeOut &po = d.out[p[1]];
         std::lock_guard<std::mutex> g(po.mu);
-        if (po.gen != p[2] || !po.pending) continue;   // already finished (its output was reused)
-        const int r = pipe_finish(d, po);
-        if (r != CV_OK) rc = r;
+        const int r = (po.gen == p[2] && po.pending) ? pipe_finish(d, po) : po.result_of(p[2]);
+        if (r != CV_OK && rc == CV_OK) rc = r;
     }
     return rc;
 }
@@ -2451,7 +2486,13 @@ int cv_wait(cv_ctx *ctx, uint64_t ticket) {
     {
         std::lock_guard<std::mutex> g(ctx->tk_mu);
         auto it = ctx->tickets.find(ticket);
-        if (it == ctx->tickets.end()) return CV_E_ARGS;
+        if (it == ctx->tickets.end()) {
+            auto dn = ctx->tickets_done.find(ticket);
+            if (dn == ctx->tickets_done.end()) return CV_E_ARGS;
+            const int rc = dn->second;
+            ctx->tickets_done.erase(dn);
+            return rc;
+        }
         parts = std::move(it->second);
         ctx->tickets.erase(it);
     }
@@ -2580,8 +2621,7 @@ static int merkle_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const
         }
         int k = 0, r = CV_OK;
         std::unique_lock<std::mutex> lk;
-        PipeOut &po = pipe_out(d, &k, lk, &r);
-        if (r != CV_OK) return r;
+        PipeOut &po = pipe_out(d, &k, lk);
         r = merkle_enqueue(ctx, d, o, po, t0, t1, in, threads);
         if (r != CV_OK) return r;
         if (ticket) {
@@ -2719,8 +2759,7 @@ static int txs_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const ui
         }
         int k = 0, r = CV_OK;
         std::unique_lock<std::mutex> lk;
-        PipeOut &po = pipe_out(d, &k, lk, &r);
-        if (r != CV_OK) return r;
+        PipeOut &po = pipe_out(d, &k, lk);
         r = txs_enqueue(ctx, d, o, po, t0, t1, in, threads, ticket != nullptr);
         if (r != CV_OK) return r;
         if (ticket) {

@@ -32,7 +32,7 @@ EXPORTED = (
     "cv_ed25519_verify_device_keyed", "cv_partial_merkle_verify", "cv_calibrate_cycles",
     "cv_diag_dedupe_keys", "cv_host_alloc", "cv_host_free", "cv_ed25519_verify_batch_async", "cv_wait",
     "cv_merkle_tx_ids_async", "cv_set_option", "cv_get_option", "cv_diag_stats",
-    "cv_verify_transactions", "cv_verify_transactions_async",
+    "cv_verify_transactions", "cv_verify_transactions_async", "cv_open_ex", "cv_msg_extent",
 )
 
 # cv_set_option names (include/cordaverify.h CV_OPT_*)
@@ -98,8 +98,8 @@ def load():
         lib.cv_get_option.restype = ctypes.c_int
         lib.cv_diag_stats.argtypes = [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), _sz, ctypes.c_int]
         lib.cv_diag_stats.restype = ctypes.c_int
-        lib.cvk_set_virtual_devices.argtypes = [ctypes.c_int]
-        lib.cvk_set_virtual_devices.restype = None
+        lib.cv_open_ex.argtypes = [ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(_vp)]
+        lib.cv_open_ex.restype = ctypes.c_int
         lib.cv_partial_merkle_verify.argtypes = [_vp, _sz, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]
         lib.cv_partial_merkle_verify.restype = ctypes.c_int
         lib.cv_merkle_tx_ids_ex.restype = ctypes.c_int
@@ -114,8 +114,8 @@ def load():
         lib.cv_host_alloc.restype = ctypes.c_int
         lib.cv_host_free.argtypes = [_vp, _vp]
         lib.cv_host_free.restype = None
-        lib.cvk_msg_end.argtypes = [_sz, _vp, _vp]
-        lib.cvk_msg_end.restype = ctypes.c_uint64
+        lib.cv_msg_extent.argtypes = [_sz, _vp, _vp]
+        lib.cv_msg_extent.restype = ctypes.c_uint64
         lib.cv_tx_verdicts.argtypes = [_sz, _vp, _vp, _vp]
         lib.cv_tx_verdicts.restype = ctypes.c_int
         lib.cv_ed25519_verify_device.argtypes = [_vp, ctypes.c_int, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
@@ -170,7 +170,20 @@ def _u8(a, shape_last=None) -> np.ndarray:
 
 def _msg_end(lib, off: np.ndarray, ln: np.ndarray) -> int:
     """max(off + len) — the arena bytes the records reach (multi-threaded in the library for big n)."""
-    return int(lib.cvk_msg_end(off.shape[0], _p(off), _p(ln)))
+    return int(lib.cv_msg_extent(off.shape[0], _p(off), _p(ln)))
+
+
+def _ids_out(ids, ntx: int) -> np.ndarray:
+    """The caller's optional ids output (the library writes ntx * 32 bytes into it): a new array when None,
+    else it must be a writable, C-contiguous uint8 array of shape (ntx, 32) — a short or strided buffer would
+    be written past its end or into the wrong bytes."""
+    if ids is None:
+        return np.zeros((ntx, 32), np.uint8)
+    if not isinstance(ids, np.ndarray) or ids.dtype != np.uint8 or ids.shape != (ntx, 32):
+        raise ValueError(f"ids must be a uint8 array of shape ({ntx}, 32)")
+    if not ids.flags.c_contiguous or not ids.flags.writeable:
+        raise ValueError("ids must be C-contiguous and writable")
+    return ids
 
 
 def _check(rc: int, what: str):
@@ -185,19 +198,15 @@ class Engine:
     pointers (ints, e.g. torch.Tensor.data_ptr()) and an optional hipStream_t (int), and return
     immediately.  The context is thread-safe: calls from several Python threads run concurrently (ctypes
     releases the GIL) and the engine routes them over its devices.
-    virtual_devices (test hook): each GPU of the mask appears that many times (independent device slots).
+    virtual_devices (cv_open_ex): each GPU of the mask appears that many times in this context (independent
+    device slots: the multi-device routing on a one-GPU box).
     """
 
     def __init__(self, device_mask: int = 0, virtual_devices: int = 1):
         lib = load()
         h = _vp()
         if virtual_devices != 1:
-            with _lock:
-                lib.cvk_set_virtual_devices(virtual_devices)
-                try:
-                    rc = lib.cv_open(ctypes.c_uint32(device_mask), ctypes.byref(h))
-                finally:
-                    lib.cvk_set_virtual_devices(1)
+            rc = lib.cv_open_ex(ctypes.c_uint32(device_mask), int(virtual_devices), ctypes.byref(h))
         else:
             rc = lib.cv_open(ctypes.c_uint32(device_mask), ctypes.byref(h))
         if rc != CV_OK:
@@ -366,7 +375,7 @@ class Engine:
         """WireTransaction.id of every transaction -> (ids (ntx,32) u8, status u8[ntx]).  ids: an optional
         output array (e.g. pinned, host_empty), so the ids are DMAed straight into it."""
         ntx, arena, leaf_off, leaf_len, tx_leaf_begin = self._merkle_args(arena, leaf_off, leaf_len, tx_leaf_begin)
-        ids = np.zeros((max(ntx, 0), 32), np.uint8) if ids is None else ids
+        ids = _ids_out(ids, max(ntx, 0))
         st = np.zeros(max(ntx, 0), np.uint8)
         _check(self._lib.cv_merkle_tx_ids_ex(self._h, ntx, _p(arena), _p(leaf_off), _p(leaf_len),
                                              _p(tx_leaf_begin), _p(ids), _p(st)), "cv_merkle_tx_ids_ex")
@@ -375,7 +384,7 @@ class Engine:
     def merkle_tx_ids_async(self, arena, leaf_off, leaf_len, tx_leaf_begin, ids=None) -> int:
         """cv_merkle_tx_ids_async: enqueue and return a ticket; wait(ticket) -> (ids, status)."""
         ntx, arena, leaf_off, leaf_len, tx_leaf_begin = self._merkle_args(arena, leaf_off, leaf_len, tx_leaf_begin)
-        ids = np.zeros((max(ntx, 0), 32), np.uint8) if ids is None else ids
+        ids = _ids_out(ids, max(ntx, 0))
         st = np.zeros(max(ntx, 0), np.uint8)
         t = ctypes.c_uint64()
         _check(self._lib.cv_merkle_tx_ids_async(self._h, ntx, _p(arena), _p(leaf_off), _p(leaf_len),
@@ -399,7 +408,7 @@ class Engine:
         if pk.size == 0:
             pk, sig = np.zeros(32, np.uint8), np.zeros(64, np.uint8)
         ntx = max(ntx, 0)
-        ids = np.zeros((ntx, 32), np.uint8) if ids is None else ids
+        ids = _ids_out(ids, ntx)
         st = np.zeros(ntx, np.uint8) if want_status else None
         sst = np.zeros(nsig, np.uint8) if want_sig_status else None
         ok = np.zeros(ntx, np.uint8)

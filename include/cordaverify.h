@@ -45,9 +45,11 @@
  *     EdDSAPublicKey).  Length errors (sig != 64 B -> SignatureException, key != 32 B) cannot be
  *     expressed in these fixed-width records; the host shim rejects them before the call.
  *   - Multi-GPU: cv_open(mask) with several bits set routes host-buffer batches over the devices: a batch
- *     up to CV_OPT_SHARD_MIN records goes whole to the least loaded device, a throughput batch (from
- *     CV_OPT_SPREAD_MIN) is cut into contiguous ranges (multiples of 64) over all of them, a batch between
- *     over the devices idle at submission.  No collective: each shard's results land in the caller's arrays.
+ *     up to CV_OPT_SHARD_MIN records goes whole to the least loaded device; a throughput batch (from
+ *     CV_OPT_SPREAD_MIN records) is cut into contiguous ranges (multiples of 64) over all of them; a batch
+ *     between the two is cut over the devices idle at submission (at most ceil(n / CV_OPT_SHARD_MIN) of
+ *     them, at least the least loaded one).  No collective: each shard's results land in the caller's
+ *     arrays.
  */
 #ifndef CORDAVERIFY_H
 #define CORDAVERIFY_H
@@ -77,6 +79,10 @@ typedef struct cv_ctx cv_ctx;
  * The first open on a device also builds that device's basepoint rows (16.8 MB, kept for the
  * process lifetime, shared by every context), so it takes a few milliseconds longer. */
 int cv_open(uint32_t device_mask, cv_ctx **out);
+/* As cv_open; slots_per_device (1..16) > 1 makes each GPU of the mask appear that many times in THIS context
+ * as independent device slots (own lock, worker thread, streams, workspaces, key pool), so the multi-device
+ * routing below runs on a one-GPU machine (tests).  slots_per_device = 1 is cv_open. */
+int cv_open_ex(uint32_t device_mask, int slots_per_device, cv_ctx **out);
 void cv_close(cv_ctx *ctx);
 const char *cv_strerror(int code);
 const char *cv_version(void);
@@ -96,9 +102,11 @@ int cv_ed25519_verify_batch(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint
  * call returns).  Four pipelined calls (verify or Merkle) per device may be in flight: a fifth first
  * completes the oldest (whose cv_wait then returns at once).  A node's batching loop submits batch k+1
  * before waiting for batch k, so its copies and kernels fill the first one's pipeline ramp and tail.
- * cv_wait may run on another thread than the submission and does not block submissions.  Tickets are
- * waited at most once; tickets never waited for are dropped once their results are in; cv_close drops
- * results not yet waited for. */
+ * cv_wait may run on another thread than the submission and does not block submissions.  It returns the
+ * call's own status — also when a later call already completed it (a HIP failure while finishing a call is
+ * reported to that call's waiter, never to the later caller).  Tickets are waited at most once (again:
+ * CV_E_ARGS); a completed ticket keeps its status for cv_wait until 4,096 later tickets have completed;
+ * cv_close drops results not yet waited for. */
 int cv_ed25519_verify_batch_async(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint8_t *sig,
                                   const uint8_t *msg_arena, const uint64_t *msg_off, const uint32_t *msg_len,
                                   uint64_t *verdict_bitmap, uint8_t *status, uint64_t *ticket);
@@ -298,6 +306,10 @@ int cv_get_option(cv_ctx *ctx, int option, int64_t *value);
 #define CV_STATS_SMALL 1
 #define CV_STATS_ROUTE 2
 int cv_diag_stats(cv_ctx *ctx, int which, double *out, size_t nout, int reset);
+
+/* max(msg_off[i] + msg_len[i]) over n records (0 for n = 0): the arena bytes a batch reaches, for the
+ * shim's bounds check before a call (multi-threaded above 2^20 records).  Host only. */
+uint64_t cv_msg_extent(size_t n, const uint64_t *msg_off, const uint32_t *msg_len);
 
 /* Diagnostics: the host-side key dedupe cv_ed25519_verify_batch runs before choosing the keyed path
  * (seeded hash of all 32 key bytes).  Returns 1 and fills key_index[n] / *nkeys (distinct keys in

@@ -349,6 +349,48 @@ static void test_tx_verdicts() {
     CHECK(cv_tx_verdicts(0, nullptr, nullptr, nullptr) == CV_OK);
 }
 
+// a pipelined call whose finish fails reports the error to its own cv_wait, also when a later call
+// reusing its output (pipe_out) or an error path's drain ran the finish; finished tickets pruned from the live
+// map keep their result.  Device ordinal 4095 does not exist, so every finish fails at hipSetDevice.
+static void test_failed_finish_reaches_waiter() {
+    cv_ctx ctx;
+    ctx.devs.emplace_back(new Device());
+    Device &d = *ctx.devs[0];
+    d.ordinal = 4095;
+    d.out[0].pending = true;
+    d.out[0].gen = 1;
+    const uint64_t t1 = ticket_add(&ctx, {Part{0, 0, 1}});
+    d.out_next = 0;
+    {
+        int k = -1;
+        std::unique_lock<std::mutex> lk;
+        PipeOut &po = pipe_out(d, &k, lk);                 // a later call takes output 0: finishes call 1
+        CHECK(k == 0 && !po.pending);
+        po.pending = true;
+        po.gen = 2;
+    }
+    const uint64_t t2 = ticket_add(&ctx, {Part{0, 0, 2}});
+    CHECK(cv_wait(&ctx, t1) == CV_E_HIP);                  // call 1's error, although its output was reused
+    CHECK(cv_wait(&ctx, t2) == CV_E_HIP);                  // call 2 finishes (and fails) in its own wait
+    CHECK(cv_wait(&ctx, t1) == CV_E_ARGS);                 // a ticket is waited once
+    // 100 calls, each output reused by the next: once 64 tickets are live the finished ones are pruned with
+    // their result, and every one of them still reports its error
+    std::vector<uint64_t> tk;
+    for (uint64_t g = 10; g < 110; g++) {
+        int k = -1;
+        std::unique_lock<std::mutex> lk;
+        PipeOut &po = pipe_out(d, &k, lk);
+        po.pending = true;
+        po.gen = g;
+        lk.unlock();
+        tk.push_back(ticket_add(&ctx, {Part{0, (uint64_t)k, g}}));
+    }
+    CHECK(ctx.tickets.size() < 64 && !ctx.tickets_done.empty());
+    for (uint64_t t : tk) CHECK(cv_wait(&ctx, t) == CV_E_HIP);
+    CHECK(ctx.tickets.empty() && ctx.tickets_done.empty());
+    ctx.devs.clear();
+}
+
 static void test_abi_guards() {
     cv_ctx *ctx = nullptr;
     CHECK(cv_open(0, nullptr) == CV_E_ARGS);
@@ -377,6 +419,7 @@ int main(int argc, char **argv) {
         test_mstage(true);
         test_pipe_cuts();
         test_tx_verdicts();
+        test_failed_finish_reaches_waiter();
         test_abi_guards();
     }
     if (g_fail) {

@@ -31,6 +31,28 @@ def test_library_exports_every_declared_symbol():
     assert set(native.EXPORTED) == declared
 
 
+def test_only_declared_symbols_exported():
+    """the product library exports the header's cv_* entry points and nothing of its own
+    beyond them (the cvk_* kernel launchers and test hooks have hidden visibility)."""
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", native.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    ours = {ln.split()[-1] for ln in out.splitlines() if ln.split() and ln.split()[1] in "TtDdBbRrWwVv"
+            and ln.split()[-1].startswith(("cv", "_Z"))}
+    assert {s for s in ours if s.startswith("cvk")} == set(), sorted(ours)
+    assert {s for s in ours if s.startswith("cv_")} == _header_functions()
+
+
+def test_msg_extent():
+    lib = native.load()
+    off = np.array([5, 100, 7], np.uint64)
+    ln = np.array([10, 0, 300], np.uint32)
+    assert lib.cv_msg_extent(3, native._p(off), native._p(ln)) == 307
+    assert lib.cv_msg_extent(0, None, None) == 0
+    big_off = np.arange(3 << 20, dtype=np.uint64) * 3
+    assert lib.cv_msg_extent(big_off.size, native._p(big_off), native._p(np.full(big_off.size, 3, np.uint32))) == 9 << 20
+
+
 def test_version_and_strerror():
     lib = native.load()
     assert b"gfx950" in lib.cv_version()
@@ -120,3 +142,19 @@ def test_dedupe_gate_and_threshold():
     t = time.perf_counter()
     assert native.dedupe_keys(big) is None
     assert time.perf_counter() - t < 0.5
+
+
+def test_ids_output_checked():
+    """the ids= output of the Merkle / transaction calls is checked before the library writes
+    ntx * 32 bytes into it (no GPU needed: the check runs before any call)."""
+    ok = np.zeros((4, 32), np.uint8)
+    assert native._ids_out(ok, 4) is ok
+    assert native._ids_out(None, 3).shape == (3, 32)
+    for bad in (np.zeros((3, 32), np.uint8), np.zeros((4, 32), np.int8), np.zeros(128, np.uint8),
+                np.zeros((4, 64), np.uint8)[:, ::2], np.zeros((8, 32), np.uint8)[::2]):
+        with pytest.raises(ValueError):
+            native._ids_out(bad, 4)
+    ro = np.zeros((4, 32), np.uint8)
+    ro.flags.writeable = False
+    with pytest.raises(ValueError):
+        native._ids_out(ro, 4)
