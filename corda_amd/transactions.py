@@ -18,7 +18,7 @@ from typing import Dict, Iterable, List, Optional, Sequence
 import numpy as np
 
 from . import native
-from .crypto import (CompositeKey, DigitalSignature, IllegalArgumentException, IllegalStateException,
+from .crypto import (CompositeKey, DigitalSignature, EdDSAPublicKey, IllegalArgumentException, IllegalStateException,
                      SignatureException, VerifyItem, verify_many)
 
 
@@ -194,6 +194,77 @@ def verify_signatures_batch(stxs: Sequence[SignedTransaction], allowed_to_be_mis
             out.append(None)
         except Exception as e:  # noqa: BLE001 - mirrored reference exceptions
             out.append(e)
+    return out
+
+
+def verify_signatures_batch_fused(stxs: Sequence[SignedTransaction], allowed_to_be_missing: Iterable[CompositeKey] = (),
+                                  engine: Optional[native.Engine] = None) -> List[Optional[Exception]]:
+    """verify_signatures_batch through ONE cv_verify_transactions call (every id recomputed on the device and
+    kept there as its signatures' message), with the same per-transaction exceptions as the sequential reference.
+
+    The fused call verifies each signature over the RECOMPUTED id; the reference verifies over the CLAIMED id
+    first (checkSignaturesAreValid, SignedTransaction.kt:82-87) and compares ids only afterwards (the `tx` getter,
+    :34-38, and :70).  So a SignatureException must win over the IllegalStateException of a mismatched id, and
+    the first failing signature names the exception.  Wherever the fused verdict does not settle that, the
+    transaction takes the separate path — its signatures re-verified over the claimed id in one more call:
+      - recomputed id != claimed id (a signature bad over the claimed id throws
+        SignatureException, not IllegalStateException);
+      - tx_ok == 0 with equal ids (which signature failed first, and whether its key is not a point);
+      - no leaves (MerkleTreeException from `tx`) or a signature the host prefilter rejects (non-EdDSA key,
+        wrong length): these never enter the fused call.
+    Every honest transaction is decided by the fused call alone (INTEGRATION.md gives the JVM shim the same
+    rule)."""
+    allowed = tuple(allowed_to_be_missing)
+    eng = engine or native.default_engine()
+    fused, slow = [], []
+    for k, stx in enumerate(stxs):
+        conforming = all(isinstance(s.by, EdDSAPublicKey) and len(s.bits) == 64 for s in stx.sigs)
+        (fused if conforming and stx._wtx.leaves else slow).append(k)
+    out: List[Optional[Exception]] = [None] * len(stxs)
+    decided = []
+    if fused:
+        leaves: List[bytes] = []
+        lbegin, sbegin = [0], [0]
+        pk, sig = [], []
+        for k in fused:
+            leaves.extend(stxs[k]._wtx.leaves)
+            lbegin.append(len(leaves))
+            for s in stxs[k].sigs:
+                pk.append(s.by.encoded)
+                sig.append(s.bits)
+            sbegin.append(len(pk))
+        lens = np.fromiter((len(b) for b in leaves), dtype=np.uint32, count=len(leaves))
+        offs = np.zeros(len(leaves), np.uint64)
+        if len(leaves) > 1:
+            offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        arena = np.frombuffer(b"".join(leaves) + b"\0" * 16, np.uint8)
+        pk_a = np.frombuffer(b"".join(pk), np.uint8).reshape(-1, 32)
+        sig_a = np.frombuffer(b"".join(sig), np.uint8).reshape(-1, 64)
+        ok, ids, _, _ = eng.verify_transactions(arena, offs, lens, np.array(lbegin, np.uint32), pk_a, sig_a,
+                                                np.array(sbegin, np.uint32), want_status=False)
+        for j, k in enumerate(fused):
+            stxs[k]._wtx._id = SecureHash(ids[j].tobytes())          # the WireTransaction's own id
+            (decided if ok[j] and stxs[k]._wtx._id == stxs[k].id else slow).append(k)
+    if slow:
+        slow.sort()
+        items: List[VerifyItem] = []
+        begin = [0]
+        for k in slow:
+            items.extend(VerifyItem(s.by, stxs[k].id.bytes, s.bits) for s in stxs[k].sigs)
+            begin.append(len(items))
+        errs = verify_many(items, eng)
+        unknown = [stxs[k]._wtx for k in slow if stxs[k]._wtx._id is None and stxs[k]._wtx.leaves]
+        if unknown:
+            compute_ids(unknown, eng)
+        for j, k in enumerate(slow):
+            out[k] = next((e for e in errs[begin[j]:begin[j + 1]] if e is not None), None)
+            if out[k] is None:
+                decided.append(k)
+    for k in decided:
+        try:
+            stxs[k]._finish_verify(allowed)
+        except Exception as e:  # noqa: BLE001 - mirrored reference exceptions
+            out[k] = e
     return out
 
 

@@ -193,11 +193,12 @@ int cv_tx_verdicts(size_t ntx, const uint64_t *verdict_bitmap, const uint32_t *t
  * the verify of their signatures over those ids, the ids staying on the device as the messages.  The signatures
  * of transaction t are records [tx_sig_begin[t], tx_sig_begin[t+1]) of pk[][32] / sig[][64].
  *   tx_ok[t]      = 1 iff the transaction has at least one leaf, at least one signature, and every signature
- *                   verifies over its id (cv_merkle_tx_ids_ex + cv_ed25519_verify_batch over the ids +
+ *                   verifies over its RECOMPUTED id (cv_merkle_tx_ids_ex + cv_ed25519_verify_batch over the ids +
  *                   cv_tx_verdicts, result for result).  The caller still compares ids with the claimed
- *                   SignedTransaction.id (line 70): where they differ the reference rejects the transaction
- *                   too — by that check, or by a signature over the claimed id — so the overall verdict
- *                   is the same.
+ *                   SignedTransaction.id (line 70).  The accept/reject verdict is the reference's; the exception
+ *                   is settled only for tx_ok == 1 with equal ids: for any other transaction the shim re-verifies
+ *                   its signatures over the CLAIMED id (cv_ed25519_verify_batch), because the reference throws
+ *                   the first bad signature's SignatureException before it compares ids.
  *   ids[ntx][32], tx_status[ntx] (CV_TX_OK / CV_TX_EMPTY), sig_status[nsig] (CV_SIG_*): optional (NULL).
  * Transactions are cut into contiguous ranges over the devices as cv_merkle_tx_ids_ex's; pinned inputs are
  * DMAed in place.  _async: ticket and cv_wait as cv_ed25519_verify_batch_async. */
