@@ -61,14 +61,43 @@ CV_HD void fe_add(fe &h, const fe &f, const fe &g) {
 #pragma unroll
     for (int i = 0; i < 10; i++) h.v[i] = f.v[i] + g.v[i];
 }
-// h = f + k*p - g   (k = 2, 3 or 4; see the bounds table above)
+// h = f + k*p - g   (k = 2, 3 or 4; see the bounds table above).  Written as |k*p_i - g_i| + f_i, which equals
+// it because g_i <= k*p_i (the asserted bound): LLVM selects ONE v_sad_u32 per limb (absolute difference plus
+// addend, the k*p limb from an SGPR) instead of an add and a subtract — 10 VALU per subtraction instead of 20.
 template <int K> CV_HD void fe_sub(fe &h, const fe &f, const fe &g) {
 #pragma unroll
     for (int i = 0; i < 10; i++) {
         CV_ASSERT(g.v[i] <= cv_kp(K, i), "fe_sub: subtrahend limb exceeds k*p");
-        h.v[i] = (f.v[i] + cv_kp(K, i)) - g.v[i];
+        uint32_t k = cv_kp(K, i);
+        const uint32_t x = g.v[i];
+#ifdef __HIP_DEVICE_COMPILE__
+        asm("" : "+s"(k));   // an opaque k: x's known range would otherwise fold the select back into add + subtract
+#endif
+        h.v[i] = (k > x ? k - x : x - k) + f.v[i];
     }
 }
+// h = f + k*p - g with its even limbs carried (fe_sub then fe_carry_even, in one pass): each odd limb's
+// v_sad_u32 takes the even limb's carry in its addend (f_odd + c), so LLVM does not merge the carry add into a
+// v_add3 that would leave the absolute difference as min / max / subtract.
+template <int K> CV_HD void fe_sub_carry_even(fe &h, const fe &f, const fe &g) {
+#pragma unroll
+    for (int i = 0; i < 10; i += 2) {
+        uint32_t k0 = cv_kp(K, i), k1 = cv_kp(K, i + 1);
+        CV_ASSERT(g.v[i] <= k0 && g.v[i + 1] <= k1, "fe_sub: subtrahend limb exceeds k*p");
+#ifdef __HIP_DEVICE_COMPILE__
+        asm("" : "+s"(k0), "+s"(k1));
+#endif
+        const uint32_t x0 = g.v[i], x1 = g.v[i + 1];
+        const uint32_t e = (k0 > x0 ? k0 - x0 : x0 - k0) + f.v[i];
+        uint32_t a1 = f.v[i + 1] + (e >> 26);
+#ifdef __HIP_DEVICE_COMPILE__
+        asm("" : "+v"(a1));   // keeps the add out of a v_add3 with the absolute difference
+#endif
+        h.v[i] = e & 0x3ffffffu;
+        h.v[i + 1] = (k1 > x1 ? k1 - x1 : x1 - k1) + a1;
+    }
+}
+
 // h = -f = 2p - f  (f tight)
 CV_HD void fe_neg(fe &h, const fe &f) {
 #pragma unroll

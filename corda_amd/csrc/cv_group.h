@@ -72,8 +72,7 @@ CV_HD void ge_p2_dbl(ge_p1p1 &r, const ge_p2 &p) {
     const fe &xx = sq[0], &yy = sq[1], &zz2 = sq[2], &aa = sq[3];
     fe_add(r.Y, yy, xx);          // H' <= 2.02 (an f operand: not carried)
     fe_sub<2>(r.Z, yy, xx);       // G  <= 3.01
-    fe_sub<3>(r.X, aa, r.Y);      // E  <= 4.01, a g operand: its even limbs carried (<= 1.0, odd <= 4.01)
-    fe_carry_even(r.X);
+    fe_sub_carry_even<3>(r.X, aa, r.Y);   // E <= 4.01, a g operand: its even limbs carried (<= 1.0, odd <= 4.01)
     fe_sub<4>(r.T, zz2, r.Z);     // F' <= 5.01
 }
 CV_HD void ge_p3_dbl(ge_p1p1 &r, const ge_p3 &p) {

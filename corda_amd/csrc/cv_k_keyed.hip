@@ -79,8 +79,10 @@ __global__ __launch_bounds__(CV_BLOCK) void cv_keyed_prep_kernel(
 // keyed phase 2: the 4-row comb.  The basepoint comb tables (66 KB) are read from global memory
 // (L2-resident: every lane of the chip reads the same table) so LDS does not cap the occupancy.
 #define CV_BCOMB_WORDS (4 * CV_BTAB_ENTRIES * CV_BTAB_STRIDE)
+// The lane's h || s record: s is replaced by its radix-2^16 digit pairs first (the record is this lane's own; the
+// finish kernel does not read it), then the comb reads both from it each window (cv_comb_straus_rec).
 template <int WAVES>
-__global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_comb_kernel(uint32_t n, const uint32_t *__restrict__ ws_hs,
+__global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_comb_kernel(uint32_t n, uint32_t *__restrict__ ws_hs,
                                                                   const uint32_t *__restrict__ key_index,
                                                                   const uint32_t *__restrict__ slot_of_key,
                                                                   const uint32_t *__restrict__ ktab_pool,
@@ -89,17 +91,23 @@ __global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_comb_kernel(uint32_t n, co
     const uint32_t i = blockIdx.x * CV_BLOCK + threadIdx.x;
     if (i >= n) return;
     const uint32_t slot = slot_of_key[key_index[i]];
+    uint32_t *rec = ws_hs + (size_t)i * CV_HS_WORDS;
+    {
+        uint32_t s[8], sd[8];
+        load_words8(s, reinterpret_cast<const uint8_t *>(rec + 8));
+        digits65536_pairs(sd, s);
+        store_words(rec + 8, sd, 2);
+    }
     ge_p2 R;
     // s * B from the radix-2^16 rows (16 madds instead of 32)
-    cv_comb_straus<true>(bw16, ws_hs + (size_t)i * CV_HS_WORDS, ktab_pool + (size_t)slot * CV_KTAB_WORDS, R);
-    uint32_t rec[CV_R_WORDS];
-    fe_store(rec, R.X);
-    fe_store(rec + 10, R.Y);
-    fe_store(rec + 20, R.Z);
-    rec[30] = rec[31] = 0;
-    store_words(ws_R + (size_t)i * CV_R_WORDS, rec, CV_R_WORDS / 4);
+    cv_comb_straus_rec(bw16, rec, ktab_pool + (size_t)slot * CV_KTAB_WORDS, R);
+    uint32_t out[CV_R_WORDS];
+    fe_store(out, R.X);
+    fe_store(out + 10, R.Y);
+    fe_store(out + 20, R.Z);
+    out[30] = out[31] = 0;
+    store_words(ws_R + (size_t)i * CV_R_WORDS, out, CV_R_WORDS / 4);
 }
-template __global__ void cv_comb_kernel<3>(uint32_t, const uint32_t *, const uint32_t *, const uint32_t *,
+template __global__ void cv_comb_kernel<3>(uint32_t, uint32_t *, const uint32_t *, const uint32_t *,
                                            const uint32_t *, uint32_t *, const uint32_t *);
-template __global__ void cv_finish_kernel<true>(uint32_t n, uint32_t nbytes, const uint8_t *sig, const uint32_t *ws_R, const uint8_t *ws_ok, uint8_t *bitmap_bytes);
 template __global__ void cv_finish_kernel<false>(uint32_t n, uint32_t nbytes, const uint8_t *sig, const uint32_t *ws_R, const uint8_t *ws_ok, uint8_t *bitmap_bytes);

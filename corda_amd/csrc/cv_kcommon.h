@@ -126,7 +126,7 @@ template <bool LAT> __global__ void cv_finish_kernel(uint32_t n, uint32_t nbytes
 __global__ void cv_comb_quad_kernel(uint32_t n, const uint32_t *ws_hs, const uint32_t *key_index, const uint32_t *slot_of_key, const uint32_t *ktab_pool, uint32_t *ws_R);
 __global__ void cv_keyprep_kernel(uint32_t nk, const uint8_t *keys, const uint32_t *slots, uint32_t *scratch, uint32_t *ktab_pool, uint8_t *kok_pool);
 __global__ void cv_keyed_prep_kernel( uint32_t n, const uint8_t *keys, const uint32_t *key_index, const uint32_t *slot_of_key, const uint8_t *kok_pool, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_hs, uint8_t *ws_ok, uint8_t *status);
-template <int WAVES> __global__ void cv_comb_kernel(uint32_t n, const uint32_t *ws_hs, const uint32_t *key_index, const uint32_t *slot_of_key, const uint32_t *ktab_pool, uint32_t *ws_R, const uint32_t *bw16);
+template <int WAVES> __global__ void cv_comb_kernel(uint32_t n, uint32_t *ws_hs, const uint32_t *key_index, const uint32_t *slot_of_key, const uint32_t *ktab_pool, uint32_t *ws_R, const uint32_t *bw16);
 template <int WAVES> __global__ void cv_scalars_kernel(uint32_t n, uint32_t cap, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t *ws_dig);
 template <int WAVES, bool SUB = false> __global__ void cv_points_one_kernel(uint32_t n, const uint8_t *pk, const uint8_t *sig, uint32_t *ws_tab, uint32_t *ws_tabR, uint8_t *ws_ok, uint8_t *status);
 template <int WAVES, bool SUB = false> __global__ void cv_hs_straus_kernel(uint32_t n, uint32_t cap, const uint32_t *ws_dig, const uint32_t *ws_tab, const uint32_t *ws_tabR, const uint8_t *ws_ok, uint64_t *bitmap, const uint32_t *bw16);

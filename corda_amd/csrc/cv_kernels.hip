@@ -241,14 +241,11 @@ hipError_t cvk_verify_keyed(const CvkPlan *plan, uint32_t n, const uint8_t *keys
                                slot_of_key, ktab_pool, ws_R, bw16);
         if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
         const uint32_t nbytes = ((m + 63) / 64) * 8;
-        if (quad)
-            hipLaunchKernelGGL(cv_finish_kernel<true>, dim3((nbytes + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
-                               stream, m, nbytes, sig + (size_t)c0 * 64, ws_R, ws_ok,
-                               reinterpret_cast<uint8_t *>(bitmap) + (size_t)c0 / 8);
-        else
-            hipLaunchKernelGGL(cv_finish_kernel<false>, dim3((nbytes + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
-                               stream, m, nbytes, sig + (size_t)c0 * 64, ws_R, ws_ok,
-                               reinterpret_cast<uint8_t *>(bitmap) + (size_t)c0 / 8);
+        // the sequential-carry finish for both comb forms: its ILP twin (the former quad-comb finish) kept its
+        // eight prefix products in 336 B of scratch
+        hipLaunchKernelGGL(cv_finish_kernel<false>, dim3((nbytes + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
+                           stream, m, nbytes, sig + (size_t)c0 * 64, ws_R, ws_ok,
+                           reinterpret_cast<uint8_t *>(bitmap) + (size_t)c0 / 8);
         if (ev && c0 == 0) (void)hipEventRecord(ev[3], stream);
     }
     return hipGetLastError();

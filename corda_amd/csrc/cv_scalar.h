@@ -252,6 +252,21 @@ CV_HD int digit256(const uint32_t n[8], int k) {
     return (int)byte - 256 * top + prev;
 }
 
+// digit256(n, 8 j + u) for a compile-time j and a run-time u (0..7): the keyed comb's row digits, read with
+// static indices and two value selects only — a run-time index into n (digit256 / sel8 there) was turned into a
+// dynamically indexed private array, i.e. scratch memory, in cv_comb_kernel.
+CV_HD int digit256_row(const uint32_t n[8], int j, int u) {
+    const bool hi = (u >> 2) != 0;
+    const uint32_t w = hi ? n[2 * j + 1] : n[2 * j];
+    const int sh = 8 * (u & 3);
+    const uint32_t byte = (w >> sh) & 255u;
+    const int top = (int)(byte >> 7);
+    // the bit below the digit: bit sh - 1 of w, or (sh == 0) bit 31 of the word before it
+    const uint32_t below = hi ? n[2 * j] : (j ? n[2 * j - 1] : 0u);
+    const int prev = sh ? (int)((w >> (sh - 1)) & 1u) : (int)(below >> 31);
+    return (int)byte - 256 * top + prev;
+}
+
 // Signed radix-2^16 digits of a scalar n < 2^253 with the carry propagated (x = raw_k + carry;
 // x >= 2^15 -> d_k = x - 2^16, carry 1), d_k in [-2^15, 2^15), sum d_k 2^(16k) = n; packed two per
 // word as 16-bit two's complement: out[j] = d_j | d_(j+8) << 16 (j = 0..7), i.e. the digit of the

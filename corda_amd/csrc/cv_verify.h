@@ -160,19 +160,30 @@ __host__ __device__ __forceinline__ void ge_cached_multiples8_half(uint32_t *tab
         ge_cached_store(tab, c);
         ge_cached_store(tab + 40, c1);
     }
-    // step 1 operand: c1 (half 0) or c2 (half 1), limb-wise select
+    // step 1 operand: c1 (half 0) or c2 (half 1), limb-wise, through an opaque lane mask: a plain select of the
+    // two structs' limbs is canonicalised into a select of their addresses, which kept both in scratch
     ge_cached x;
+    uint32_t m = half1 ? 0xffffffffu : 0u;
+#ifdef __HIP_DEVICE_COMPILE__
+    asm("" : "+v"(m));
+#endif
 #pragma unroll
     for (int i = 0; i < 10; i++) {
-        x.YplusX.v[i] = half1 ? c2.YplusX.v[i] : c1.YplusX.v[i];
-        x.YminusX.v[i] = half1 ? c2.YminusX.v[i] : c1.YminusX.v[i];
-        x.Z.v[i] = half1 ? c2.Z.v[i] : c1.Z.v[i];
-        x.T2d.v[i] = half1 ? c2.T2d.v[i] : c1.T2d.v[i];
+        x.YplusX.v[i] = (c2.YplusX.v[i] & m) | (c1.YplusX.v[i] & ~m);
+        x.YminusX.v[i] = (c2.YminusX.v[i] & m) | (c1.YminusX.v[i] & ~m);
+        x.Z.v[i] = (c2.Z.v[i] & m) | (c1.Z.v[i] & ~m);
+        x.T2d.v[i] = (c2.T2d.v[i] & m) | (c1.T2d.v[i] & ~m);
     }
     const int k0 = half1 ? 4 : 3;
+    // step 0 adds x, steps 1 and 2 add c2: written out, not as a reference select (`s == 0 ? x : c2` is a
+    // pointer select when SROA runs, before the loop is unrolled, and it kept both operands in scratch)
+    ge_add(t, Q, x);
+    ge_p1p1_to_p3(Q, t);
+    ge_p3_to_cached(c, Q);
+    ge_cached_store(tab + 40 * k0, c);
 #pragma unroll
-    for (int s = 0; s < 3; s++) {
-        ge_add(t, Q, s == 0 ? x : c2);
+    for (int s = 1; s < 3; s++) {
+        ge_add(t, Q, c2);
         ge_p1p1_to_p3(Q, t);
         ge_p3_to_cached(c, Q);
         ge_cached_store(tab + 40 * (k0 + 2 * s), c);
@@ -522,7 +533,7 @@ __host__ __device__ __forceinline__ void cv_comb_straus(const uint32_t *bcomb, c
 #pragma unroll
         for (int j = 0; j < CV_COMB_ROWS; j++) {
             ge_precomp e;
-            krow_select(e, ktab + j * CV_KROW_WORDS, W16 ? digit256(h, 8 * j + u) : digit16(h, 16 * j + u));
+            krow_select(e, ktab + j * CV_KROW_WORDS, W16 ? digit256_row(h, j, u) : digit16(h, 16 * j + u));
             ge_madd(t, R3, e);
             if (j + 1 < CV_COMB_ROWS || with_b) ge_p1p1_to_p3(R3, t);
         }
@@ -539,6 +550,60 @@ __host__ __device__ __forceinline__ void cv_comb_straus(const uint32_t *bcomb, c
                 } else {
                     btab_select(e, bcomb + j * CV_BTAB_ENTRIES * CV_BTAB_STRIDE, digit256(s, 8 * j + (u >> 1)));
                 }
+                ge_madd(t, R3, e);
+                if (j + 1 < CV_COMB_ROWS) ge_p1p1_to_p3(R3, t);
+            }
+        }
+        ge_p1p1_to_p2(R, t);
+    }
+    out = R;
+}
+
+// cv_comb_straus<true> with the scalars read from memory each window instead of held in VGPRs across the loop:
+// rec[0..7] = h, rec[8..15] = s's radix-2^16 digit pairs (digits65536_pairs, written there by the caller).  Sixteen
+// fewer registers live through the loop let cv_comb_kernel fit 3 waves/SIMD without spilling;
+// the reloads are two 16-B loads per window plus one word per basepoint window, from the lane's own L2-hot record.
+__host__ __device__ __forceinline__ void cv_comb_straus_rec(const uint32_t *bcomb, const uint32_t *rec,
+                                                            const uint32_t *ktab, ge_p2 &out) {
+    ge_p2 R;
+    ge_p2_identity(R);
+#pragma unroll 1
+    for (int u = 7; u >= 0; u--) {
+        ge_p1p1 t;
+        ge_p3 R3;
+        if (u != 7) {
+#pragma unroll 1
+            for (int d = 0; d < 7; d++) {
+                ge_p2_dbl(t, R);
+                ge_p1p1_to_p2(R, t);
+            }
+            ge_p2_dbl(t, R);
+            ge_p1p1_to_p3(R3, t);
+        } else {
+            ge_p3_identity(R3);
+        }
+        const bool with_b = (u & 1) == 0;
+#pragma unroll
+        for (int j = 0; j < CV_COMB_ROWS; j++) {
+            // the words of h this row's digit reads (2j - 1 .. 2j + 1), loaded where they are used
+            uint32_t h[8] = {};
+            if (j) h[2 * j - 1] = rec[2 * j - 1];
+            h[2 * j] = rec[2 * j];
+            h[2 * j + 1] = rec[2 * j + 1];
+            ge_precomp e;
+            krow_select(e, ktab + j * CV_KROW_WORDS, digit256_row(h, j, u));
+            ge_madd(t, R3, e);
+            if (j + 1 < CV_COMB_ROWS || with_b) ge_p1p1_to_p3(R3, t);
+        }
+        if (with_b) {
+#pragma unroll
+            for (int j = 0; j < CV_COMB_ROWS; j++) {
+                ge_precomp e;
+                // digit k = 4j + u/2 of s: the low half of pair word k (k < 8) or the high half of word k - 8
+                const int k = 4 * j + (u >> 1);
+                const uint32_t word = rec[8 + (k & 7)];
+                const int d = k < 8 ? (int)(int16_t)(word & 0xffffu) : (int)word >> 16;
+                btab_select(e, bcomb + j * CV_BW16_ROW, d);
                 ge_madd(t, R3, e);
                 if (j + 1 < CV_COMB_ROWS) ge_p1p1_to_p3(R3, t);
             }

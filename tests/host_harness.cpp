@@ -241,6 +241,11 @@ int cvh_digit256(const uint8_t *s, int k) {
     words_from_bytes(w, s, 8);
     return digit256(w, k);
 }
+int cvh_digit256_row(const uint8_t *s, int j, int u) {
+    uint32_t w[8];
+    words_from_bytes(w, s, 8);
+    return digit256_row(w, j, u);
+}
 void cvh_sha512(const uint8_t *pre, int npre, const uint8_t *msg, uint32_t mlen, uint8_t *out) {
     uint32_t p[16] = {0}, o[16];
     words_from_bytes(p, pre, npre / 4);

@@ -152,6 +152,20 @@ def test_signed_digits(host_harness):
         assert all(-128 <= H.cvh_digit256(_b(s), k) <= 128 for k in range(32))
 
 
+def test_comb_row_digits(host_harness):
+    """The keyed comb's row digits (digit256_row, static word indices): equal to digit256(h, 8 j + u) for every
+    row j and window u, on random scalars and on the carry edges (bytes 0x7f / 0x80 / 0xff at word borders)."""
+    H = host_harness
+    rng = random.Random(16)
+    cases = [rng.getrandbits(255).to_bytes(32, "little") for _ in range(300)]
+    cases += [bytes([b]) * 31 + bytes([b & 0x7f]) for b in (0x00, 0x7f, 0x80, 0xff)]
+    cases += [bytes(4 * q) + b"\x80\x00\x00\x00" + bytes(28 - 4 * q) for q in range(7)]
+    for s in cases:
+        for j in range(4):
+            for u in range(8):
+                assert H.cvh_digit256_row(_b(s), j, u) == H.cvh_digit256(_b(s), 8 * j + u), (s.hex(), j, u)
+
+
 def test_radix65536_digit_pairs(host_harness):
     """The throughput group's basepoint digits (cv_scalar.h digits65536_pairs): 16 signed radix-2^16
     digits of w < L with the carry propagated, in [-2^15, 2^15), packed (d_j, d_(j+8)) as 16-bit
