@@ -80,6 +80,9 @@ HS_BWIN = 8
 W_MAC_HS_STRAUS = (HS_NW - 1) * (16 * 55 + 13 * 100) + HS_NW * 15 * 100 + HS_BWIN * 14 * 100
 # whole half-size group: + 2 point decodes (254 S + 19 M each) + 2 odd-multiple tables (4 S + 59 M each)
 W_MAC_HS_GROUP = W_MAC_HS_STRAUS + 2 * (258 * 55 + 78 * 100)
+# keyed comb (cv_comb_kernel, DESIGN.md "Keyed"): 7 x 8 = 56 doublings (4 S + 3 M each, the last of a window
+# 4 S + 4 M) + 32 key-row and 16 basepoint mixed additions (7 M each with their conversion) = 224 S + 535 M per verify
+W_MAC_COMB = 224 * 55 + 535 * 100
 MSG_BYTES = {"c2": 300, "c5": 32, "c3": 32}
 CONFIG_NAME = {
     "c2": "C2: 1M single-signer Ed25519 txs, 300-byte msg, distinct keys, SoA batch",
@@ -92,20 +95,23 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(n: int, hs: bool):
-    """HBM bytes per launch of the dominant kernel from the committed PMC pass (profiles/pmc_hs_straus.json
-    or pmc_straus.json, written by scripts/pmc.sh + tools/pmc_summary.py on the same build and
-    workload), scaled to n.  Returns (bytes, provenance): the figure is a committed measurement, not one
-    taken in this run (PMC counters need their own rocprofv3 pass)."""
-    name = "pmc_hs_straus.json" if hs else "pmc_straus.json"
-    p = os.path.join(REPO, "profiles", name)
+# The PMC record of the dominant kernel on the current kernel code: scripts/pmc.sh + tools/pmc_summary.py, named
+# with the commit it was measured on (the round-3 file described an older build)
+PMC_HS_FILE = "profiles/pmc_hs_straus_db4f697c32.json"
+
+
+def pmc_traffic(n: int):
+    """HBM bytes per launch of the dominant kernel from the committed PMC pass (PMC_HS_FILE), scaled to n.
+    Returns (bytes, provenance, VALU wave-instructions per verify): the figures are a committed measurement, not
+    one taken in this run (PMC counters need their own rocprofv3 pass)."""
+    p = os.path.join(REPO, PMC_HS_FILE)
     if not os.path.exists(p):
-        return None, None
+        return None, None, None
     with open(p) as f:
         d = json.load(f)
-    src = (f"profiles/{name}: FETCH_SIZE+WRITE_SIZE of one {d['n']}-signature launch "
+    src = (f"{PMC_HS_FILE}: FETCH_SIZE+WRITE_SIZE of one {d['n']}-signature launch "
            f"({d.get('build', 'build of that commit')}), scaled to n; not measured in this run")
-    return d["hbm_bytes_per_launch"] * n / d["n"], src
+    return d["hbm_bytes_per_launch"] * n / d["n"], src, d.get("SQ_INSTS_VALU", 0) / d["n"]
 
 
 def pcie_h2d_probe(dev, mb: int = 256, reps: int = 5) -> float:
@@ -1084,13 +1090,14 @@ def main():
         mad_rate, femul_rate = eng.calibrate(local)
         achieved = n * W_MAC_HS_STRAUS / (straus_ms * 1e-3)
         group = n * W_MAC_HS_GROUP / (kern_ms * 1e-3)
-        traffic, traffic_src = pmc_traffic(n, True)
+        traffic, traffic_src, valu_per_verify = pmc_traffic(n)
         cyc = eng.calibrate_cycles(local)
         other_key = f"{'two' if other_streams == 2 else 'single'}_stream"
         # everything measured, in full: written to the detail file; the printed line is a digest of it
         D_ = {"roofline": {
             "bound": "valu", "achieved": achieved / 1e12, "peak": mad_rate / 1e12, "unit": "Tmac/s",
             "frac": achieved / mad_rate, "traffic": traffic, "traffic_source": traffic_src,
+            "pmc_valu_wave_instr_per_verify": valu_per_verify,
             "kernel": "cv_hs_straus_kernel", "kernel_ms": straus_ms,
             "work_per_unit": (f"{W_MAC_HS_STRAUS} 32x32->64 MAC per verify in the half-size Straus phase at {HS_NW} "
                               f"windows (512 S + 1023 M: 16 basepoint madds from the radix-2^16 rows)"),
@@ -1162,7 +1169,7 @@ def main():
                          "frac_vs_2p4ghz": r3(R["cycle_basis"]["frac_vs_2p4ghz"]),
                          "clock_ghz": r3(cyc["clock_ghz"]), "group_frac": r3(R["group"]["frac"]),
                          "phase_ms": {k: r3(v) for k, v in R["phase_ms"].items()},
-                         "work_per_unit": f"{W_MAC_HS_STRAUS} MAC/verify", "traffic_source": "profiles/pmc_hs_straus.json"},
+                         "work_per_unit": f"{W_MAC_HS_STRAUS} MAC/verify", "traffic_source": PMC_HS_FILE},
         }
         if "cpu_baseline" in D_:
             c = D_["cpu_baseline"]
@@ -1203,7 +1210,15 @@ def main():
                                      ("devices", "value", "ms_per_call", "async_value", "single_device_value",
                                       "efficiency_vs_devices_x_single", "async_efficiency_vs_devices_x_single")}
         if "keyed" in D_:
-            result["keyed"] = {"value": r3(D_["keyed"]["value"]), "comb_ms": r3(D_["keyed"]["phase_ms"]["comb"])}
+            K = D_["keyed"]
+            comb_rate = n * W_MAC_COMB / (K["phase_ms"]["comb"] * 1e-3)
+            K["roofline"] = {"bound": "valu", "kernel": "cv_comb_kernel", "achieved": comb_rate / 1e12,
+                             "peak": mad_rate / 1e12, "unit": "Tmac/s", "frac": comb_rate / mad_rate,
+                             "work_per_unit": f"{W_MAC_COMB} MAC/verify (224 S + 535 M)"}
+            result["keyed"] = {"value": r3(K["value"]), "comb_ms": r3(K["phase_ms"]["comb"]),
+                               "roofline": {"achieved": r3(comb_rate / 1e12), "peak": r3(mad_rate / 1e12),
+                                            "unit": "Tmac/s", "frac": r3(comb_rate / mad_rate),
+                                            "work_per_unit": f"{W_MAC_COMB} MAC/verify"}}
         if "notary" in D_:
             N = D_["notary"]
             result["notary"] = {"batch": 4096, "p50_ms": r3(N["p50_ms"]), "p99_ms": r3(N["p99_ms"]),

@@ -373,7 +373,8 @@ struct Device {
 // grows to a call's distinct keys when they exceed it)
 constexpr uint32_t kDefaultKeyCap = 1u << 14;
 constexpr size_t kKtabBytes = 16512 * 4;  // CV_KTAB_WORDS: 4 comb rows x 129 affine entries x 128 B
-constexpr size_t kTabBytes = 9 * 40 * 4;  // CV_TAB_WORDS: k*P, k = 0..8, cached form (cv_verify.h)
+constexpr size_t kTabBytes = 9 * 48 * 4;  // CV_TAB48_WORDS: k*P, k = 0..8, cached form, the throughput form's 48-word
+                                          // entries (the latency forms use 40 of them, cv_verify.h)
 // new keys' tables are computed in launches of at most this many keys (bounded keyprep scratch: 270 MB)
 constexpr size_t kKeyprepBatch = 4096;
 
@@ -1501,6 +1502,8 @@ static int verify_shard_small(cv_ctx *ctx, Device &d, const Opts &o, size_t b, s
                                      o.small_zc == 2 || (o.small_zc == 3 && n >= 2048));
     const size_t words = (n + 63) / 64;
     const size_t o_bm = 0, o_st = al16(words * 8), total_out = o_st + al16(n);
+    double t[6];                 // host phases (cv_diag_stats CV_STATS_SMALL, as the zero-copy form)
+    t[0] = t_plan;
     Slot &sl = d.slot[0];
     hipStream_t s = nullptr;
     CV_TRY(slot_stream(d, 0, &s));
@@ -1512,6 +1515,7 @@ static int verify_shard_small(cv_ctx *ctx, Device &d, const Opts &o, size_t b, s
     uint8_t *h = sl.pin_in.as<uint8_t>();
     uint8_t *dv = sl.packed.as<uint8_t>();
     auto drain = on_exit([s] { (void)hipStreamSynchronize(s); });   // error paths: no DMA outlives the call
+    t[1] = now_s();
     // Two-stage staging above 1 MB of keys + signatures: they are packed and their DMA is issued
     // first, so it runs while the offsets, lengths and message bytes are packed (notary 65,536:
     // 1.29-1.34 -> 1.21-1.25 ms p50); below, one DMA (a second DMA's ~6 us would cost more than it hides).
@@ -1531,15 +1535,24 @@ static int verify_shard_small(cv_ctx *ctx, Device &d, const Opts &o, size_t b, s
         else
             CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, s));
     }
+    t[2] = now_s();
     uint8_t *dout = d.bitmap.as<uint8_t>();
     CV_TRY(launch_verify(d, o.plan, sl, (uint32_t)n, dv + st.o_pk, dv + st.o_sig, dv + st.o_ar - st.lo,
                          reinterpret_cast<const uint64_t *>(dv + st.o_off), reinterpret_cast<const uint32_t *>(dv + st.o_len),
                          reinterpret_cast<uint64_t *>(dout + o_bm), in.status ? dout + o_st : nullptr, s, nullptr, true));
     CV_TRY(hipMemcpyAsync(d.pin_out.p, dout, in.status ? o_st + n : words * 8, hipMemcpyDeviceToHost, s));
+    t[3] = now_s();
     CV_TRY(hipStreamSynchronize(s));
     drain.armed = false;
+    t[4] = now_s();
     std::memcpy(in.bitmap + b / 64, d.pin_out.as<uint8_t>() + o_bm, words * 8);
     if (in.status) std::memcpy(in.status + b, d.pin_out.as<uint8_t>() + o_st, n);
+    t[5] = now_s();
+    {
+        std::lock_guard<std::mutex> g(ctx->st_mu);
+        for (int k = 0; k < 5; k++) ctx->stats.small[k] += t[k + 1] - t[k];
+        ctx->stats.small_calls++;
+    }
     return CV_OK;
 }
 

@@ -300,7 +300,8 @@ int cv_get_option(cv_ctx *ctx, int option, int64_t *value);
  * of values of that kind (fills at most nout of them), or CV_E_ARGS.
  *   CV_STATS_PIPE  {plan, pack, wait, enqueue, sync seconds of the pipelined host path; calls; sub-chunks;
  *                   sub-chunks DMAed in place from pinned inputs}
- *   CV_STATS_SMALL {setup, pack, launch, sync, assemble seconds of the zero-copy notary path; calls}
+ *   CV_STATS_SMALL {setup, pack (+ input DMA issue), launch, sync, assemble seconds of the unpipelined host path
+ *                   (notary-sized batches: zero-copy and one-DMA forms); calls}
  *   CV_STATS_ROUTE {calls, routed whole to one device, cut over several, shards, keyed shards, keyed
  *                   sub-chunks, Merkle calls, Merkle sub-chunks} */
 #define CV_STATS_PIPE 0

@@ -44,6 +44,7 @@ def main():
                     help="space-separated 'NAME:OPTION=V,OPTION=V' (cv_set_option names, e.g. small:small_zero_copy=1); "
                          "rounds interleave them")
     ap.add_argument("--rounds", type=int, default=1)
+    ap.add_argument("--pinned", action="store_true", help="also time the host call from pinned (cv_host_alloc) inputs")
     args = ap.parse_args()
     # variants: "name:option=value,option=value ..." (per-context options, cv_set_option names)
     variants = []
@@ -70,8 +71,18 @@ def main():
                 eng.stats("small", reset=True)
                 host = p50(lambda: eng.verify_batch(pk, sig, arena, off, ln, want_status=False), args.reps)
                 st = eng.stats("small", reset=True)
+                pinned = None
+                if args.pinned:
+                    pin = [eng.host_copy(x) for x in (pk, sig, arena, off, ln)]
+                    eng.stats("small", reset=True)
+                    pinned = p50(lambda: eng.verify_batch(*pin, want_status=False), args.reps)
+                    st = eng.stats("small", reset=True)
+                    pin_us = {k: round(st[k + "_s"] / max(st["calls"], 1) * 1e6, 1) for k in
+                              ("setup", "pack", "launch", "sync", "assemble")} if st["calls"] else None
+                    del pin
                 zc_us = {k: round(st[k + "_s"] / max(st["calls"], 1) * 1e6, 1) for k in
                          ("setup", "pack", "launch", "sync", "assemble")} if st["calls"] else None
+                pin_us = None
                 bm_h, _ = eng.verify_batch(pk, sig, arena, off, ln, want_status=False)
                 assert np.array_equal(native.bitmap_to_bools(bm_h, n), expect)
                 d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in
@@ -92,9 +103,11 @@ def main():
                                          for _ in range(20)]), axis=0)
                 nbytes = pk.nbytes + sig.nbytes + arena.nbytes + off.nbytes + ln.nbytes
                 print(json.dumps({"variant": vname, "round": rnd, "n": n, "host_p50_p99_ms": host,
+                                  "pinned_p50_p99_ms": pinned,
                                   "device_p50_p99_ms": device,
                                   "phase_ms": {"hash": float(ph[0]), "prep": float(ph[1]), "straus": float(ph[2])},
-                                  "input_bytes": int(nbytes), "zc_host_us_mean": zc_us}), flush=True)
+                                  "input_bytes": int(nbytes), "host_phases_us_mean": zc_us,
+                                  "pinned_host_phases_us_mean": pin_us}), flush=True)
         apply([])
     eng.close()
 
