@@ -11,6 +11,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <chrono>
+#include <cmath>
 #include <deque>
 #include <functional>
 #include <map>
@@ -373,8 +374,7 @@ struct Device {
 // grows to a call's distinct keys when they exceed it)
 constexpr uint32_t kDefaultKeyCap = 1u << 14;
 constexpr size_t kKtabBytes = 16512 * 4;  // CV_KTAB_WORDS: 4 comb rows x 129 affine entries x 128 B
-constexpr size_t kTabBytes = 9 * 48 * 4;  // CV_TAB48_WORDS: k*P, k = 0..8, cached form, the throughput form's 48-word
-                                          // entries (the latency forms use 40 of them, cv_verify.h)
+constexpr size_t kTabBytes = 9 * 40 * 4;  // CV_TAB_WORDS: k*P, k = 0..8, cached form (cv_verify.h)
 // new keys' tables are computed in launches of at most this many keys (bounded keyprep scratch: 270 MB)
 constexpr size_t kKeyprepBatch = 4096;
 
@@ -1158,11 +1158,11 @@ static hipError_t mstage_dma_direct(const MStage &st, uint8_t *dv, const uint32_
 // Host-side key dedupe of the plain entry points: keys = the distinct key bytes in first-seen order,
 // key_index[i] = its index.  Returns false when the batch does not repeat keys enough for the keyed path to
 // pay (fewer than eight signatures per distinct key: a key's 66 KB of tables cost about 7 plain verifies).
-//   - n > 16,384: a gate first samples 4,096 signatures at pseudo-random positions (a fixed sequence, so a
-//     batch always gets the same decision) and counts repeated keys among them; a batch of c distinct keys
-//     shows about s^2 / 2c repeats in a sample of s, so fewer than 4 s^2 / 2n repeats (an estimated ratio
-//     below four signatures per key) is taken as distinct-keyed without touching the rest.  A performance
-//     guess only: both paths give the same verdicts.
+//   - n > 4,096: a gate first samples s = 4 sqrt(n) signatures (512 .. 4,096) at pseudo-random positions (a fixed
+//     sequence, so a batch always gets the same decision) and counts repeated keys among them; a batch of c
+//     distinct keys shows about s^2 / 2c repeats in a sample of s, so fewer than 4 s^2 / 2n repeats (an
+//     estimated ratio below four signatures per key) is taken as distinct-keyed without touching the rest.  A
+//     performance guess only: both paths give the same verdicts.
 //   - the dedupe proper runs in slices on the pool, each with its own growing open-addressing table (a
 //     1,024-key pool stays in cache), giving up once any slice has seen more than n / 8 distinct keys;
 //     the slices' key lists are then merged in slice order (first-seen order overall) and the slices'
@@ -1222,9 +1222,14 @@ struct FlatKeys {
     }
 };
 
+// The sample: s = 4 sqrt(n) records (512 .. 4,096): a batch with eight signatures per key then shows about
+// 4 s^2 / n = 64 repeats, a distinct-keyed one about s^2 / (2 n) = 8, against a threshold of 2 s^2 / n = 32 —
+// Poisson tails far below 10^-6 either way.  Round 4 sampled 4,096 records at every size above 16,384 and deduped
+// every batch up to 16,384 in full: 60-100 us of host time on each distinct-keyed notary batch of 16,384-65,536
+// signatures (tools/notary_probe.py host phases), for a decision that only picks the faster path.
 static bool dedupe_gate(size_t n, const uint8_t *pk) {
-    if (n <= 16384) return true;
-    constexpr uint32_t kS = 4096;
+    if (n <= 4096) return true;                    // the estimate needs s << n; a full dedupe of <= 4,096 is cheap
+    const uint32_t kS = (uint32_t)std::min<double>(4096.0, std::max(512.0, 4.0 * std::sqrt((double)n)));
     FlatKeys t(2 * kS);
     uint64_t x = 0x9E3779B97F4A7C15ull;
     uint32_t rep = 0;
@@ -1427,6 +1432,9 @@ struct VerifyIn {
     bool auto_keyed = false;             // dedupe pk per shard and take the keyed path
     uint64_t *bitmap = nullptr;
     uint8_t *status = nullptr;
+    // cv_ed25519_verify_batch_ex: the arena's size; every staging scan (which finds the byte range its records
+    // reach anyway) rejects a shard or sub-chunk whose records reach past it before anything reads the arena
+    uint64_t arena_bytes = UINT64_MAX;
 };
 
 // Zero-copy form of the small path for tri-chain batches (the notary batches).  The records are packed into
@@ -1497,6 +1505,7 @@ static int verify_shard_small(cv_ctx *ctx, Device &d, const Opts &o, size_t b, s
     WorkerPool *pool = n >= 16384 ? &d.workers(threads) : nullptr;
     const double t_plan = now_s();
     const Stage st = stage_plan(b, e, in.off, in.len, pool);
+    if (st.hi > in.arena_bytes) return CV_E_ARGS;
     if (o.small_zc && cvk_tri_zc_ok(&o.plan, (uint32_t)n, (uint32_t)n))
         return verify_shard_small_zc(ctx, d, o, st, b, in, pool, t_plan,
                                      o.small_zc == 2 || (o.small_zc == 3 && n >= 2048));
@@ -1831,6 +1840,7 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
         hipStream_t s = f.ss[j % kPipeSlots];
         double t0 = now_s();
         const Stage st = stage_plan(c0, c1, in.off, in.len, pool, keyed);
+        if (st.hi > in.arena_bytes) return CV_E_ARGS;   // before this sub-chunk's copy (drain: the ones before it)
         const bool direct = stage_direct(st, c0, in.pk, kidx, in.sig, in.arena, in.off, in.len);
         double t1 = now_s();
         f.t[0] += t1 - t0;
@@ -2489,6 +2499,25 @@ int cv_ed25519_verify_batch_async(cv_ctx *ctx, size_t n, const uint8_t *pk, cons
     in.len = msg_len;
     in.bitmap = verdict_bitmap;
     in.status = status;
+    return verify_call(ctx, n, in, ticket);
+}
+
+int cv_ed25519_verify_batch_ex(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg_arena,
+                               uint64_t arena_bytes, const uint64_t *msg_off, const uint32_t *msg_len,
+                               uint64_t *verdict_bitmap, uint8_t *status, uint64_t *ticket) {
+    if (!ctx) return CV_E_ARGS;
+    if (ticket) *ticket = 0;
+    if (n == 0) return CV_OK;
+    if (!pk || !sig || !msg_off || !msg_len || !verdict_bitmap) return CV_E_ARGS;
+    VerifyIn in;
+    in.pk = pk;
+    in.sig = sig;
+    in.arena = msg_arena;
+    in.off = msg_off;
+    in.len = msg_len;
+    in.bitmap = verdict_bitmap;
+    in.status = status;
+    in.arena_bytes = arena_bytes;
     return verify_call(ctx, n, in, ticket);
 }
 

@@ -81,24 +81,20 @@ CV_HD void ge_p3_dbl(ge_p1p1 &r, const ge_p3 &p) {
     ge_p2_dbl(r, q);
 }
 
-// r = p + q (q cached, possibly conditionally negated).  Z2X2: q.Z holds 2 Z2 (the throughput Straus' 48-word
-// tables store it doubled), so 2 Z1 Z2 is the product itself — ten field additions fewer per addition.
-template <bool Z2X2 = false> CV_HD void ge_add(ge_p1p1 &r, const ge_p3 &p, const ge_cached &q) {
+// r = p + q (q cached, possibly conditionally negated)
+CV_HD void ge_add(ge_p1p1 &r, const ge_p3 &p, const ge_cached &q) {
     fe s, d, m[4];
     fe_add(s, p.Y, p.X);          // <= 2.02
     fe_sub<2>(d, p.Y, p.X);       // <= 3.01
-    const fe f[4] = {q.YplusX, q.YminusX, q.T2d, p.Z}, g[4] = {s, d, p.T, q.Z};   // q.Z (or 2 q.Z) <= 2.02
+    const fe f[4] = {q.YplusX, q.YminusX, q.T2d, p.Z}, g[4] = {s, d, p.T, q.Z};
     fe_mul_n<4>(m, f, g);
     const fe &a = m[0], &b = m[1], &c = m[2];
     fe dd;
-    if (Z2X2)
-        dd = m[3];                // 2 Z1 Z2, tight
-    else
-        fe_add(dd, m[3], m[3]);
+    fe_add(dd, m[3], m[3]);
     fe_sub<2>(r.X, a, b);         // E <= 3.01
     fe_add(r.Y, a, b);            // H <= 2.02
-    fe_add(r.Z, dd, c);           // G <= 3.03 (2.02 for Z2X2)
-    fe_sub<2>(r.T, dd, c);        // F <= 4.02 (3.01 for Z2X2)
+    fe_add(r.Z, dd, c);           // G <= 3.03
+    fe_sub<2>(r.T, dd, c);        // F <= 4.02
 }
 // r = p + q (q affine precomp)
 CV_HD void ge_madd(ge_p1p1 &r, const ge_p3 &p, const ge_precomp &q) {
@@ -117,12 +113,21 @@ CV_HD void ge_madd(ge_p1p1 &r, const ge_p3 &p, const ge_precomp &q) {
 
 // Conditional negation of a table entry, branch-free: -(x,y) = (-x, y) swaps Y+X <-> Y-X and
 // negates T (2p - T, still within the g <= 3.3 budget).
+// -2dT = 2p - 2dT as (x XOR m) + (m AND (2p + 1)) with m all ones or zero: one v_xad_u32 per limb instead of a
+// subtraction and a select (the mask is opaque, or LLVM turns the xor-add back into a select).
 CV_HD void ge_cached_cneg(ge_cached &r, bool neg) {
-    fe a = r.YplusX, b = r.YminusX, t;
+    fe a = r.YplusX, b = r.YminusX;
     fe_sel(r.YplusX, a, b, neg);
     fe_sel(r.YminusX, b, a, neg);
-    fe_neg(t, r.T2d);
-    fe_sel(r.T2d, r.T2d, t, neg);
+    uint32_t m = neg ? 0xffffffffu : 0u;
+#ifdef __HIP_DEVICE_COMPILE__
+    asm("" : "+v"(m));
+#endif
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        CV_ASSERT(r.T2d.v[i] <= cv_kp(2, i), "ge_cached_cneg: 2dT limb exceeds 2p");
+        r.T2d.v[i] = (r.T2d.v[i] ^ m) + (m & (cv_kp(2, i) + 1u));
+    }
 }
 CV_HD void ge_precomp_cneg(ge_precomp &r, bool neg) {
     fe a = r.yplusx, b = r.yminusx, t;

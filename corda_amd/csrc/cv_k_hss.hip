@@ -29,9 +29,9 @@ __global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_hs_straus_kernel(uint32_t 
         nw = x > nw ? x : nw;
     }
     nw = __builtin_amdgcn_readfirstlane(nw);
-    const bool eq = cv_hs_straus<CV_BTAB_STRIDE, true, 48>(bw16, bw16 + 2 * CV_BW16_ROW, ws_dig + i, cap,
-                                                           ws_tab + (size_t)i * CV_TAB48_WORDS,
-                                                           ws_tabR + (size_t)i * CV_TAB48_WORDS, nw);
+    const bool eq = cv_hs_straus<CV_BTAB_STRIDE, true>(bw16, bw16 + 2 * CV_BW16_ROW, ws_dig + i, cap,
+                                                       ws_tab + (size_t)i * CV_TAB_WORDS,
+                                                       ws_tabR + (size_t)i * CV_TAB_WORDS, nw);
     const bool acc = eq && ws_ok[i] && i0 < n;
     const uint64_t bits = __ballot(acc);
     if ((threadIdx.x & 63u) == 0) bitmap[wave0 >> 6] = bits;

@@ -113,7 +113,7 @@ __device__ __forceinline__ void cv_points_one_lane(uint32_t g, uint32_t n, const
     const bool is_r = (g & 1u) != 0;
     uint32_t w[8];
     load_words8(w, is_r ? sig + (size_t)i * 64 : pk + (size_t)i * 32);
-    const bool ok = cv_hs_point_one<false, 48>(w, is_r, (is_r ? ws_tabR : ws_tab) + (size_t)i * CV_TAB48_WORDS);
+    const bool ok = cv_hs_point_one<false>(w, is_r, (is_r ? ws_tabR : ws_tab) + (size_t)i * CV_TAB_WORDS);
     const bool r_ok = __shfl_xor((int)ok, 1) != 0;
     if (!is_r) {
         ws_ok[i] = (ok && r_ok) ? 1 : 0;

@@ -121,10 +121,7 @@ hipError_t cvk_verify(const CvkPlan *plan, uint32_t n, const uint8_t *pk, const 
         const hipError_t e = bw16_table(&bw16, stream);
         if (e != hipSuccess) return e;
     }
-    // the latency forms' tables have 40-word entries, the throughput form's 48-word ones (CV_TAB48_WORDS); the
-    // workspace holds 2 * ws_cap of the larger
-    const bool tp = n > plan->quad_max;
-    uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * (tp ? CV_TAB48_WORDS : CV_TAB_WORDS);
+    uint32_t *ws_tabR = ws_tab + (size_t)ws_cap * CV_TAB_WORDS;
     for (uint32_t c0 = 0; c0 < n; c0 += ws_cap) {
         const uint32_t m = (n - c0 < ws_cap) ? n - c0 : ws_cap;
         const uint32_t blocks = (m + CV_BLOCK - 1) / CV_BLOCK;
@@ -180,12 +177,12 @@ hipError_t cvk_verify(const CvkPlan *plan, uint32_t n, const uint8_t *pk, const 
                 hipStream_t st = h ? ax->s2 : stream;
                 const uint32_t a = c0 + sub0[h], mm = subn[h], bl = (mm + CV_BLOCK - 1) / CV_BLOCK;
                 launch_prep_tp<true>(mm, ws_cap, pk + (size_t)a * 32, sig + (size_t)a * 64, arena, off + a, len + a,
-                                     ws_dig + sub0[h], ws_tab + (size_t)sub0[h] * CV_TAB48_WORDS,
-                                     ws_tabR + (size_t)sub0[h] * CV_TAB48_WORDS, ws_ok + sub0[h],
+                                     ws_dig + sub0[h], ws_tab + (size_t)sub0[h] * CV_TAB_WORDS,
+                                     ws_tabR + (size_t)sub0[h] * CV_TAB_WORDS, ws_ok + sub0[h],
                                      status ? status + a : nullptr, st, nullptr);
                 hipLaunchKernelGGL((cv_hs_straus_kernel<3, true>), dim3(bl), dim3(CV_BLOCK), 0, st, mm, ws_cap,
-                                   ws_dig + sub0[h], ws_tab + (size_t)sub0[h] * CV_TAB48_WORDS,
-                                   ws_tabR + (size_t)sub0[h] * CV_TAB48_WORDS, ws_ok + sub0[h], bitmap + a / 64, bw16);
+                                   ws_dig + sub0[h], ws_tab + (size_t)sub0[h] * CV_TAB_WORDS,
+                                   ws_tabR + (size_t)sub0[h] * CV_TAB_WORDS, ws_ok + sub0[h], bitmap + a / 64, bw16);
             }
             (void)hipEventRecord(ax->done2, ax->s2);
             (void)hipStreamWaitEvent(stream, ax->done2, 0);

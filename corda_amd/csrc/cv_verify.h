@@ -71,10 +71,6 @@ CV_HD void ge_p3_encode(uint32_t w[8], const ge_p3 &p) {
 
 #define CV_TAB_ENTRIES 9            // k*P, k = 0..8 (entry 0 = the identity: a digit 0 is a plain lookup)
 #define CV_TAB_WORDS (CV_TAB_ENTRIES * 40)
-// The throughput Straus' tables (cv_hs_straus, cv_points_one_kernel): 48-word entries, Y+X at word 0 and Y-X at
-// word 12 (each 16-B aligned, padded to 12 words), 2Z at 24 (doubled: ge_add<true>), 2dT at 34.  A negative digit then swaps Y+X and Y-X
-// by the load ADDRESS instead of 20 v_cndmask, and 2dT is negated by one v_xad_u32 per limb (tab_cached_select).
-#define CV_TAB48_WORDS (CV_TAB_ENTRIES * 48)
 #define CV_HS_WORDS 16              // h (8 words) || s (8 words)
 #define CV_R_WORDS 32               // X, Y, Z (10 limbs each) + 2 pad (16-B aligned records)
 #define CV_FIN_CHUNK 8              // signatures per lane in the finish phase
@@ -91,21 +87,11 @@ CV_HD void fe_load(fe &f, const uint32_t *p) {
 #pragma unroll
     for (int i = 0; i < 10; i++) f.v[i] = p[i];
 }
-// EW = entry words: 40 (latency and full-width tables) or 48 (throughput tables, CV_TAB48_WORDS)
-// 48-word entries hold 2Z in the Z field (ge_add<true> multiplies by it directly); Z is tight, 2Z <= 2.02.
-template <int EW = 40> CV_HD void ge_cached_store(uint32_t *p, const ge_cached &c) {
-    static_assert(EW == 40 || EW == 48, "cached table entry: 40 or 48 words");
-    constexpr int OM = EW == 48 ? 12 : 10, OZ = EW == 48 ? 24 : 20, OT = EW == 48 ? 34 : 30;
+CV_HD void ge_cached_store(uint32_t *p, const ge_cached &c) {
     fe_store(p, c.YplusX);
-    fe_store(p + OM, c.YminusX);
-    if (EW == 48) {
-        fe z2;
-        fe_add(z2, c.Z, c.Z);
-        fe_store(p + OZ, z2);
-    } else {
-        fe_store(p + OZ, c.Z);
-    }
-    fe_store(p + OT, c.T2d);
+    fe_store(p + 10, c.YminusX);
+    fe_store(p + 20, c.Z);
+    fe_store(p + 30, c.T2d);
 }
 // 40 words, 16-byte aligned: ten 16-byte loads
 CV_HD void ge_cached_load(ge_cached &c, const uint32_t *p) {
@@ -131,26 +117,26 @@ CV_HD void ge_p3_neg(ge_p3 &r, const ge_p3 &a) {
     fe_carry(r.T, r.T);
 }
 
-// tab[k] = k * P (k = 0..8) in cached form, EW words per entry (16-B aligned); entry 0 is the
+// tab[k] = k * P (k = 0..8) in cached form, 40 words per entry (16-B aligned); entry 0 is the
 // identity (1, 1, 1, 0), so a window digit of 0 is the same lookup as any other (no identity select)
-template <int EW = 40> __host__ __device__ __forceinline__ void ge_cached_multiples8(uint32_t *tab, const ge_p3 &P1) {
+__host__ __device__ __forceinline__ void ge_cached_multiples8(uint32_t *tab, const ge_p3 &P1) {
     ge_cached c1, c;
     ge_p3 P;
     ge_cached_identity(c);
-    ge_cached_store<EW>(tab, c);
+    ge_cached_store(tab, c);
     ge_p3_to_cached(c1, P1);
-    ge_cached_store<EW>(tab + EW, c1);
+    ge_cached_store(tab + 40, c1);
     ge_p1p1 t;
     ge_p3_dbl(t, P1);
     ge_p1p1_to_p3(P, t);
     ge_p3_to_cached(c, P);
-    ge_cached_store<EW>(tab + 2 * EW, c);
+    ge_cached_store(tab + 80, c);
 #pragma unroll 1
     for (int k = 3; k <= 8; k++) {
         ge_add(t, P, c1);
         ge_p1p1_to_p3(P, t);
         ge_p3_to_cached(c, P);
-        ge_cached_store<EW>(tab + EW * k, c);
+        ge_cached_store(tab + 40 * k, c);
     }
 }
 
@@ -205,7 +191,7 @@ __host__ __device__ __forceinline__ void ge_cached_multiples8_half(uint32_t *tab
 }
 
 // Phase 1.  Returns key_ok.  hs = h || s (16 words), tab = CV_TAB_WORDS words (16-B aligned).
-template <bool LAT = false, int EW = 40> __host__ __device__ __forceinline__ bool cv_verify_prep(const uint32_t aw[8], const uint32_t rw[8], const uint32_t sw[8],
+template <bool LAT = false> __host__ __device__ __forceinline__ bool cv_verify_prep(const uint32_t aw[8], const uint32_t rw[8], const uint32_t sw[8],
                                                const uint8_t *msg, uint32_t mlen, uint32_t *hs, uint32_t *tab) {
     // hash first (its state is dead before the point decode starts: small live set)
     {
@@ -228,7 +214,7 @@ template <bool LAT = false, int EW = 40> __host__ __device__ __forceinline__ boo
     const bool key_ok = ge_decode_0_1_0<LAT>(A, aw);
     if (!key_ok) ge_p3_identity(A);
     ge_p3_neg(nA, A);
-    ge_cached_multiples8<EW>(tab, nA);
+    ge_cached_multiples8(tab, nA);
     return key_ok;
 }
 
@@ -724,7 +710,7 @@ template <bool LAT = false> __host__ __device__ __forceinline__ bool ge_decode_c
     return ok && diff == 0;
 }
 
-template <bool LAT = false, bool W16 = false, int EW = 40>
+template <bool LAT = false, bool W16 = false>
 __host__ __device__ __forceinline__ bool cv_hs_prep(const uint32_t rw[8], const uint32_t *hs, uint32_t *dig, size_t stride,
                                                     uint32_t *tabR, bool reduce = true) {
     {
@@ -753,51 +739,15 @@ __host__ __device__ __forceinline__ bool cv_hs_prep(const uint32_t rw[8], const 
     ge_p3 R;
     const bool r_ok = ge_decode_canonical<LAT>(R, rw);
     if (!r_ok) ge_p3_identity(R);
-    ge_cached_multiples8<EW>(tabR, R);
+    ge_cached_multiples8(tabR, R);
     return r_ok;
 }
 
-// entry |d| of a cached k*P table (entry 0 = identity), negated for d < 0.
-//   EW = 40: the entry's ten 16-B loads, then the branch-free negation (ge_cached_cneg: 40 VALU).
-//   EW = 48: -(Y+X, Y-X, Z, 2dT) = (Y-X, Y+X, Z, -2dT): Y+X and Y-X are loaded from the swapped addresses (each
-//     field is 16-B aligned), and -2dT = 2p - 2dT as (x XOR m) + (m AND (2p + 1)) with m all ones or zero — one
-//     v_xad_u32 per limb: ~20 VALU per lookup instead of 40 (two more 16-B loads).
-template <int EW = 40> CV_HD void tab_cached_select(ge_cached &e, const uint32_t *tab, int d) {
+// entry |d| of a cached k*P table (entry 0 = identity), negated for d < 0
+CV_HD void tab_cached_select(ge_cached &e, const uint32_t *tab, int d) {
     const int m = d < 0 ? -d : d;
-    if constexpr (EW == 40) {
-        ge_cached_load(e, tab + 40 * m);
-        ge_cached_cneg(e, d < 0);
-    } else {
-        static_assert(EW == 48, "cached table entry: 40 or 48 words");
-        const uint32_t *p = tab + 48 * m;
-        const int o = d < 0 ? 12 : 0;
-        const uint4 *qp = reinterpret_cast<const uint4 *>(p + o), *qm = reinterpret_cast<const uint4 *>(p + (12 - o));
-        const uint4 *qz = reinterpret_cast<const uint4 *>(p + 24);
-        uint32_t a[12], b[12], z[20];
-#pragma unroll
-        for (int j = 0; j < 3; j++) {
-            const uint4 u = qp[j], v = qm[j];
-            a[4 * j] = u.x; a[4 * j + 1] = u.y; a[4 * j + 2] = u.z; a[4 * j + 3] = u.w;
-            b[4 * j] = v.x; b[4 * j + 1] = v.y; b[4 * j + 2] = v.z; b[4 * j + 3] = v.w;
-        }
-#pragma unroll
-        for (int j = 0; j < 5; j++) {
-            const uint4 u = qz[j];
-            z[4 * j] = u.x; z[4 * j + 1] = u.y; z[4 * j + 2] = u.z; z[4 * j + 3] = u.w;
-        }
-        fe_load(e.YplusX, a);
-        fe_load(e.YminusX, b);
-        fe_load(e.Z, z);
-        uint32_t msk = d < 0 ? 0xffffffffu : 0u;
-#ifdef __HIP_DEVICE_COMPILE__
-        asm("" : "+v"(msk));   // an opaque mask: the xor-add stays a v_xad_u32 instead of a select
-#endif
-#pragma unroll
-        for (int i = 0; i < 10; i++) {
-            CV_ASSERT(z[10 + i] <= cv_kp(2, i), "tab_cached_select: 2dT limb exceeds 2p");
-            e.T2d.v[i] = (z[10 + i] ^ msk) + (msk & (cv_kp(2, i) + 1u));
-        }
-    }
+    ge_cached_load(e, tab + 40 * m);
+    ge_cached_cneg(e, d < 0);
 }
 
 // E = [v]R + [u]A + [w]B from the packed digits (tabA = k*(-A), tabR = k*R); nw (>= 32, uniform
@@ -805,7 +755,7 @@ template <int EW = 40> CV_HD void tab_cached_select(ge_cached &e, const uint32_t
 // W16 = false: radix-256 digits of w in the even window words, rows k*B / k*2^128*B for k = 0..128
 // (CV_BCOMB); W16 = true: radix-2^16 digit pairs in their own words, added every fourth window from
 // the CV_BW16 rows (k = 0..2^15).  Returns E == O.
-template <int BSTRIDE = CV_BTAB_STRIDE, bool W16 = false, int EW = 40>
+template <int BSTRIDE = CV_BTAB_STRIDE, bool W16 = false>
 __host__ __device__ __forceinline__ bool cv_hs_straus(const uint32_t *blo, const uint32_t *bhi, const uint32_t *dig,
                                                       size_t stride, const uint32_t *tabA, const uint32_t *tabR, int nw) {
     ge_p2 R;
@@ -830,14 +780,14 @@ __host__ __device__ __forceinline__ bool cv_hs_straus(const uint32_t *blo, const
         }
         {
             ge_cached e;
-            tab_cached_select<EW>(e, tabR, cv_sfield(dw, 5, 5));
-            ge_add<EW == 48>(t, R3, e);
+            tab_cached_select(e, tabR, cv_sfield(dw, 5, 5));
+            ge_add(t, R3, e);
         }
         ge_p1p1_to_p3(R3, t);
         {
             ge_cached e;
-            tab_cached_select<EW>(e, tabA, cv_sfield(dw, 0, 5));
-            ge_add<EW == 48>(t, R3, e);
+            tab_cached_select(e, tabA, cv_sfield(dw, 0, 5));
+            ge_add(t, R3, e);
         }
         if (W16 ? ((win & 3) == 0 && win < 32) : ((win & 1) == 0 && win < 32)) {
             int dlo, dhi;
@@ -870,14 +820,14 @@ __host__ __device__ __forceinline__ bool cv_verify_one_hs(const uint32_t *bcomb,
                                                           const uint32_t sw[8], const uint8_t *msg, uint32_t mlen,
                                                           bool *key_ok_out, uint32_t *dig_out) {
     uint32_t hs[CV_HS_WORDS];
-    alignas(16) uint32_t tab[CV_TAB48_WORDS];
-    alignas(16) uint32_t tabR[CV_TAB48_WORDS];
+    alignas(16) uint32_t tab[CV_TAB_WORDS];
+    alignas(16) uint32_t tabR[CV_TAB_WORDS];
     uint32_t dig[CV_HS_DIGWORDS];
-    const bool key_ok = cv_verify_prep<false, 48>(aw, rw, sw, msg, mlen, hs, tab);
-    const bool r_ok = cv_hs_prep<false, false, 48>(rw, hs, dig, 1, tabR);
+    const bool key_ok = cv_verify_prep(aw, rw, sw, msg, mlen, hs, tab);
+    const bool r_ok = cv_hs_prep(rw, hs, dig, 1, tabR);
     int nw = (int)dig[64];
     if (nw < 32) nw = 32;
-    const bool eq = cv_hs_straus<CV_BTAB_STRIDE, false, 48>(bcomb, bcomb + 2 * CV_BTAB_ENTRIES * CV_BTAB_STRIDE, dig, 1, tab, tabR, nw);
+    const bool eq = cv_hs_straus(bcomb, bcomb + 2 * CV_BTAB_ENTRIES * CV_BTAB_STRIDE, dig, 1, tab, tabR, nw);
     *key_ok_out = key_ok;
     if (dig_out)
         for (int q = 0; q < CV_HS_DIGWORDS; q++) dig_out[q] = dig[q];
@@ -1066,7 +1016,7 @@ CV_HD bool cv_r_canonical(const uint32_t rw[8]) {
 
 // points, both decodes interleaved in one lane (throughput form).  Returns key_ok; ok_out = key_ok
 // AND r_ok.
-template <bool LAT = false, int EW = 40>
+template <bool LAT = false>
 __host__ __device__ __forceinline__ bool cv_hs_points(const uint32_t aw[8], const uint32_t rw[8], uint32_t *tabA,
                                                       uint32_t *tabR, bool &ok_out) {
     ge_p3 P[2];
@@ -1077,8 +1027,8 @@ __host__ __device__ __forceinline__ bool cv_hs_points(const uint32_t aw[8], cons
     if (!r_ok) ge_p3_identity(P[1]);
     ge_p3 nA;
     ge_p3_neg(nA, P[0]);
-    ge_cached_multiples8<EW>(tabA, nA);
-    ge_cached_multiples8<EW>(tabR, P[1]);
+    ge_cached_multiples8(tabA, nA);
+    ge_cached_multiples8(tabR, P[1]);
     ok_out = key_ok && r_ok;
     return key_ok;
 }
@@ -1086,7 +1036,7 @@ __host__ __device__ __forceinline__ bool cv_hs_points(const uint32_t aw[8], cons
 // points, one encoding per lane (latency form: a lane pair per signature runs the two decodes side by
 // side): is_r = false decodes the key A into k*(-A), true decodes R (canonical) into k*R.  Both lanes
 // run the same instructions.  Returns the lane's decode verdict (key_ok or r_ok).
-template <bool LAT = true, int EW = 40>
+template <bool LAT = true>
 __host__ __device__ __forceinline__ bool cv_hs_point_one(const uint32_t w[8], bool is_r, uint32_t *tab,
                                                          int half = -1) {
     ge_p3 P, nP;
@@ -1096,28 +1046,28 @@ __host__ __device__ __forceinline__ bool cv_hs_point_one(const uint32_t w[8], bo
     ge_p3_neg(nP, P);
     if (!is_r) P = nP;
     if (half < 0)
-        ge_cached_multiples8<EW>(tab, P);
+        ge_cached_multiples8(tab, P);
     else
         ge_cached_multiples8_half(tab, P, half == 1);   // two lanes per point, half of the table each
     return ok;
 }
 
 // hash + scalars + points in one pass (host harness, and the reference order of the GPU kernels)
-template <bool LAT = false, int EW = 40>
+template <bool LAT = false>
 __host__ __device__ __forceinline__ bool cv_hs_prep_fused_hs(const uint32_t aw[8], const uint32_t rw[8],
                                                              const uint32_t hs[CV_HS_WORDS], uint32_t *dig,
                                                              size_t stride, uint32_t *tabA, uint32_t *tabR,
                                                              bool &ok_out) {
     cv_hs_scalars(hs, dig, stride);
-    return cv_hs_points<LAT, EW>(aw, rw, tabA, tabR, ok_out);
+    return cv_hs_points<LAT>(aw, rw, tabA, tabR, ok_out);
 }
-template <bool LAT = false, int EW = 40>
+template <bool LAT = false>
 __host__ __device__ __forceinline__ bool cv_hs_prep_fused(const uint32_t aw[8], const uint32_t rw[8], const uint32_t sw[8],
                                                           const uint8_t *msg, uint32_t mlen, uint32_t *dig, size_t stride,
                                                           uint32_t *tabA, uint32_t *tabR, bool &ok_out) {
     uint32_t hs[CV_HS_WORDS];
     cv_keyed_hs(aw, rw, sw, msg, mlen, hs);            // h = SHA-512(R || Abyte || M) mod L, effective s
-    return cv_hs_prep_fused_hs<LAT, EW>(aw, rw, hs, dig, stride, tabA, tabR, ok_out);
+    return cv_hs_prep_fused_hs<LAT>(aw, rw, hs, dig, stride, tabA, tabR, ok_out);
 }
 
 // Single-signature convenience of the fused schedule (host harness).
@@ -1125,17 +1075,14 @@ template <bool LAT = false>
 __host__ __device__ __forceinline__ bool cv_verify_one_hs_fused(const uint32_t *bcomb, const uint32_t aw[8],
                                                                 const uint32_t rw[8], const uint32_t sw[8],
                                                                 const uint8_t *msg, uint32_t mlen, bool *key_ok_out) {
-    // the throughput kernels' 48-word tables for the sequential-carry form, the latency kernels' 40-word ones
-    constexpr int EW = LAT ? 40 : 48;
-    alignas(16) uint32_t tab[CV_TAB_ENTRIES * EW];
-    alignas(16) uint32_t tabR[CV_TAB_ENTRIES * EW];
+    alignas(16) uint32_t tab[CV_TAB_WORDS];
+    alignas(16) uint32_t tabR[CV_TAB_WORDS];
     uint32_t dig[CV_HS_DIGWORDS];
     bool ok = false;
-    *key_ok_out = cv_hs_prep_fused<LAT, EW>(aw, rw, sw, msg, mlen, dig, 1, tab, tabR, ok);
+    *key_ok_out = cv_hs_prep_fused<LAT>(aw, rw, sw, msg, mlen, dig, 1, tab, tabR, ok);
     int nw = (int)dig[64];
     if (nw < 32) nw = 32;
-    const bool eq = cv_hs_straus<CV_BTAB_STRIDE, false, EW>(bcomb, bcomb + 2 * CV_BTAB_ENTRIES * CV_BTAB_STRIDE, dig, 1, tab,
-                                                            tabR, nw);
+    const bool eq = cv_hs_straus(bcomb, bcomb + 2 * CV_BTAB_ENTRIES * CV_BTAB_STRIDE, dig, 1, tab, tabR, nw);
     return ok && eq;
 }
 

@@ -33,6 +33,7 @@ EXPORTED = (
     "cv_diag_dedupe_keys", "cv_host_alloc", "cv_host_free", "cv_ed25519_verify_batch_async", "cv_wait",
     "cv_merkle_tx_ids_async", "cv_set_option", "cv_get_option", "cv_diag_stats",
     "cv_verify_transactions", "cv_verify_transactions_async", "cv_open_ex", "cv_msg_extent",
+    "cv_ed25519_verify_batch_ex",
 )
 
 # cv_set_option names (include/cordaverify.h CV_OPT_*)
@@ -108,6 +109,9 @@ def load():
         lib.cv_ed25519_verify_batch_async.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                                       ctypes.POINTER(ctypes.c_uint64)]
         lib.cv_ed25519_verify_batch_async.restype = ctypes.c_int
+        lib.cv_ed25519_verify_batch_ex.argtypes = [_vp, _sz, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, _vp, _vp,
+                                                   ctypes.POINTER(ctypes.c_uint64)]
+        lib.cv_ed25519_verify_batch_ex.restype = ctypes.c_int
         lib.cv_wait.argtypes = [_vp, ctypes.c_uint64]
         lib.cv_wait.restype = ctypes.c_int
         lib.cv_host_alloc.argtypes = [_vp, _sz, ctypes.POINTER(_vp)]
@@ -268,12 +272,14 @@ class Engine:
         ln = np.ascontiguousarray(ln, dtype=np.uint32)
         if off.shape[0] != n or ln.shape[0] != n:
             raise ValueError("off/len must have n entries")
-        if n and _msg_end(self._lib, off, ln) > arena.size:
-            raise ValueError("message range exceeds the arena")
         bitmap = np.zeros((n + 63) // 64, np.uint64)
         status = np.zeros(n, np.uint8) if want_status else None
-        _check(self._lib.cv_ed25519_verify_batch(self._h, n, _p(pk), _p(sig), _p(arena), _p(off), _p(ln),
-                                                 _p(bitmap), _p(status)), "cv_ed25519_verify_batch")
+        # the arena bound is checked by the engine's own staging scan (cv_ed25519_verify_batch_ex)
+        rc = self._lib.cv_ed25519_verify_batch_ex(self._h, n, _p(pk), _p(sig), _p(arena), arena.size, _p(off), _p(ln),
+                                                  _p(bitmap), _p(status), None)
+        if rc == -3 and n and _msg_end(self._lib, off, ln) > arena.size:
+            raise ValueError("message range exceeds the arena")
+        _check(rc, "cv_ed25519_verify_batch")
         return bitmap, status
 
     def verify_batch_async(self, pk, sig, arena, off, ln, want_status: bool = True) -> int:
@@ -289,14 +295,14 @@ class Engine:
         ln = np.ascontiguousarray(ln, dtype=np.uint32)
         if off.shape[0] != n or ln.shape[0] != n:
             raise ValueError("off/len must have n entries")
-        if n and _msg_end(self._lib, off, ln) > arena.size:
-            raise ValueError("message range exceeds the arena")
         bitmap = np.zeros((n + 63) // 64, np.uint64)
         status = np.zeros(n, np.uint8) if want_status else None
         t = ctypes.c_uint64()
-        _check(self._lib.cv_ed25519_verify_batch_async(self._h, n, _p(pk), _p(sig), _p(arena), _p(off), _p(ln),
-                                                       _p(bitmap), _p(status), ctypes.byref(t)),
-               "cv_ed25519_verify_batch_async")
+        rc = self._lib.cv_ed25519_verify_batch_ex(self._h, n, _p(pk), _p(sig), _p(arena), arena.size, _p(off), _p(ln),
+                                                  _p(bitmap), _p(status), ctypes.byref(t))
+        if rc == -3 and n and _msg_end(self._lib, off, ln) > arena.size:
+            raise ValueError("message range exceeds the arena")
+        _check(rc, "cv_ed25519_verify_batch_async")
         with self.mu:
             self._inflight[t.value] = (bitmap, status, (pk, sig, arena, off, ln))
         return t.value

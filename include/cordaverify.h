@@ -112,6 +112,16 @@ int cv_ed25519_verify_batch_async(cv_ctx *ctx, size_t n, const uint8_t *pk, cons
                                   uint64_t *verdict_bitmap, uint8_t *status, uint64_t *ticket);
 int cv_wait(cv_ctx *ctx, uint64_t ticket);
 
+/* cv_ed25519_verify_batch (ticket NULL) or its _async form (ticket non-NULL) with the arena's size: a call whose
+ * records reach past msg_arena[arena_bytes) returns CV_E_ARGS before the engine reads past it.  The check rides on
+ * the staging scan every call makes anyway (the byte range its records reach, per shard and sub-chunk), so a
+ * binding gets bounds safety without scanning the offsets itself (cv_msg_extent, an extra pass over 12 B per
+ * record).  With a ticket, records past the bound in a later shard may be found after earlier shards were
+ * enqueued: the call then waits for those before it returns CV_E_ARGS. */
+int cv_ed25519_verify_batch_ex(cv_ctx *ctx, size_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *msg_arena,
+                               uint64_t arena_bytes, const uint64_t *msg_off, const uint32_t *msg_len,
+                               uint64_t *verdict_bitmap, uint8_t *status, uint64_t *ticket);
+
 /* Pinned host memory for the host-buffer API's inputs (hipHostMalloc).  When all five input arrays of
  * cv_ed25519_verify_batch lie in pinned memory (from here, or any page-locked / registered host memory),
  * the engine DMAs each sub-chunk's records straight out of them and skips its packing copy into its own
@@ -316,9 +326,10 @@ uint64_t cv_msg_extent(size_t n, const uint64_t *msg_off, const uint32_t *msg_le
 /* Diagnostics: the host-side key dedupe cv_ed25519_verify_batch runs before choosing the keyed path
  * (seeded hash of all 32 key bytes).  Returns 1 and fills key_index[n] / *nkeys (distinct keys in
  * first-seen order) when the batch repeats keys enough for the keyed path (n >= 64, at least eight
- * signatures per distinct key), else 0.  Above 16,384 signatures a sample of 4,096 at pseudo-random
- * positions first estimates the repetition (birthday count) and a batch estimated below four signatures
- * per key is taken as distinct-keyed without hashing the rest.  Host only: needs no device and no context. */
+ * signatures per distinct key), else 0.  Above 4,096 signatures a sample of 4 sqrt(n) (512 .. 4,096) at
+ * pseudo-random positions first estimates the repetition (birthday count) and a batch estimated below four
+ * signatures per key is taken as distinct-keyed without hashing the rest.  Host only: needs no device and no
+ * context. */
 int cv_diag_dedupe_keys(size_t n, const uint8_t *pk, uint32_t *key_index, size_t *nkeys);
 
 #ifdef __cplusplus

@@ -119,9 +119,9 @@ def test_dedupe_resists_shared_key_bytes():
 
 
 def test_dedupe_gate_and_threshold():
-    """The keyed decision (cv_diag_dedupe_keys = the host dedupe cv_ed25519_verify_batch runs): at most 16,384
-    signatures are deduped in full; above, a birthday count over 4,096 pseudo-random positions skips batches
-    estimated below four signatures per key (a performance guess: the verdicts are the same either way).
+    """The keyed decision (cv_diag_dedupe_keys = the host dedupe cv_ed25519_verify_batch runs): above 4,096 signatures a
+    birthday count over 4 sqrt(n) (512 .. 4,096) pseudo-random positions skips batches estimated below four
+    signatures per key (a performance guess: the verdicts are the same either way).
     The full dedupe then takes the keyed path at eight or more signatures per distinct key, whatever the
     order of the records (a distinct-looking prefix included)."""
     rng = np.random.default_rng(9)

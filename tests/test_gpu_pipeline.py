@@ -335,3 +335,30 @@ def test_async_calls_in_flight_match_sync(engine, corpus, oracle_c):
     assert np.array_equal(_bits(r2[0], n2), e2) and int(r2[1].sum()) == kidx.size
     assert np.array_equal(_bits(r3[0], n3), corpus["verdict"][sel].astype(bool))
     assert np.array_equal(r3[1], corpus["status"][sel])
+
+
+@pytest.mark.parametrize("n", [100, 9001, 200_000])
+def test_verify_batch_ex_arena_bound(engine, corpus, n):
+    """cv_ed25519_verify_batch_ex: a record reaching past arena_bytes is rejected (CV_E_ARGS) by the engine's
+    staging scan, in the small, zero-copy and pipelined forms and in the async form, and nothing is read past the
+    bound; the same batch with the true size verifies exactly (golden tiles)."""
+    lib = native.load()
+    idx = np.arange(n) % len(corpus["pk"])
+    pk, sig = np.ascontiguousarray(corpus["pk"][idx]), np.ascontiguousarray(corpus["sig"][idx])
+    arena, off, ln = corpus["arena"], np.ascontiguousarray(corpus["off"][idx]), np.ascontiguousarray(corpus["len"][idx])
+    extent = int((off + ln.astype(np.uint64)).max())
+    p = native._p
+    for async_ in (False, True):
+        bm = np.zeros((n + 63) // 64, np.uint64)
+        t = ctypes.c_uint64()
+        rc = lib.cv_ed25519_verify_batch_ex(engine._h, n, p(pk), p(sig), p(arena), extent - 1, p(off), p(ln), p(bm),
+                                            None, ctypes.byref(t) if async_ else None)
+        assert rc == -3, (async_, rc)
+        rc = lib.cv_ed25519_verify_batch_ex(engine._h, n, p(pk), p(sig), p(arena), extent, p(off), p(ln), p(bm),
+                                            None, ctypes.byref(t) if async_ else None)
+        assert rc == 0
+        if async_:
+            assert lib.cv_wait(engine._h, t.value) == 0
+        assert np.array_equal(_bits(bm, n), corpus["verdict"][idx].astype(bool))
+    with pytest.raises(ValueError, match="exceeds the arena"):
+        engine.verify_batch(pk, sig, arena[:extent - 1], off, ln)

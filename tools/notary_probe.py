@@ -71,7 +71,9 @@ def main():
                 eng.stats("small", reset=True)
                 host = p50(lambda: eng.verify_batch(pk, sig, arena, off, ln, want_status=False), args.reps)
                 st = eng.stats("small", reset=True)
-                pinned = None
+                zc_us = {k: round(st[k + "_s"] / max(st["calls"], 1) * 1e6, 1) for k in
+                         ("setup", "pack", "launch", "sync", "assemble")} if st["calls"] else None
+                pinned = pin_us = None
                 if args.pinned:
                     pin = [eng.host_copy(x) for x in (pk, sig, arena, off, ln)]
                     eng.stats("small", reset=True)
@@ -80,9 +82,6 @@ def main():
                     pin_us = {k: round(st[k + "_s"] / max(st["calls"], 1) * 1e6, 1) for k in
                               ("setup", "pack", "launch", "sync", "assemble")} if st["calls"] else None
                     del pin
-                zc_us = {k: round(st[k + "_s"] / max(st["calls"], 1) * 1e6, 1) for k in
-                         ("setup", "pack", "launch", "sync", "assemble")} if st["calls"] else None
-                pin_us = None
                 bm_h, _ = eng.verify_batch(pk, sig, arena, off, ln, want_status=False)
                 assert np.array_equal(native.bitmap_to_bools(bm_h, n), expect)
                 d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in
