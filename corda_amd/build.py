@@ -66,7 +66,8 @@ def build(verbose: bool = False, force: bool = False) -> str:
         if force or _stale(op, [sp] + deps):
             cmd = [HIPCC] + CFLAGS + KERNEL_FLAGS + SRC_FLAGS.get(src, []) + ["-c", sp, "-o", op]
             if src.endswith(".cpp"):
-                cmd = [HIPCC, "-x", "hip"] + CFLAGS + ["-c", sp, "-o", op]
+                # host code only (no kernels): no device pass, so host-only attributes such as target_clones work
+                cmd = [HIPCC, "-x", "hip", "--offload-host-only"] + CFLAGS + ["-c", sp, "-o", op]
             cmds.append(cmd)
     jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
     if verbose:

@@ -404,12 +404,14 @@ static const OptDesc kOpt[CV_OPT_COUNT] = {
     {4096, 64, (int64_t)1 << 40},       // CV_OPT_SHARD_MIN
     {262144, 64, (int64_t)1 << 40},     // CV_OPT_SPREAD_MIN
     {262144, 1, 1 << 24},               // CV_OPT_MERKLE_CHUNK
+    {16384, 1, (int64_t)1 << 40},       // CV_OPT_PREP_OVERLAP_MIN
 };
 
 // A snapshot of a context's options, taken once per call.
 struct Opts {
     CvkPlan plan;
     size_t pipe_min, pipe_first, pipe_chunk, async_chunk, small_direct_min, shard_min, spread_min, merkle_chunk;
+    size_t prep_overlap_min;
     int threads, small_zc, auto_keyed;
 };
 
@@ -530,13 +532,17 @@ hipError_t pool_end(KeyCache &kc, hipStream_t s) {
 // One verify launch group on slot sl, stream s.  split: the drain-overlap sub-chunks may be used.
 hipError_t launch_verify(Device &d, const CvkPlan &plan, Slot &sl, uint32_t n, const uint8_t *pk, const uint8_t *sig,
                          const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint64_t *bitmap,
-                         uint8_t *status, hipStream_t s, hipEvent_t *ev, bool split) {
+                         uint8_t *status, hipStream_t s, hipEvent_t *ev, bool split,
+                         const CvkPrepOverlap *po = nullptr) {
     hipError_t e = ensure_verify_ws(sl, n);
+    const hipStream_t prev = sl.last;
     if (e == hipSuccess) e = ws_begin(d, sl, s);
+    // the helper stream writes the workspace too: it waits for the slot's previous user as s does
+    if (e == hipSuccess && po && prev && prev != s) e = hipStreamWaitEvent(po->aux, sl.ev, 0);
     if (e != hipSuccess) return e;
     if (split && plan.split && n >= 131072) (void)slot_split(d, sl);   // without a helper the chunk runs whole
     e = cvk_verify(&plan, n, pk, sig, arena, off, len, bitmap, status, sl.ws_tab.as<uint32_t>(), sl.ws_ok.as<uint8_t>(),
-                   sl.ws_dig.as<uint32_t>(), sl.ws_cap, s, ev, split && sl.split.s2 ? &sl.split : nullptr);
+                   sl.ws_dig.as<uint32_t>(), sl.ws_cap, s, ev, split && sl.split.s2 ? &sl.split : nullptr, po);
     const hipError_t e2 = ws_end(sl, s);
     return e != hipSuccess ? e : e2;
 }
@@ -598,6 +604,7 @@ struct cv_ctx {
         o.shard_min = (size_t)opt[CV_OPT_SHARD_MIN].load();
         o.spread_min = (size_t)opt[CV_OPT_SPREAD_MIN].load();
         o.merkle_chunk = (size_t)opt[CV_OPT_MERKLE_CHUNK].load();
+        o.prep_overlap_min = (size_t)opt[CV_OPT_PREP_OVERLAP_MIN].load();
         return o;
     }
 };
@@ -952,19 +959,45 @@ static void par_copy(const std::vector<CopyJob> &jobs, WorkerPool *pool) {
 struct Span {
     uint64_t lo = UINT64_MAX, hi = 0, bytes = 0;
 };
+// One slice of arena_span.  The unsigned 64-bit min / max vectorise only with AVX2 (the x86-64 baseline has
+// no 64-bit compare): the AVX2 instance runs where the CPU has it (65,536 records: 150 -> 48 us on one core
+// of this build host).  Dispatched by a cached cpuid test rather than target_clones, whose load-time resolver
+// runs before ThreadSanitizer's runtime is up (tests/sanitize).
+template <int> static inline void span_slice_impl(size_t i0, size_t i1, const uint64_t *off, const uint32_t *len,
+                                                  uint64_t *out) {
+    uint64_t lo = UINT64_MAX, hi = 0, bytes = 0;
+    for (size_t i = i0; i < i1; i++) {
+        lo = std::min<uint64_t>(lo, off[i]);
+        hi = std::max<uint64_t>(hi, off[i] + len[i]);
+        bytes += len[i];
+    }
+    out[0] = lo;
+    out[1] = hi;
+    out[2] = bytes;
+}
+__attribute__((target("avx2"))) static void span_slice_avx2(size_t i0, size_t i1, const uint64_t *off,
+                                                            const uint32_t *len, uint64_t *out) {
+    span_slice_impl<1>(i0, i1, off, len, out);
+}
+static void span_slice(size_t i0, size_t i1, const uint64_t *off, const uint32_t *len, uint64_t *out) {
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2)
+        span_slice_avx2(i0, i1, off, len, out);
+    else
+        span_slice_impl<0>(i0, i1, off, len, out);
+}
 static Span arena_span(size_t b, size_t e, const uint64_t *off, const uint32_t *len, WorkerPool *pool) {
-    constexpr size_t kSlice = 65536;
+    // with a pool: slices of 8,192 records, so a notary batch of 16,384-131,072 spreads over the workers
+    // (its staging plan is on the call's critical path: ~54 us at 65,536 on one core)
+    const size_t kSlice = pool ? 8192 : 65536;
     const size_t nslices = (e - b + kSlice - 1) / kSlice;
     std::vector<Span> part(std::max<size_t>(nslices, 1));
     auto scan = [&](size_t k) {
-        Span r;
-        const size_t i1 = std::min(e, b + (k + 1) * kSlice);
-        for (size_t i = b + k * kSlice; i < i1; i++) {
-            r.lo = std::min<uint64_t>(r.lo, off[i]);
-            r.hi = std::max<uint64_t>(r.hi, off[i] + len[i]);
-            r.bytes += len[i];
-        }
-        part[k] = r;
+        uint64_t r[3];
+        span_slice(b + k * kSlice, std::min(e, b + (k + 1) * kSlice), off, len, r);
+        part[k].lo = r[0];
+        part[k].hi = r[1];
+        part[k].bytes = r[2];
     };
     if (pool && nslices > 1)
         pool->run(nslices, scan);
@@ -1075,11 +1108,12 @@ static bool stage_direct(const Stage &st, size_t b, const uint8_t *pk, const uin
 // profiles/r03d_timeline_pinned.txt).
 static hipError_t stage_dma_direct(const Stage &st, uint8_t *dv, size_t b, const uint8_t *pk, const uint32_t *kidx,
                                    const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
-                                   hipStream_t s) {
+                                   hipStream_t s, hipEvent_t keys_sigs = nullptr) {
     const size_t n = st.n;
     hipError_t e = st.keyed ? hipMemcpyAsync(dv + st.o_kidx, kidx + b, n * 4, hipMemcpyHostToDevice, s)
                             : hipMemcpyAsync(dv + st.o_pk, pk + b * 32, n * 32, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(dv + st.o_sig, sig + b * 64, n * 64, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && keys_sigs) e = hipEventRecord(keys_sigs, s);   // (keys | key indices) and signatures
     if (e == hipSuccess) e = hipMemcpyAsync(dv + st.o_off, off + b, n * 8, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(dv + st.o_len, len + b, n * 4, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && st.hi > st.lo)
@@ -1523,7 +1557,20 @@ static int verify_shard_small(cv_ctx *ctx, Device &d, const Opts &o, size_t b, s
     CV_TRY(d.bitmap.ensure(total_out));
     uint8_t *h = sl.pin_in.as<uint8_t>();
     uint8_t *dv = sl.packed.as<uint8_t>();
-    auto drain = on_exit([s] { (void)hipStreamSynchronize(s); });   // error paths: no DMA outlives the call
+    // Prep overlap from prep_overlap_min: the point decodes (keys and signatures only) start on the slot's
+    // helper stream as soon as those are resident, beside the DMA of offsets, lengths and messages and the
+    // scalars (cvk_verify, CvkPrepOverlap)
+    CvkPrepOverlap po;
+    if (n >= o.prep_overlap_min && slot_split(d, sl) == hipSuccess) {
+        po.aux = sl.split.s2;
+        po.ready = sl.split.start;
+        po.done = sl.split.done2;
+    }
+    hipStream_t aux = po.aux;
+    auto drain = on_exit([s, aux] {   // error paths: no DMA or helper-stream kernel outlives the call
+        (void)hipStreamSynchronize(s);
+        if (aux) (void)hipStreamSynchronize(aux);
+    });
     t[1] = now_s();
     // Two-stage staging above 1 MB of keys + signatures: they are packed and their DMA is issued
     // first, so it runs while the offsets, lengths and message bytes are packed (notary 65,536:
@@ -1532,23 +1579,26 @@ static int verify_shard_small(cv_ctx *ctx, Device &d, const Opts &o, size_t b, s
     // below small_direct_min signatures one packed DMA beats five direct ones even from pinned arrays
     // (notary 4,096: 0.328 ms p50 packed vs 0.342 direct; 65,536: 1.28 vs 1.10, profiles/r03h_bench.json)
     if (n >= o.small_direct_min && stage_direct(st, b, in.pk, nullptr, in.sig, in.arena, in.off, in.len)) {
-        CV_TRY(stage_dma_direct(st, dv, b, in.pk, nullptr, in.sig, in.arena, in.off, in.len, s));
+        CV_TRY(stage_dma_direct(st, dv, b, in.pk, nullptr, in.sig, in.arena, in.off, in.len, s, po.ready));
     } else {
         hipError_t e1 = hipSuccess;
         stage_pack(st, h, b, in.pk, nullptr, in.sig, in.arena, in.off, in.len, pool, [&] {
             if (two_stage) e1 = hipMemcpyAsync(dv, h, st.o_off, hipMemcpyHostToDevice, s);
+            if (two_stage && e1 == hipSuccess && po.ready) e1 = hipEventRecord(po.ready, s);
         });
         CV_TRY(e1);
         if (two_stage)
             CV_TRY(hipMemcpyAsync(dv + st.o_off, h + st.o_off, st.total - st.o_off, hipMemcpyHostToDevice, s));
         else
             CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, s));
+        if (!two_stage && po.ready) CV_TRY(hipEventRecord(po.ready, s));
     }
     t[2] = now_s();
     uint8_t *dout = d.bitmap.as<uint8_t>();
     CV_TRY(launch_verify(d, o.plan, sl, (uint32_t)n, dv + st.o_pk, dv + st.o_sig, dv + st.o_ar - st.lo,
                          reinterpret_cast<const uint64_t *>(dv + st.o_off), reinterpret_cast<const uint32_t *>(dv + st.o_len),
-                         reinterpret_cast<uint64_t *>(dout + o_bm), in.status ? dout + o_st : nullptr, s, nullptr, true));
+                         reinterpret_cast<uint64_t *>(dout + o_bm), in.status ? dout + o_st : nullptr, s, nullptr, true,
+                         po.aux ? &po : nullptr));
     CV_TRY(hipMemcpyAsync(d.pin_out.p, dout, in.status ? o_st + n : words * 8, hipMemcpyDeviceToHost, s));
     t[3] = now_s();
     CV_TRY(hipStreamSynchronize(s));

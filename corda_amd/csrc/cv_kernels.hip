@@ -112,9 +112,12 @@ hipError_t cvk_verify_tri_zc(const CvkPlan *plan, uint32_t n, const uint8_t *pk,
 hipError_t cvk_verify(const CvkPlan *plan, uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
                       const uint64_t *off, const uint32_t *len, uint64_t *bitmap, uint8_t *status, uint32_t *ws_tab,
                       uint8_t *ws_ok, uint32_t *ws_dig, uint32_t ws_cap, hipStream_t stream, hipEvent_t *ev,
-                      const CvkSplit *ax) {
+                      const CvkSplit *ax, const CvkPrepOverlap *po) {
     if (n == 0) return hipSuccess;
     if (!plan || ws_cap == 0 || ws_cap % 512) return hipErrorInvalidValue;
+    // prep overlap (one chunk only): points on po->aux after po->ready, scalars here, Straus after both
+    const bool ov = po && po->aux && po->ready && po->done && n <= ws_cap && !ev;
+    if (ov) (void)hipStreamWaitEvent(po->aux, po->ready, 0);
     // the radix-2^16 basepoint rows, for the throughput and quad forms
     const uint32_t *bw16 = nullptr;
     if (n > plan->tri_max || n > plan->quad_max) {
@@ -132,7 +135,24 @@ hipError_t cvk_verify(const CvkPlan *plan, uint32_t n, const uint8_t *pk, const 
             // tri-chain Straus ORs each wave's bits in
             const bool tri = m <= plan->tri_max;
             const uint32_t nbp = ((tri ? 4 : 2) * m + 63) / 64, nbs = (m + 63) / 64;
-            if (tri)
+            if (ov) {
+                // the same kernel as two launches: point blocks only (grid nbp) on aux, scalar blocks only
+                // (nbp = 0) here; the scalar blocks also clear the verdict words
+                if (tri) {
+                    hipLaunchKernelGGL((cv_prep_lat_kernel<true, false>), dim3(nbp), dim3(64), 0, po->aux, m, ws_cap, nbp,
+                                       1u, pk, sig, arena, off, len, ws_dig, ws_tab, ws_tabR, ws_ok, status, bitmap);
+                    (void)hipEventRecord(po->done, po->aux);
+                    hipLaunchKernelGGL((cv_prep_lat_kernel<true, false>), dim3(nbs), dim3(64), 0, stream, m, ws_cap, 0u, 1u,
+                                       pk, sig, arena, off, len, ws_dig, ws_tab, ws_tabR, ws_ok, status, bitmap);
+                } else {
+                    hipLaunchKernelGGL((cv_prep_lat_kernel<false, false>), dim3(nbp), dim3(64), 0, po->aux, m, ws_cap, nbp,
+                                       0u, pk, sig, arena, off, len, ws_dig, ws_tab, ws_tabR, ws_ok, status, bitmap);
+                    (void)hipEventRecord(po->done, po->aux);
+                    hipLaunchKernelGGL((cv_prep_lat_kernel<false, false>), dim3(nbs), dim3(64), 0, stream, m, ws_cap, 0u, 0u,
+                                       pk, sig, arena, off, len, ws_dig, ws_tab, ws_tabR, ws_ok, status, bitmap);
+                }
+                (void)hipStreamWaitEvent(stream, po->done, 0);
+            } else if (tri)
                 hipLaunchKernelGGL((cv_prep_lat_kernel<true, false>), dim3(nbp + nbs), dim3(64), 0, stream, m, ws_cap, nbp, 1u,
                                    pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_dig,
                                    ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr, bitmap + (size_t)c0 / 64);
@@ -158,7 +178,7 @@ hipError_t cvk_verify(const CvkPlan *plan, uint32_t n, const uint8_t *pk, const 
         // (90 %) on `stream` and a tail on the slot's helper stream starting with it, so the tail's waves
         // fill the head's drain (1M signatures = 5.09 rounds of 3,072 resident waves: 11.0-11.2 -> 10.7 ms).
         bool split = false;
-        if (ax && ax->s2 && plan->split && !ev && m >= 131072) {
+        if (!ov && ax && ax->s2 && plan->split && !ev && m >= 131072) {
             const uint32_t resident = (uint32_t)ax->cus * 4u * 3u;   // hs_straus waves in one round
             const uint32_t last = ((m + 63) / 64) % resident;
             split = plan->split == 2 || (resident && last && last * 100u <= resident * 12u);
@@ -189,6 +209,17 @@ hipError_t cvk_verify(const CvkPlan *plan, uint32_t n, const uint8_t *pk, const 
             continue;
         }
         // throughput group: scalars (hash, lattice, digits) | points (decodes, tables) | hs_straus
+        if (ov) {
+            hipLaunchKernelGGL((cv_points_one_kernel<3, false>), dim3((2 * m + CV_BLOCK - 1) / CV_BLOCK), dim3(CV_BLOCK), 0,
+                               po->aux, m, pk, sig, ws_tab, ws_tabR, ws_ok, status);
+            (void)hipEventRecord(po->done, po->aux);
+            hipLaunchKernelGGL(cv_scalars_kernel<3>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, pk, sig, arena, off,
+                               len, ws_dig);
+            (void)hipStreamWaitEvent(stream, po->done, 0);
+            hipLaunchKernelGGL(cv_hs_straus_kernel<3>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, ws_dig, ws_tab,
+                               ws_tabR, ws_ok, bitmap, bw16);
+            continue;
+        }
         launch_prep_tp<false>(m, ws_cap, pk + (size_t)c0 * 32, sig + (size_t)c0 * 64, arena, off + c0, len + c0, ws_dig,
                               ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr, stream,
                               ev && c0 == 0 ? ev[1] : nullptr);

@@ -13,6 +13,15 @@ struct CvkSplit {
     int cus = 0;   // compute units of the device (resident waves per round = cus * 4 SIMDs * 3 waves)
 };
 
+// Prep overlap of a one-chunk verify (cv_api.cpp verify_shard_small): the caller records `ready` on the
+// launch stream once the keys and signatures are enqueued for DMA, before the offsets, lengths and message
+// bytes.  The point decodes and tables (which read only keys and signatures) wait for `ready` on `aux` and run
+// beside the rest of the DMA and the scalars; the launch stream waits for `done` before the Straus kernel.
+struct CvkPrepOverlap {
+    hipStream_t aux = nullptr;
+    hipEvent_t ready = nullptr, done = nullptr;
+};
+
 // The launch plan of one verify call, from the context's options (cv_set_option): which kernel form a
 // batch of n signatures takes.  Read per call, so no launcher state is shared between contexts.
 struct CvkPlan {
@@ -26,10 +35,11 @@ extern "C" {
 // Verify n signatures with the workspace (capacity ws_cap signatures, a multiple of 512), in chunks of
 // ws_cap.  split == nullptr disables the drain-overlap sub-chunks (the host pipeline overlaps its own
 // sub-chunks across slots instead).  ev (optional, 4 events): phase boundaries of the first chunk.
+// po (optional): prep overlap, taken when the batch is one chunk and ev is null (else ignored).
 hipError_t cvk_verify(const CvkPlan *plan, uint32_t n, const uint8_t *pk, const uint8_t *sig, const uint8_t *arena,
                       const uint64_t *off, const uint32_t *len, uint64_t *bitmap, uint8_t *status, uint32_t *ws_tab,
                       uint8_t *ws_ok, uint32_t *ws_dig, uint32_t ws_cap, hipStream_t stream, hipEvent_t *ev,
-                      const CvkSplit *split);
+                      const CvkSplit *split, const CvkPrepOverlap *po);
 hipError_t cvk_sign(uint32_t n, const uint8_t *seed, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
                     uint8_t *pk, uint8_t *sig, hipStream_t stream);
 hipError_t cvk_pmt_verify(uint32_t ntrees, const uint8_t *kind, const uint32_t *left, const uint32_t *right,

@@ -19,7 +19,7 @@ extern "C" {
 // launcher stubs: nothing in this test reaches the device
 hipError_t cvk_verify(const CvkPlan *, uint32_t, const uint8_t *, const uint8_t *, const uint8_t *, const uint64_t *,
                       const uint32_t *, uint64_t *, uint8_t *, uint32_t *, uint8_t *, uint32_t *, uint32_t, hipStream_t,
-                      hipEvent_t *, const CvkSplit *) { return hipErrorNoDevice; }
+                      hipEvent_t *, const CvkSplit *, const CvkPrepOverlap *) { return hipErrorNoDevice; }
 hipError_t cvk_sign(uint32_t, const uint8_t *, const uint8_t *, const uint64_t *, const uint32_t *, uint8_t *, uint8_t *,
                     hipStream_t) { return hipErrorNoDevice; }
 hipError_t cvk_pmt_verify(uint32_t, const uint8_t *, const uint32_t *, const uint32_t *, const uint8_t *, const uint32_t *,

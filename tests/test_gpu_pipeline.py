@@ -362,3 +362,39 @@ def test_verify_batch_ex_arena_bound(engine, corpus, n):
         assert np.array_equal(_bits(bm, n), corpus["verdict"][idx].astype(bool))
     with pytest.raises(ValueError, match="exceeds the arena"):
         engine.verify_batch(pk, sig, arena[:extent - 1], off, ln)
+
+
+@pytest.mark.parametrize("n,overlap_min", [(1000, 64), (16384, 16384), (32768, 16384), (65536, 16384)])
+def test_notary_midsize_forms_golden_and_oracle(engine, corpus, oracle_c, n, overlap_min):
+    """Notary batches from the tri form to the mid sizes (16,384 and 32,768: quad form; 65,536: throughput form),
+    unpipelined host path, with the prep overlap (point decodes on the slot's helper stream once keys and
+    signatures are resident, beside the rest of the DMA and the scalars: CV_OPT_PREP_OVERLAP_MIN) and without it,
+    from pageable and pinned inputs: a golden tile (1/16 of the records drawn from the corpus's rejected classes)
+    gives the pinned verdicts and status bytes, and a corrupted random batch the C oracle's."""
+    rng = np.random.default_rng(n + 101)
+    rej = np.where(corpus["verdict"] == 0)[0]
+    acc = np.where(corpus["verdict"] == 1)[0]
+    sel = rng.choice(acc, n)
+    bad = rng.random(n) < 1 / 16
+    sel[bad] = rng.choice(rej, int(bad.sum()))
+    gold = (corpus["pk"][sel], corpus["sig"][sel], corpus["arena"], corpus["off"][sel], corpus["len"][sel])
+    seeds = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    arena = rng.integers(0, 256, n * 32 + 16, dtype=np.uint8)
+    off = np.arange(n, dtype=np.uint64) * 32
+    ln = np.full(n, 32, np.uint32)
+    pk, sig = engine.sign_batch(seeds, arena, off, ln)
+    sig[1::5, 35] ^= 4
+    sig[3::11, 63] |= 0x20                      # S >= 2^253 on some records
+    pk[2::7, 3] ^= 0x40
+    rand = (pk, sig, arena, off, ln)
+    ref, rst = oracle_c.verify_batch(pk, sig, arena, off, ln, nthreads=8)
+    for om in (1 << 40, overlap_min):
+        with _opts(engine, prep_overlap_min=om, small_zero_copy=0):
+            for arrs, ev, es in ((gold, corpus["verdict"][sel], corpus["status"][sel]), (rand, ref, rst)):
+                for pinned in (False, True):
+                    a = [engine.host_copy(x) for x in arrs] if pinned else arrs
+                    bitmap, status = engine.verify_batch(*a)
+                    assert np.array_equal(_bits(bitmap, n), ev.astype(bool)), (om, pinned)
+                    assert np.array_equal(status, es), (om, pinned)
+                    if n % 64:
+                        assert int(bitmap[-1]) >> (n % 64) == 0
