@@ -40,7 +40,8 @@ Extra fields on the JSON line:
   notary        C4: p50/p99 end-to-end latency of a 4096-signature notary batch (host buffers in and
                 out, 1/16 adversarial records from the golden corpus's rejected classes), with the
                 p50 breakdown (transfers + host, launch + sync, per kernel) and the CPU restatement on
-                the same batch; notary_sweep = the same at 2^k, k = 8..16 (k != 12); notary_keyed = 64 signers
+                the same batch; notary_sweep = the same at 2^k, k = 8..16 (k != 12), pageable p50/p99, with
+                notary_sweep_pinned the p50 from cv_host_alloc inputs; notary_keyed = 64 signers
   resolve_chain p50/p99 latency of a 5,000-tx dependency chain (2 signers/tx, 6 leaves/tx): one
                 Merkle call + one verify call + per-tx AND with the id check
 The printed line keeps every headline value and stays under ~4 KB; per-kernel breakdowns and the full
@@ -1226,6 +1227,8 @@ def main():
                                 "cpu_threads": N.get("cpu_threads"),
                                 "kernels_ms": {k: r3(v) for k, v in N.get("breakdown_p50_ms", {}).get("kernels", {}).items()}}
             result["notary_sweep_p50_p99_ms"] = {str(x["batch"]): [r3(x["p50_ms"]), r3(x["p99_ms"])] for x in D_["notary_sweep"]}
+            result["notary_sweep_pinned_p50_ms"] = {str(x["batch"]): r3(x["pinned_inputs"]["p50_ms"])
+                                                    for x in D_["notary_sweep"]}
             result["notary_keyed_p50_ms"] = r3(D_["notary_keyed"]["p50_ms"])
             result["resolve_chain"] = {"p50_ms": r3(D_["resolve_chain"]["p50_ms"]),
                                        "cpu_p50_ms": r3(D_["resolve_chain"].get("cpu_p50_ms"))}

@@ -219,6 +219,9 @@ class WorkerPool {
         for (auto &t : th_) t.join();
     }
     int threads() const { return (int)th_.size() + 1; }
+    // The caller works through the tasks too and returns once every task is done and every helper that
+    // joined has left: helpers still asleep are not waited for (their wake-up, 10-30 us, used to be on
+    // every call's critical path), and one that wakes after the run finds no job and sleeps again.
     void run(size_t ntasks, const std::function<void(size_t)> &fn) {
         if (ntasks == 0) return;
         if (th_.empty() || ntasks == 1) {
@@ -230,19 +233,22 @@ class WorkerPool {
             job_ = &fn;
             ntasks_ = ntasks;
             next_.store(0);
-            busy_ = th_.size();
+            done_.store(0);
             gen_++;
         }
         cv_.notify_all();
         drain(fn, ntasks);
         std::unique_lock<std::mutex> lk(mu_);
-        done_cv_.wait(lk, [this] { return busy_ == 0; });
+        done_cv_.wait(lk, [&] { return active_ == 0 && done_.load() == ntasks; });
         job_ = nullptr;
     }
 
   private:
     void drain(const std::function<void(size_t)> &fn, size_t ntasks) {
-        for (size_t i; (i = next_.fetch_add(1)) < ntasks;) fn(i);
+        for (size_t i; (i = next_.fetch_add(1)) < ntasks;) {
+            fn(i);
+            done_.fetch_add(1);
+        }
     }
     void loop() {
         uint64_t seen = 0;
@@ -254,13 +260,15 @@ class WorkerPool {
                 cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
                 if (stop_) return;
                 seen = gen_;
+                if (!job_) continue;   // that run is over
                 job = job_;
                 ntasks = ntasks_;
+                active_++;
             }
             drain(*job, ntasks);
             {
                 std::lock_guard<std::mutex> g(mu_);
-                if (--busy_ == 0) done_cv_.notify_one();
+                if (--active_ == 0) done_cv_.notify_one();
             }
         }
     }
@@ -268,8 +276,8 @@ class WorkerPool {
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
     const std::function<void(size_t)> *job_ = nullptr;
-    size_t ntasks_ = 0, busy_ = 0;
-    std::atomic<size_t> next_{0};
+    size_t ntasks_ = 0, active_ = 0;
+    std::atomic<size_t> next_{0}, done_{0};
     uint64_t gen_ = 0;
     bool stop_ = false;
 };
@@ -404,7 +412,7 @@ static const OptDesc kOpt[CV_OPT_COUNT] = {
     {4096, 64, (int64_t)1 << 40},       // CV_OPT_SHARD_MIN
     {262144, 64, (int64_t)1 << 40},     // CV_OPT_SPREAD_MIN
     {262144, 1, 1 << 24},               // CV_OPT_MERKLE_CHUNK
-    {16384, 1, (int64_t)1 << 40},       // CV_OPT_PREP_OVERLAP_MIN
+    {32768, 1, (int64_t)1 << 40},       // CV_OPT_PREP_OVERLAP_MIN
 };
 
 // A snapshot of a context's options, taken once per call.

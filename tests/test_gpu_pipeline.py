@@ -364,7 +364,7 @@ def test_verify_batch_ex_arena_bound(engine, corpus, n):
         engine.verify_batch(pk, sig, arena[:extent - 1], off, ln)
 
 
-@pytest.mark.parametrize("n,overlap_min", [(1000, 64), (16384, 16384), (32768, 16384), (65536, 16384)])
+@pytest.mark.parametrize("n,overlap_min", [(1000, 64), (16384, 16384), (32768, 32768), (65536, 32768)])
 def test_notary_midsize_forms_golden_and_oracle(engine, corpus, oracle_c, n, overlap_min):
     """Notary batches from the tri form to the mid sizes (16,384 and 32,768: quad form; 65,536: throughput form),
     unpipelined host path, with the prep overlap (point decodes on the slot's helper stream once keys and
