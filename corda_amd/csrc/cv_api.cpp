@@ -739,10 +739,17 @@ int cv_open_ex(uint32_t device_mask, int slots_per_device, cv_ctx **out) {
             // Created lazily, after the device API's split helpers or a caller's own streams, the copy
             // stream could share a queue with a compute stream and its copies wait behind that stream's
             // kernels (C5 host path 86-90 -> 75 ms, profiles/r03p_c5host_eager_streams_ab.log).
+            // The copy and result-copy streams are created at the highest stream priority: the runtime keeps a
+            // separate hardware-queue pool per priority, so they get queues of their own whatever the
+            // process created before (with 4 normal-priority queues already shared by a caller's streams, the
+            // synchronous C2 call slowed 10.4 -> 11.8 ms, gpurun_out/r05k).
             hipStream_t s1 = nullptr;
-            if (hipSetDevice(d) != hipSuccess || hipStreamCreateWithFlags(&dd.stream, hipStreamNonBlocking) != hipSuccess ||
-                slot_stream(dd, 1, &s1) != hipSuccess || hipStreamCreateWithFlags(&dd.copy, hipStreamNonBlocking) != hipSuccess ||
-                hipStreamCreateWithFlags(&dd.outs, hipStreamNonBlocking) != hipSuccess) {
+            int prio_lo = 0, prio_hi = 0;
+            if (hipSetDevice(d) != hipSuccess || hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
+                hipStreamCreateWithFlags(&dd.stream, hipStreamNonBlocking) != hipSuccess ||
+                slot_stream(dd, 1, &s1) != hipSuccess ||
+                hipStreamCreateWithPriority(&dd.copy, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+                hipStreamCreateWithPriority(&dd.outs, hipStreamNonBlocking, prio_hi) != hipSuccess) {
                 cv_close(ctx);
                 return CV_E_HIP;
             }
