@@ -98,7 +98,7 @@ def log(*a):
 
 # The PMC record of the dominant kernel on the current kernel code: scripts/pmc.sh + tools/pmc_summary.py, named
 # with the commit it was measured on (the round-3 file described an older build)
-PMC_HS_FILE = "profiles/pmc_hs_straus_db4f697c32.json"
+PMC_HS_FILE = "profiles/pmc_hs_straus_fc6614b.json"
 
 
 def pmc_traffic(n: int):

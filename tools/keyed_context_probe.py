@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Why the keyed host call is slower inside bench.py than alone: one engine, the keyed host
+call (C2, 1,024-key pool, pinned, two async calls in flight) measured fresh, then again after each step of the
+bench's sequence — a device-resident keyed run on a torch stream (bench.py keyed_rate) and a device-resident
+C2 run on two torch streams — with the host pipeline's phase times per call.
+
+    python tools/keyed_context_probe.py [--calls 8]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from corda_amd import native, workload  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--calls", type=int, default=8)
+    ap.add_argument("--order", default="host,dev_keyed,host,dev_c2,host")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    eng = native.Engine(1)
+    sh = torch.cuda.Stream(dev)
+    n = 1_000_000
+    b = workload.make_batch(eng, 0, n, 300, seed=4243, key_pool=1024, stream=sh.cuda_stream)
+    host = tuple(eng.host_copy(x) for x in b.to_host())
+    del b
+    torch.cuda.empty_cache()
+
+    def host_keyed(tag):
+        def loop(k):
+            pend, bm = [], None
+            for _ in range(k):
+                pend.append(eng.verify_batch_async(*host, want_status=False))
+                if len(pend) == 2:
+                    bm, _ = eng.wait(pend.pop(0))
+            for t in pend:
+                bm, _ = eng.wait(t)
+            return bm
+        loop(2)
+        eng.stats("pipe", reset=True)
+        t = time.perf_counter()
+        bm = loop(a.calls)
+        dt = (time.perf_counter() - t) / a.calls
+        st = eng.stats("pipe", reset=True)
+        assert native.bitmap_to_bools(bm, n).all()
+        print(json.dumps({"step": tag, "keyed_host_async_ms_per_call": dt * 1e3,
+                          "host_ms_per_call": {k[:-2]: round(v / a.calls * 1e3, 3) for k, v in st.items()
+                                               if k.endswith("_s")}}), flush=True)
+
+    def dev_keyed():
+        kb = workload.make_batch(eng, 0, n, 300, seed=4242, key_pool=1024, stream=sh.cuda_stream)
+        bm = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+        args = (0, n, kb.nkeys, kb.pk.data_ptr(), kb.key_index.data_ptr(), kb.sig.data_ptr(), kb.arena.data_ptr(),
+                kb.off.data_ptr(), kb.len.data_ptr(), bm.data_ptr(), 0, sh.cuda_stream)
+        for _ in range(6):
+            eng.verify_device_keyed(*args, timed=True)
+        torch.cuda.synchronize()
+        del kb, bm
+        torch.cuda.empty_cache()
+
+    def dev_c2():
+        cb = workload.make_batch(eng, 0, n, 300, seed=77, stream=sh.cuda_stream)
+        streams = [sh, torch.cuda.Stream(dev)]
+        bms = [torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev) for _ in streams]
+        torch.cuda.synchronize()
+        for k in range(12):
+            s = streams[k % 2]
+            eng.verify_device(0, n, cb.pk.data_ptr(), cb.sig.data_ptr(), cb.arena.data_ptr(), cb.off.data_ptr(),
+                              cb.len.data_ptr(), bms[k % 2].data_ptr(), 0, s.cuda_stream)
+        torch.cuda.synchronize()
+        del cb, bms
+        torch.cuda.empty_cache()
+
+    steps = {"dev_keyed": dev_keyed, "dev_c2": dev_c2}
+    for i, st in enumerate(a.order.split(",")):
+        if st == "host":
+            host_keyed(f"host#{i}")
+        else:
+            steps[st]()
+            print(json.dumps({"step": st, "done": True}), flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
