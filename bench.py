@@ -160,8 +160,15 @@ def host_api_rate(eng, batch, steps: int, device_value: float, name: str, async_
     asteps = async_steps or steps
 
     def timed_async(a):
-        """K calls with two in flight (cv_ed25519_verify_batch_async / cv_wait): submit k+1, then wait k."""
-        eng.wait(eng.verify_batch_async(*a, want_status=False))
+        """K calls with two in flight (cv_ed25519_verify_batch_async / cv_wait): submit k+1, then wait k.
+        Warm-up: five calls, so every input-ring block has carried an async-sized sub-chunk (see host_keyed_rate)."""
+        pend = []
+        for _ in range(5):
+            pend.append(eng.verify_batch_async(*a, want_status=False))
+            if len(pend) == 2:
+                eng.wait(pend.pop(0))
+        for tk in pend:
+            eng.wait(tk)
         t = time.perf_counter()
         pend = []
         for _ in range(asteps):
@@ -376,11 +383,17 @@ def host_keyed_rate(eng, local, sh, n: int, msg_len: int, steps: int, device_val
         return bm
 
     eng.stats("route", reset=True)
-    loop(2, False)
+    # warm until every block of the device's 16-block input ring has carried a keyed sub-chunk (4 per call): a
+    # block first grows to the call's sub-chunk size at its next use, and growing frees device memory, which
+    # synchronises the device — inside the timed calls that cost ~2 ms per call (9.1-9.3 vs 7.3 ms per call
+    # with a 2-call warm-up after the C2 host calls had sized the blocks for their smaller sub-chunks; r05s)
+    loop(6, False)
     assert eng.stats("route")["keyed_shards"] >= 1, "the host keyed path was not taken"
+    eng.stats("pipe", reset=True)
     t = time.perf_counter()
     bm = loop(steps, False)
     dt = time.perf_counter() - t
+    st = eng.stats("pipe", reset=True)
     assert native.bitmap_to_bools(bm, n).all(), "host keyed path rejected an honest signature"
     t = time.perf_counter()
     loop(max(2, steps // 2), True)
@@ -391,6 +404,7 @@ def host_keyed_rate(eng, local, sh, n: int, msg_len: int, steps: int, device_val
             "ratio_to_device_value": v / device_value, "device_value": device_value,
             "sync_pinned_value": n / dts, "pcie_bound_value": pcie_gbs * 1e9 / per_sig,
             "ratio_to_pcie_bound": v / (pcie_gbs * 1e9 / per_sig),
+            "host_ms_per_call": {k[:-2]: st[k] / steps * 1e3 for k in st if k.endswith("_s")},
             "path": "cv_ed25519_verify_batch_async on plain records with a 1,024-key pool from pinned buffers, two "
                     "in flight; host dedupe + keyed pipeline"}
 

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Why the keyed host call is slower inside bench.py than alone: one engine, the keyed host
 call (C2, 1,024-key pool, pinned, two async calls in flight) measured fresh, then again after each step of the
-bench's sequence — a device-resident keyed run on a torch stream (bench.py keyed_rate) and a device-resident
-C2 run on two torch streams — with the host pipeline's phase times per call.
+bench's sequence — a device-resident keyed run on a torch stream (bench.py keyed_rate), a device-resident
+C2 run on two torch streams, C2 host calls from pinned or pageable buffers (bench.py host_api_rate) — with the
+host pipeline's phase times per call (--order picks the sequence).
 
     python tools/keyed_context_probe.py [--calls 8]
 """
@@ -22,7 +23,7 @@ from corda_amd import native, workload  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=8)
-    ap.add_argument("--order", default="host,dev_keyed,host,dev_c2,host")
+    ap.add_argument("--order", default="host,c2_host_pinned,host,c2_host_pageable,host")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     eng = native.Engine(1)
@@ -78,7 +79,62 @@ def main():
         del cb, bms
         torch.cuda.empty_cache()
 
-    steps = {"dev_keyed": dev_keyed, "dev_c2": dev_c2}
+    def c2_host_calls(pinned_form, pageable_form):
+        def run():
+            cb = workload.make_batch(eng, 0, n, 300, seed=78, stream=sh.cuda_stream)
+            page = cb.to_host()
+            del cb
+            torch.cuda.empty_cache()
+            if pageable_form:
+                for _ in range(4):
+                    eng.verify_batch(*page, want_status=False)
+            if pinned_form:
+                pin = tuple(eng.host_copy(x) for x in page)
+                for _ in range(4):
+                    eng.verify_batch(*pin, want_status=False)
+                pend = []
+                for _ in range(4):
+                    pend.append(eng.verify_batch_async(*pin, want_status=False))
+                    if len(pend) == 2:
+                        eng.wait(pend.pop(0))
+                for t in pend:
+                    eng.wait(t)
+                del pin
+            if pageable_form:
+                pend = []
+                for _ in range(4):
+                    pend.append(eng.verify_batch_async(*page, want_status=False))
+                    if len(pend) == 2:
+                        eng.wait(pend.pop(0))
+                for t in pend:
+                    eng.wait(t)
+        return run
+
+    import bench  # noqa: E402  (the bench's own steps, for fidelity)
+
+    def set_stream():
+        torch.cuda.set_stream(sh)
+
+    def calibrate():
+        eng.calibrate(0)
+        eng.calibrate_cycles(0)
+
+    def pcie():
+        bench.pcie_h2d_probe(dev)
+
+    def bench_c2_host():
+        cb = workload.make_batch(eng, 0, n, 300, seed=79, stream=sh.cuda_stream)
+        bench.host_api_rate(eng, cb, 6, 1e8, "c2")
+        del cb
+        torch.cuda.empty_cache()
+
+    def bench_dev_keyed():
+        bench.keyed_rate(eng, 0, n, 300, 5, sh.cuda_stream)
+        torch.cuda.empty_cache()
+
+    steps = {"dev_keyed": dev_keyed, "dev_c2": dev_c2, "c2_host_pinned": c2_host_calls(True, False),
+             "c2_host_pageable": c2_host_calls(False, True), "set_stream": set_stream, "calibrate": calibrate,
+             "pcie": pcie, "bench_c2_host": bench_c2_host, "bench_dev_keyed": bench_dev_keyed}
     for i, st in enumerate(a.order.split(",")):
         if st == "host":
             host_keyed(f"host#{i}")
