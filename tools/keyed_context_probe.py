@@ -132,7 +132,35 @@ def main():
         bench.keyed_rate(eng, 0, n, 300, 5, sh.cuda_stream)
         torch.cuda.empty_cache()
 
-    steps = {"dev_keyed": dev_keyed, "dev_c2": dev_c2, "c2_host_pinned": c2_host_calls(True, False),
+    def c2_host_other_engine():
+        # the C2 host calls on a second context, then closed: is the slow state per context or per process?
+        other = native.Engine(1)
+        cb = workload.make_batch(other, 0, n, 300, seed=80, stream=sh.cuda_stream)
+        page = cb.to_host()
+        del cb
+        pin = tuple(other.host_copy(x) for x in page)
+        for _ in range(4):
+            other.verify_batch(*pin, want_status=False)
+        pend = []
+        for _ in range(4):
+            pend.append(other.verify_batch_async(*pin, want_status=False))
+            if len(pend) == 2:
+                other.wait(pend.pop(0))
+        for t in pend:
+            other.wait(t)
+        del pin
+        other.close()
+        torch.cuda.empty_cache()
+
+    hbuf = torch.empty(4 << 20, dtype=torch.uint8, pin_memory=True)
+    dbuf = torch.empty(4 << 20, dtype=torch.uint8, device=dev)
+
+    def dma1():
+        # one 4 MB host-to-device copy outside the engine: does the DMA engine a copy lands on rotate per copy?
+        dbuf.copy_(hbuf, non_blocking=True)
+        torch.cuda.synchronize()
+
+    steps = {"dma1": dma1, "c2_host_other_engine": c2_host_other_engine, "dev_keyed": dev_keyed, "dev_c2": dev_c2, "c2_host_pinned": c2_host_calls(True, False),
              "c2_host_pageable": c2_host_calls(False, True), "set_stream": set_stream, "calibrate": calibrate,
              "pcie": pcie, "bench_c2_host": bench_c2_host, "bench_dev_keyed": bench_dev_keyed}
     for i, st in enumerate(a.order.split(",")):
