@@ -34,12 +34,14 @@ namespace {
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
-    hipError_t ensure(size_t bytes) {
+    // slack: allocate 1.25x the request (buffers that grow with the batch); exact sizes for buffers whose
+    // caller already sized them (the input ring's blocks)
+    hipError_t ensure(size_t bytes, bool slack = true) {
         if (bytes <= cap) return hipSuccess;
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
-        size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
+        size_t want = std::max<size_t>(slack ? bytes + bytes / 4 : bytes, 4096);
         hipError_t e = hipMalloc(&p, want);
         if (e != hipSuccess) {
             p = nullptr;
@@ -1761,10 +1763,12 @@ struct PipeFrame {
         d.ring_next = (d.ring_next + 1) % kRing;
         if (bytes > d.inblk[q].cap) {
             if (d.in_used[q]) CV_TRY(hipEventSynchronize(d.in_free[q]));
+            // one size for every block: ring_max itself, not 1.25x of it — with the buffer's own slack on top,
+            // each growth made the next block 1.25x larger again (16 blocks: the last 28x the first; a C3 ring
+            // reached ~35 GB)
             const size_t want = std::max(bytes, hint);
             d.ring_max = std::max(d.ring_max, want + want / 4);
-            CV_TRY(d.inblk[q].ensure(d.ring_max));
-            d.ring_max = std::max(d.ring_max, d.inblk[q].cap);
+            CV_TRY(d.inblk[q].ensure(d.ring_max, false));
         }
         if (d.in_used[q]) CV_TRY(hipStreamWaitEvent(d.copy, d.in_free[q], 0));
         *q_out = q;

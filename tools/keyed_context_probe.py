@@ -79,6 +79,26 @@ def main():
         del cb, bms
         torch.cuda.empty_cache()
 
+    def c2_host_one(sync_form):
+        def run():
+            cb = workload.make_batch(eng, 0, n, 300, seed=81, stream=sh.cuda_stream)
+            pin = tuple(eng.host_copy(x) for x in cb.to_host())
+            del cb
+            if sync_form:
+                for _ in range(4):
+                    eng.verify_batch(*pin, want_status=False)
+            else:
+                pend = []
+                for _ in range(4):
+                    pend.append(eng.verify_batch_async(*pin, want_status=False))
+                    if len(pend) == 2:
+                        eng.wait(pend.pop(0))
+                for t in pend:
+                    eng.wait(t)
+            del pin
+            torch.cuda.empty_cache()
+        return run
+
     def c2_host_calls(pinned_form, pageable_form):
         def run():
             cb = workload.make_batch(eng, 0, n, 300, seed=78, stream=sh.cuda_stream)
@@ -160,7 +180,7 @@ def main():
         dbuf.copy_(hbuf, non_blocking=True)
         torch.cuda.synchronize()
 
-    steps = {"dma1": dma1, "c2_host_other_engine": c2_host_other_engine, "dev_keyed": dev_keyed, "dev_c2": dev_c2, "c2_host_pinned": c2_host_calls(True, False),
+    steps = {"c2_sync_only": c2_host_one(True), "c2_async_only": c2_host_one(False), "dma1": dma1, "c2_host_other_engine": c2_host_other_engine, "dev_keyed": dev_keyed, "dev_c2": dev_c2, "c2_host_pinned": c2_host_calls(True, False),
              "c2_host_pageable": c2_host_calls(False, True), "set_stream": set_stream, "calibrate": calibrate,
              "pcie": pcie, "bench_c2_host": bench_c2_host, "bench_dev_keyed": bench_dev_keyed}
     for i, st in enumerate(a.order.split(",")):
