@@ -1004,9 +1004,10 @@ static void span_slice(size_t i0, size_t i1, const uint64_t *off, const uint32_t
         span_slice_impl<0>(i0, i1, off, len, out);
 }
 static Span arena_span(size_t b, size_t e, const uint64_t *off, const uint32_t *len, WorkerPool *pool) {
-    // with a pool: slices of 8,192 records, so a notary batch of 16,384-131,072 spreads over the workers
-    // (its staging plan is on the call's critical path: ~54 us at 65,536 on one core)
-    const size_t kSlice = pool ? 8192 : 65536;
+    // slices of 65,536 records over the pool from 262,144 records; below, one thread (AVX2): waking the
+    // pool's helpers cost ~20 us, more than the scan of a notary batch
+    const size_t kSlice = 65536;
+    if (e - b < 262144) pool = nullptr;
     const size_t nslices = (e - b + kSlice - 1) / kSlice;
     std::vector<Span> part(std::max<size_t>(nslices, 1));
     auto scan = [&](size_t k) {
