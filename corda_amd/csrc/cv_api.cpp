@@ -1004,10 +1004,9 @@ static void span_slice(size_t i0, size_t i1, const uint64_t *off, const uint32_t
         span_slice_impl<0>(i0, i1, off, len, out);
 }
 static Span arena_span(size_t b, size_t e, const uint64_t *off, const uint32_t *len, WorkerPool *pool) {
-    // slices of 65,536 records over the pool from 262,144 records; below, one thread (AVX2): waking the
-    // pool's helpers cost ~20 us, more than the scan of a notary batch
-    const size_t kSlice = 65536;
-    if (e - b < 262144) pool = nullptr;
+    // with a pool: slices of 8,192 records (the pipeline's sub-chunks: their scans precede their packing on
+    // the call's critical path); without, one thread (AVX2)
+    const size_t kSlice = pool ? 8192 : 65536;
     const size_t nslices = (e - b + kSlice - 1) / kSlice;
     std::vector<Span> part(std::max<size_t>(nslices, 1));
     auto scan = [&](size_t k) {
@@ -1556,7 +1555,11 @@ static int verify_shard_small(cv_ctx *ctx, Device &d, const Opts &o, size_t b, s
     const size_t n = e - b;
     WorkerPool *pool = n >= 16384 ? &d.workers(threads) : nullptr;
     const double t_plan = now_s();
-    const Stage st = stage_plan(b, e, in.off, in.len, pool);
+    // pinned inputs (DMAed in place, nothing to pack): the range scan on this thread — waking the pool's helpers
+    // cost ~20 us, more than the scan of a notary batch (16,384 0.409 -> 0.391 ms p50); pageable inputs: on the
+    // pool, whose helpers the packing needs next anyway
+    const bool in_place = pool && n >= o.small_direct_min && host_pinned(in.pk + b * 32, n * 32);
+    const Stage st = stage_plan(b, e, in.off, in.len, in_place ? nullptr : pool);
     if (st.hi > in.arena_bytes) return CV_E_ARGS;
     if (o.small_zc && cvk_tri_zc_ok(&o.plan, (uint32_t)n, (uint32_t)n))
         return verify_shard_small_zc(ctx, d, o, st, b, in, pool, t_plan,
