@@ -159,6 +159,8 @@ struct Slot {
     hipStream_t stream = nullptr; // the slot's own stream (slot 0: the device stream)
     PinBuf pin_in;                // small-path staging of one batch: pk | sig | off | len | arena
     DevBuf packed;                // its device copy
+    PinBuf pin_head;              // mid-size batches (verify_shard_mid): pk | sig, staged before the range scan
+    DevBuf head;                  // its device copy
 };
 constexpr int kSlots = 4;
 constexpr int kPipeSlots = 2;   // compute slots the pipeline deals its sub-chunks over (see pipe_enqueue)
@@ -1063,6 +1065,8 @@ static Stage stage_plan(size_t b, size_t e, const uint64_t *off, const uint32_t 
 }
 // Packs records [b, e) into h by the plan (keys / key indices + signatures first: `first_part` runs after
 // them, so their DMA can start while the rest is packed).
+static void stage_pack_tail(const Stage &st, uint8_t *h, size_t b, const uint8_t *arena, const uint64_t *off,
+                            const uint32_t *len, WorkerPool *pool);
 template <class F>
 static void stage_pack(const Stage &st, uint8_t *h, size_t b, const uint8_t *pk, const uint32_t *kidx,
                        const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
@@ -1073,6 +1077,12 @@ static void stage_pack(const Stage &st, uint8_t *h, size_t b, const uint8_t *pk,
     else
         par_copy({{h + st.o_pk, pk + b * 32, n * 32}, {h + st.o_sig, sig + b * 64, n * 64}}, pool);
     first_part();
+    stage_pack_tail(st, h, b, arena, off, len, pool);
+}
+// The offsets, lengths and message bytes of a stage (its parts from o_off on).
+static void stage_pack_tail(const Stage &st, uint8_t *h, size_t b, const uint8_t *arena, const uint64_t *off,
+                            const uint32_t *len, WorkerPool *pool) {
+    const size_t n = st.n;
     uint64_t *hoff = reinterpret_cast<uint64_t *>(h + st.o_off);
     uint8_t *har = h + st.o_ar;
     if (st.compact) {
@@ -1125,12 +1135,11 @@ static bool stage_direct(const Stage &st, size_t b, const uint8_t *pk, const uin
 // profiles/r03d_timeline_pinned.txt).
 static hipError_t stage_dma_direct(const Stage &st, uint8_t *dv, size_t b, const uint8_t *pk, const uint32_t *kidx,
                                    const uint8_t *sig, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
-                                   hipStream_t s, hipEvent_t keys_sigs = nullptr) {
+                                   hipStream_t s) {
     const size_t n = st.n;
     hipError_t e = st.keyed ? hipMemcpyAsync(dv + st.o_kidx, kidx + b, n * 4, hipMemcpyHostToDevice, s)
                             : hipMemcpyAsync(dv + st.o_pk, pk + b * 32, n * 32, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(dv + st.o_sig, sig + b * 64, n * 64, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && keys_sigs) e = hipEventRecord(keys_sigs, s);   // (keys | key indices) and signatures
     if (e == hipSuccess) e = hipMemcpyAsync(dv + st.o_off, off + b, n * 8, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(dv + st.o_len, len + b, n * 4, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && st.hi > st.lo)
@@ -1550,11 +1559,94 @@ static int verify_shard_small_zc(cv_ctx *ctx, Device &d, const Opts &o, const St
 // by one DMA (two above 1 MB: the first overlaps packing the second part) into one device block, verified,
 // and the bitmap (+ status) come back by one DMA.  b is a multiple of 64, so the shard's bitmap words are
 // whole words of the caller's bitmap.
+// Mid-size unpipelined batches (from prep_overlap_min): the keys and signatures — all the point kernels read —
+// are staged into their own device block and their DMA issued FIRST, before the range scan of the offsets and
+// lengths; the scan, the tail's packing (pageable inputs) and its DMA then run beside that DMA, and the point
+// decodes start on the slot's helper stream as soon as it lands (cvk_verify, CvkPrepOverlap).
+static int verify_shard_mid(cv_ctx *ctx, Device &d, const Opts &o, size_t b, size_t e, const VerifyIn &in,
+                            WorkerPool *pool, double t_plan) {
+    const size_t n = e - b;
+    const size_t words = (n + 63) / 64;
+    const size_t o_bm = 0, o_st = al16(words * 8), total_out = o_st + al16(n);
+    const size_t h_sig = al16(n * 32), h_total = h_sig + al16(n * 64);
+    double t[6];
+    t[0] = t_plan;
+    Slot &sl = d.slot[0];
+    hipStream_t s = nullptr;
+    CV_TRY(slot_stream(d, 0, &s));
+    CV_TRY(slot_events(sl));
+    CV_TRY(slot_split(d, sl));
+    CvkPrepOverlap po;
+    po.aux = sl.split.s2;
+    po.ready = sl.split.start;
+    po.done = sl.split.done2;
+    CV_TRY(sl.head.ensure(h_total));
+    CV_TRY(d.pin_out.ensure(total_out));
+    CV_TRY(d.bitmap.ensure(total_out));
+    uint8_t *dh = sl.head.as<uint8_t>();
+    hipStream_t aux = po.aux;
+    auto drain = on_exit([s, aux] {   // error paths: no DMA or helper-stream kernel outlives the call
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamSynchronize(aux);
+    });
+    // ---- head: keys | signatures, in place from pinned arrays or packed on the pool
+    const bool head_pinned = n >= o.small_direct_min && host_pinned(in.pk + b * 32, n * 32) &&
+                             host_pinned(in.sig + b * 64, n * 64);
+    if (head_pinned) {
+        CV_TRY(hipMemcpyAsync(dh, in.pk + b * 32, n * 32, hipMemcpyHostToDevice, s));
+        CV_TRY(hipMemcpyAsync(dh + h_sig, in.sig + b * 64, n * 64, hipMemcpyHostToDevice, s));
+    } else {
+        CV_TRY(sl.pin_head.ensure(h_total));
+        uint8_t *hh = sl.pin_head.as<uint8_t>();
+        par_copy({{hh, in.pk + b * 32, n * 32}, {hh + h_sig, in.sig + b * 64, n * 64}}, pool);
+        CV_TRY(hipMemcpyAsync(dh, hh, h_total, hipMemcpyHostToDevice, s));
+    }
+    CV_TRY(hipEventRecord(po.ready, s));
+    t[1] = now_s();
+    // ---- tail: offsets | lengths | message bytes (the Stage layout from o_off on), behind the head's DMA
+    const Stage st = stage_plan(b, e, in.off, in.len, head_pinned ? nullptr : pool);
+    if (st.hi > in.arena_bytes) return CV_E_ARGS;   // (drain: the head's DMA is waited for)
+    CV_TRY(sl.packed.ensure(st.total));
+    uint8_t *dv = sl.packed.as<uint8_t>();
+    if (n >= o.small_direct_min && stage_direct(st, b, in.pk, nullptr, in.sig, in.arena, in.off, in.len)) {
+        CV_TRY(hipMemcpyAsync(dv + st.o_off, in.off + b, n * 8, hipMemcpyHostToDevice, s));
+        CV_TRY(hipMemcpyAsync(dv + st.o_len, in.len + b, n * 4, hipMemcpyHostToDevice, s));
+        if (st.hi > st.lo)
+            CV_TRY(hipMemcpyAsync(dv + st.o_ar, in.arena + st.lo, st.hi - st.lo, hipMemcpyHostToDevice, s));
+    } else {
+        CV_TRY(sl.pin_in.ensure(st.total));
+        uint8_t *h = sl.pin_in.as<uint8_t>();
+        stage_pack_tail(st, h, b, in.arena, in.off, in.len, pool);
+        CV_TRY(hipMemcpyAsync(dv + st.o_off, h + st.o_off, st.total - st.o_off, hipMemcpyHostToDevice, s));
+    }
+    t[2] = now_s();
+    uint8_t *dout = d.bitmap.as<uint8_t>();
+    CV_TRY(launch_verify(d, o.plan, sl, (uint32_t)n, dh, dh + h_sig, dv + st.o_ar - st.lo,
+                         reinterpret_cast<const uint64_t *>(dv + st.o_off), reinterpret_cast<const uint32_t *>(dv + st.o_len),
+                         reinterpret_cast<uint64_t *>(dout + o_bm), in.status ? dout + o_st : nullptr, s, nullptr, true, &po));
+    CV_TRY(hipMemcpyAsync(d.pin_out.p, dout, in.status ? o_st + n : words * 8, hipMemcpyDeviceToHost, s));
+    t[3] = now_s();
+    CV_TRY(hipStreamSynchronize(s));
+    drain.armed = false;
+    t[4] = now_s();
+    std::memcpy(in.bitmap + b / 64, d.pin_out.as<uint8_t>() + o_bm, words * 8);
+    if (in.status) std::memcpy(in.status + b, d.pin_out.as<uint8_t>() + o_st, n);
+    t[5] = now_s();
+    {
+        std::lock_guard<std::mutex> g(ctx->st_mu);
+        for (int k = 0; k < 5; k++) ctx->stats.small[k] += t[k + 1] - t[k];
+        ctx->stats.small_calls++;
+    }
+    return CV_OK;
+}
+
 static int verify_shard_small(cv_ctx *ctx, Device &d, const Opts &o, size_t b, size_t e, const VerifyIn &in,
                               int threads) {
     const size_t n = e - b;
     WorkerPool *pool = n >= 16384 ? &d.workers(threads) : nullptr;
     const double t_plan = now_s();
+    if (n >= o.prep_overlap_min && (!o.small_zc || !cvk_tri_zc_ok(&o.plan, (uint32_t)n, (uint32_t)n)))
+        return verify_shard_mid(ctx, d, o, b, e, in, pool, t_plan);
     // pinned inputs (DMAed in place, nothing to pack): the range scan on this thread — waking the pool's helpers
     // cost ~20 us, more than the scan of a notary batch (16,384 0.409 -> 0.391 ms p50); pageable inputs: on the
     // pool, whose helpers the packing needs next anyway
@@ -1578,20 +1670,7 @@ static int verify_shard_small(cv_ctx *ctx, Device &d, const Opts &o, size_t b, s
     CV_TRY(d.bitmap.ensure(total_out));
     uint8_t *h = sl.pin_in.as<uint8_t>();
     uint8_t *dv = sl.packed.as<uint8_t>();
-    // Prep overlap from prep_overlap_min: the point decodes (keys and signatures only) start on the slot's
-    // helper stream as soon as those are resident, beside the DMA of offsets, lengths and messages and the
-    // scalars (cvk_verify, CvkPrepOverlap)
-    CvkPrepOverlap po;
-    if (n >= o.prep_overlap_min && slot_split(d, sl) == hipSuccess) {
-        po.aux = sl.split.s2;
-        po.ready = sl.split.start;
-        po.done = sl.split.done2;
-    }
-    hipStream_t aux = po.aux;
-    auto drain = on_exit([s, aux] {   // error paths: no DMA or helper-stream kernel outlives the call
-        (void)hipStreamSynchronize(s);
-        if (aux) (void)hipStreamSynchronize(aux);
-    });
+    auto drain = on_exit([s] { (void)hipStreamSynchronize(s); });   // error paths: no DMA outlives the call
     t[1] = now_s();
     // Two-stage staging above 1 MB of keys + signatures: they are packed and their DMA is issued
     // first, so it runs while the offsets, lengths and message bytes are packed (notary 65,536:
@@ -1600,26 +1679,23 @@ static int verify_shard_small(cv_ctx *ctx, Device &d, const Opts &o, size_t b, s
     // below small_direct_min signatures one packed DMA beats five direct ones even from pinned arrays
     // (notary 4,096: 0.328 ms p50 packed vs 0.342 direct; 65,536: 1.28 vs 1.10, profiles/r03h_bench.json)
     if (n >= o.small_direct_min && stage_direct(st, b, in.pk, nullptr, in.sig, in.arena, in.off, in.len)) {
-        CV_TRY(stage_dma_direct(st, dv, b, in.pk, nullptr, in.sig, in.arena, in.off, in.len, s, po.ready));
+        CV_TRY(stage_dma_direct(st, dv, b, in.pk, nullptr, in.sig, in.arena, in.off, in.len, s));
     } else {
         hipError_t e1 = hipSuccess;
         stage_pack(st, h, b, in.pk, nullptr, in.sig, in.arena, in.off, in.len, pool, [&] {
             if (two_stage) e1 = hipMemcpyAsync(dv, h, st.o_off, hipMemcpyHostToDevice, s);
-            if (two_stage && e1 == hipSuccess && po.ready) e1 = hipEventRecord(po.ready, s);
         });
         CV_TRY(e1);
         if (two_stage)
             CV_TRY(hipMemcpyAsync(dv + st.o_off, h + st.o_off, st.total - st.o_off, hipMemcpyHostToDevice, s));
         else
             CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, s));
-        if (!two_stage && po.ready) CV_TRY(hipEventRecord(po.ready, s));
     }
     t[2] = now_s();
     uint8_t *dout = d.bitmap.as<uint8_t>();
     CV_TRY(launch_verify(d, o.plan, sl, (uint32_t)n, dv + st.o_pk, dv + st.o_sig, dv + st.o_ar - st.lo,
                          reinterpret_cast<const uint64_t *>(dv + st.o_off), reinterpret_cast<const uint32_t *>(dv + st.o_len),
-                         reinterpret_cast<uint64_t *>(dout + o_bm), in.status ? dout + o_st : nullptr, s, nullptr, true,
-                         po.aux ? &po : nullptr));
+                         reinterpret_cast<uint64_t *>(dout + o_bm), in.status ? dout + o_st : nullptr, s, nullptr, true));
     CV_TRY(hipMemcpyAsync(d.pin_out.p, dout, in.status ? o_st + n : words * 8, hipMemcpyDeviceToHost, s));
     t[3] = now_s();
     CV_TRY(hipStreamSynchronize(s));

@@ -337,11 +337,12 @@ def test_async_calls_in_flight_match_sync(engine, corpus, oracle_c):
     assert np.array_equal(r3[1], corpus["status"][sel])
 
 
-@pytest.mark.parametrize("n", [100, 9001, 200_000])
+@pytest.mark.parametrize("n", [100, 9001, 65536, 200_000])
 def test_verify_batch_ex_arena_bound(engine, corpus, n):
     """cv_ed25519_verify_batch_ex: a record reaching past arena_bytes is rejected (CV_E_ARGS) by the engine's
-    staging scan, in the small, zero-copy and pipelined forms and in the async form, and nothing is read past the
-    bound; the same batch with the true size verifies exactly (golden tiles)."""
+    staging scan, in the small, zero-copy, mid-size (keys and signatures already in DMA when the scan finds it)
+    and pipelined forms and in the async form, and nothing is read past the bound; the same batch with the true
+    size verifies exactly (golden tiles)."""
     lib = native.load()
     idx = np.arange(n) % len(corpus["pk"])
     pk, sig = np.ascontiguousarray(corpus["pk"][idx]), np.ascontiguousarray(corpus["sig"][idx])
