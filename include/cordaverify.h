@@ -302,8 +302,9 @@ int cv_calibrate_cycles(cv_ctx *ctx, int device, double *out);
 #define CV_OPT_SHARD_MIN 13         /* routing: batches up to this go whole to one device; fewer per shard never (4096) */
 #define CV_OPT_SPREAD_MIN 14        /* routing: batches from this size are cut over all devices (262144) */
 #define CV_OPT_MERKLE_CHUNK 15      /* leaves per Merkle pipeline sub-chunk (262144) */
-#define CV_OPT_PREP_OVERLAP_MIN 16  /* unpipelined host batches from this size decode their points on a helper stream
-                                       while the rest of their inputs is still in DMA (32768) */
+#define CV_OPT_PREP_OVERLAP_MIN 16  /* unpipelined host batches from this size send keys and signatures first and
+                                       decode their points on a helper stream while the rest of their inputs is still
+                                       in DMA (32768) */
 #define CV_OPT_COUNT 17
 int cv_set_option(cv_ctx *ctx, int option, int64_t value);
 int cv_get_option(cv_ctx *ctx, int option, int64_t *value);
