@@ -2502,7 +2502,12 @@ static int verify_shard(cv_ctx *ctx, Device &d, const Opts &o, size_t b, size_t 
     if (!async && !keyed && n <= o.pipe_min) return verify_shard_small(ctx, d, o, b, e, in, threads);
     int k = 0;
     std::unique_lock<std::mutex> lk;
-    PipeOut &po = pipe_out(d, &k, lk);
+    const double tw = now_s();
+    PipeOut &po = pipe_out(d, &k, lk);   // (finishes that output's previous call if still pending)
+    {
+        std::lock_guard<std::mutex> g(ctx->st_mu);
+        ctx->stats.pipe[2] += now_s() - tw;
+    }
     int rc = pipe_enqueue(ctx, d, o, po, b, e, in, threads, async);
     if (rc != CV_OK) return rc;
     if (keyed) {

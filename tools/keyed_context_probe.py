@@ -35,23 +35,31 @@ def main():
     torch.cuda.empty_cache()
 
     def host_keyed(tag):
+        tw = [0.0, 0.0]
+
         def loop(k):
             pend, bm = [], None
             for _ in range(k):
+                t0 = time.perf_counter()
                 pend.append(eng.verify_batch_async(*host, want_status=False))
+                t1 = time.perf_counter()
+                tw[0] += t1 - t0
                 if len(pend) == 2:
                     bm, _ = eng.wait(pend.pop(0))
+                    tw[1] += time.perf_counter() - t1
             for t in pend:
                 bm, _ = eng.wait(t)
             return bm
         loop(2)
         eng.stats("pipe", reset=True)
+        tw[0] = tw[1] = 0.0
         t = time.perf_counter()
         bm = loop(a.calls)
         dt = (time.perf_counter() - t) / a.calls
         st = eng.stats("pipe", reset=True)
         assert native.bitmap_to_bools(bm, n).all()
         print(json.dumps({"step": tag, "keyed_host_async_ms_per_call": dt * 1e3,
+                          "submit_ms_per_call": tw[0] / a.calls * 1e3, "wait_ms_per_call": tw[1] / a.calls * 1e3,
                           "host_ms_per_call": {k[:-2]: round(v / a.calls * 1e3, 3) for k, v in st.items()
                                                if k.endswith("_s")}}), flush=True)
 
@@ -79,9 +87,9 @@ def main():
         del cb, bms
         torch.cuda.empty_cache()
 
-    def c2_host_one(sync_form):
+    def c2_host_one(sync_form, nn=None):
         def run():
-            cb = workload.make_batch(eng, 0, n, 300, seed=81, stream=sh.cuda_stream)
+            cb = workload.make_batch(eng, 0, nn or n, 300, seed=81, stream=sh.cuda_stream)
             pin = tuple(eng.host_copy(x) for x in cb.to_host())
             del cb
             if sync_form:
@@ -180,7 +188,8 @@ def main():
         dbuf.copy_(hbuf, non_blocking=True)
         torch.cuda.synchronize()
 
-    steps = {"c2_sync_only": c2_host_one(True), "c2_async_only": c2_host_one(False), "dma1": dma1, "c2_host_other_engine": c2_host_other_engine, "dev_keyed": dev_keyed, "dev_c2": dev_c2, "c2_host_pinned": c2_host_calls(True, False),
+    steps = {"c2_sync_only": c2_host_one(True), "c2_async_only": c2_host_one(False),
+             "c2_async_5sub": c2_host_one(False, 5 * 262144), "dma1": dma1, "c2_host_other_engine": c2_host_other_engine, "dev_keyed": dev_keyed, "dev_c2": dev_c2, "c2_host_pinned": c2_host_calls(True, False),
              "c2_host_pageable": c2_host_calls(False, True), "set_stream": set_stream, "calibrate": calibrate,
              "pcie": pcie, "bench_c2_host": bench_c2_host, "bench_dev_keyed": bench_dev_keyed}
     for i, st in enumerate(a.order.split(",")):
