@@ -188,7 +188,26 @@ def main():
         dbuf.copy_(hbuf, non_blocking=True)
         torch.cuda.synchronize()
 
-    steps = {"c2_sync_only": c2_host_one(True), "c2_async_only": c2_host_one(False),
+    def c2_async_small_chunks():
+        # the asynchronous form with sync-like sub-chunk sizes (many launches per call on the same streams)
+        old = eng.get_option("async_chunk")
+        eng.set_option("async_chunk", 65536)
+        c2_host_one(False)()
+        eng.set_option("async_chunk", old)
+
+    def with_opts(fn, **kw):
+        def run():
+            old = {k: eng.get_option(k) for k in kw}
+            for k, v in kw.items():
+                eng.set_option(k, v)
+            fn()
+            for k, v in old.items():
+                eng.set_option(k, v)
+        return run
+
+    steps = {"c2_async_quad": with_opts(c2_host_one(False), async_chunk=32768),
+             "c2_sync_noquad": with_opts(c2_host_one(True), quad_max=0),
+             "c2_async_small": c2_async_small_chunks, "c2_sync_only": c2_host_one(True), "c2_async_only": c2_host_one(False),
              "c2_async_5sub": c2_host_one(False, 5 * 262144), "dma1": dma1, "c2_host_other_engine": c2_host_other_engine, "dev_keyed": dev_keyed, "dev_c2": dev_c2, "c2_host_pinned": c2_host_calls(True, False),
              "c2_host_pageable": c2_host_calls(False, True), "set_stream": set_stream, "calibrate": calibrate,
              "pcie": pcie, "bench_c2_host": bench_c2_host, "bench_dev_keyed": bench_dev_keyed}
