@@ -205,7 +205,17 @@ def main():
                 eng.set_option(k, v)
         return run
 
-    steps = {"c2_async_quad": with_opts(c2_host_one(False), async_chunk=32768),
+    def c2_async_serial():
+        # asynchronous calls joined one at a time (the synchronous call's completion pattern)
+        cb = workload.make_batch(eng, 0, n, 300, seed=82, stream=sh.cuda_stream)
+        pin = tuple(eng.host_copy(x) for x in cb.to_host())
+        del cb
+        for _ in range(4):
+            eng.wait(eng.verify_batch_async(*pin, want_status=False))
+        del pin
+        torch.cuda.empty_cache()
+
+    steps = {"c2_async_serial": c2_async_serial, "c2_async_quad": with_opts(c2_host_one(False), async_chunk=32768),
              "c2_sync_noquad": with_opts(c2_host_one(True), quad_max=0),
              "c2_async_small": c2_async_small_chunks, "c2_sync_only": c2_host_one(True), "c2_async_only": c2_host_one(False),
              "c2_async_5sub": c2_host_one(False, 5 * 262144), "dma1": dma1, "c2_host_other_engine": c2_host_other_engine, "dev_keyed": dev_keyed, "dev_c2": dev_c2, "c2_host_pinned": c2_host_calls(True, False),
