@@ -196,6 +196,7 @@ struct PipeOut {
     DevBuf kdev;
     PinBuf kstage, kidx;
     PinBuf tstage;   // transaction calls: the shard's signature boundaries when the caller's are pageable
+    hipEvent_t copied = nullptr;   // after the call's result copies on the output stream (pipe_copy_back)
     // calls on this output whose finish failed: (gen, error), kept after the output is reused so a cv_wait on
     // such a call still returns its error (bounded: the last 64 failures)
     std::deque<std::pair<uint64_t, int>> failed;
@@ -805,6 +806,7 @@ void cv_close(cv_ctx *ctx) {
             o.tstage.release();
             for (hipEvent_t v : o.slot_done)
                 if (v) (void)hipEventDestroy(v);
+            if (o.copied) (void)hipEventDestroy(o.copied);
         }
         if (d.outs) (void)hipStreamDestroy(d.outs);
         for (int q = 0; q < kRing; q++) {
@@ -1761,7 +1763,12 @@ static int pipe_copy_back(Device &d, PipeOut &po) {
             CV_TRY(hipMemcpyAsync(po.hout.as<uint8_t>() + sg.off, po.dout.as<uint8_t>() + sg.off, sg.len,
                                   hipMemcpyDeviceToHost, d.outs));
     }
-    CV_TRY(hipStreamSynchronize(d.outs));
+    // joined by an event after this call's copies, not by hipStreamSynchronize(d.outs): once calls had been
+    // joined one at a time (each draining the device), the stream synchronise of this stream kept costing ~1.2
+    // ms per call of two later calls in flight (keyed host C2 8.5-8.7 -> 7.3 ms, DESIGN "Host runtime effects")
+    if (!po.copied) CV_TRY(hipEventCreateWithFlags(&po.copied, hipEventDisableTiming));
+    CV_TRY(hipEventRecord(po.copied, d.outs));
+    CV_TRY(hipEventSynchronize(po.copied));
     for (int k = 0; k < po.nseg; k++) {
         const PipeOut::Seg &sg = po.seg[k];
         if (sg.len && sg.len < kDirect) std::memcpy(sg.dst, po.hout.as<uint8_t>() + sg.off, sg.len);
