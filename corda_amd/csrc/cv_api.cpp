@@ -790,8 +790,10 @@ void cv_close(cv_ctx *ctx) {
         d.zc_out.release();
         for (int k = 0; k < kSlots; k++) {
             Slot &sl = d.slot[k];
-            for (DevBuf *b : {&sl.ws_hs, &sl.ws_tab, &sl.ws_R, &sl.ws_ok, &sl.ws_dig, &sl.mdig, &sl.packed}) b->release();
+            for (DevBuf *b : {&sl.ws_hs, &sl.ws_tab, &sl.ws_R, &sl.ws_ok, &sl.ws_dig, &sl.mdig, &sl.packed, &sl.head})
+                b->release();
             sl.pin_in.release();
+            sl.pin_head.release();
             for (hipEvent_t v : {sl.ev, sl.split.start, sl.split.done2})
                 if (v) (void)hipEventDestroy(v);
             if (sl.split.s2) (void)hipStreamDestroy(sl.split.s2);
