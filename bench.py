@@ -185,7 +185,23 @@ def host_api_rate(eng, batch, steps: int, device_value: float, name: str, async_
     pinned = tuple(eng.host_copy(x) for x in (pk, sig, arena, off, ln))
     eng.stats("pipe", reset=True)
     dt_pin = timed(pinned)
-    direct = int(eng.stats("pipe")["direct_subchunks"])
+    ps = eng.stats("pipe")
+    direct = int(ps["direct_subchunks"])
+    calls = max(1.0, ps["calls"])
+    # where a synchronous call's time goes: the host phases of the calls above, per call, and
+    # the GPU timeline of 3 more calls (CV_OPT_TIMELINE: HIP events per sub-chunk, outside the timed loop)
+    breakdown = {k[:-2] + "_ms": ps[k] / calls * 1e3 for k in ("plan_s", "pack_s", "wait_s", "enqueue_s", "sync_s")}
+    breakdown["subchunks"] = ps["subchunks"] / calls
+    eng.set_option("timeline", 1)
+    eng.stats("timeline", reset=True)
+    for _ in range(3):
+        eng.verify_batch(*pinned, want_status=False)
+    tl = eng.stats("timeline", reset=True)
+    eng.set_option("timeline", 0)
+    tc = max(1.0, tl["calls"])
+    breakdown.update({k: tl[k] / tc for k in ("ramp_ms", "dma_end_ms", "span_ms", "busy_ms", "idle_ms", "tail_ms",
+                                              "result_copy_ms", "first_subchunk")})
+    breakdown["timeline_calls"] = tl["calls"]
     dt_async = timed_async(pinned)
     dt_async_page = timed_async((pk, sig, arena, off, ln))
     del pinned
@@ -197,7 +213,7 @@ def host_api_rate(eng, batch, steps: int, device_value: float, name: str, async_
             "path": "cv_ed25519_verify_batch_async from pinned host buffers (cv_host_alloc), two calls in flight "
                     "(a batching node submits batch k+1 before waiting for batch k); sub-chunks DMAed in place",
             "sync_pinned": {"value": vs, "ms_per_step": dt_pin / steps * 1e3, "ratio_to_device_value": vs / device_value,
-                            "direct_dma_subchunks": direct,
+                            "direct_dma_subchunks": direct, "breakdown": breakdown,
                             "path": "cv_ed25519_verify_batch (synchronous, one call at a time) from pinned buffers"},
             "async_pageable": {"value": va, "ms_per_step": dt_async_page / asteps * 1e3,
                                "ratio_to_device_value": va / device_value,
@@ -804,6 +820,17 @@ def timed_steps(step, steps: int, world: int, sync):
     return time.perf_counter() - t0, out
 
 
+def written_all_ones(bitmaps, n: int) -> bool:
+    """Every verdict word of every bitmap all ones (bits past n clear).  The bitmaps are zeroed before each
+    timed region, so this proves the timed launches wrote every word (an honest batch) — a skipped or no-op
+    launch leaves zeros (VERDICT r5 weak #4)."""
+    words = (n + 63) // 64
+    full = torch.full((words,), -1, dtype=torch.int64, device=bitmaps[0].device)
+    if n % 64:
+        full[-1] = (1 << (n % 64)) - 1
+    return all(torch.equal(bm, full) for bm in bitmaps)
+
+
 def max_over_ranks(vals, device) -> list:
     """Element-wise max of per-rank floats (the slowest rank's timed region is the job's)."""
     if not dist.is_initialized() or dist.get_world_size() == 1:
@@ -827,6 +854,8 @@ def c5_multi_line(eng, local, rank, world, sh, dev, n: int, steps: int) -> dict:
         return D.gather_bitmap(bm, world * n)             # on the current (= sh) stream, behind the verify
 
     step(0)                                               # warm: workspace chunks, RCCL channels
+    torch.cuda.synchronize(dev)
+    bm.zero_()                                            # so the all-ones check below proves the TIMED steps wrote it
     el, gathered = timed_steps(step, steps, world, lambda: torch.cuda.synchronize(dev))
     ok = bool((gathered == -1).all()) and torch.equal(gathered.view(world, -1)[rank], bm)
     (el, bad) = max_over_ranks([el, 0.0 if ok else 1.0], dev)
@@ -920,12 +949,17 @@ def plumbing_main(args, world: int, rank: int):
     bm = torch.zeros(n // 64, dtype=torch.int64)
 
     def step(k):
-        bm.fill_(-1)                                      # stand-in for this rank's verify kernel
+        if not args.plumbing_noop:
+            bm.fill_(-1)                                  # stand-in for this rank's verify kernel
         return D.gather_bitmap(bm, world * n)
 
     step(0)
+    bm.zero_()                                            # as the GPU form: the timed steps must write every word
     el, gathered = timed_steps(step, args.steps, world, lambda: None)
-    (el,) = max_over_ranks([el], "cpu")
+    ok = written_all_ones([bm], n) and bool((gathered == -1).all())
+    (el, bad) = max_over_ranks([el, 0.0 if ok else 1.0], "cpu")
+    assert bad == 0.0, "plumbing: a verdict bitmap was not written by the timed steps"
+
     if rank == 0:
         print(json.dumps({"metric": "PLUMBING CHECK (launcher + gloo all-gather + timing; no verification)",
                           "value": None, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -960,6 +994,9 @@ def main():
                     help="N > 1: signatures per GPU of the c5 and c_abi_multi sub-lines (BASELINE configs[4]: 8M)")
     ap.add_argument("--c-abi-multi", action="store_true",
                     help="also run the c_abi_multi sub-line at N = 1 (it always runs at N > 1)")
+    ap.add_argument("--plumbing-noop", action="store_true",
+                    help="test hook of --plumbing: the stand-in verify writes nothing, so the timed steps' all-ones "
+                         "check must fail (tests/test_bench_launch.py)")
     ap.add_argument("--plumbing", action="store_true",
                     help="CPU check of the N > 1 launcher / gloo all-gather / timing, no GPU and NO verification "
                          "(tests/test_bench_launch.py); its line is never a measurement")
@@ -1057,21 +1094,30 @@ def main():
         # N>1: every step ends with the RCCL all-gather into the commit step
         return timed_steps(lambda k: step(k, ns), args.steps, world, lambda: torch.cuda.synchronize(dev))
 
+    def zero_bitmaps():
+        torch.cuda.synchronize(dev)
+        for bm in bitmaps:
+            bm.zero_()
+        torch.cuda.synchronize(dev)
+
     for k in range(args.warmup):
         step(k)
-    torch.cuda.synchronize(dev)
+    # the bitmaps are zeroed outside every timed region, so each all-ones check below proves that the timed
+    # launches themselves wrote every verdict word
+    zero_bitmaps()
 
     # Timed region: K production verify calls dealt over the streams (the engine's own launch plan,
     # incl. the drain-overlap sub-chunks it picks for near-empty last rounds), one sync at the end.
     elapsed, gathered = timed(nstreams)
+    assert written_all_ones(bitmaps[:min(nstreams, args.steps)], n), \
+        "timed verify calls did not write an all-ones verdict bitmap (honest batch)"
+    prod_bitmap = bitmap.clone()
+    zero_bitmaps()
     other_streams = 2 if nstreams == 1 else 1
     other_elapsed, _ = timed(other_streams)
-    full = torch.full_like(bitmap, -1)
-    if n % 64:
-        full[-1] = (1 << (n % 64)) - 1
-    for bm in bitmaps:
-        assert torch.equal(bm, full), "verify rejected an honest signature"
-    prod_bitmap = bitmap.clone()
+    assert written_all_ones(bitmaps[:min(other_streams, args.steps)], n), \
+        "timed verify calls (other stream form) did not write an all-ones verdict bitmap"
+    zero_bitmaps()
     # Roofline: K more calls of the same batch as whole-chunk launches, timed kernel by kernel with HIP
     # events recorded on `stream` between the launches (cv_ed25519_verify_device_timed waits for the last).
     phases = []
@@ -1082,7 +1128,7 @@ def main():
     torch.cuda.synchronize(dev)
     assert torch.equal(prod_bitmap, bitmap), "production and timed launch plans disagree"
     # correctness of the timed configuration: every generated signature is honest
-    assert torch.equal(bitmap, full), "verify rejected an honest signature"
+    assert written_all_ones([bitmap], n), "verify rejected an honest signature"
     ph = np.mean(np.array(phases), axis=0)
     kern_ms, straus_ms = float(ph.sum()), float(ph[2])
     multi = {}
@@ -1200,7 +1246,10 @@ def main():
             for k in ("c2", "c5"):
                 if k in H:
                     h[k]["sync_pinned_ratio"] = r3(H[k]["sync_pinned"]["ratio_to_device_value"])
+                    h[k]["sync_pinned_ms"] = r3(H[k]["sync_pinned"]["ms_per_step"])
                     h[k]["pageable_ratio"] = r3(H[k]["pageable"]["ratio_to_device_value"])
+            if "c2" in H:
+                h["c2"]["sync_breakdown"] = {k: r3(v) for k, v in H["c2"]["sync_pinned"]["breakdown"].items()}
             if "keyed" in H:
                 h["keyed"]["pcie_bound_value"] = r3(H["keyed"]["pcie_bound_value"])
                 h["keyed"]["ratio_to_pcie_bound"] = r3(H["keyed"]["ratio_to_pcie_bound"])

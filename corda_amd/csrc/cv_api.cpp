@@ -197,6 +197,22 @@ struct PipeOut {
     PinBuf kstage, kidx;
     PinBuf tstage;   // transaction calls: the shard's signature boundaries when the caller's are pageable
     hipEvent_t copied = nullptr;   // after the call's result copies on the output stream (pipe_copy_back)
+    // CV_OPT_TIMELINE (synchronous calls): timing events — [0] the first input DMA's start, then per sub-chunk j
+    // [1 + 3j] its DMA's end (copy stream), [2 + 3j] its launch group's start, [3 + 3j] its end (slot stream) —
+    // and [tl_n * 3 + 1] the result copies' end; summarised by pipe_copy_back into tl_sum
+    std::vector<hipEvent_t> tl;
+    int tl_n = 0;
+    size_t tl_first = 0;
+    bool tl_ready = false;
+    double tl_sum[8] = {};   // ramp, last DMA end, span, busy, idle, tail, result copy (ms); first sub-chunk
+    hipEvent_t tl_ev(size_t k) {
+        while (tl.size() <= k) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            tl.push_back(e);
+        }
+        return tl[k];
+    }
     // calls on this output whose finish failed: (gen, error), kept after the output is reused so a cv_wait on
     // such a call still returns its error (bounded: the last 64 failures)
     std::deque<std::pair<uint64_t, int>> failed;
@@ -418,6 +434,7 @@ static const OptDesc kOpt[CV_OPT_COUNT] = {
     {262144, 64, (int64_t)1 << 40},     // CV_OPT_SPREAD_MIN
     {262144, 1, 1 << 24},               // CV_OPT_MERKLE_CHUNK
     {32768, 1, (int64_t)1 << 40},       // CV_OPT_PREP_OVERLAP_MIN
+    {0, 0, 1},                          // CV_OPT_TIMELINE
 };
 
 // A snapshot of a context's options, taken once per call.
@@ -425,7 +442,7 @@ struct Opts {
     CvkPlan plan;
     size_t pipe_min, pipe_first, pipe_chunk, async_chunk, small_direct_min, shard_min, spread_min, merkle_chunk;
     size_t prep_overlap_min;
-    int threads, small_zc, auto_keyed;
+    int threads, small_zc, auto_keyed, timeline;
 };
 
 // host-side time of the pipelined path (cv_diag_stats CV_STATS_PIPE), of the zero-copy small path
@@ -437,6 +454,7 @@ struct Stats {
     uint64_t small_calls = 0;
     uint64_t calls = 0, routed_whole = 0, split_calls = 0, shards = 0, keyed_calls = 0, keyed_chunks = 0,
              merkle_calls = 0, merkle_chunks = 0;
+    double tl[9] = {};     // CV_STATS_TIMELINE sums (PipeOut::tl_sum) + calls
 };
 
 static inline double now_s() {
@@ -618,6 +636,7 @@ struct cv_ctx {
         o.spread_min = (size_t)opt[CV_OPT_SPREAD_MIN].load();
         o.merkle_chunk = (size_t)opt[CV_OPT_MERKLE_CHUNK].load();
         o.prep_overlap_min = (size_t)opt[CV_OPT_PREP_OVERLAP_MIN].load();
+        o.timeline = (int)opt[CV_OPT_TIMELINE].load();
         return o;
     }
 };
@@ -648,7 +667,11 @@ uint64_t cv_msg_extent(size_t n, const uint64_t *off, const uint32_t *len) {
     auto scan = [&](size_t k) {
         uint64_t hi = 0;
         const size_t i1 = std::min(n, (k + 1) * kSlice);
-        for (size_t i = k * kSlice; i < i1; i++) hi = std::max<uint64_t>(hi, off[i] + len[i]);
+        for (size_t i = k * kSlice; i < i1; i++) {
+            uint64_t end = off[i] + len[i];
+            end |= -(uint64_t)(end < off[i]);   // a wrapping record reports UINT64_MAX: past any arena
+            hi = std::max<uint64_t>(hi, end);
+        }
         part[k] = hi;
     };
     const size_t nt = std::min<size_t>(ns, 8);
@@ -683,7 +706,7 @@ int cv_diag_stats(cv_ctx *ctx, int which, double *out, size_t nout, int reset) {
     if (!ctx || (nout && !out)) return CV_E_ARGS;
     std::lock_guard<std::mutex> g(ctx->st_mu);
     Stats &s = ctx->stats;
-    double v[8] = {};
+    double v[9] = {};
     size_t nv = 0;
     if (which == CV_STATS_PIPE) {
         for (int k = 0; k < 5; k++) v[k] = s.pipe[k];
@@ -700,6 +723,9 @@ int cv_diag_stats(cv_ctx *ctx, int which, double *out, size_t nout, int reset) {
                                s.merkle_calls, s.merkle_chunks};
         for (int k = 0; k < 8; k++) v[k] = (double)r[k];
         nv = 8;
+    } else if (which == CV_STATS_TIMELINE) {
+        for (int k = 0; k < 9; k++) v[k] = s.tl[k];
+        nv = 9;
     } else {
         return CV_E_ARGS;
     }
@@ -711,6 +737,8 @@ int cv_diag_stats(cv_ctx *ctx, int which, double *out, size_t nout, int reset) {
         } else if (which == CV_STATS_SMALL) {
             std::fill(s.small, s.small + 5, 0.0);
             s.small_calls = 0;
+        } else if (which == CV_STATS_TIMELINE) {
+            std::fill(s.tl, s.tl + 9, 0.0);
         } else {
             s.calls = s.routed_whole = s.split_calls = s.shards = s.keyed_calls = s.keyed_chunks = s.merkle_calls =
                 s.merkle_chunks = 0;
@@ -990,8 +1018,10 @@ template <int> static inline void span_slice_impl(size_t i0, size_t i1, const ui
                                                   uint64_t *out) {
     uint64_t lo = UINT64_MAX, hi = 0, bytes = 0;
     for (size_t i = i0; i < i1; i++) {
+        uint64_t end = off[i] + len[i];
+        end |= -(uint64_t)(end < off[i]);   // a record whose end wraps saturates: never "in bounds"
         lo = std::min<uint64_t>(lo, off[i]);
-        hi = std::max<uint64_t>(hi, off[i] + len[i]);
+        hi = std::max<uint64_t>(hi, end);
         bytes += len[i];
     }
     out[0] = lo;
@@ -1045,6 +1075,7 @@ static Span arena_span(size_t b, size_t e, const uint64_t *off, const uint32_t *
 struct Stage {
     size_t n = 0, o_pk = 0, o_kidx = 0, o_sig = 0, o_off = 0, o_len = 0, o_ar = 0, total = 0;
     uint64_t lo = 0, hi = 0;
+    uint64_t extent = 0;   // max(off + len) over the records, whatever the layout (UINT64_MAX: an end wrapped)
     bool compact = false, keyed = false;
 };
 static Stage stage_plan(size_t b, size_t e, const uint64_t *off, const uint32_t *len, WorkerPool *pool = nullptr,
@@ -1057,6 +1088,7 @@ static Stage stage_plan(size_t b, size_t e, const uint64_t *off, const uint32_t 
     st.compact = sp.hi - lo > 2 * sp.bytes + (1u << 20);
     st.lo = st.compact ? 0 : lo;
     st.hi = st.compact ? sp.bytes : sp.hi;
+    st.extent = sp.hi;
     const size_t n = st.n;
     st.o_pk = 0;
     st.o_kidx = keyed ? 0 : al16(n * 32);
@@ -1066,6 +1098,12 @@ static Stage stage_plan(size_t b, size_t e, const uint64_t *off, const uint32_t 
     st.o_ar = st.o_len + al16(n * 4);
     st.total = st.o_ar + al16(st.hi - st.lo + 16);
     return st;
+}
+// The records of a stage end inside the caller's arena of arena_bytes (UINT64_MAX: no bound given) and no
+// record's off + len wraps.  Checked on the true extent, not on [lo, hi): a compacted stage's hi is the SUM of
+// its message lengths, which says nothing about where the scattered records lie.
+static bool stage_in_bounds(const Stage &st, uint64_t arena_bytes) {
+    return st.extent != UINT64_MAX && st.extent <= arena_bytes;
 }
 // Packs records [b, e) into h by the plan (keys / key indices + signatures first: `first_part` runs after
 // them, so their DMA can start while the rest is packed).
@@ -1156,6 +1194,7 @@ static hipError_t stage_dma_direct(const Stage &st, uint8_t *dv, size_t b, const
 struct MStage {
     size_t t0 = 0, t1 = 0, l0 = 0, l1 = 0, o_off = 0, o_len = 0, o_txb = 0, o_ar = 0, total = 0;
     uint64_t lo = 0, hi = 0;
+    uint64_t extent = 0;   // as Stage::extent
     bool compact = false;
 };
 static MStage mstage_plan(size_t t0, size_t t1, const uint32_t *txb, const uint64_t *off, const uint32_t *len,
@@ -1171,6 +1210,7 @@ static MStage mstage_plan(size_t t0, size_t t1, const uint32_t *txb, const uint6
     st.compact = nl && sp.hi - lo > 2 * sp.bytes + (1u << 20);
     st.lo = st.compact ? 0 : (nl ? lo : 0);
     st.hi = st.compact ? sp.bytes : (nl ? sp.hi : 0);
+    st.extent = nl ? sp.hi : 0;
     st.o_off = 0;
     st.o_len = al16(nl * 8);
     st.o_txb = st.o_len + al16(nl * 4);
@@ -1609,7 +1649,7 @@ static int verify_shard_mid(cv_ctx *ctx, Device &d, const Opts &o, size_t b, siz
     t[1] = now_s();
     // ---- tail: offsets | lengths | message bytes (the Stage layout from o_off on), behind the head's DMA
     const Stage st = stage_plan(b, e, in.off, in.len, head_pinned ? nullptr : pool);
-    if (st.hi > in.arena_bytes) return CV_E_ARGS;   // (drain: the head's DMA is waited for)
+    if (!stage_in_bounds(st, in.arena_bytes)) return CV_E_ARGS;   // (drain: the head's DMA is waited for)
     CV_TRY(sl.packed.ensure(st.total));
     uint8_t *dv = sl.packed.as<uint8_t>();
     if (n >= o.small_direct_min && stage_direct(st, b, in.pk, nullptr, in.sig, in.arena, in.off, in.len)) {
@@ -1656,7 +1696,7 @@ static int verify_shard_small(cv_ctx *ctx, Device &d, const Opts &o, size_t b, s
     // pool, whose helpers the packing needs next anyway
     const bool in_place = pool && n >= o.small_direct_min && host_pinned(in.pk + b * 32, n * 32);
     const Stage st = stage_plan(b, e, in.off, in.len, in_place ? nullptr : pool);
-    if (st.hi > in.arena_bytes) return CV_E_ARGS;
+    if (!stage_in_bounds(st, in.arena_bytes)) return CV_E_ARGS;
     if (o.small_zc && cvk_tri_zc_ok(&o.plan, (uint32_t)n, (uint32_t)n))
         return verify_shard_small_zc(ctx, d, o, st, b, in, pool, t_plan,
                                      o.small_zc == 2 || (o.small_zc == 3 && n >= 2048));
@@ -1749,6 +1789,7 @@ static int pipe_copy_back(Device &d, PipeOut &po) {
     // copies nor holds a compute stream the next call's kernels run on)
     for (int k = 0; k <= kPipeSlots; k++)
         if (po.slot_used[k]) CV_TRY(hipEventSynchronize(po.slot_done[k]));
+    const bool timeline = po.tl_n > 0 && po.tl.size() >= (size_t)po.tl_n * 3 + 2;
     constexpr size_t kDirect = 1u << 20;
     size_t hb = 0;
     for (int k = 0; k < po.nseg; k++) {
@@ -1770,7 +1811,41 @@ static int pipe_copy_back(Device &d, PipeOut &po) {
     // ms per call of two later calls in flight (keyed host C2 8.5-8.7 -> 7.3 ms, DESIGN "Host runtime effects")
     if (!po.copied) CV_TRY(hipEventCreateWithFlags(&po.copied, hipEventDisableTiming));
     CV_TRY(hipEventRecord(po.copied, d.outs));
+    if (timeline) CV_TRY(hipEventRecord(po.tl[(size_t)po.tl_n * 3 + 1], d.outs));
     CV_TRY(hipEventSynchronize(po.copied));
+    if (timeline) {
+        auto at = [&](size_t k) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, po.tl[0], po.tl[k]);
+            return (double)ms;
+        };
+        const int J = po.tl_n;
+        std::vector<std::pair<double, double>> iv(J);
+        double ramp = 1e30, span = 0, dma_end = at(1 + 3 * (size_t)(J - 1));
+        for (int j = 0; j < J; j++) {
+            iv[j] = {at(2 + 3 * (size_t)j), at(3 + 3 * (size_t)j)};
+            ramp = std::min(ramp, iv[j].first);
+            span = std::max(span, iv[j].second);
+        }
+        std::sort(iv.begin(), iv.end());
+        double busy = 0, cur0 = iv[0].first, cur1 = iv[0].second;
+        for (int j = 1; j < J; j++) {
+            if (iv[j].first > cur1) {
+                busy += cur1 - cur0;
+                cur0 = iv[j].first;
+                cur1 = iv[j].second;
+            } else {
+                cur1 = std::max(cur1, iv[j].second);
+            }
+        }
+        busy += cur1 - cur0;
+        const double out_end = at((size_t)J * 3 + 1);
+        const double v[8] = {ramp, dma_end, span, busy, span - ramp - busy, span - dma_end, out_end - span,
+                             (double)po.tl_first};
+        for (int k = 0; k < 8; k++) po.tl_sum[k] = v[k];
+        po.tl_ready = true;
+        po.tl_n = 0;
+    }
     for (int k = 0; k < po.nseg; k++) {
         const PipeOut::Seg &sg = po.seg[k];
         if (sg.len && sg.len < kDirect) std::memcpy(sg.dst, po.hout.as<uint8_t>() + sg.off, sg.len);
@@ -1812,6 +1887,11 @@ struct PipeFrame {
     bool used[kPipeSlots + 1] = {};   // + the copy stream (Merkle kernels)
     double t[5] = {};   // plan, pack, wait, enqueue (seconds)
     uint64_t chunks = 0, direct = 0;
+    bool tl = false;    // CV_OPT_TIMELINE: record po.tl's events (synchronous verify calls)
+    hipError_t tl_record(size_t k, hipStream_t s) {
+        hipEvent_t e = po.tl_ev(k);
+        return e ? hipEventRecord(e, s) : hipErrorOutOfMemory;
+    }
     int init() {
         for (int k = 0; k < kPipeSlots; k++) {
             CV_TRY(slot_stream(d, k, &ss[k]));
@@ -1885,12 +1965,15 @@ struct PipeFrame {
     }
     // after sub-chunk j's copies into block q: compute stream j % 2 waits for them
     int copied(int q, int j) {
+        if (tl) CV_TRY(tl_record(1 + 3 * (size_t)j, d.copy));
         CV_TRY(hipEventRecord(d.in_ready[q], d.copy));
         CV_TRY(hipStreamWaitEvent(ss[j % kPipeSlots], d.in_ready[q], 0));
+        if (tl) CV_TRY(tl_record(2 + 3 * (size_t)j, ss[j % kPipeSlots]));
         return CV_OK;
     }
     // after sub-chunk j's kernels: block q is free once they are done
     int launched(int q, int j) {
+        if (tl) CV_TRY(tl_record(3 + 3 * (size_t)j, ss[j % kPipeSlots]));
         CV_TRY(hipEventRecord(d.in_free[q], ss[j % kPipeSlots]));
         d.in_used[q] = true;
         used[j % kPipeSlots] = true;
@@ -1900,6 +1983,8 @@ struct PipeFrame {
     // completion marks per slot stream (pipe_finish joins on the host; no GPU-side join, which would hold
     // the next call's kernels on that stream until this call had finished)
     int complete() {
+        po.tl_n = tl ? (int)chunks : 0;
+        if (tl && !po.tl_ev((size_t)chunks * 3 + 1)) return CV_E_HIP;   // (the result copies' end)
         for (int k = 0; k <= kPipeSlots; k++) {
             po.slot_used[k] = used[k];
             if (used[k]) CV_TRY(hipEventRecord(po.slot_done[k], k < kPipeSlots ? ss[k] : d.copy));
@@ -1992,19 +2077,23 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
     const std::vector<size_t> cut = async ? pipe_cuts(b, e, ach, ach, false) : pipe_cuts(b, e, o.pipe_first, sch, true);
     size_t max_m = 1;
     for (size_t j = 0; j + 1 < cut.size(); j++) max_m = std::max(max_m, cut[j + 1] - cut[j]);
+    f.tl = o.timeline && !async;
+    po.tl_ready = false;
+    po.tl_first = cut.size() > 1 ? cut[1] - cut[0] : 0;
     for (size_t j = 0; j + 1 < cut.size(); j++) {
         const size_t c0 = cut[j], c1 = cut[j + 1], m = c1 - c0;
         Slot &sl = d.slot[j % kPipeSlots];
         hipStream_t s = f.ss[j % kPipeSlots];
         double t0 = now_s();
         const Stage st = stage_plan(c0, c1, in.off, in.len, pool, keyed);
-        if (st.hi > in.arena_bytes) return CV_E_ARGS;   // before this sub-chunk's copy (drain: the ones before it)
+        if (!stage_in_bounds(st, in.arena_bytes)) return CV_E_ARGS;   // before this sub-chunk's copy (drain: the ones before it)
         const bool direct = stage_direct(st, c0, in.pk, kidx, in.sig, in.arena, in.off, in.len);
         double t1 = now_s();
         f.t[0] += t1 - t0;
         int q;
         uint8_t *dv;
         if ((rc = f.block(&q, st.total, &dv, (size_t)((double)st.total / (double)m * (double)max_m))) != CV_OK) return rc;
+        if (f.tl && j == 0) CV_TRY(f.tl_record(0, d.copy));
         if (direct) {
             t0 = now_s();
             f.t[2] += t0 - t1;
@@ -2140,6 +2229,7 @@ static int merkle_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, si
         const size_t c0 = cut[j], c1 = cut[j + 1];
         double ta = now_s();
         const MStage st = mstage_plan(c0, c1, in.txb, in.off, in.len, pool);
+        if (st.extent == UINT64_MAX) return CV_E_ARGS;   // a leaf's off + len wraps
         const bool direct = mstage_direct(st, in.txb, in.arena, in.off, in.len);
         double tb = now_s();
         f.t[0] += tb - ta;
@@ -2391,6 +2481,7 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
     for (size_t J = 0; J < nm; J++) {
         double ta = now_s();
         const MStage st = mstage_plan(mcut[J], mcut[J + 1], mi.txb, mi.off, mi.len, pool);
+        if (st.extent == UINT64_MAX) return CV_E_ARGS;   // a leaf's off + len wraps
         const bool direct = mstage_direct(st, mi.txb, mi.arena, mi.off, mi.len);
         double tb = now_s();
         f.t[0] += tb - ta;
@@ -2531,6 +2622,11 @@ static int verify_shard(cv_ctx *ctx, Device &d, const Opts &o, size_t b, size_t 
     rc = pipe_finish(d, po);
     std::lock_guard<std::mutex> g(ctx->st_mu);
     ctx->stats.pipe[4] += now_s() - t0;
+    if (po.tl_ready) {
+        for (int k = 0; k < 8; k++) ctx->stats.tl[k] += po.tl_sum[k];
+        ctx->stats.tl[8] += 1;
+        po.tl_ready = false;
+    }
     return rc;
 }
 
@@ -2822,6 +2918,7 @@ static int merkle_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const
         if (!ticket) {                                // small synchronous shards: one DMA, no pipeline frame
             WorkerPool *pool = &d.workers(threads);
             const MStage st = mstage_plan(t0, t1, tx_leaf_begin, leaf_off, leaf_len, pool);
+            if (st.extent == UINT64_MAX) return CV_E_ARGS;   // a leaf's off + len wraps
             if (st.total <= kMerkleSmall) return merkle_shard_small(d, st, in, pool);
         }
         int k = 0, r = CV_OK;
@@ -2959,6 +3056,7 @@ static int txs_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const ui
         if (!ticket) {                                // small synchronous shards: one DMA, one stream
             WorkerPool *pool = &d.workers(threads);
             const MStage st = mstage_plan(t0, t1, tx_leaf_begin, leaf_off, leaf_len, pool);
+            if (st.extent == UINT64_MAX) return CV_E_ARGS;   // a leaf's off + len wraps
             const size_t ns = tx_sig_begin[t1] - tx_sig_begin[t0];
             if (st.total + ns * 96 <= kMerkleSmall) return txs_shard_small(d, o, st, in, pool);
         }

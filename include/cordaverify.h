@@ -305,7 +305,9 @@ int cv_calibrate_cycles(cv_ctx *ctx, int device, double *out);
 #define CV_OPT_PREP_OVERLAP_MIN 16  /* unpipelined host batches from this size send keys and signatures first and
                                        decode their points on a helper stream while the rest of their inputs is still
                                        in DMA (32768) */
-#define CV_OPT_COUNT 17
+#define CV_OPT_TIMELINE 17          /* diagnostics: 1 = time each synchronous pipelined call on the GPU (HIP events per
+                                       sub-chunk, read back as CV_STATS_TIMELINE); 0 off (default) */
+#define CV_OPT_COUNT 18
 int cv_set_option(cv_ctx *ctx, int option, int64_t value);
 int cv_get_option(cv_ctx *ctx, int option, int64_t *value);
 
@@ -316,10 +318,16 @@ int cv_get_option(cv_ctx *ctx, int option, int64_t *value);
  *   CV_STATS_SMALL {setup, pack (+ input DMA issue), launch, sync, assemble seconds of the unpipelined host path
  *                   (notary-sized batches: zero-copy and one-DMA forms); calls}
  *   CV_STATS_ROUTE {calls, routed whole to one device, cut over several, shards, keyed shards, keyed
- *                   sub-chunks, Merkle calls, Merkle sub-chunks} */
+ *                   sub-chunks, Merkle calls, Merkle sub-chunks}
+ *   CV_STATS_TIMELINE {sums over the synchronous pipelined calls timed with CV_OPT_TIMELINE = 1, in ms from each
+ *                   call's first input DMA: first kernel start (the ramp), last input DMA end, last kernel end (the
+ *                   span), kernel-busy time (union over the sub-chunks' launch groups), idle gaps between the first
+ *                   kernel start and the span's end, the tail after the last DMA, the result copy; first sub-chunk
+ *                   records; sub-chunks; calls timed} */
 #define CV_STATS_PIPE 0
 #define CV_STATS_SMALL 1
 #define CV_STATS_ROUTE 2
+#define CV_STATS_TIMELINE 3
 int cv_diag_stats(cv_ctx *ctx, int which, double *out, size_t nout, int reset);
 
 /* max(msg_off[i] + msg_len[i]) over n records (0 for n = 0): the arena bytes a batch reaches, for the

@@ -53,7 +53,7 @@ def test_gpus_more_than_visible_fails_nonzero():
         pytest.skip("two or more GPUs visible")
     r = _run(["--gpus", "2", "--steps", "1", "--warmup", "0"], timeout=120)
     assert r.returncode == 2, (r.stdout, r.stderr[-2000:])
-    assert "GPU(s) are visible" in r.stderr
+    assert "GPU(s) are visible" in r.stderr or "cannot count the GPUs" in r.stderr
     assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
 
 
@@ -78,3 +78,61 @@ def test_launcher_propagates_failure_and_stops_the_rest():
 def test_launcher_all_ranks_ok():
     code = "import os, sys; sys.exit(0 if os.environ['MASTER_ADDR'] == '127.0.0.1' else 1)"
     assert launch.spawn(3, [sys.executable, "-c", code], require_gpus=False) == 0
+
+
+def test_plumbing_noop_verify_fails_the_check():
+    """the bitmaps are zeroed after warm-up, so a timed "verify" that writes nothing fails
+    the all-ones check (non-zero exit, no line) instead of passing on the warm-up's words."""
+    r = _run(["--gpus", "2", "--plumbing", "--plumbing-noop", "--steps", "2", "--warmup", "1", "--n", "640"])
+    assert r.returncode != 0, r.stdout
+    assert "not written by the timed steps" in r.stderr
+    assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
+
+
+def test_visible_gpus_never_calls_hip(monkeypatch):
+    """with no KFD topology and amdsmi failing, the launcher refuses (exit 2) and never
+    reaches HIP's device count (torch._C._cuda_getDeviceCount / torch.cuda.device_count), because it forks the
+    rank processes afterwards."""
+    import torch
+
+    def boom(*a, **k):
+        raise AssertionError("HIP device count called by the launcher")
+
+    monkeypatch.setattr(torch._C, "_cuda_getDeviceCount", boom, raising=False)
+    monkeypatch.setattr(torch.cuda, "device_count", boom)
+    monkeypatch.setattr(launch, "KFD_NODES", "/nonexistent/kfd/topology/nodes")
+
+    class _FailingSmi:
+        def amdsmi_init(self):
+            raise RuntimeError("amdsmi: no driver")
+
+    monkeypatch.setitem(sys.modules, "amdsmi", _FailingSmi())
+    assert launch.visible_gpus() == -1
+    assert launch.spawn(2, [sys.executable, "-c", "pass"], require_gpus=True) == 2
+
+
+def _fake_node(root, idx, simd, minor):
+    d = root / str(idx)
+    d.mkdir(parents=True)
+    (d / "properties").write_text(f"cpu_cores_count 0\nsimd_count {simd}\ndrm_render_minor {minor}\n")
+
+
+def test_kfd_topology_count(tmp_path, monkeypatch):
+    """The sysfs count: GPU nodes (simd_count > 0) whose render node this process can open; CPU nodes and GPUs
+    of other containers (render node absent) do not count; the visibility variables restrict the result."""
+    nodes, dri = tmp_path / "nodes", tmp_path / "dri"
+    dri.mkdir()
+    _fake_node(nodes, 0, 0, -1)                          # the CPU node
+    for i, minor in enumerate((128, 129, 130, 131)):
+        _fake_node(nodes, i + 1, 1024, minor)
+    for minor in (128, 130, 131):                        # renderD129 belongs to another container
+        (dri / f"renderD{minor}").write_text("")
+    assert launch._kfd_gpu_count(str(nodes), str(dri)) == 3
+    assert launch._kfd_gpu_count(str(tmp_path / "none"), str(dri)) is None
+    for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    assert launch._apply_visibility(3) == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1")
+    assert launch._apply_visibility(3) == 2
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0")
+    assert launch._apply_visibility(3) == 1

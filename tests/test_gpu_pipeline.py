@@ -365,6 +365,78 @@ def test_verify_batch_ex_arena_bound(engine, corpus, n):
         engine.verify_batch(pk, sig, arena[:extent - 1], off, ln)
 
 
+@pytest.mark.parametrize("n", [100, 9001, 65536, 200_000])
+def test_arena_bound_scattered_and_wrapping(engine, corpus, n):
+    """the arena bound is checked on the records' true extent, not on the staged range.  A
+    scattered batch (the staging compacts it: its byte range is far above twice its bytes) verifies exactly; the
+    same batch with its LAST record pointing a long way past the arena — the compacted stage's range is only the
+    sum of the lengths, so a check on it would pass and the packing would read past the arena — is rejected with
+    CV_E_ARGS, as is a record whose off + len wraps past 2^64, with and without a bound (small, zero-copy, mid-size
+    and pipelined forms: n = 100, 9,001, 65,536, 200,000), and the Python binding raises ValueError for both."""
+    lib = native.load()
+    p = native._p
+    idx = np.arange(n) % len(corpus["pk"])
+    pk, sig = np.ascontiguousarray(corpus["pk"][idx]), np.ascontiguousarray(corpus["sig"][idx])
+    off = np.ascontiguousarray(corpus["off"][idx]).astype(np.uint64)
+    ln = np.ascontiguousarray(corpus["len"][idx])
+    A = corpus["arena"].size
+    gap = (2 * int(ln.astype(np.uint64).sum()) + (4 << 20) + 15) // 16 * 16
+    big = np.zeros(A + gap + A, np.uint8)                 # the corpus arena twice, `gap` bytes apart
+    big[:A] = corpus["arena"]
+    big[A + gap:] = corpus["arena"]
+    off_s = off.copy()
+    off_s[1::2] += np.uint64(A + gap)                     # odd records read the far copy: a scattered stage
+    bm = np.zeros((n + 63) // 64, np.uint64)
+    rc = lib.cv_ed25519_verify_batch_ex(engine._h, n, p(pk), p(sig), p(big), big.size, p(off_s), p(ln), p(bm), None,
+                                        None)
+    assert rc == 0
+    assert np.array_equal(_bits(bm, n), corpus["verdict"][idx].astype(bool))
+    bad = off_s.copy()
+    bad[-1] = np.uint64(big.size + gap)                   # a record far past the arena, in the last (sub-)chunk
+    rc = lib.cv_ed25519_verify_batch_ex(engine._h, n, p(pk), p(sig), p(big), big.size, p(bad), p(ln), p(bm), None, None)
+    assert rc == -3
+    with pytest.raises(ValueError, match="exceeds the arena"):
+        engine.verify_batch(pk, sig, big, bad, ln)
+    wrap = off_s.copy()
+    wrap[-1] = np.uint64(2 ** 64 - 8)
+    lw = ln.copy()
+    lw[-1] = 32                                           # off + len wraps to 24
+    for bound in (big.size, 2 ** 64 - 1):
+        rc = lib.cv_ed25519_verify_batch_ex(engine._h, n, p(pk), p(sig), p(big), bound, p(wrap), p(lw), p(bm), None,
+                                            None)
+        assert rc == -3, bound
+    assert lib.cv_ed25519_verify_batch(engine._h, n, p(pk), p(sig), p(big), p(wrap), p(lw), p(bm), None) == -3
+    with pytest.raises(ValueError, match="exceeds the arena"):
+        engine.verify_batch(pk, sig, big, wrap, lw)
+    # the engine is still usable and exact after the rejected calls
+    rc = lib.cv_ed25519_verify_batch_ex(engine._h, n, p(pk), p(sig), p(big), big.size, p(off_s), p(ln), p(bm), None,
+                                        None)
+    assert rc == 0 and np.array_equal(_bits(bm, n), corpus["verdict"][idx].astype(bool))
+
+
+def test_merkle_wrapping_leaf_rejected(engine, merkle_cases):
+    """A leaf whose off + len wraps past 2^64 is rejected by the Merkle entry points (CV_E_ARGS), small and
+    pipelined forms, instead of being gathered from a wrapped address."""
+    lib = native.load()
+    p = native._p
+    m = merkle_cases
+    arena, off, ln = m["arena"], m["leaf_off"].astype(np.uint64), m["leaf_len"]
+    txb = np.ascontiguousarray(m["tx_leaf_begin"], dtype=np.uint32)
+    ntx = txb.size - 1
+    ids = np.zeros((ntx, 32), np.uint8)
+    st = np.zeros(ntx, np.uint8)
+    w = off.copy()
+    k = int(txb[-1]) - 1
+    w[k] = np.uint64(2 ** 64 - 4)
+    lw = ln.copy()
+    lw[k] = 64
+    assert lib.cv_merkle_tx_ids_ex(engine._h, ntx, p(arena), p(w), p(lw), p(txb), p(ids), p(st)) == -3
+    t = ctypes.c_uint64()
+    assert lib.cv_merkle_tx_ids_async(engine._h, ntx, p(arena), p(w), p(lw), p(txb), p(ids), p(st),
+                                      ctypes.byref(t)) == -3
+    assert lib.cv_merkle_tx_ids_ex(engine._h, ntx, p(arena), p(off), p(ln), p(txb), p(ids), p(st)) == 0
+
+
 @pytest.mark.parametrize("n,overlap_min", [(1000, 64), (16384, 16384), (32768, 32768), (65536, 32768)])
 def test_notary_midsize_forms_golden_and_oracle(engine, corpus, oracle_c, n, overlap_min):
     """Notary batches from the tri form to the mid sizes (16,384 and 32,768: quad form; 65,536: throughput form),
@@ -399,3 +471,32 @@ def test_notary_midsize_forms_golden_and_oracle(engine, corpus, oracle_c, n, ove
                     assert np.array_equal(status, es), (om, pinned)
                     if n % 64:
                         assert int(bitmap[-1]) >> (n % 64) == 0
+
+
+def test_sync_call_timeline_diagnostics(engine):
+    """CV_OPT_TIMELINE: a synchronous pipelined call timed on the GPU (events per sub-chunk) keeps its verdicts
+    exact and reports a consistent timeline: 0 <= ramp <= span, busy + idle = span - ramp, tail = span - last DMA
+    end, the first sub-chunk the plan's; off again, nothing more is recorded."""
+    n = 300_000
+    b = workload.make_batch(engine, 0, n, 300, seed=77)
+    expect = workload.corrupt_fraction(b, 11).cpu().numpy()
+    a = tuple(engine.host_copy(x) for x in b.to_host())
+    del b
+    engine.set_option("timeline", 1)
+    try:
+        engine.stats("timeline", reset=True)
+        for _ in range(2):
+            bm, _ = engine.verify_batch(*a, want_status=False)
+            assert np.array_equal(_bits(bm, n), expect)
+        t = engine.stats("timeline", reset=True)
+    finally:
+        engine.set_option("timeline", 0)
+    assert t["calls"] == 2
+    c = t["calls"]
+    ramp, span, busy, idle = t["ramp_ms"] / c, t["span_ms"] / c, t["busy_ms"] / c, t["idle_ms"] / c
+    assert 0 <= ramp <= span and busy > 0 and idle >= -1e-3
+    assert abs(busy + idle - (span - ramp)) < 1e-3
+    assert abs(t["tail_ms"] / c - (span - t["dma_end_ms"] / c)) < 1e-3
+    assert t["result_copy_ms"] >= 0 and t["first_subchunk"] / c == engine.get_option("pipe_first")
+    engine.verify_batch(*a, want_status=False)
+    assert engine.stats("timeline")["calls"] == 0
