@@ -171,6 +171,7 @@ constexpr int kPipeSlots = 2;   // compute slots the pipeline deals its sub-chun
 constexpr int kRing = 16;
 constexpr int kStage = 6;       // pinned host staging blocks (pageable inputs are packed into them)
 constexpr int kOuts = 4;        // pipelined host calls in flight per device (async verify + Merkle calls)
+constexpr size_t kFailKeep = 1024;   // failed asynchronous calls remembered per output (PipeOut::failed)
 
 // The output of one pipelined host call on one device: its results on the device (dout), the pinned
 // copy they come back through, and what pipe_finish copies where.  pending: enqueued, results not yet in
@@ -198,8 +199,8 @@ struct PipeOut {
     PinBuf tstage;   // transaction calls: the shard's signature boundaries when the caller's are pageable
     hipEvent_t copied = nullptr;   // after the call's result copies on the output stream (pipe_copy_back)
     // CV_OPT_TIMELINE (synchronous calls): timing events — [0] the first input DMA's start, then per sub-chunk j
-    // [1 + 3j] its DMA's end (copy stream), [2 + 3j] its launch group's start, [3 + 3j] its end (slot stream) —
-    // and [tl_n * 3 + 1] the result copies' end; summarised by pipe_copy_back into tl_sum
+    // [1 + 3j] its DMA's end (copy stream), [2 + 3j] its launch group's start, [3 + 3j] its end (slot stream);
+    // summarised by pipe_copy_back into tl_sum (the result copies timed on the host there)
     std::vector<hipEvent_t> tl;
     int tl_n = 0;
     size_t tl_first = 0;
@@ -213,8 +214,13 @@ struct PipeOut {
         }
         return tl[k];
     }
-    // calls on this output whose finish failed: (gen, error), kept after the output is reused so a cv_wait on
-    // such a call still returns its error (bounded: the last 64 failures)
+    // asynchronous calls on this output whose finish failed: (gen, error), kept after the output is reused so a
+    // cv_wait on such a call still returns its error.  Only ticketed calls are recorded (a synchronous call returns
+    // its error itself), and a ticket whose call has finished leaves the live map, with its result, at the next
+    // ticket_add once 64 are live; so fewer than 64 + kOuts x devices recorded failures can still be needed, and
+    // the list keeps kFailKeep (a fixed 64 could evict a live ticket's failure behind failing
+    // synchronous calls, and cv_wait then returned CV_OK).
+    bool ticketed = false;
     std::deque<std::pair<uint64_t, int>> failed;
     int result_of(uint64_t g) const {
         for (const auto &f : failed)
@@ -435,6 +441,9 @@ static const OptDesc kOpt[CV_OPT_COUNT] = {
     {262144, 1, 1 << 24},               // CV_OPT_MERKLE_CHUNK
     {32768, 1, (int64_t)1 << 40},       // CV_OPT_PREP_OVERLAP_MIN
     {0, 0, 1},                          // CV_OPT_TIMELINE
+    {16, 1, 1024},                      // CV_OPT_PIPE_SPLIT
+    {1, 0, 1},                          // CV_OPT_PIPE_OVERLAP_FIRST
+    {4, 1, 16},                         // CV_OPT_MID_PIECES
 };
 
 // A snapshot of a context's options, taken once per call.
@@ -442,7 +451,8 @@ struct Opts {
     CvkPlan plan;
     size_t pipe_min, pipe_first, pipe_chunk, async_chunk, small_direct_min, shard_min, spread_min, merkle_chunk;
     size_t prep_overlap_min;
-    int threads, small_zc, auto_keyed, timeline;
+    size_t pipe_split, mid_pieces;
+    int threads, small_zc, auto_keyed, timeline, pipe_overlap_first;
 };
 
 // host-side time of the pipelined path (cv_diag_stats CV_STATS_PIPE), of the zero-copy small path
@@ -637,6 +647,9 @@ struct cv_ctx {
         o.merkle_chunk = (size_t)opt[CV_OPT_MERKLE_CHUNK].load();
         o.prep_overlap_min = (size_t)opt[CV_OPT_PREP_OVERLAP_MIN].load();
         o.timeline = (int)opt[CV_OPT_TIMELINE].load();
+        o.pipe_split = (size_t)opt[CV_OPT_PIPE_SPLIT].load();
+        o.pipe_overlap_first = (int)opt[CV_OPT_PIPE_OVERLAP_FIRST].load();
+        o.mid_pieces = (size_t)opt[CV_OPT_MID_PIECES].load();
         return o;
     }
 };
@@ -1613,6 +1626,8 @@ static int verify_shard_mid(cv_ctx *ctx, Device &d, const Opts &o, size_t b, siz
     const size_t words = (n + 63) / 64;
     const size_t o_bm = 0, o_st = al16(words * 8), total_out = o_st + al16(n);
     const size_t h_sig = al16(n * 32), h_total = h_sig + al16(n * 64);
+    // pageable inputs go up in about 1 MB pieces of keys + signatures (at most CV_OPT_MID_PIECES)
+    const size_t pieces = pool ? std::max<size_t>(1, std::min<size_t>(o.mid_pieces, h_total >> 20)) : 1;
     double t[6];
     t[0] = t_plan;
     Slot &sl = d.slot[0];
@@ -1640,10 +1655,17 @@ static int verify_shard_mid(cv_ctx *ctx, Device &d, const Opts &o, size_t b, siz
         CV_TRY(hipMemcpyAsync(dh, in.pk + b * 32, n * 32, hipMemcpyHostToDevice, s));
         CV_TRY(hipMemcpyAsync(dh + h_sig, in.sig + b * 64, n * 64, hipMemcpyHostToDevice, s));
     } else {
+        // pageable keys and signatures: packed into pinned staging and DMAed in `pieces` record ranges, each range's
+        // two DMAs issued as soon as it is packed, so the DMA runs beside the packing of the next range
         CV_TRY(sl.pin_head.ensure(h_total));
         uint8_t *hh = sl.pin_head.as<uint8_t>();
-        par_copy({{hh, in.pk + b * 32, n * 32}, {hh + h_sig, in.sig + b * 64, n * 64}}, pool);
-        CV_TRY(hipMemcpyAsync(dh, hh, h_total, hipMemcpyHostToDevice, s));
+        for (size_t p = 0; p < pieces; p++) {
+            const size_t r0 = n * p / pieces, r1 = n * (p + 1) / pieces;
+            par_copy({{hh + r0 * 32, in.pk + (b + r0) * 32, (r1 - r0) * 32},
+                      {hh + h_sig + r0 * 64, in.sig + (b + r0) * 64, (r1 - r0) * 64}}, pool);
+            CV_TRY(hipMemcpyAsync(dh + r0 * 32, hh + r0 * 32, (r1 - r0) * 32, hipMemcpyHostToDevice, s));
+            CV_TRY(hipMemcpyAsync(dh + h_sig + r0 * 64, hh + h_sig + r0 * 64, (r1 - r0) * 64, hipMemcpyHostToDevice, s));
+        }
     }
     CV_TRY(hipEventRecord(po.ready, s));
     t[1] = now_s();
@@ -1657,6 +1679,20 @@ static int verify_shard_mid(cv_ctx *ctx, Device &d, const Opts &o, size_t b, siz
         CV_TRY(hipMemcpyAsync(dv + st.o_len, in.len + b, n * 4, hipMemcpyHostToDevice, s));
         if (st.hi > st.lo)
             CV_TRY(hipMemcpyAsync(dv + st.o_ar, in.arena + st.lo, st.hi - st.lo, hipMemcpyHostToDevice, s));
+    } else if (pieces > 1 && !st.compact) {
+        // pageable tail: offsets and lengths, then the message bytes in `pieces` ranges, each DMAed once packed
+        CV_TRY(sl.pin_in.ensure(st.total));
+        uint8_t *h = sl.pin_in.as<uint8_t>();
+        par_copy({{h + st.o_off, in.off + b, n * 8}, {h + st.o_len, in.len + b, n * 4}}, pool);
+        CV_TRY(hipMemcpyAsync(dv + st.o_off, h + st.o_off, st.o_ar - st.o_off, hipMemcpyHostToDevice, s));
+        const size_t span = st.hi - st.lo;
+        for (size_t p = 0; p < pieces; p++) {
+            const size_t a0 = span * p / pieces, a1 = span * (p + 1) / pieces;
+            if (a1 > a0) par_copy({{h + st.o_ar + a0, in.arena + st.lo + a0, a1 - a0}}, pool);
+            if (p + 1 == pieces) std::memset(h + st.o_ar + span, 0, 16);
+            const size_t len = a1 - a0 + (p + 1 == pieces ? 16 : 0);
+            if (len) CV_TRY(hipMemcpyAsync(dv + st.o_ar + a0, h + st.o_ar + a0, len, hipMemcpyHostToDevice, s));
+        }
     } else {
         CV_TRY(sl.pin_in.ensure(st.total));
         uint8_t *h = sl.pin_in.as<uint8_t>();
@@ -1789,7 +1825,8 @@ static int pipe_copy_back(Device &d, PipeOut &po) {
     // copies nor holds a compute stream the next call's kernels run on)
     for (int k = 0; k <= kPipeSlots; k++)
         if (po.slot_used[k]) CV_TRY(hipEventSynchronize(po.slot_done[k]));
-    const bool timeline = po.tl_n > 0 && po.tl.size() >= (size_t)po.tl_n * 3 + 2;
+    const bool timeline = po.tl_n > 0 && po.tl.size() >= (size_t)po.tl_n * 3 + 1;
+    const double t_copy = now_s();   // (timeline: the result copies' host-side time, from the join on)
     constexpr size_t kDirect = 1u << 20;
     size_t hb = 0;
     for (int k = 0; k < po.nseg; k++) {
@@ -1811,9 +1848,9 @@ static int pipe_copy_back(Device &d, PipeOut &po) {
     // ms per call of two later calls in flight (keyed host C2 8.5-8.7 -> 7.3 ms, DESIGN "Host runtime effects")
     if (!po.copied) CV_TRY(hipEventCreateWithFlags(&po.copied, hipEventDisableTiming));
     CV_TRY(hipEventRecord(po.copied, d.outs));
-    if (timeline) CV_TRY(hipEventRecord(po.tl[(size_t)po.tl_n * 3 + 1], d.outs));
     CV_TRY(hipEventSynchronize(po.copied));
     if (timeline) {
+        const double copy_ms = (now_s() - t_copy) * 1e3;
         auto at = [&](size_t k) {
             float ms = 0.f;
             (void)hipEventElapsedTime(&ms, po.tl[0], po.tl[k]);
@@ -1839,8 +1876,7 @@ static int pipe_copy_back(Device &d, PipeOut &po) {
             }
         }
         busy += cur1 - cur0;
-        const double out_end = at((size_t)J * 3 + 1);
-        const double v[8] = {ramp, dma_end, span, busy, span - ramp - busy, span - dma_end, out_end - span,
+        const double v[8] = {ramp, dma_end, span, busy, span - ramp - busy, span - dma_end, copy_ms,
                              (double)po.tl_first};
         for (int k = 0; k < 8; k++) po.tl_sum[k] = v[k];
         po.tl_ready = true;
@@ -1859,10 +1895,14 @@ static int pipe_copy_back(Device &d, PipeOut &po) {
 static int pipe_finish(Device &d, PipeOut &po) {
     if (!po.pending) return CV_OK;
     po.pending = false;
+    const bool ticketed = po.ticketed;
+    po.ticketed = false;
     const int rc = pipe_copy_back(d, po);
     if (rc != CV_OK) {
-        po.failed.emplace_back(po.gen, rc);
-        if (po.failed.size() > 64) po.failed.pop_front();
+        if (ticketed) {
+            po.failed.emplace_back(po.gen, rc);
+            if (po.failed.size() > kFailKeep) po.failed.pop_front();
+        }
     }
     return rc;
 }
@@ -1964,11 +2004,11 @@ struct PipeFrame {
         return CV_OK;
     }
     // after sub-chunk j's copies into block q: compute stream j % 2 waits for them
-    int copied(int q, int j) {
+    int copied(int q, int j, bool start_recorded = false) {
         if (tl) CV_TRY(tl_record(1 + 3 * (size_t)j, d.copy));
         CV_TRY(hipEventRecord(d.in_ready[q], d.copy));
         CV_TRY(hipStreamWaitEvent(ss[j % kPipeSlots], d.in_ready[q], 0));
-        if (tl) CV_TRY(tl_record(2 + 3 * (size_t)j, ss[j % kPipeSlots]));
+        if (tl && !start_recorded) CV_TRY(tl_record(2 + 3 * (size_t)j, ss[j % kPipeSlots]));
         return CV_OK;
     }
     // after sub-chunk j's kernels: block q is free once they are done
@@ -1984,7 +2024,6 @@ struct PipeFrame {
     // the next call's kernels on that stream until this call had finished)
     int complete() {
         po.tl_n = tl ? (int)chunks : 0;
-        if (tl && !po.tl_ev((size_t)chunks * 3 + 1)) return CV_E_HIP;   // (the result copies' end)
         for (int k = 0; k <= kPipeSlots; k++) {
             po.slot_used[k] = used[k];
             if (used[k]) CV_TRY(hipEventRecord(po.slot_done[k], k < kPipeSlots ? ss[k] : d.copy));
@@ -2073,7 +2112,8 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
     // (tools/sync_pipe_sweep.py, two rounds on one box): 262,144-record sub-chunks 13.0-13.3 ms, 98,304 12.0,
     // 65,536 11.6, 49,152 12.9, 32,768 13.3; an 8M C5 call is compute-bound and keeps 262,144 (74 ms).
     // (keyed calls keep pipe_chunk: each of their sub-chunks carries more fixed work)
-    const size_t sch = keyed ? o.pipe_chunk : std::min(o.pipe_chunk, std::max(2 * o.pipe_first, (n / 16 + 63) / 64 * 64));
+    const size_t sch = keyed ? o.pipe_chunk
+                             : std::min(o.pipe_chunk, std::max(2 * o.pipe_first, (n / o.pipe_split + 63) / 64 * 64));
     const std::vector<size_t> cut = async ? pipe_cuts(b, e, ach, ach, false) : pipe_cuts(b, e, o.pipe_first, sch, true);
     size_t max_m = 1;
     for (size_t j = 0; j + 1 < cut.size(); j++) max_m = std::max(max_m, cut[j + 1] - cut[j]);
@@ -2094,10 +2134,32 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
         uint8_t *dv;
         if ((rc = f.block(&q, st.total, &dv, (size_t)((double)st.total / (double)m * (double)max_m))) != CV_OK) return rc;
         if (f.tl && j == 0) CV_TRY(f.tl_record(0, d.copy));
+        // Synchronous calls: the first sub-chunk's keys and signatures (all the point decodes read: 96 of its ~400 B
+        // per C2 record) are DMAed first and its point blocks start on the slot's helper stream as soon as they
+        // land, beside the rest of the DMA and the scalars (CvkPrepOverlap, as the mid-size path): the ramp before
+        // the first kernel is the DMA of 3 MB instead of 13 MB.
+        CvkPrepOverlap pov;
+        const bool overlap0 = !async && !keyed && j == 0 && o.pipe_overlap_first && m <= kVerifyChunk;
+        if (overlap0) {
+            CV_TRY(slot_split(d, sl));
+            pov.aux = sl.split.s2;
+            pov.ready = sl.split.start;
+            pov.done = sl.split.done2;
+        }
         if (direct) {
             t0 = now_s();
             f.t[2] += t0 - t1;
-            CV_TRY(stage_dma_direct(st, dv, c0, in.pk, kidx, in.sig, in.arena, in.off, in.len, d.copy));
+            if (overlap0) {
+                CV_TRY(hipMemcpyAsync(dv + st.o_pk, in.pk + c0 * 32, m * 32, hipMemcpyHostToDevice, d.copy));
+                CV_TRY(hipMemcpyAsync(dv + st.o_sig, in.sig + c0 * 64, m * 64, hipMemcpyHostToDevice, d.copy));
+                CV_TRY(hipEventRecord(pov.ready, d.copy));
+                CV_TRY(hipMemcpyAsync(dv + st.o_off, in.off + c0, m * 8, hipMemcpyHostToDevice, d.copy));
+                CV_TRY(hipMemcpyAsync(dv + st.o_len, in.len + c0, m * 4, hipMemcpyHostToDevice, d.copy));
+                if (st.hi > st.lo)
+                    CV_TRY(hipMemcpyAsync(dv + st.o_ar, in.arena + st.lo, st.hi - st.lo, hipMemcpyHostToDevice, d.copy));
+            } else {
+                CV_TRY(stage_dma_direct(st, dv, c0, in.pk, kidx, in.sig, in.arena, in.off, in.len, d.copy));
+            }
             f.direct++;
         } else {
             uint8_t *h;
@@ -2105,14 +2167,25 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
             if ((rc = f.staging(&sk, st.total, &h)) != CV_OK) return rc;
             t0 = now_s();
             f.t[2] += t0 - t1;
-            stage_pack(st, h, c0, in.pk, kidx, in.sig, in.arena, in.off, in.len, pool, [] {});
+            hipError_t e1 = hipSuccess;
+            stage_pack(st, h, c0, in.pk, kidx, in.sig, in.arena, in.off, in.len, pool, [&] {
+                if (!overlap0) return;
+                e1 = hipMemcpyAsync(dv, h, st.o_off, hipMemcpyHostToDevice, d.copy);
+                if (e1 == hipSuccess) e1 = hipEventRecord(pov.ready, d.copy);
+            });
+            CV_TRY(e1);
             t1 = now_s();
             f.t[1] += t1 - t0;
             t0 = t1;
-            CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, d.copy));
+            const size_t from = overlap0 ? st.o_off : 0;
+            CV_TRY(hipMemcpyAsync(dv + from, h + from, st.total - from, hipMemcpyHostToDevice, d.copy));
             if ((rc = f.staged(sk)) != CV_OK) return rc;
         }
-        if ((rc = f.copied(q, (int)j)) != CV_OK) return rc;
+        if (f.tl && overlap0) {   // the timeline's first kernel start: the point blocks on the helper stream
+            CV_TRY(hipStreamWaitEvent(pov.aux, pov.ready, 0));
+            CV_TRY(f.tl_record(2, pov.aux));
+        }
+        if ((rc = f.copied(q, (int)j, f.tl && overlap0)) != CV_OK) return rc;
         const size_t w0 = (c0 - b) / 64;
         const uint64_t *doff = reinterpret_cast<const uint64_t *>(dv + st.o_off);
         const uint32_t *dlen = reinterpret_cast<const uint32_t *>(dv + st.o_len);
@@ -2131,7 +2204,7 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
             CV_TRY(e2);
         } else {
             CV_TRY(launch_verify(d, o.plan, sl, (uint32_t)m, dv + st.o_pk, dv + st.o_sig, dv + st.o_ar - st.lo, doff, dlen,
-                                 dbm, dst, s, nullptr, false));
+                                 dbm, dst, s, nullptr, false, overlap0 ? &pov : nullptr));
         }
         if ((rc = f.launched(q, (int)j)) != CV_OK) return rc;
         f.t[3] += now_s() - t0;
@@ -2616,6 +2689,7 @@ static int verify_shard(cv_ctx *ctx, Device &d, const Opts &o, size_t b, size_t 
     }
     if (async) {
         *part = {(uint64_t)dev_index(ctx, d), (uint64_t)k, po.gen};
+        po.ticketed = true;
         return CV_OK;
     }
     const double t0 = now_s();
@@ -2928,6 +3002,7 @@ static int merkle_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const
         if (r != CV_OK) return r;
         if (ticket) {
             parts[dev_index(ctx, d)] = {(uint64_t)dev_index(ctx, d), (uint64_t)k, po.gen};
+            po.ticketed = true;
             return CV_OK;
         }
         return pipe_finish(d, po);
@@ -3067,6 +3142,7 @@ static int txs_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const ui
         if (r != CV_OK) return r;
         if (ticket) {
             parts[dev_index(ctx, d)] = {(uint64_t)dev_index(ctx, d), (uint64_t)k, po.gen};
+            po.ticketed = true;
             return CV_OK;
         }
         const double ts = now_s();

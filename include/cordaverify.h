@@ -307,7 +307,14 @@ int cv_calibrate_cycles(cv_ctx *ctx, int device, double *out);
                                        in DMA (32768) */
 #define CV_OPT_TIMELINE 17          /* diagnostics: 1 = time each synchronous pipelined call on the GPU (HIP events per
                                        sub-chunk, read back as CV_STATS_TIMELINE); 0 off (default) */
-#define CV_OPT_COUNT 18
+#define CV_OPT_PIPE_SPLIT 18        /* synchronous pipelined calls: about n / this records per sub-chunk after the ramp,
+                                       clamped to [2 x CV_OPT_PIPE_FIRST, CV_OPT_PIPE_CHUNK] (16) */
+#define CV_OPT_PIPE_OVERLAP_FIRST 19 /* synchronous pipelined calls: the first sub-chunk's keys and signatures go first and
+                                       its point decodes start as soon as they land: 1 on (default), 0 off */
+#define CV_OPT_MID_PIECES 20        /* unpipelined mid-size batches from pageable inputs: packed and DMAed in up to this
+                                       many pieces (about 1 MB of keys + signatures each), the DMA of one piece beside
+                                       the packing of the next (4; 1 = one DMA per part) */
+#define CV_OPT_COUNT 21
 int cv_set_option(cv_ctx *ctx, int option, int64_t value);
 int cv_get_option(cv_ctx *ctx, int option, int64_t *value);
 
@@ -322,7 +329,7 @@ int cv_get_option(cv_ctx *ctx, int option, int64_t *value);
  *   CV_STATS_TIMELINE {sums over the synchronous pipelined calls timed with CV_OPT_TIMELINE = 1, in ms from each
  *                   call's first input DMA: first kernel start (the ramp), last input DMA end, last kernel end (the
  *                   span), kernel-busy time (union over the sub-chunks' launch groups), idle gaps between the first
- *                   kernel start and the span's end, the tail after the last DMA, the result copy; first sub-chunk
+ *                   kernel start and the span's end, the tail after the last DMA, the result copy (host-timed); first sub-chunk
  *                   records; sub-chunks; calls timed} */
 #define CV_STATS_PIPE 0
 #define CV_STATS_SMALL 1

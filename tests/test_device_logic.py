@@ -479,3 +479,55 @@ def test_tx_sig_refs_and_verdicts(host_harness):
         ref = np.array([int(counts[t] > 0 and bits[tsb[t]:tsb[t + 1]].all()) for t in range(nt)], np.uint8)
         assert np.array_equal(ok, ref) and 0 < ref.sum()
         assert np.array_equal(ok, native.tx_verdicts(words, tsb))
+
+
+def test_limb_bounds_on_max_limb_encodings(host_harness):
+    """fe_sub computes |k p_i - g_i| + f_i, which equals f + k p - g only while every limb
+    g_i <= k p_i, so that bound is exact, not slack.  The checking build (CV_BOUNDS_CHECK: every fe_sub /
+    fe_sub_carry_even asserts g_i <= k p_i and every multiply its column bound, aborting on a violation) runs
+    every verify form — half-size, fused prep in both field forms, full width, keyed comb — over encodings whose
+    limbs sit at their maxima: keys and R with y in [2^255 - 64, 2^255) (non-canonical y >= p included) and
+    y = 2^255 - 2^j, both sign bits; S at 2^256 - 1, 2^255 and around L; verdicts and key status equal the
+    oracle's."""
+    H = host_harness
+    rng = random.Random(20261018)
+    ys = [(1 << 255) - 1 - k for k in range(64)] + [(1 << 255) - (1 << j) for j in range(1, 255, 7)]
+    encs = []
+    for y in ys:
+        for sign in (0, 1):
+            e = (y | (sign << 255)).to_bytes(32, "little")
+            try:
+                E.decode_point_0_1_0(e)
+                encs.append(e)
+            except Exception:
+                pass
+    assert len(encs) >= 40
+    svals = [(1 << 256) - 1, 1 << 255, (1 << 255) + 12345, L, L - 1, L + 1, (1 << 253) + rng.getrandbits(200)]
+    cases = []
+    for _ in range(160):
+        pk, r = rng.choice(encs), rng.choice(encs)
+        s = rng.choice(svals)
+        cases.append((pk, r + s.to_bytes(32, "little"), rng.randbytes(rng.choice([0, 32, 300]))))
+    # the same max-limb R over a real key, and honest signatures rewritten to the non-canonical key encoding
+    seed = bytes(range(32))
+    pk_h = E.public_key_of(seed)
+    for r in encs[:24]:
+        cases.append((pk_h, r + ((1 << 256) - 1).to_bytes(32, "little"), b"corda"))
+    bad = []
+    sc = (ctypes.c_uint32 * 73)()
+    for pk, sig, m in cases:
+        st_ref, ok_ref = E.verify_ex(pk, m, sig)
+        want = (1 if (st_ref == 0 and ok_ref) else 0, 0 if st_ref == 0 else 1)
+        for form in ("hs", "fused0", "fused1", "full", "keyed"):
+            st = ctypes.c_int(0)
+            if form == "hs":
+                v = H.cvh_verify_hs(_b(pk), _b(sig), _b(m), len(m), ctypes.byref(st), sc)
+            elif form.startswith("fused"):
+                v = H.cvh_verify_hs_fused(_b(pk), _b(sig), _b(m), len(m), ctypes.byref(st), int(form[-1]))
+            elif form == "full":
+                v = H.cvh_verify(_b(pk), _b(sig), _b(m), len(m), ctypes.byref(st))
+            else:
+                v = H.cvh_verify_keyed(_b(pk), _b(sig), _b(m), len(m), ctypes.byref(st))
+            if (v, st.value) != want:
+                bad.append((form, pk.hex()[:16], sig.hex()[:16], (v, st.value), want))
+    assert not bad, bad[:8]

@@ -95,15 +95,18 @@ def test_host_pipeline_sync_subchunk_plan_exact(engine, n):
         assert int(bitmap[-1]) >> (n % 64) == 0
 
 
-@pytest.mark.parametrize("first,chunk", [(64, 64 * 17), (64 * 5, 64 * 3), (1024, 4096)])
-def test_host_pipeline_small_subchunks_golden(engine, corpus, first, chunk):
+@pytest.mark.parametrize("first,chunk,overlap", [(64, 64 * 17, 1), (64 * 5, 64 * 3, 1), (1024, 4096, 1),
+                                                 (1024, 4096, 0), (8192, 8192, 1)])
+def test_host_pipeline_small_subchunks_golden(engine, corpus, first, chunk, overlap):
     """The pipeline forced onto tiny sub-chunks (first / steady sizes, so one batch has hundreds of
     them, in every kernel form from tri-chain to throughput) over the golden corpus tiled to a ragged
-    9,001 records in random order: every verdict and status byte equals the pinned corpus values."""
+    9,001 records in random order: every verdict and status byte equals the pinned corpus values; with and
+    without the first sub-chunk's keys-first prep overlap (CV_OPT_PIPE_OVERLAP_FIRST)."""
     rng = np.random.default_rng(first + chunk)
     n = 9001
     sel = rng.integers(0, len(corpus["pk"]), n)
-    with _opts(engine, pipe_min=512, pipe_first=first, pipe_chunk=chunk, host_threads=3, auto_keyed=0):
+    with _opts(engine, pipe_min=512, pipe_first=first, pipe_chunk=chunk, host_threads=3, auto_keyed=0,
+               pipe_overlap_first=overlap):
         bitmap, status = engine.verify_batch(corpus["pk"][sel], corpus["sig"][sel], corpus["arena"],
                                              corpus["off"][sel], corpus["len"][sel])
     assert np.array_equal(_bits(bitmap, n), corpus["verdict"][sel].astype(bool))
@@ -443,7 +446,8 @@ def test_notary_midsize_forms_golden_and_oracle(engine, corpus, oracle_c, n, ove
     unpipelined host path, with the prep overlap (point decodes on the slot's helper stream once keys and
     signatures are resident, beside the rest of the DMA and the scalars: CV_OPT_PREP_OVERLAP_MIN) and without it,
     from pageable and pinned inputs: a golden tile (1/16 of the records drawn from the corpus's rejected classes)
-    gives the pinned verdicts and status bytes, and a corrupted random batch the C oracle's."""
+    gives the pinned verdicts and status bytes, and a corrupted random batch the C oracle's; pageable inputs both
+    packed and DMAed in pieces (CV_OPT_MID_PIECES, default) and in one DMA per part."""
     rng = np.random.default_rng(n + 101)
     rej = np.where(corpus["verdict"] == 0)[0]
     acc = np.where(corpus["verdict"] == 1)[0]
@@ -461,14 +465,16 @@ def test_notary_midsize_forms_golden_and_oracle(engine, corpus, oracle_c, n, ove
     pk[2::7, 3] ^= 0x40
     rand = (pk, sig, arena, off, ln)
     ref, rst = oracle_c.verify_batch(pk, sig, arena, off, ln, nthreads=8)
-    for om in (1 << 40, overlap_min):
-        with _opts(engine, prep_overlap_min=om, small_zero_copy=0):
+    for om, pieces in ((1 << 40, 4), (overlap_min, 4), (overlap_min, 1)):
+        with _opts(engine, prep_overlap_min=om, small_zero_copy=0, mid_pieces=pieces):
             for arrs, ev, es in ((gold, corpus["verdict"][sel], corpus["status"][sel]), (rand, ref, rst)):
                 for pinned in (False, True):
+                    if pinned and pieces == 1:
+                        continue                    # (pieces apply to pageable inputs only)
                     a = [engine.host_copy(x) for x in arrs] if pinned else arrs
                     bitmap, status = engine.verify_batch(*a)
-                    assert np.array_equal(_bits(bitmap, n), ev.astype(bool)), (om, pinned)
-                    assert np.array_equal(status, es), (om, pinned)
+                    assert np.array_equal(_bits(bitmap, n), ev.astype(bool)), (om, pinned, pieces)
+                    assert np.array_equal(status, es), (om, pinned, pieces)
                     if n % 64:
                         assert int(bitmap[-1]) >> (n % 64) == 0
 

@@ -139,6 +139,8 @@ def txsmall(eng, reps):
 def c3f(eng, reps):
     import bench  # noqa: E402
     pcie = bench.pcie_h2d_probe(torch.device("cuda", 0))
+    if os.environ.get("ASYNC_CHUNK"):                 # the async sub-chunk (CV_OPT_ASYNC_CHUNK) under test
+        eng.set_option("async_chunk", int(os.environ["ASYNC_CHUNK"]))
     for sync in (False, True) * int(os.environ.get("C3F_ROUNDS", "1")):
         eng.stats("pipe", reset=True)
         try:
@@ -147,7 +149,8 @@ def c3f(eng, reps):
             print(json.dumps({"what": "c3_fused", "sync": sync, "error": str(e)}), flush=True)
             continue
         r.pop("ratio_to_device_value", None)
-        print(json.dumps({"what": "c3_fused", "sync": sync, **r, "pipe_stats": eng.stats("pipe")}), flush=True)
+        print(json.dumps({"what": "c3_fused", "sync": sync, "async_chunk": eng.get_option("async_chunk"), **r,
+                          "pipe_stats": eng.stats("pipe")}), flush=True)
 
 
 def main():

@@ -47,12 +47,24 @@ def main():
             for k, x in sets:
                 eng.set_option(k, x)
             eng.verify_batch(*pinned, want_status=False)
+            eng.stats("pipe", reset=True)
             ts = []
             for _ in range(a.reps):
                 t = time.perf_counter()
                 bm, _ = eng.verify_batch(*pinned, want_status=False)
                 ts.append(time.perf_counter() - t)
             assert native.bitmap_to_bools(bm, a.n).all()
+            ps = eng.stats("pipe", reset=True)
+            calls = max(1.0, ps["calls"])
+            host = {k[:-2]: round(ps[k] / calls * 1e3, 3) for k in ("plan_s", "pack_s", "wait_s", "enqueue_s", "sync_s")}
+            host["subchunks"] = ps["subchunks"] / calls
+            eng.set_option("timeline", 1)
+            eng.stats("timeline", reset=True)
+            for _ in range(2):
+                eng.verify_batch(*pinned, want_status=False)
+            tl = eng.stats("timeline", reset=True)
+            eng.set_option("timeline", 0)
+            tl = {k: round(v / max(1.0, tl["calls"]), 3) for k, v in tl.items() if k != "calls"}
             torch.cuda.synchronize()
             t = time.perf_counter()
             for _ in range(3):
@@ -62,7 +74,8 @@ def main():
             dev_ms = (time.perf_counter() - t) / 3 * 1e3
             med = float(np.median(ts) * 1e3)
             print(json.dumps({"n": a.n, "msg": a.msg, "pageable": a.pageable, "round": rnd, "setting": name, "sync_pinned_ms": round(med, 3),
-                              "device_ms": round(dev_ms, 3), "ratio": round(dev_ms / med, 4)}), flush=True)
+                              "device_ms": round(dev_ms, 3), "ratio": round(dev_ms / med, 4), "host_ms": host,
+                              "timeline": tl}), flush=True)
     eng.close()
 
 
