@@ -26,7 +26,7 @@ Default workload (N=1): BASELINE config C2 — 1,000,000 single-signer Ed25519 s
 
 Extra fields on the JSON line:
   roofline      VALU-issue roofline of the dominant kernel (cv_hs_straus_kernel: 130,460 32x32->64
-                MACs per verify, DESIGN.md "Half-size scalars") against the measured v_mad_u64_u32
+                MACs per verify) against the measured v_mad_u64_u32
                 peak of this GPU, kernel time from HIP events on whole-chunk launches of the same
                 batch; "group" = the whole launch group against its own MAC count
   roofline.cycle_basis  the same peak priced per shader cycle (SIMDs x 64 / cycles per wave-level
@@ -71,9 +71,9 @@ from corda_amd import distributed as D, native, workload  # noqa: E402
 
 W_MAC_PER_VERIFY = 2.28e5       # algorithmic 32x32->64 MACs per verify (32-byte msg)
 # Straus phase alone (cv_straus_kernel, the dominant kernel): 63 windows x (16 S + 13 M) + 64 -A adds x 7 M
-# + 32 B madds x 7 M = 1008 S + 1491 M, at S = 55 and M = 100 limb products (DESIGN.md "Roofline")
+# + 32 B madds x 7 M = 1008 S + 1491 M, at S = 55 and M = 100 limb products (profiles/README.md, round 1)
 W_MAC_STRAUS = 1008 * 55 + 1491 * 100
-# Half-size schedule (DESIGN.md "Half-size scalars"), cv_hs_straus_kernel at the typical 33 windows:
+# Half-size schedule, cv_hs_straus_kernel at the typical 33 windows:
 # 32 x 4 doublings (16 S + 13 M) + 33 x (R add + A add: 15 M) + 8 x 2 B madds from the radix-2^16
 # rows (14 M per B window) = 512 S + 1023 M  (round 2 start: 16 B windows from radix-256 rows, 1135 M)
 HS_NW = 33
@@ -81,7 +81,7 @@ HS_BWIN = 8
 W_MAC_HS_STRAUS = (HS_NW - 1) * (16 * 55 + 13 * 100) + HS_NW * 15 * 100 + HS_BWIN * 14 * 100
 # whole half-size group: + 2 point decodes (254 S + 19 M each) + 2 odd-multiple tables (4 S + 59 M each)
 W_MAC_HS_GROUP = W_MAC_HS_STRAUS + 2 * (258 * 55 + 78 * 100)
-# keyed comb (cv_comb_kernel, DESIGN.md "Keyed"): 7 x 8 = 56 doublings (4 S + 3 M each, the last of a window
+# keyed comb (cv_comb_kernel): 7 x 8 = 56 doublings (4 S + 3 M each, the last of a window
 # 4 S + 4 M) + 32 key-row and 16 basepoint mixed additions (7 M each with their conversion) = 224 S + 535 M per verify
 W_MAC_COMB = 224 * 55 + 535 * 100
 MSG_BYTES = {"c2": 300, "c5": 32, "c3": 32}
@@ -98,21 +98,23 @@ def log(*a):
 
 # The PMC record of the dominant kernel on the current kernel code: scripts/pmc.sh + tools/pmc_summary.py, named
 # with the commit it was measured on (the round-3 file described an older build)
-PMC_HS_FILE = "profiles/pmc_hs_straus_fc6614b.json"
+PMC_HS_FILE = "profiles/pmc_hs_straus_r06.json"
 
 
 def pmc_traffic(n: int):
     """HBM bytes per launch of the dominant kernel from the committed PMC pass (PMC_HS_FILE), scaled to n.
-    Returns (bytes, provenance, VALU wave-instructions per verify): the figures are a committed measurement, not
-    one taken in this run (PMC counters need their own rocprofv3 pass)."""
+    Returns (bytes, provenance, VALU wave-instructions per verify, derived issue model): the figures are a committed
+    measurement, not one taken in this run (PMC counters need their own rocprofv3 pass)."""
     p = os.path.join(REPO, PMC_HS_FILE)
     if not os.path.exists(p):
-        return None, None, None
+        return None, None, None, {}
     with open(p) as f:
         d = json.load(f)
     src = (f"{PMC_HS_FILE}: FETCH_SIZE+WRITE_SIZE of one {d['n']}-signature launch "
            f"({d.get('build', 'build of that commit')}), scaled to n; not measured in this run")
-    return d["hbm_bytes_per_launch"] * n / d["n"], src, d.get("SQ_INSTS_VALU", 0) / d["n"]
+    der = dict(d.get("derived", {}))
+    der["lds_bank_conflict_cycles"] = d.get("SQ_LDS_BANK_CONFLICT")
+    return d["hbm_bytes_per_launch"] * n / d["n"], src, d.get("SQ_INSTS_VALU", 0) / d["n"], der
 
 
 def pcie_h2d_probe(dev, mb: int = 256, reps: int = 5) -> float:
@@ -361,12 +363,28 @@ def host_c3_fused_rate(eng, local, sh, ntx: int, steps: int, device_value: float
     ok = run(steps)
     dt = time.perf_counter() - t
     assert ok, f"fused C3 step rejected an honest transaction: {fails}"
+    # where a fused call's time goes: two synchronous calls timed on the GPU (CV_OPT_TIMELINE:
+    # per launch group, Merkle and verify groups apart), outside the timed loop
+    eng.set_option("timeline", 1)
+    eng.stats("timeline", reset=True)
+    ts = time.perf_counter()
+    for k in range(2):
+        okk, idk, _, _ = eng.verify_transactions(*args, ids=bufs[k % 3], want_status=False)
+        assert check(okk, idk), f"fused C3 (timed call) rejected an honest transaction: {fails}"
+    sync_ms = (time.perf_counter() - ts) / 2 * 1e3
+    tl = eng.stats("timeline", reset=True)
+    eng.set_option("timeline", 0)
+    tc = max(1.0, tl["calls"])
+    breakdown = {k: tl[k] / tc for k in ("ramp_ms", "merkle_dma_end_ms", "dma_end_ms", "merkle_busy_ms",
+                                         "verify_busy_ms", "busy_ms", "idle_ms", "span_ms", "tail_ms",
+                                         "result_copy_ms", "groups")}
+    breakdown["sync_call_ms"] = sync_ms
     in_bytes = leaf_bytes + ntx * 6 * 12 + 2 * (ntx + 1) * 4 + n * (32 + 64)
     v = n * steps / dt
     return {"value": v, "unit": "verifies/s", "tx_ids_per_s": ntx * steps / dt, "ms_per_step": dt / steps * 1e3,
             "steps": steps, "ratio_to_device_value": v / device_value, "device_value": device_value,
             "input_bytes_per_step": in_bytes, "pcie_floor_ms_per_step": in_bytes / (pcie_gbs * 1e9) * 1e3,
-            "host_blocked_ms_per_step": {k: v / steps for k, v in blocked.items()},
+            "host_blocked_ms_per_step": {k: v / steps for k, v in blocked.items()}, "breakdown": breakdown,
             "path": ("cv_verify_transactions (synchronous)" if sync else
                      "cv_verify_transactions_async, two in flight") +
                     ": leaves + keys + signatures from pinned host buffers, ids kept on the device as the messages, "
@@ -1131,6 +1149,18 @@ def main():
     assert written_all_ones([bitmap], n), "verify rejected an honest signature"
     ph = np.mean(np.array(phases), axis=0)
     kern_ms, straus_ms = float(ph.sum()), float(ph[2])
+    # the dominant kernel over whole rounds of resident waves (3 per SIMD x 4 SIMDs per CU x 64 lanes) of the same
+    # batch: its steady-state rate, without the 1M launch's partly filled last round (roofline.frac_whole_rounds)
+    per_round = torch.cuda.get_device_properties(dev).multi_processor_count * 4 * 3 * 64
+    n_whole = (n // per_round) * per_round
+    whole_rounds = {}
+    if n_whole and n_whole != n:
+        wph = [eng.verify_device_timed(local, n_whole, batch.pk.data_ptr(), batch.sig.data_ptr(), batch.arena.data_ptr(),
+                                       batch.off.data_ptr(), batch.len.data_ptr(), bitmap.data_ptr(), sh)
+               for _ in range(max(3, args.steps // 2))]
+        whole_rounds = {"n": n_whole, "rounds": n_whole // per_round, "hs_straus_ms": float(np.mean([w[2] for w in wph]))}
+        torch.cuda.synchronize(dev)
+        bitmap.copy_(prod_bitmap)
     multi = {}
     if world > 1:
         elapsed, kern_ms, straus_ms, other_elapsed = max_over_ranks([elapsed, kern_ms, straus_ms, other_elapsed], dev)
@@ -1150,15 +1180,18 @@ def main():
     if rank == 0:
         mad_rate, femul_rate = eng.calibrate(local)
         achieved = n * W_MAC_HS_STRAUS / (straus_ms * 1e-3)
+        if whole_rounds:
+            whole_rounds["frac"] = whole_rounds["n"] * W_MAC_HS_STRAUS / (whole_rounds["hs_straus_ms"] * 1e-3) / mad_rate
         group = n * W_MAC_HS_GROUP / (kern_ms * 1e-3)
-        traffic, traffic_src, valu_per_verify = pmc_traffic(n)
+        traffic, traffic_src, valu_per_verify, pmc = pmc_traffic(n)
         cyc = eng.calibrate_cycles(local)
         other_key = f"{'two' if other_streams == 2 else 'single'}_stream"
         # everything measured, in full: written to the detail file; the printed line is a digest of it
         D_ = {"roofline": {
             "bound": "valu", "achieved": achieved / 1e12, "peak": mad_rate / 1e12, "unit": "Tmac/s",
             "frac": achieved / mad_rate, "traffic": traffic, "traffic_source": traffic_src,
-            "pmc_valu_wave_instr_per_verify": valu_per_verify,
+            "pmc_valu_wave_instr_per_verify": valu_per_verify, "pmc_issue_model": pmc,
+            "whole_rounds": whole_rounds,
             "kernel": "cv_hs_straus_kernel", "kernel_ms": straus_ms,
             "work_per_unit": (f"{W_MAC_HS_STRAUS} 32x32->64 MAC per verify in the half-size Straus phase at {HS_NW} "
                               f"windows (512 S + 1023 M: 16 basepoint madds from the radix-2^16 rows)"),
@@ -1230,7 +1263,19 @@ def main():
                          "frac_vs_2p4ghz": r3(R["cycle_basis"]["frac_vs_2p4ghz"]),
                          "clock_ghz": r3(cyc["clock_ghz"]), "group_frac": r3(R["group"]["frac"]),
                          "phase_ms": {k: r3(v) for k, v in R["phase_ms"].items()},
-                         "work_per_unit": f"{W_MAC_HS_STRAUS} MAC/verify", "traffic_source": PMC_HS_FILE},
+                         "work_per_unit": f"{W_MAC_HS_STRAUS} MAC/verify", "traffic_source": PMC_HS_FILE,
+                         # north_star's counters (committed PMC pass, PMC_HS_FILE): resident waves per SIMD, VALU
+                         # instructions per MAC, SIMD cycles per VALU instruction, share of SIMD cycles issuing, LDS
+                         # bank-conflict cycles
+                         "occupancy": r3(pmc.get("occupancy_waves_per_simd")),
+                         "valu_instr_per_mac": r3(pmc.get("valu_per_mac")),
+                         "simd_cycles_per_valu_instr": r3(pmc.get("simd_cycles_per_valu")),
+                         "valu_busy": r3(pmc.get("issue_active")),
+                         "lds_bank_conflicts": pmc.get("lds_bank_conflict_cycles"),
+                         # the same kernel over the largest whole number of resident-wave rounds <= n (HIP events):
+                         # the 1M launch's partly filled last round is what separates frac from this
+                         "frac_whole_rounds": r3(whole_rounds.get("frac")),
+                         "whole_rounds_n": whole_rounds.get("n")},
         }
         if "cpu_baseline" in D_:
             c = D_["cpu_baseline"]
@@ -1250,6 +1295,9 @@ def main():
                     h[k]["pageable_ratio"] = r3(H[k]["pageable"]["ratio_to_device_value"])
             if "c2" in H:
                 h["c2"]["sync_breakdown"] = {k: r3(v) for k, v in H["c2"]["sync_pinned"]["breakdown"].items()}
+            if "c3_fused" in H:
+                h["c3_fused"]["breakdown"] = {k: r3(v) for k, v in H["c3_fused"]["breakdown"].items()}
+                h["c3_fused"]["pcie_floor_ms_per_step"] = r3(H["c3_fused"]["pcie_floor_ms_per_step"])
             if "keyed" in H:
                 h["keyed"]["pcie_bound_value"] = r3(H["keyed"]["pcie_bound_value"])
                 h["keyed"]["ratio_to_pcie_bound"] = r3(H["keyed"]["ratio_to_pcie_bound"])

@@ -30,7 +30,7 @@ SOURCES = ["cv_k_hs.hip", "cv_k_hss.hip", "cv_k_lat.hip", "cv_k_keyed.hip", "cv_
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
           "-Wno-unused-variable", "-Xarch_host", "-fvisibility=hidden"]
 # kernels: LLVM's max-ILP machine scheduler (A/B on one MI355X, 3 alternating rounds: C2 1M verify
-# 11.34 -> 11.15 ms median; the iterative-ILP strategy was 5 % slower) — DESIGN.md "Kernels"
+# 11.34 -> 11.15 ms median; the iterative-ILP strategy was 5 % slower) — profiles/README.md, round 2
 KERNEL_FLAGS = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
 # per-translation-unit extra flags (CV_HSS_FLAGS overrides the Straus kernel's, for A/Bs)
 SRC_FLAGS = {"cv_k_hss.hip": os.environ["CV_HSS_FLAGS"].split() if os.environ.get("CV_HSS_FLAGS") else []}

@@ -172,6 +172,7 @@ constexpr int kRing = 16;
 constexpr int kStage = 6;       // pinned host staging blocks (pageable inputs are packed into them)
 constexpr int kOuts = 4;        // pipelined host calls in flight per device (async verify + Merkle calls)
 constexpr size_t kFailKeep = 1024;   // failed asynchronous calls remembered per output (PipeOut::failed)
+constexpr int kTlVals = 12;          // CV_STATS_TIMELINE values per timed call (PipeOut::tl_sum)
 
 // The output of one pipelined host call on one device: its results on the device (dout), the pinned
 // copy they come back through, and what pipe_finish copies where.  pending: enqueued, results not yet in
@@ -205,7 +206,10 @@ struct PipeOut {
     int tl_n = 0;
     size_t tl_first = 0;
     bool tl_ready = false;
-    double tl_sum[8] = {};   // ramp, last DMA end, span, busy, idle, tail, result copy (ms); first sub-chunk
+    // ramp, last DMA end, span, busy, idle, tail, result copy (ms); first sub-chunk; Merkle-group busy, verify-group
+    // busy, last Merkle DMA end (ms); launch groups
+    double tl_sum[kTlVals] = {};
+    std::vector<uint8_t> tl_merkle;   // per launch group: 1 = a Merkle group (cv_verify_transactions), 0 = verify
     hipEvent_t tl_ev(size_t k) {
         while (tl.size() <= k) {
             hipEvent_t e = nullptr;
@@ -464,7 +468,7 @@ struct Stats {
     uint64_t small_calls = 0;
     uint64_t calls = 0, routed_whole = 0, split_calls = 0, shards = 0, keyed_calls = 0, keyed_chunks = 0,
              merkle_calls = 0, merkle_chunks = 0;
-    double tl[9] = {};     // CV_STATS_TIMELINE sums (PipeOut::tl_sum) + calls
+    double tl[kTlVals + 1] = {};   // CV_STATS_TIMELINE sums (PipeOut::tl_sum) + calls
 };
 
 static inline double now_s() {
@@ -719,7 +723,7 @@ int cv_diag_stats(cv_ctx *ctx, int which, double *out, size_t nout, int reset) {
     if (!ctx || (nout && !out)) return CV_E_ARGS;
     std::lock_guard<std::mutex> g(ctx->st_mu);
     Stats &s = ctx->stats;
-    double v[9] = {};
+    double v[kTlVals + 1] = {};
     size_t nv = 0;
     if (which == CV_STATS_PIPE) {
         for (int k = 0; k < 5; k++) v[k] = s.pipe[k];
@@ -737,8 +741,8 @@ int cv_diag_stats(cv_ctx *ctx, int which, double *out, size_t nout, int reset) {
         for (int k = 0; k < 8; k++) v[k] = (double)r[k];
         nv = 8;
     } else if (which == CV_STATS_TIMELINE) {
-        for (int k = 0; k < 9; k++) v[k] = s.tl[k];
-        nv = 9;
+        for (int k = 0; k <= kTlVals; k++) v[k] = s.tl[k];
+        nv = kTlVals + 1;
     } else {
         return CV_E_ARGS;
     }
@@ -751,7 +755,7 @@ int cv_diag_stats(cv_ctx *ctx, int which, double *out, size_t nout, int reset) {
             std::fill(s.small, s.small + 5, 0.0);
             s.small_calls = 0;
         } else if (which == CV_STATS_TIMELINE) {
-            std::fill(s.tl, s.tl + 9, 0.0);
+            std::fill(s.tl, s.tl + kTlVals + 1, 0.0);
         } else {
             s.calls = s.routed_whole = s.split_calls = s.shards = s.keyed_calls = s.keyed_chunks = s.merkle_calls =
                 s.merkle_chunks = 0;
@@ -901,7 +905,7 @@ static Device *find_dev(cv_ctx *ctx, int device) {
 
 // ---------------------------------------------------------------- routing (dispatch)
 // Runs fn(device, b, e, packing threads) over shards of [0, n) and returns the first error.  The shard
-// plan (DESIGN.md "Routing"):
+// plan ("Routing and threading"):
 //   - one device, or n <= shard_min: the whole batch on ONE device — the least loaded (shards in progress
 //     or queued on it), ties broken by a rotating start, so concurrent notary batches land on different
 //     GPUs instead of each being cut eight ways (a shard below the tri-chain size costs the kernel
@@ -1857,28 +1861,39 @@ static int pipe_copy_back(Device &d, PipeOut &po) {
             return (double)ms;
         };
         const int J = po.tl_n;
-        std::vector<std::pair<double, double>> iv(J);
-        double ramp = 1e30, span = 0, dma_end = at(1 + 3 * (size_t)(J - 1));
-        for (int j = 0; j < J; j++) {
-            iv[j] = {at(2 + 3 * (size_t)j), at(3 + 3 * (size_t)j)};
-            ramp = std::min(ramp, iv[j].first);
-            span = std::max(span, iv[j].second);
-        }
-        std::sort(iv.begin(), iv.end());
-        double busy = 0, cur0 = iv[0].first, cur1 = iv[0].second;
-        for (int j = 1; j < J; j++) {
-            if (iv[j].first > cur1) {
-                busy += cur1 - cur0;
-                cur0 = iv[j].first;
-                cur1 = iv[j].second;
-            } else {
-                cur1 = std::max(cur1, iv[j].second);
+        // the union length of a set of [start, end) intervals
+        auto union_len = [](std::vector<std::pair<double, double>> iv) {
+            if (iv.empty()) return 0.0;
+            std::sort(iv.begin(), iv.end());
+            double busy = 0, cur0 = iv[0].first, cur1 = iv[0].second;
+            for (size_t j = 1; j < iv.size(); j++) {
+                if (iv[j].first > cur1) {
+                    busy += cur1 - cur0;
+                    cur0 = iv[j].first;
+                    cur1 = iv[j].second;
+                } else {
+                    cur1 = std::max(cur1, iv[j].second);
+                }
             }
+            return busy + cur1 - cur0;
+        };
+        std::vector<std::pair<double, double>> all, mk, vf;
+        double ramp = 1e30, span = 0, dma_end = 0, mdma_end = 0;
+        for (int j = 0; j < J; j++) {
+            const std::pair<double, double> w{at(2 + 3 * (size_t)j), at(3 + 3 * (size_t)j)};
+            const double de = at(1 + 3 * (size_t)j);
+            const bool merkle = (size_t)j < po.tl_merkle.size() && po.tl_merkle[j];
+            all.push_back(w);
+            (merkle ? mk : vf).push_back(w);
+            ramp = std::min(ramp, w.first);
+            span = std::max(span, w.second);
+            dma_end = std::max(dma_end, de);
+            if (merkle) mdma_end = std::max(mdma_end, de);
         }
-        busy += cur1 - cur0;
-        const double v[8] = {ramp, dma_end, span, busy, span - ramp - busy, span - dma_end, copy_ms,
-                             (double)po.tl_first};
-        for (int k = 0; k < 8; k++) po.tl_sum[k] = v[k];
+        const double busy = union_len(all);
+        const double v[kTlVals] = {ramp, dma_end, span, busy, span - ramp - busy, span - dma_end, copy_ms,
+                                   (double)po.tl_first, union_len(mk), union_len(vf), mdma_end, (double)J};
+        for (int k = 0; k < kTlVals; k++) po.tl_sum[k] = v[k];
         po.tl_ready = true;
         po.tl_n = 0;
     }
@@ -2119,6 +2134,7 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
     for (size_t j = 0; j + 1 < cut.size(); j++) max_m = std::max(max_m, cut[j + 1] - cut[j]);
     f.tl = o.timeline && !async;
     po.tl_ready = false;
+    po.tl_merkle.clear();
     po.tl_first = cut.size() > 1 ? cut[1] - cut[0] : 0;
     for (size_t j = 0; j + 1 < cut.size(); j++) {
         const size_t c0 = cut[j], c1 = cut[j + 1], m = c1 - c0;
@@ -2412,7 +2428,7 @@ static int merkle_shard_small(Device &d, const MStage &st, const MerkleIn &in, W
 // and whether every one of its signatures verifies over that id.  The ids are computed into the output's device
 // buffer and read there as the signatures' messages: no id round trip through the host and no message upload,
 // so a verify never waits for the host to hand it the ids of a Merkle call (the separate calls left the verify
-// kernels idle ~6 ms per C3 step, DESIGN.md "Next" item 5).
+// kernels idle ~6 ms per C3 step, profiles/README.md, round 4).
 //
 // One shard = transactions [t0, t1) and their signatures [s0, s1) on device d.  Sub-chunks of whole transactions
 // (about merkle_chunk leaves, ramped: a quarter, a half, then full) and of signatures (multiples of 64 from s0,
@@ -2451,6 +2467,11 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
     uint64_t *dbm = reinterpret_cast<uint64_t *>(dout + o_bm);
     auto drain = on_exit([&f] { f.drain(); });
     WorkerPool *pool = &d.workers(threads);
+    f.tl = o.timeline && !async;   // (timeline: groups tagged Merkle / verify in po.tl_merkle)
+    po.tl_ready = false;
+    po.tl_merkle.clear();
+    po.tl_first = 0;
+    if (f.tl) CV_TRY(f.tl_record(0, d.copy));
     // the shard's signature boundaries go first on the copy stream, so every group's copy event covers them
     {
         const double ta = now_s();
@@ -2543,6 +2564,7 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
             CV_TRY(cvk_tx_sig_refs((uint32_t)m, (uint32_t)c0, (uint32_t)nt, (uint32_t)s0, dtsb, doff, dlen, s));
             CV_TRY(launch_verify(d, o.plan, sl, (uint32_t)m, dv, dv + o_sig, dout, doff + c0, dlen + c0, dbm + c0 / 64,
                                  in.sig_status ? dout + o_sst + c0 : nullptr, s, nullptr, false));
+            if (f.tl) po.tl_merkle.push_back(0);
             if ((r = f.launched(q, g++)) != CV_OK) return r;
             f.t[3] += now_s() - tb;
             p += m;
@@ -2596,6 +2618,7 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
             CV_TRY(e2);
             CV_TRY(hipEventRecord(d.mev[J], s));
         }
+        if (f.tl) po.tl_merkle.push_back(1);
         if ((rc = f.launched(q, g++)) != CV_OK) return rc;
         f.t[3] += now_s() - ta;
         if (J > 0 && (rc = emit_sigs(J - 1, false)) != CV_OK) return rc;
@@ -2625,6 +2648,14 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
         ctx->stats.merkle_chunks += nm;
     }
     return CV_OK;
+}
+
+// A finished synchronous call's GPU timeline (CV_OPT_TIMELINE) into the context's sums.  The caller holds st_mu.
+static void timeline_account(cv_ctx *ctx, PipeOut &po) {
+    if (!po.tl_ready) return;
+    for (int k = 0; k < kTlVals; k++) ctx->stats.tl[k] += po.tl_sum[k];
+    ctx->stats.tl[kTlVals] += 1;
+    po.tl_ready = false;
 }
 
 // A pipelined call's part on one device, for its ticket: (device index, output index, gen).
@@ -2696,11 +2727,7 @@ static int verify_shard(cv_ctx *ctx, Device &d, const Opts &o, size_t b, size_t 
     rc = pipe_finish(d, po);
     std::lock_guard<std::mutex> g(ctx->st_mu);
     ctx->stats.pipe[4] += now_s() - t0;
-    if (po.tl_ready) {
-        for (int k = 0; k < 8; k++) ctx->stats.tl[k] += po.tl_sum[k];
-        ctx->stats.tl[8] += 1;
-        po.tl_ready = false;
-    }
+    timeline_account(ctx, po);
     return rc;
 }
 
@@ -3149,6 +3176,7 @@ static int txs_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const ui
         r = pipe_finish(d, po);
         std::lock_guard<std::mutex> g(ctx->st_mu);
         ctx->stats.pipe[4] += now_s() - ts;
+        timeline_account(ctx, po);
         return r;
     });
     std::vector<Part> live;

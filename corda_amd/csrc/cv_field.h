@@ -7,7 +7,7 @@
 // one floor-carry chain (logical shifts + masks: no rounding constants, no signed fix-ups).
 // This is VALU integer work by design (no MFMA): see DESIGN.md.
 //
-// Bounds (in units of M_i per limb; checked on the host by CV_BOUNDS_CHECK, derivation in DESIGN.md):
+// Bounds (in units of M_i per limb; checked on the host by CV_BOUNDS_CHECK):
 //   T  "tight"  : output of fe_mul / fe_sq / fe_sq2 / fe_carry            <= 1.01
 //   fe_mul(h, f, g): g <= 3.3 (19*g_j must fit 32 bits), f <= 8 (column sums stay < 2^64)
 //   fe_sq(h, f) / fe_sq2: f <= 3.3 (38*f_odd, 19*f_even fit 32 bits; doubled columns < 2^64)
@@ -204,7 +204,7 @@ CV_HD void fe_wrap_carry(fe &out, uint64_t c, uint32_t r[10]) {
 
 // h[m] = f[m] * g[m] for m < N, interleaved (g[m] is the operand multiplied by 19: g <= 3.3, f <= 8).
 // Column k holds f_i g_j for i + j = k (mod 10): x2 when i and j are both odd (half-bit offsets),
-// x19 when i + j >= 10 (2^255 = 19).  Column sums stay < 2^63.7 (DESIGN.md "Field arithmetic").
+// x19 when i + j >= 10 (2^255 = 19).  Column sums stay < 2^63.7.
 template <int N> CV_HD void fe_mul_n(fe (&h)[N], const fe (&f)[N], const fe (&g)[N]) {
     uint32_t fd[N][10], g19[N][10];
 #pragma unroll

@@ -1,6 +1,6 @@
 // cv_kernels.hip — the launchers of the gfx950 kernels (internal C ABI used by cv_api.cpp, cv_launch.h).
 //
-//   verify (half-size scalars, DESIGN.md "Kernels"): eddsa-0.1.0-exact Ed25519 verify behind
+//   verify (half-size scalars): eddsa-0.1.0-exact Ed25519 verify behind
 //       PublicKey.verifyWithECDSA (reference core/src/main/kotlin/net/corda/core/crypto/CryptoUtilities.kt:90-96),
 //       in three forms by batch size (CvkPlan): throughput (scalars -> points -> hs_straus, one signature per
 //       lane), quad (4 lanes per signature) and tri-chain (16 lanes per signature) for notary-sized batches

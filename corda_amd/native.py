@@ -47,7 +47,8 @@ STATS = {"pipe": (0, ("plan_s", "pack_s", "wait_s", "enqueue_s", "sync_s", "call
          "route": (2, ("calls", "routed_whole", "split_calls", "shards", "keyed_shards", "keyed_subchunks",
                        "merkle_calls", "merkle_subchunks")),
          "timeline": (3, ("ramp_ms", "dma_end_ms", "span_ms", "busy_ms", "idle_ms", "tail_ms", "result_copy_ms",
-                          "first_subchunk", "calls"))}
+                          "first_subchunk", "merkle_busy_ms", "verify_busy_ms", "merkle_dma_end_ms", "groups",
+                          "calls"))}
 
 
 class NativeUnavailable(RuntimeError):

@@ -226,7 +226,7 @@ int cv_verify_transactions_async(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_ar
  * enqueued on `stream` (a hipStream_t, NULL = the context's stream for that device) and the call
  * returns without synchronising.  These are the entry points bench.py times (inputs resident in HBM).
  * A large batch may internally run part of its work on a per-device helper stream of the engine (the
- * drain overlap, DESIGN.md "Schedules"); `stream` waits on that work before anything the caller
+ * drain overlap); `stream` waits on that work before anything the caller
  * enqueues after the call, so completion is still stream-ordered on `stream`.
  * Calls may use different streams, from any thread: the engine orders every use of a device's shared
  * verify workspace and key pool (a call on a new stream first waits for the previous call's work on
@@ -326,11 +326,12 @@ int cv_get_option(cv_ctx *ctx, int option, int64_t *value);
  *                   (notary-sized batches: zero-copy and one-DMA forms); calls}
  *   CV_STATS_ROUTE {calls, routed whole to one device, cut over several, shards, keyed shards, keyed
  *                   sub-chunks, Merkle calls, Merkle sub-chunks}
- *   CV_STATS_TIMELINE {sums over the synchronous pipelined calls timed with CV_OPT_TIMELINE = 1, in ms from each
- *                   call's first input DMA: first kernel start (the ramp), last input DMA end, last kernel end (the
- *                   span), kernel-busy time (union over the sub-chunks' launch groups), idle gaps between the first
- *                   kernel start and the span's end, the tail after the last DMA, the result copy (host-timed); first sub-chunk
- *                   records; sub-chunks; calls timed} */
+ *   CV_STATS_TIMELINE {sums over the synchronous pipelined calls (cv_ed25519_verify_batch, cv_verify_transactions)
+ *                   timed with CV_OPT_TIMELINE = 1, in ms from each call's first input DMA: first kernel start (the
+ *                   ramp), last input DMA end, last kernel end (the span), kernel-busy time (union over the launch
+ *                   groups), idle gaps between the first kernel start and the span's end, the tail after the last DMA,
+ *                   the result copy (host-timed); first sub-chunk records; Merkle-group busy, verify-group busy, last
+ *                   Merkle DMA end (ms; cv_verify_transactions); launch groups; calls timed} */
 #define CV_STATS_PIPE 0
 #define CV_STATS_SMALL 1
 #define CV_STATS_ROUTE 2

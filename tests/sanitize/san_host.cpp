@@ -358,6 +358,7 @@ static void test_failed_finish_reaches_waiter() {
     Device &d = *ctx.devs[0];
     d.ordinal = 4095;
     d.out[0].pending = true;
+    d.out[0].ticketed = true;                              // (as the async entry points mark a ticketed call)
     d.out[0].gen = 1;
     const uint64_t t1 = ticket_add(&ctx, {Part{0, 0, 1}});
     d.out_next = 0;
@@ -367,6 +368,7 @@ static void test_failed_finish_reaches_waiter() {
         PipeOut &po = pipe_out(d, &k, lk);                 // a later call takes output 0: finishes call 1
         CHECK(k == 0 && !po.pending);
         po.pending = true;
+        po.ticketed = true;
         po.gen = 2;
     }
     const uint64_t t2 = ticket_add(&ctx, {Part{0, 0, 2}});
@@ -381,6 +383,7 @@ static void test_failed_finish_reaches_waiter() {
         std::unique_lock<std::mutex> lk;
         PipeOut &po = pipe_out(d, &k, lk);
         po.pending = true;
+        po.ticketed = true;
         po.gen = g;
         lk.unlock();
         tk.push_back(ticket_add(&ctx, {Part{0, (uint64_t)k, g}}));
@@ -388,6 +391,32 @@ static void test_failed_finish_reaches_waiter() {
     CHECK(ctx.tickets.size() < 64 && !ctx.tickets_done.empty());
     for (uint64_t t : tk) CHECK(cv_wait(&ctx, t) == CV_E_HIP);
     CHECK(ctx.tickets.empty() && ctx.tickets_done.empty());
+    // a ticketed call's failure is not evicted by later failing SYNCHRONOUS calls on the same output
+    // (they return their error themselves and record nothing): 200 of them, then the ticket still reports its own
+    {
+        int k = -1;
+        std::unique_lock<std::mutex> lk;
+        PipeOut &po = pipe_out(d, &k, lk);
+        po.pending = true;
+        po.ticketed = true;
+        po.gen = 500;
+        lk.unlock();
+        const uint64_t ta = ticket_add(&ctx, {Part{0, (uint64_t)k, 500}});
+        size_t before = 0;
+        for (PipeOut &o : d.out) before += o.failed.size();
+        for (uint64_t g = 501; g < 701; g++) {
+            std::unique_lock<std::mutex> lk2;
+            int k2 = -1;
+            PipeOut &p2 = pipe_out(d, &k2, lk2);              // finishes (and fails) the call before on this output
+            p2.pending = true;                              // an unticketed (synchronous) call
+            p2.gen = g;
+            CHECK(pipe_finish(d, p2) == CV_E_HIP);
+        }
+        size_t recorded = 0;
+        for (PipeOut &o : d.out) recorded += o.failed.size();
+        CHECK(recorded == before + 1);                      // call 500's; the synchronous failures were not recorded
+        CHECK(cv_wait(&ctx, ta) == CV_E_HIP);
+    }
     ctx.devs.clear();
 }
 

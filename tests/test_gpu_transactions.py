@@ -150,7 +150,8 @@ def test_verify_transactions_c3_shaped(engine):
     """C3-shaped transactions (6 leaves, 8 signers each, workload.make_tx_batch), 200,000 of them (1.6M signatures,
     the default sub-chunk plans: signature groups that start inside the previous Merkle sub-chunk): one in 16
     with a mutated leaf, one in 32 with a bad signature; tx_ok equals the expectation and the ids the claimed
-    ids wherever the leaves are intact — synchronous, and three async calls in flight."""
+    ids wherever the leaves are intact — synchronous (the last call also timed on the GPU), and three async calls in
+    flight."""
     ntx, signers = 200_000, 8
     tb = workload.make_tx_batch(engine, 0, ntx, signers, seed=4402)
     arena = tb.leaf_arena.cpu().numpy().copy()
@@ -171,9 +172,20 @@ def test_verify_transactions_c3_shaped(engine):
     args = (arena, leaf_off, leaf_len, tx_begin, pk, sig, sig_begin)
     intact = np.isin(np.arange(ntx), bad_leaf, invert=True)
     for rep in range(3):
-        ok, ids, st, _ = engine.verify_transactions(*args)
+        if rep == 2:                                        # the last one timed on the GPU (CV_OPT_TIMELINE)
+            engine.set_option("timeline", 1)
+            engine.stats("timeline", reset=True)
+        try:
+            ok, ids, st, _ = engine.verify_transactions(*args)
+        finally:
+            engine.set_option("timeline", 0)
         assert np.array_equal(ok.astype(bool), expect), (rep, np.nonzero(ok.astype(bool) != expect)[0][:10])
         assert np.array_equal((ids == claimed).all(axis=1), intact) and (st == 0).all()
+    t = engine.stats("timeline", reset=True)             # Merkle and verify groups timed apart, consistently
+    assert t["calls"] == 1 and t["groups"] >= 2 and t["merkle_busy_ms"] > 0 and t["verify_busy_ms"] > 0
+    assert t["merkle_dma_end_ms"] <= t["dma_end_ms"] <= t["span_ms"] and t["ramp_ms"] <= t["span_ms"]
+    assert max(t["merkle_busy_ms"], t["verify_busy_ms"]) <= t["busy_ms"] + 1e-3
+    assert abs(t["busy_ms"] + t["idle_ms"] - (t["span_ms"] - t["ramp_ms"])) < 1e-3
     pinned = [engine.host_copy(x) for x in args]
     tickets = [engine.verify_transactions_async(*(pinned if k % 2 else args)) for k in range(3)]
     for t in tickets:

@@ -18,7 +18,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRCS = sorted(glob.glob(os.path.join(REPO, "corda_amd", "csrc", "cv_k_*.hip")))
 
-# measured clk per wave64 instruction on MI355X (DESIGN.md "Instruction rates"), default 2.4
+# measured clk per wave64 instruction on MI355X (profiles/README.md, round 2; round 6: profiles/r06a_issue_cost.txt), default 2.4
 COST = {"v_mad_u64_u32": 5.0, "v_mad_i64_i32": 5.7, "v_lshrrev_b64": 4.2, "v_lshlrev_b64": 4.2,
         "v_lshl_add_u64": 4.2, "v_ashrrev_i64": 4.2, "v_mul_lo_u32": 4.15, "v_mul_hi_u32": 4.15,
         "v_alignbit_b32": 4.15, "v_lshl_add_u32": 4.15, "v_add3_u32": 4.15, "v_mad_u32_u24": 4.15,

@@ -1,6 +1,6 @@
 // instr_mix.hip — issue cost of the field layer's instruction classes on gfx950, alone and mixed
 // with v_mad_u64_u32 (the MAC).  Answers: does a 32-bit ALU op / 64-bit shift cost the SIMD the same
-// issue time as a MAC, and does it hide behind one?  (DESIGN.md "Field arithmetic", round 2.)
+// issue time as a MAC, and does it hide behind one?  (profiles/README.md, round 2; superseded by issue_cost.hip.)
 //   hipcc --offload-arch=gfx950 -O3 instr_mix.hip -o instr_mix && ./instr_mix
 // Each kernel: 8 independent chains x 16 unrolled slots per iteration; WAVES waves per SIMD.
 // Reported: cycles per SLOT per SIMD (a slot = one MAC plus the ops the variant adds), with the clock

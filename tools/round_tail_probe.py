@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """hs_straus launched whole over n signatures for n at whole rounds of resident waves (3 waves per SIMD x 1,024
 SIMDs x 64 = 196,608 signatures per round) and just past them: separates the kernel's steady-state rate from the
-cost of a launch's partly filled last round (DESIGN.md "Roofline").  HIP-event phases of verify_device_timed.
+cost of a launch's partly filled last round.  HIP-event phases of verify_device_timed.
 
     python tools/round_tail_probe.py [--sizes 983040,1000000,1179648] [--reps 5]
 """
