@@ -201,8 +201,8 @@ def host_api_rate(eng, batch, steps: int, device_value: float, name: str, async_
     tl = eng.stats("timeline", reset=True)
     eng.set_option("timeline", 0)
     tc = max(1.0, tl["calls"])
-    breakdown.update({k: tl[k] / tc for k in ("ramp_ms", "dma_end_ms", "span_ms", "busy_ms", "idle_ms", "tail_ms",
-                                              "result_copy_ms", "first_subchunk")})
+    breakdown.update({k: tl[k] / tc for k in ("host_pre_ms", "ramp_ms", "dma_end_ms", "span_ms", "busy_ms", "idle_ms",
+                                              "tail_ms", "result_copy_ms", "host_post_ms", "first_subchunk")})
     breakdown["timeline_calls"] = tl["calls"]
     dt_async = timed_async(pinned)
     dt_async_page = timed_async((pk, sig, arena, off, ln))
@@ -377,7 +377,7 @@ def host_c3_fused_rate(eng, local, sh, ntx: int, steps: int, device_value: float
     tc = max(1.0, tl["calls"])
     breakdown = {k: tl[k] / tc for k in ("ramp_ms", "merkle_dma_end_ms", "dma_end_ms", "merkle_busy_ms",
                                          "verify_busy_ms", "busy_ms", "idle_ms", "span_ms", "tail_ms",
-                                         "result_copy_ms", "groups")}
+                                         "result_copy_ms", "host_post_ms", "groups")}
     breakdown["sync_call_ms"] = sync_ms
     in_bytes = leaf_bytes + ntx * 6 * 12 + 2 * (ntx + 1) * 4 + n * (32 + 64)
     v = n * steps / dt

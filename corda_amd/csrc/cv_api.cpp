@@ -163,7 +163,7 @@ struct Slot {
     DevBuf head;                  // its device copy
 };
 constexpr int kSlots = 4;
-constexpr int kPipeSlots = 2;   // compute slots the pipeline deals its sub-chunks over (see pipe_enqueue)
+constexpr int kPipeSlots = 3;   // most compute slots a pipelined call deals its sub-chunks over (PipeFrame::ns)
 // input blocks of the host pipeline on the device: copies run up to kRing sub-chunks ahead of the kernels, so
 // a call's copies are all queued early and a Merkle call submitted behind a verify call copies its leaves
 // while that verify's kernels run (round 4: with 6 blocks the verify's copies were paced by its kernels and
@@ -172,7 +172,7 @@ constexpr int kRing = 16;
 constexpr int kStage = 6;       // pinned host staging blocks (pageable inputs are packed into them)
 constexpr int kOuts = 4;        // pipelined host calls in flight per device (async verify + Merkle calls)
 constexpr size_t kFailKeep = 1024;   // failed asynchronous calls remembered per output (PipeOut::failed)
-constexpr int kTlVals = 12;          // CV_STATS_TIMELINE values per timed call (PipeOut::tl_sum)
+constexpr int kTlVals = 14;          // CV_STATS_TIMELINE values per timed call (PipeOut::tl_sum)
 
 // The output of one pipelined host call on one device: its results on the device (dout), the pinned
 // copy they come back through, and what pipe_finish copies where.  pending: enqueued, results not yet in
@@ -207,8 +207,10 @@ struct PipeOut {
     size_t tl_first = 0;
     bool tl_ready = false;
     // ramp, last DMA end, span, busy, idle, tail, result copy (ms); first sub-chunk; Merkle-group busy, verify-group
-    // busy, last Merkle DMA end (ms); launch groups
+    // busy, last Merkle DMA end (ms); launch groups; host: call entry -> first input DMA enqueued, GPU work joined ->
+    // results in the caller's arrays (ms)
     double tl_sum[kTlVals] = {};
+    double tl_pre_ms = 0, tl_join_s = 0;
     std::vector<uint8_t> tl_merkle;   // per launch group: 1 = a Merkle group (cv_verify_transactions), 0 = verify
     hipEvent_t tl_ev(size_t k) {
         while (tl.size() <= k) {
@@ -446,8 +448,9 @@ static const OptDesc kOpt[CV_OPT_COUNT] = {
     {32768, 1, (int64_t)1 << 40},       // CV_OPT_PREP_OVERLAP_MIN
     {0, 0, 1},                          // CV_OPT_TIMELINE
     {16, 1, 1024},                      // CV_OPT_PIPE_SPLIT
-    {1, 0, 1},                          // CV_OPT_PIPE_OVERLAP_FIRST
-    {4, 1, 16},                         // CV_OPT_MID_PIECES
+    {0, 0, 1},                          // CV_OPT_PIPE_OVERLAP_FIRST
+    {1, 1, 16},                         // CV_OPT_MID_PIECES
+    {2, 2, 3},                          // CV_OPT_PIPE_SLOTS
 };
 
 // A snapshot of a context's options, taken once per call.
@@ -455,7 +458,7 @@ struct Opts {
     CvkPlan plan;
     size_t pipe_min, pipe_first, pipe_chunk, async_chunk, small_direct_min, shard_min, spread_min, merkle_chunk;
     size_t prep_overlap_min;
-    size_t pipe_split, mid_pieces;
+    size_t pipe_split, mid_pieces, pipe_slots;
     int threads, small_zc, auto_keyed, timeline, pipe_overlap_first;
 };
 
@@ -654,6 +657,7 @@ struct cv_ctx {
         o.pipe_split = (size_t)opt[CV_OPT_PIPE_SPLIT].load();
         o.pipe_overlap_first = (int)opt[CV_OPT_PIPE_OVERLAP_FIRST].load();
         o.mid_pieces = (size_t)opt[CV_OPT_MID_PIECES].load();
+        o.pipe_slots = (size_t)opt[CV_OPT_PIPE_SLOTS].load();
         return o;
     }
 };
@@ -854,6 +858,9 @@ void cv_close(cv_ctx *ctx) {
             for (hipEvent_t v : o.slot_done)
                 if (v) (void)hipEventDestroy(v);
             if (o.copied) (void)hipEventDestroy(o.copied);
+            for (hipEvent_t v : o.tl)
+                if (v) (void)hipEventDestroy(v);
+            o.tl.clear();
         }
         if (d.outs) (void)hipStreamDestroy(d.outs);
         for (int q = 0; q < kRing; q++) {
@@ -1556,6 +1563,7 @@ struct VerifyIn {
     // cv_ed25519_verify_batch_ex: the arena's size; every staging scan (which finds the byte range its records
     // reach anyway) rejects a shard or sub-chunk whose records reach past it before anything reads the arena
     uint64_t arena_bytes = UINT64_MAX;
+    double t_entry = 0;   // host time the call entered the engine (CV_OPT_TIMELINE's host_pre)
 };
 
 // Zero-copy form of the small path for tri-chain batches (the notary batches).  The records are packed into
@@ -1831,6 +1839,7 @@ static int pipe_copy_back(Device &d, PipeOut &po) {
         if (po.slot_used[k]) CV_TRY(hipEventSynchronize(po.slot_done[k]));
     const bool timeline = po.tl_n > 0 && po.tl.size() >= (size_t)po.tl_n * 3 + 1;
     const double t_copy = now_s();   // (timeline: the result copies' host-side time, from the join on)
+    po.tl_join_s = t_copy;
     constexpr size_t kDirect = 1u << 20;
     size_t hb = 0;
     for (int k = 0; k < po.nseg; k++) {
@@ -1892,7 +1901,8 @@ static int pipe_copy_back(Device &d, PipeOut &po) {
         }
         const double busy = union_len(all);
         const double v[kTlVals] = {ramp, dma_end, span, busy, span - ramp - busy, span - dma_end, copy_ms,
-                                   (double)po.tl_first, union_len(mk), union_len(vf), mdma_end, (double)J};
+                                   (double)po.tl_first, union_len(mk), union_len(vf), mdma_end, (double)J,
+                                   po.tl_pre_ms, 0.0};
         for (int k = 0; k < kTlVals; k++) po.tl_sum[k] = v[k];
         po.tl_ready = true;
         po.tl_n = 0;
@@ -1938,8 +1948,9 @@ static PipeOut &pipe_out(Device &d, int *index, std::unique_lock<std::mutex> &lk
 struct PipeFrame {
     Device &d;
     PipeOut &po;
+    int ns = 2;                       // compute slots this call uses (CV_OPT_PIPE_SLOTS for verify calls; set before init)
     hipStream_t ss[kPipeSlots] = {};
-    bool used[kPipeSlots + 1] = {};   // + the copy stream (Merkle kernels)
+    bool used[kPipeSlots + 1] = {};   // + the copy stream (Merkle kernels), always at index kPipeSlots
     double t[5] = {};   // plan, pack, wait, enqueue (seconds)
     uint64_t chunks = 0, direct = 0;
     bool tl = false;    // CV_OPT_TIMELINE: record po.tl's events (synchronous verify calls)
@@ -1948,7 +1959,7 @@ struct PipeFrame {
         return e ? hipEventRecord(e, s) : hipErrorOutOfMemory;
     }
     int init() {
-        for (int k = 0; k < kPipeSlots; k++) {
+        for (int k = 0; k < ns; k++) {
             CV_TRY(slot_stream(d, k, &ss[k]));
             CV_TRY(slot_events(d.slot[k]));
         }
@@ -1966,7 +1977,7 @@ struct PipeFrame {
     // this device (an earlier call still in flight keeps its results)
     void drain() {
         (void)hipStreamSynchronize(d.copy);
-        for (int k = 0; k < kPipeSlots; k++) (void)hipStreamSynchronize(ss[k]);
+        for (int k = 0; k < ns; k++) (void)hipStreamSynchronize(ss[k]);
         for (int q = 0; q < kRing; q++) d.in_used[q] = false;
         for (int k = 0; k < kStage; k++) d.stage_busy[k] = false;
         for (PipeOut &o : d.out)
@@ -2022,16 +2033,16 @@ struct PipeFrame {
     int copied(int q, int j, bool start_recorded = false) {
         if (tl) CV_TRY(tl_record(1 + 3 * (size_t)j, d.copy));
         CV_TRY(hipEventRecord(d.in_ready[q], d.copy));
-        CV_TRY(hipStreamWaitEvent(ss[j % kPipeSlots], d.in_ready[q], 0));
-        if (tl && !start_recorded) CV_TRY(tl_record(2 + 3 * (size_t)j, ss[j % kPipeSlots]));
+        CV_TRY(hipStreamWaitEvent(ss[j % ns], d.in_ready[q], 0));
+        if (tl && !start_recorded) CV_TRY(tl_record(2 + 3 * (size_t)j, ss[j % ns]));
         return CV_OK;
     }
     // after sub-chunk j's kernels: block q is free once they are done
     int launched(int q, int j) {
-        if (tl) CV_TRY(tl_record(3 + 3 * (size_t)j, ss[j % kPipeSlots]));
-        CV_TRY(hipEventRecord(d.in_free[q], ss[j % kPipeSlots]));
+        if (tl) CV_TRY(tl_record(3 + 3 * (size_t)j, ss[j % ns]));
+        CV_TRY(hipEventRecord(d.in_free[q], ss[j % ns]));
         d.in_used[q] = true;
-        used[j % kPipeSlots] = true;
+        used[j % ns] = true;
         chunks++;
         return CV_OK;
     }
@@ -2085,6 +2096,7 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
     const size_t words = (n + 63) / 64;
     const size_t o_st = al16(words * 8), total_out = o_st + al16(n);
     PipeFrame f{d, po};
+    f.ns = (int)o.pipe_slots;
     CV_TRY(hipSetDevice(d.ordinal));
     int rc = f.init();
     if (rc != CV_OK) return rc;
@@ -2104,13 +2116,13 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
             std::memcpy(po.kidx.p, kidx + b, n * 4);
             kidx = po.kidx.as<uint32_t>() - b;     // so kidx[i] is record i's key, i in [b, e)
         }
-        for (int k = 0; k < kPipeSlots; k++) CV_TRY(pool_begin(d.kc, f.ss[k]));
+        for (int k = 0; k < f.ns; k++) CV_TRY(pool_begin(d.kc, f.ss[k]));
         std::vector<uint32_t> sok;
         bool prepared = false;
         rc = key_resolve(d, ctx->key_cap.load(), nkeys, keys, in.used, sok, f.ss[0], &prepared);
         if (rc != CV_OK) return rc;
         if (prepared)                              // the other compute stream waits for the new tables
-            for (int k = 1; k < kPipeSlots; k++) CV_TRY(pool_begin(d.kc, f.ss[k]));
+            for (int k = 1; k < f.ns; k++) CV_TRY(pool_begin(d.kc, f.ss[k]));
         const size_t kb = al16(nkeys * 32) + al16(nkeys * 4);
         CV_TRY(po.kstage.ensure(kb));
         CV_TRY(po.kdev.ensure(kb));
@@ -2135,11 +2147,12 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
     f.tl = o.timeline && !async;
     po.tl_ready = false;
     po.tl_merkle.clear();
+    po.tl_pre_ms = 0;
     po.tl_first = cut.size() > 1 ? cut[1] - cut[0] : 0;
     for (size_t j = 0; j + 1 < cut.size(); j++) {
         const size_t c0 = cut[j], c1 = cut[j + 1], m = c1 - c0;
-        Slot &sl = d.slot[j % kPipeSlots];
-        hipStream_t s = f.ss[j % kPipeSlots];
+        Slot &sl = d.slot[j % f.ns];
+        hipStream_t s = f.ss[j % f.ns];
         double t0 = now_s();
         const Stage st = stage_plan(c0, c1, in.off, in.len, pool, keyed);
         if (!stage_in_bounds(st, in.arena_bytes)) return CV_E_ARGS;   // before this sub-chunk's copy (drain: the ones before it)
@@ -2197,6 +2210,7 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
             CV_TRY(hipMemcpyAsync(dv + from, h + from, st.total - from, hipMemcpyHostToDevice, d.copy));
             if ((rc = f.staged(sk)) != CV_OK) return rc;
         }
+        if (f.tl && j == 0 && in.t_entry > 0) po.tl_pre_ms = (now_s() - in.t_entry) * 1e3;
         if (f.tl && overlap0) {   // the timeline's first kernel start: the point blocks on the helper stream
             CV_TRY(hipStreamWaitEvent(pov.aux, pov.ready, 0));
             CV_TRY(f.tl_record(2, pov.aux));
@@ -2226,7 +2240,7 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
         f.t[3] += now_s() - t0;
     }
     if (keyed) {
-        for (int k = 0; k < kPipeSlots; k++)
+        for (int k = 0; k < f.ns; k++)
             if (f.used[k]) CV_TRY(pool_end(d.kc, f.ss[k]));   // (the pool's last user: either stream)
         std::lock_guard<std::mutex> g(ctx->st_mu);
         ctx->stats.keyed_chunks += f.chunks;
@@ -2470,6 +2484,7 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
     f.tl = o.timeline && !async;   // (timeline: groups tagged Merkle / verify in po.tl_merkle)
     po.tl_ready = false;
     po.tl_merkle.clear();
+    po.tl_pre_ms = 0;
     po.tl_first = 0;
     if (f.tl) CV_TRY(f.tl_record(0, d.copy));
     // the shard's signature boundaries go first on the copy stream, so every group's copy event covers them
@@ -2501,7 +2516,7 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
     const size_t nm = mcut.size() - 1;
     size_t max_nl = 0;
     for (size_t j = 0; j < nm; j++) max_nl = std::max<size_t>(max_nl, mi.txb[mcut[j + 1]] - mi.txb[mcut[j]]);
-    for (int k = 0; k < kPipeSlots; k++) {   // the two slots' leaf-digest workspaces
+    for (int k = 0; k < f.ns; k++) {   // the two slots' leaf-digest workspaces
         Slot &sl = d.slot[k];
         if (max_nl * 32 + 32 > sl.mdig.cap) {
             if (sl.last && sl.ev) CV_TRY(hipEventSynchronize(sl.ev));
@@ -2553,8 +2568,8 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
                 if ((r = f.staged(sk)) != CV_OK) return r;
             }
             if ((r = f.copied(q, g)) != CV_OK) return r;
-            Slot &sl = d.slot[g % kPipeSlots];
-            hipStream_t s = f.ss[g % kPipeSlots];
+            Slot &sl = d.slot[g % f.ns];
+            hipStream_t s = f.ss[g % f.ns];
             // every Merkle group holding one of its transactions: the first one's (the largest t with tsb[t] <= p)
             // through jc — a group on the other stream may not have run yet
             const size_t tf = (size_t)(std::upper_bound(in.tsb + t0, in.tsb + t1 + 1, (uint32_t)p) - in.tsb) - 1;
@@ -2605,8 +2620,8 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
         }
         if ((rc = f.copied(q, g)) != CV_OK) return rc;
         {
-            Slot &sl = d.slot[g % kPipeSlots];
-            hipStream_t s = f.ss[g % kPipeSlots];
+            Slot &sl = d.slot[g % f.ns];
+            hipStream_t s = f.ss[g % f.ns];
             CV_TRY(ws_begin(d, sl, s));
             const hipError_t ek = cvk_merkle((uint32_t)(st.t1 - st.t0), (uint32_t)(st.l1 - st.l0), (uint32_t)st.l0,
                                              dv + st.o_ar - st.lo, reinterpret_cast<const uint64_t *>(dv + st.o_off),
@@ -2626,9 +2641,9 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
     if ((rc = emit_sigs(nm - 1, true)) != CV_OK) return rc;
     // ---- per-transaction verdicts, behind both streams' last groups
     {
-        const int kl = (g - 1) % kPipeSlots;
+        const int kl = (g - 1) % f.ns;
         hipStream_t s = f.ss[kl];
-        for (int k = 0; k < kPipeSlots; k++)
+        for (int k = 0; k < f.ns; k++)
             if (k != kl && f.used[k]) {
                 CV_TRY(hipEventRecord(d.mev[nm], f.ss[k]));
                 CV_TRY(hipStreamWaitEvent(s, d.mev[nm], 0));
@@ -2653,6 +2668,7 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
 // A finished synchronous call's GPU timeline (CV_OPT_TIMELINE) into the context's sums.  The caller holds st_mu.
 static void timeline_account(cv_ctx *ctx, PipeOut &po) {
     if (!po.tl_ready) return;
+    po.tl_sum[kTlVals - 1] = (now_s() - po.tl_join_s) * 1e3;   // GPU work joined -> the call's results are back
     for (int k = 0; k < kTlVals; k++) ctx->stats.tl[k] += po.tl_sum[k];
     ctx->stats.tl[kTlVals] += 1;
     po.tl_ready = false;
@@ -2804,6 +2820,7 @@ int cv_diag_dedupe_keys(size_t n, const uint8_t *pk, uint32_t *key_index, size_t
 }
 
 static int verify_call(cv_ctx *ctx, size_t n, VerifyIn in, uint64_t *ticket) {
+    in.t_entry = now_s();
     const Opts o = ctx->opts();
     const bool async = ticket != nullptr;
     if (!in.keys && want_keyed(o, n, in.pk)) in.auto_keyed = true;

@@ -41,14 +41,15 @@ OPTIONS = {"tri_max": 1, "quad_max": 2, "drain_split": 3, "drain_split_pct": 4, 
            "pipe_chunk": 7, "async_chunk": 8, "host_threads": 9, "small_zero_copy": 10, "small_direct_min": 11,
            "auto_keyed": 12, "shard_min": 13, "spread_min": 14, "merkle_chunk": 15,
            "prep_overlap_min": 16, "timeline": 17, "pipe_split": 18,
-           "pipe_overlap_first": 19, "mid_pieces": 20}
+           "pipe_overlap_first": 19, "mid_pieces": 20,
+           "pipe_slots": 21}
 STATS = {"pipe": (0, ("plan_s", "pack_s", "wait_s", "enqueue_s", "sync_s", "calls", "subchunks", "direct_subchunks")),
          "small": (1, ("setup_s", "pack_s", "launch_s", "sync_s", "assemble_s", "calls")),
          "route": (2, ("calls", "routed_whole", "split_calls", "shards", "keyed_shards", "keyed_subchunks",
                        "merkle_calls", "merkle_subchunks")),
          "timeline": (3, ("ramp_ms", "dma_end_ms", "span_ms", "busy_ms", "idle_ms", "tail_ms", "result_copy_ms",
                           "first_subchunk", "merkle_busy_ms", "verify_busy_ms", "merkle_dma_end_ms", "groups",
-                          "calls"))}
+                          "host_pre_ms", "host_post_ms", "calls"))}
 
 
 class NativeUnavailable(RuntimeError):

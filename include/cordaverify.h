@@ -310,11 +310,15 @@ int cv_calibrate_cycles(cv_ctx *ctx, int device, double *out);
 #define CV_OPT_PIPE_SPLIT 18        /* synchronous pipelined calls: about n / this records per sub-chunk after the ramp,
                                        clamped to [2 x CV_OPT_PIPE_FIRST, CV_OPT_PIPE_CHUNK] (16) */
 #define CV_OPT_PIPE_OVERLAP_FIRST 19 /* synchronous pipelined calls: the first sub-chunk's keys and signatures go first and
-                                       its point decodes start as soon as they land: 1 on (default), 0 off */
+                                       its point decodes start as soon as they land: 1 on, 0 off (default: measured
+                                       neutral — the ramp shortens, the call does not) */
 #define CV_OPT_MID_PIECES 20        /* unpipelined mid-size batches from pageable inputs: packed and DMAed in up to this
                                        many pieces (about 1 MB of keys + signatures each), the DMA of one piece beside
-                                       the packing of the next (4; 1 = one DMA per part) */
-#define CV_OPT_COUNT 21
+                                       the packing of the next (1 = one DMA per part, the default: measured neutral to
+                                       slower at 65,536) */
+#define CV_OPT_PIPE_SLOTS 21        /* compute streams (workspace slots) a pipelined verify call deals its sub-chunks over
+                                       (2; 3 allowed) */
+#define CV_OPT_COUNT 22
 int cv_set_option(cv_ctx *ctx, int option, int64_t value);
 int cv_get_option(cv_ctx *ctx, int option, int64_t *value);
 
@@ -331,7 +335,9 @@ int cv_get_option(cv_ctx *ctx, int option, int64_t *value);
  *                   ramp), last input DMA end, last kernel end (the span), kernel-busy time (union over the launch
  *                   groups), idle gaps between the first kernel start and the span's end, the tail after the last DMA,
  *                   the result copy (host-timed); first sub-chunk records; Merkle-group busy, verify-group busy, last
- *                   Merkle DMA end (ms; cv_verify_transactions); launch groups; calls timed} */
+ *                   Merkle DMA end (ms; cv_verify_transactions); launch groups; host time from the call's entry to
+ *                   its first input DMA enqueued (verify calls) and from the GPU work joined to the results in the
+ *                   caller's arrays (ms); calls timed} */
 #define CV_STATS_PIPE 0
 #define CV_STATS_SMALL 1
 #define CV_STATS_ROUTE 2

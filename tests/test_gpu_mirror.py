@@ -232,7 +232,8 @@ def test_fused_batch_keeps_exception_precedence(engine):
 
 def test_fused_batch_random_matches_separate(engine):
     """200 transactions with random faults (tampered leaves, swapped / zeroed signatures, missing signers):
-    the fused entry point and the separate-call batch give the same exception, transaction by transaction."""
+    the fused entry point and the separate-call batch give the same exception, transaction by transaction, and
+    both the outcome the oracle restatements (eddsa-0.1.0 verify, Merkle id) give in the reference's order."""
     rng = np.random.default_rng(55)
     stxs = []
     for i in range(200):
@@ -251,6 +252,20 @@ def test_fused_batch_random_matches_separate(engine):
     sep = verify_signatures_batch([SignedTransaction(s._wtx, s.sigs, s.id) for s in stxs], engine=engine)
     assert [(type(a), str(a)) for a in got] == [(type(b), str(b)) for b in sep]
     assert sum(x is None for x in got) > 100
+    # independent check: the literal eddsa-0.1.0 restatement over each signature and the
+    # oracle's Merkle id of each transaction's leaves give the reference's outcome, in its precedence order
+    import merkle_ref as M
+    for st, g in zip(stxs, got):
+        first_bad = next((i for i, sg in enumerate(st.sigs) if not E.verify(sg.by.encoded, st.id.bytes, sg.bits)), None)
+        if first_bad is not None:
+            assert isinstance(g, SignatureException) and not isinstance(g, SignaturesMissingException), g
+        elif M.get_merkle_tree([M.sha256(x) for x in st._wtx.leaves]).hash != st.id.bytes:
+            # getMissingSignatures reads the lazy `tx`, whose id check throws first (SignedTransaction.kt:34-38)
+            assert isinstance(g, IllegalStateException), g
+        elif stx_missing(st):
+            assert isinstance(g, SignaturesMissingException), g
+        else:
+            assert g is None, g
 
 
 def test_compute_ids_golden():

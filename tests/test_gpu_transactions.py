@@ -146,12 +146,12 @@ def test_verify_transactions_edges(engine):
     assert ex.value.code == -3
 
 
-def test_verify_transactions_c3_shaped(engine):
+def test_verify_transactions_c3_shaped(engine, oracle_c):
     """C3-shaped transactions (6 leaves, 8 signers each, workload.make_tx_batch), 200,000 of them (1.6M signatures,
     the default sub-chunk plans: signature groups that start inside the previous Merkle sub-chunk): one in 16
     with a mutated leaf, one in 32 with a bad signature; tx_ok equals the expectation and the ids the claimed
     ids wherever the leaves are intact — synchronous (the last call also timed on the GPU), and three async calls in
-    flight."""
+    flight; the expectation itself is the C oracle's on the first 3,000 transactions."""
     ntx, signers = 200_000, 8
     tb = workload.make_tx_batch(engine, 0, ntx, signers, seed=4402)
     arena = tb.leaf_arena.cpu().numpy().copy()
@@ -171,6 +171,17 @@ def test_verify_transactions_c3_shaped(engine):
     sig_begin = np.arange(0, ntx * signers + 1, signers, dtype=np.uint32)
     args = (arena, leaf_off, leaf_len, tx_begin, pk, sig, sig_begin)
     intact = np.isin(np.arange(ntx), bad_leaf, invert=True)
+    # the constructed expectation, checked against the C oracle on a slice: the slice's ids
+    # recomputed from its leaves, its signatures verified over the CLAIMED ids, tx_ok = ids match AND all valid
+    k = 3000
+    l_end = int(tx_begin[k])
+    o_ids, o_st = oracle_c.merkle_tx_ids(arena, leaf_off[:l_end], leaf_len[:l_end], tx_begin[:k + 1])
+    c_arena = np.concatenate([claimed[:k].reshape(-1), np.zeros(16, np.uint8)])
+    o_v, _ = oracle_c.verify_batch(pk[:k * signers], sig[:k * signers], c_arena,
+                                   (np.arange(k * signers, dtype=np.uint64) // signers) * 32,
+                                   np.full(k * signers, 32, np.uint32), nthreads=8)
+    o_ok = (o_ids == claimed[:k]).all(axis=1) & (o_st == 0) & o_v.reshape(k, signers).astype(bool).all(axis=1)
+    assert np.array_equal(o_ok, expect[:k]) and not o_ok.all() and o_ok.sum() > k // 2
     for rep in range(3):
         if rep == 2:                                        # the last one timed on the GPU (CV_OPT_TIMELINE)
             engine.set_option("timeline", 1)

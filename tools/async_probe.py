@@ -26,6 +26,8 @@ def main():
     import torch  # noqa: F401
     from corda_amd import native, workload
     eng = native.Engine(1)
+    if os.environ.get("PIPE_SLOTS"):                  # compute streams of the pipelined calls (CV_OPT_PIPE_SLOTS)
+        eng.set_option("pipe_slots", int(os.environ["PIPE_SLOTS"]))
     n, ml = (1_000_000, 300) if a.shape == "c2" else (8_000_000, 32)
     b = workload.make_batch(eng, 0, n, ml, seed=11)
     page = b.to_host()
@@ -51,7 +53,8 @@ def main():
                 bm, _ = eng.wait(tk)
             ms = (time.perf_counter() - t) / a.calls * 1e3
             assert native.bitmap_to_bools(bm, n).all()
-            print(json.dumps({"shape": a.shape, "inputs": name, "async_chunk": ch, "async_ms_per_call": ms,
+            print(json.dumps({"shape": a.shape, "inputs": name, "pipe_slots": eng.get_option("pipe_slots"),
+                              "async_chunk": ch, "async_ms_per_call": ms,
                               "sync_ms_per_call": sync_ms}), flush=True)
     eng.close()
 

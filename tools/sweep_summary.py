@@ -15,4 +15,5 @@ for f in sys.argv[1:]:
               f'r {d["ratio"]:.3f} | plan {h.get("plan", 0):.2f} pack {h.get("pack", 0):.2f} '
               f'enq {h.get("enqueue", 0):.2f} sync {h.get("sync", 0):.2f} sub {h.get("subchunks", 0):.0f} | '
               f'ramp {t.get("ramp_ms", 0):.2f} dma {t.get("dma_end_ms", 0):.2f} span {t.get("span_ms", 0):.2f} '
-              f'busy {t.get("busy_ms", 0):.2f} idle {t.get("idle_ms", 0):.2f} tail {t.get("tail_ms", 0):.2f}')
+              f'busy {t.get("busy_ms", 0):.2f} idle {t.get("idle_ms", 0):.2f} tail {t.get("tail_ms", 0):.2f} | '
+              f'host pre {t.get("host_pre_ms", 0):.2f} post {t.get("host_post_ms", 0):.2f}')
