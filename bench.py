@@ -375,7 +375,7 @@ def host_c3_fused_rate(eng, local, sh, ntx: int, steps: int, device_value: float
     tl = eng.stats("timeline", reset=True)
     eng.set_option("timeline", 0)
     tc = max(1.0, tl["calls"])
-    breakdown = {k: tl[k] / tc for k in ("ramp_ms", "merkle_dma_end_ms", "dma_end_ms", "merkle_busy_ms",
+    breakdown = {k: tl[k] / tc for k in ("host_pre_ms", "ramp_ms", "merkle_dma_end_ms", "dma_end_ms", "merkle_busy_ms",
                                          "verify_busy_ms", "busy_ms", "idle_ms", "span_ms", "tail_ms",
                                          "result_copy_ms", "host_post_ms", "groups")}
     breakdown["sync_call_ms"] = sync_ms

@@ -437,7 +437,7 @@ static const OptDesc kOpt[CV_OPT_COUNT] = {
     {131072, 64, (int64_t)1 << 40},     // CV_OPT_PIPE_MIN
     {32768, 64, 1 << 24},               // CV_OPT_PIPE_FIRST
     {262144, 64, 1 << 24},              // CV_OPT_PIPE_CHUNK
-    {262144, 64, 1 << 24},              // CV_OPT_ASYNC_CHUNK
+    {196608, 64, 1 << 24},              // CV_OPT_ASYNC_CHUNK (one round of resident waves on MI355X)
     {8, 1, 64},                         // CV_OPT_HOST_THREADS
     {3, 0, 3},                          // CV_OPT_SMALL_ZERO_COPY
     {16384, 1, (int64_t)1 << 40},       // CV_OPT_SMALL_DIRECT_MIN
@@ -662,6 +662,8 @@ struct cv_ctx {
     }
 };
 
+static void span_slice(size_t i0, size_t i1, const uint64_t *off, const uint32_t *len, uint64_t *out);
+
 extern "C" {
 
 const char *cv_version(void) { return "cordaverify-mi355x 0.3 (gfx950)"; }
@@ -682,22 +684,19 @@ const char *cv_strerror(int code) {
 // check); slices of 2^20 records on up to 8 threads.
 uint64_t cv_msg_extent(size_t n, const uint64_t *off, const uint32_t *len) {
     if (!n || !off || !len) return 0;
-    constexpr size_t kSlice = 1u << 20;
+    // slices of 2^18 records through span_slice (the AVX2 min / max where the CPU has it; a wrapping record
+    // saturates to UINT64_MAX), on up to 8 threads
+    constexpr size_t kSlice = 1u << 18;
     const size_t ns = (n + kSlice - 1) / kSlice;
     std::vector<uint64_t> part(ns, 0);
     auto scan = [&](size_t k) {
-        uint64_t hi = 0;
-        const size_t i1 = std::min(n, (k + 1) * kSlice);
-        for (size_t i = k * kSlice; i < i1; i++) {
-            uint64_t end = off[i] + len[i];
-            end |= -(uint64_t)(end < off[i]);   // a wrapping record reports UINT64_MAX: past any arena
-            hi = std::max<uint64_t>(hi, end);
-        }
-        part[k] = hi;
+        uint64_t r[3];
+        span_slice(k * kSlice, std::min(n, (k + 1) * kSlice), off, len, r);
+        part[k] = r[1];
     };
-    const size_t nt = std::min<size_t>(ns, 8);
+    const size_t nt = std::min<size_t>((ns + 3) / 4, 8);
     if (nt <= 1) {
-        scan(0);
+        for (size_t k = 0; k < ns; k++) scan(k);
     } else {
         std::atomic<size_t> next{0};
         std::vector<std::thread> th;
@@ -1809,6 +1808,12 @@ static int verify_shard_small(cv_ctx *ctx, Device &d, const Opts &o, size_t b, s
 // but e is b + a multiple of `align`.  With ramp, the sizes after the first double (first, 2 first, ...)
 // until they reach C: each sub-chunk's copy then takes about as long as the kernels of the one before it,
 // so the GPU is not left waiting for a big second sub-chunk while a small first one has long finished.
+// The sub-chunk of an asynchronous pipelined call of n records: 1 or 2 x CV_OPT_ASYNC_CHUNK, the multiple nearest
+// n / 16 (so a call has about 16 or fewer launch groups, each a whole number of async chunks).
+static size_t async_sub_chunk(const Opts &o, size_t n) {
+    const size_t c = std::max<size_t>(64, o.async_chunk / 64 * 64);
+    return c * std::min<size_t>(2, std::max<size_t>(1, (n / 16 + c / 2) / c));
+}
 static std::vector<size_t> pipe_cuts(size_t b, size_t e, size_t first, size_t C, bool ramp = false, size_t align = 64) {
     std::vector<size_t> cut{b};
     if (e <= b) return cut;
@@ -2134,7 +2139,11 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
     }
     const uint8_t *kdev_keys = po.kdev.as<uint8_t>();
     const uint32_t *kdev_slot = keyed ? reinterpret_cast<const uint32_t *>(po.kdev.as<uint8_t>() + al16(nkeys * 32)) : nullptr;
-    const size_t ach = std::max(o.async_chunk, std::min(2 * o.async_chunk, n / 16 / 64 * 64));
+    // asynchronous calls: whole multiples of CV_OPT_ASYNC_CHUNK (default one round of resident hs_straus waves,
+    // 3 per SIMD x 1,024 SIMDs x 64 lanes = 196,608), one or two of them by the shard's size (n / 16), so each launch
+    // group ends on a full round (profiles/r06d: C2 1M 9.80 ms per call at 196,608 against 9.91 at 262,144; C5 8M
+    // 71.2 at 393,216 against 72-74)
+    const size_t ach = async_sub_chunk(o, n);
     // synchronous calls: about 16 sub-chunks after the ramp, between 2 x pipe_first and pipe_chunk.  A 1M C2 call
     // (tools/sync_pipe_sweep.py, two rounds on one box): 262,144-record sub-chunks 13.0-13.3 ms, 98,304 12.0,
     // 65,536 11.6, 49,152 12.9, 32,768 13.3; an 8M C5 call is compute-bound and keeps 262,144 (74 ms).
@@ -2460,6 +2469,7 @@ struct TxIn {
     const uint32_t *tsb;    // ntx + 1 signature boundaries
     uint8_t *sig_status;    // may be null
     uint8_t *tx_ok;
+    double t_entry = 0;     // host time the call entered the engine (CV_OPT_TIMELINE's host_pre)
 };
 static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_t t0, size_t t1, const TxIn &in,
                        int threads, bool async) {
@@ -2498,6 +2508,7 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
         }
         CV_TRY(hipMemcpyAsync(dout + o_tsb, src, (nt + 1) * 4, hipMemcpyHostToDevice, d.copy));
         f.t[0] += now_s() - ta;
+        if (f.tl) po.tl_pre_ms = (now_s() - in.t_entry) * 1e3;
     }
     // Merkle sub-chunks: whole transactions, ramped up to `per` leaves (at least one transaction each)
     const size_t nl_all = mi.txb[t1] - mi.txb[t0];
@@ -2530,7 +2541,7 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
         d.mev.push_back(v);
     }
     // signature sub-chunks: as pipe_enqueue's plan for ns records; at least vmin unless the shard ends there
-    const size_t vch = async ? std::max(o.async_chunk, std::min(2 * o.async_chunk, ns / 16 / 64 * 64))
+    const size_t vch = async ? async_sub_chunk(o, ns)
                              : std::min(o.pipe_chunk, std::max(2 * o.pipe_first, (ns / 16 + 63) / 64 * 64));
     const size_t vmin = std::min(vch, std::max<size_t>(o.pipe_first, 4096));
     int g = 0;           // launch groups so far (group g runs on compute stream g % 2)
@@ -3033,7 +3044,11 @@ static int merkle_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const
     const int rc = dispatch(ctx, o, ntx, 1, [&](Device &d, size_t t0, size_t t1, int threads) {
         if (t1 <= t0) return CV_OK;
         CV_TRY(hipSetDevice(d.ordinal));
-        if (!ticket) {                                // small synchronous shards: one DMA, no pipeline frame
+        // small synchronous shards: one DMA, no pipeline frame.  Their records alone (12 B per leaf, 4 per
+        // transaction) bound the staging from below, so a shard past kMerkleSmall by them skips the range scan
+        // of its leaves (C3's 6M leaves: several ms on the synchronous call's critical path)
+        const size_t nlv = (size_t)tx_leaf_begin[t1] - tx_leaf_begin[t0];
+        if (!ticket && nlv * 12 + (t1 - t0) * 4 <= kMerkleSmall) {
             WorkerPool *pool = &d.workers(threads);
             const MStage st = mstage_plan(t0, t1, tx_leaf_begin, leaf_off, leaf_len, pool);
             if (st.extent == UINT64_MAX) return CV_E_ARGS;   // a leaf's off + len wraps
@@ -3163,7 +3178,8 @@ static int txs_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const ui
     // shards of whole transactions, scaled as merkle_call's (~4,096 signatures' worth at C3's 8 per transaction)
     o.shard_min = std::max<size_t>(1, o.shard_min / 8);
     o.spread_min = std::max<size_t>(1, o.spread_min / 8);
-    TxIn in{{leaf_arena, leaf_off, leaf_len, tx_leaf_begin, ids, tx_status}, pk, sig, tx_sig_begin, sig_status, tx_ok};
+    TxIn in{{leaf_arena, leaf_off, leaf_len, tx_leaf_begin, ids, tx_status}, pk, sig, tx_sig_begin, sig_status, tx_ok,
+            now_s()};
     {
         std::lock_guard<std::mutex> g(ctx->st_mu);
         ctx->stats.merkle_calls++;
@@ -3172,11 +3188,14 @@ static int txs_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const ui
     const int rc = dispatch(ctx, o, ntx, 1, [&](Device &d, size_t t0, size_t t1, int threads) {
         if (t1 <= t0) return CV_OK;
         CV_TRY(hipSetDevice(d.ordinal));
-        if (!ticket) {                                // small synchronous shards: one DMA, one stream
+        // small synchronous shards: one DMA, one stream (the records alone bound the staging from below: a shard
+        // past kMerkleSmall by them skips the range scan of its leaves, as merkle_call)
+        const size_t nlv = (size_t)tx_leaf_begin[t1] - tx_leaf_begin[t0];
+        const size_t ns = tx_sig_begin[t1] - tx_sig_begin[t0];
+        if (!ticket && nlv * 12 + (t1 - t0) * 4 + ns * 96 <= kMerkleSmall) {
             WorkerPool *pool = &d.workers(threads);
             const MStage st = mstage_plan(t0, t1, tx_leaf_begin, leaf_off, leaf_len, pool);
             if (st.extent == UINT64_MAX) return CV_E_ARGS;   // a leaf's off + len wraps
-            const size_t ns = tx_sig_begin[t1] - tx_sig_begin[t0];
             if (st.total + ns * 96 <= kMerkleSmall) return txs_shard_small(d, o, st, in, pool);
         }
         int k = 0, r = CV_OK;

@@ -294,7 +294,8 @@ int cv_calibrate_cycles(cv_ctx *ctx, int device, double *out);
 #define CV_OPT_PIPE_FIRST 6         /* first sub-chunk of a synchronous pipelined call (32768; sizes then double) */
 #define CV_OPT_PIPE_CHUNK 7         /* largest sub-chunk of a synchronous pipelined call (262144); a call of n records
                                        uses about n / 16 per sub-chunk, at least 2 x CV_OPT_PIPE_FIRST */
-#define CV_OPT_ASYNC_CHUNK 8        /* sub-chunk of the asynchronous calls (262144) */
+#define CV_OPT_ASYNC_CHUNK 8        /* sub-chunk unit of the asynchronous calls: 1 or 2 of them per launch group, the
+                                       multiple nearest n / 16 (196608 = one round of resident verify waves) */
 #define CV_OPT_HOST_THREADS 9       /* host threads per device packing pageable inputs / deduping keys (8) */
 #define CV_OPT_SMALL_ZERO_COPY 10   /* tri-form host batches: 0 DMA, 1 zero-copy reads, 2 gather kernel, 3 auto (default) */
 #define CV_OPT_SMALL_DIRECT_MIN 11  /* unpipelined batches from pinned inputs DMA them in place from this size (16384) */

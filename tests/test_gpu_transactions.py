@@ -87,6 +87,8 @@ def test_verify_transactions_vs_oracle(engine, oracle_c, corpus):
     pinned_s = [engine.host_copy(x) for x in sigs]
     for k in (1, 3):
         e = engine if k == 1 else native.Engine(1, virtual_devices=k)
+        saved = {name: e.get_option(name) for name in ("merkle_chunk", "pipe_first", "pipe_chunk", "async_chunk",
+                                                        "shard_min")}
         try:
             e.set_option("merkle_chunk", 3000)
             e.set_option("pipe_first", 1024)
@@ -110,8 +112,7 @@ def test_verify_transactions_vs_oracle(engine, oracle_c, corpus):
             ok, ids, st, sst = e.verify_transactions(*leaves, *sigs, want_status=False)
             assert st is None and sst is None and np.array_equal(ok, ref[3]) and np.array_equal(ids, ref[0])
         finally:
-            for name, v in (("merkle_chunk", 262144), ("pipe_first", 32768), ("pipe_chunk", 262144),
-                            ("async_chunk", 262144), ("shard_min", 4096)):
+            for name, v in saved.items():
                 e.set_option(name, v)
             if k != 1:
                 e.close()
