@@ -37,7 +37,7 @@ __global__ __launch_bounds__(CV_BLOCK, WAVES) void cv_hs_straus_kernel(uint32_t 
     if ((threadIdx.x & 63u) == 0) bitmap[wave0 >> 6] = bits;
 }
 
-template __global__ void cv_hs_straus_kernel<3>(uint32_t, uint32_t, const uint32_t *, const uint32_t *,
+template __global__ void cv_hs_straus_kernel<CV_HSS_WAVES>(uint32_t, uint32_t, const uint32_t *, const uint32_t *,
                                                 const uint32_t *, const uint8_t *, uint64_t *, const uint32_t *);
-template __global__ void cv_hs_straus_kernel<3, true>(uint32_t, uint32_t, const uint32_t *, const uint32_t *,
+template __global__ void cv_hs_straus_kernel<CV_HSS_WAVES, true>(uint32_t, uint32_t, const uint32_t *, const uint32_t *,
                                                 const uint32_t *, const uint8_t *, uint64_t *, const uint32_t *);

@@ -14,6 +14,11 @@
 #include "cv_hsquad.h"
 
 #define CV_BLOCK 256
+// waves per SIMD the throughput Straus kernel is built for (its __launch_bounds__; 168 VGPRs fit 3).  A build
+// knob for A/Bs only (tools/ab_build_waves.sh NAME 2): both cv_k_hss.hip and the launchers must agree.
+#ifndef CV_HSS_WAVES
+#define CV_HSS_WAVES 3
+#endif
 
 __device__ __forceinline__ void stage_btab(uint32_t *lds) {
     for (int i = threadIdx.x; i < CV_BTAB_ENTRIES * CV_BTAB_STRIDE; i += blockDim.x) lds[i] = CV_BTAB[i];

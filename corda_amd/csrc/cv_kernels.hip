@@ -200,7 +200,7 @@ hipError_t cvk_verify(const CvkPlan *plan, uint32_t n, const uint8_t *pk, const 
                                      ws_dig + sub0[h], ws_tab + (size_t)sub0[h] * CV_TAB_WORDS,
                                      ws_tabR + (size_t)sub0[h] * CV_TAB_WORDS, ws_ok + sub0[h],
                                      status ? status + a : nullptr, st, nullptr);
-                hipLaunchKernelGGL((cv_hs_straus_kernel<3, true>), dim3(bl), dim3(CV_BLOCK), 0, st, mm, ws_cap,
+                hipLaunchKernelGGL((cv_hs_straus_kernel<CV_HSS_WAVES, true>), dim3(bl), dim3(CV_BLOCK), 0, st, mm, ws_cap,
                                    ws_dig + sub0[h], ws_tab + (size_t)sub0[h] * CV_TAB_WORDS,
                                    ws_tabR + (size_t)sub0[h] * CV_TAB_WORDS, ws_ok + sub0[h], bitmap + a / 64, bw16);
             }
@@ -216,7 +216,7 @@ hipError_t cvk_verify(const CvkPlan *plan, uint32_t n, const uint8_t *pk, const 
             hipLaunchKernelGGL(cv_scalars_kernel<3>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, pk, sig, arena, off,
                                len, ws_dig);
             (void)hipStreamWaitEvent(stream, po->done, 0);
-            hipLaunchKernelGGL(cv_hs_straus_kernel<3>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, ws_dig, ws_tab,
+            hipLaunchKernelGGL(cv_hs_straus_kernel<CV_HSS_WAVES>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, ws_dig, ws_tab,
                                ws_tabR, ws_ok, bitmap, bw16);
             continue;
         }
@@ -224,7 +224,7 @@ hipError_t cvk_verify(const CvkPlan *plan, uint32_t n, const uint8_t *pk, const 
                               ws_tab, ws_tabR, ws_ok, status ? status + c0 : nullptr, stream,
                               ev && c0 == 0 ? ev[1] : nullptr);
         if (ev && c0 == 0) (void)hipEventRecord(ev[2], stream);
-        hipLaunchKernelGGL(cv_hs_straus_kernel<3>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, ws_dig, ws_tab,
+        hipLaunchKernelGGL(cv_hs_straus_kernel<CV_HSS_WAVES>, dim3(blocks), dim3(CV_BLOCK), 0, stream, m, ws_cap, ws_dig, ws_tab,
                            ws_tabR, ws_ok, bitmap + (size_t)c0 / 64, bw16);
         if (ev && c0 == 0) (void)hipEventRecord(ev[3], stream);
     }

@@ -32,7 +32,7 @@ def _line(out: str) -> dict:
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_self_launch_gathers_over_ranks(world):
     """--gpus N without a launcher starts N ranks (RANK / LOCAL_RANK / WORLD_SIZE set by the parent), every
     timed step all-gathers the ranks' bitmaps, and rank 0's single line reports n_gpus = N."""
