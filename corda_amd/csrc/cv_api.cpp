@@ -395,6 +395,10 @@ struct Device {
     int stage_next = 0;
     // transaction calls: after each Merkle launch group (the signature groups wait for it), + one join event
     std::vector<hipEvent_t> mev;
+    // transaction calls with CV_OPT_TXS_MERKLE_STREAM = 2: the stream their Merkle groups run on (created on first
+    // use) and those groups' leaf-digest buffer (the groups run one after another on it)
+    hipStream_t mstream = nullptr;
+    DevBuf mdigest;
     WorkerPool &workers(int threads) {
         if (!pool || pool->threads() != threads) {
             pool.reset();
@@ -451,6 +455,7 @@ static const OptDesc kOpt[CV_OPT_COUNT] = {
     {0, 0, 1},                          // CV_OPT_PIPE_OVERLAP_FIRST
     {1, 1, 16},                         // CV_OPT_MID_PIECES
     {2, 2, 3},                          // CV_OPT_PIPE_SLOTS
+    {0, 0, 2},                          // CV_OPT_TXS_MERKLE_STREAM
 };
 
 // A snapshot of a context's options, taken once per call.
@@ -459,6 +464,7 @@ struct Opts {
     size_t pipe_min, pipe_first, pipe_chunk, async_chunk, small_direct_min, shard_min, spread_min, merkle_chunk;
     size_t prep_overlap_min;
     size_t pipe_split, mid_pieces, pipe_slots;
+    int txs_merkle_stream;
     int threads, small_zc, auto_keyed, timeline, pipe_overlap_first;
 };
 
@@ -658,6 +664,7 @@ struct cv_ctx {
         o.pipe_overlap_first = (int)opt[CV_OPT_PIPE_OVERLAP_FIRST].load();
         o.mid_pieces = (size_t)opt[CV_OPT_MID_PIECES].load();
         o.pipe_slots = (size_t)opt[CV_OPT_PIPE_SLOTS].load();
+        o.txs_merkle_stream = (int)opt[CV_OPT_TXS_MERKLE_STREAM].load();
         return o;
     }
 };
@@ -830,7 +837,7 @@ void cv_close(cv_ctx *ctx) {
         (void)hipSetDevice(d.ordinal);
         (void)hipDeviceSynchronize();
         for (DevBuf *b : {&d.pk, &d.sig, &d.arena, &d.off, &d.len, &d.bitmap, &d.status, &d.seed, &d.tx_begin,
-                          &d.digest, &d.ids, &d.pmt, &d.kc.ktab, &d.kc.kok, &d.kc.keys, &d.kc.slots,
+                          &d.digest, &d.mdigest, &d.ids, &d.pmt, &d.kc.ktab, &d.kc.kok, &d.kc.keys, &d.kc.slots,
                           &d.kc.slot_of_key, &d.kc.scratch})
             b->release();
         d.pin_out.release();
@@ -874,6 +881,7 @@ void cv_close(cv_ctx *ctx) {
         for (hipEvent_t v : d.mev) (void)hipEventDestroy(v);
         d.mev.clear();
         if (d.copy) (void)hipStreamDestroy(d.copy);
+        if (d.mstream) (void)hipStreamDestroy(d.mstream);
         d.kc.pin.release();
         for (hipEvent_t v : {d.kc.ev, d.kc.pin_ev, d.kc.wev})
             if (v) (void)hipEventDestroy(v);
@@ -1982,6 +1990,7 @@ struct PipeFrame {
     // this device (an earlier call still in flight keeps its results)
     void drain() {
         (void)hipStreamSynchronize(d.copy);
+        if (d.mstream) (void)hipStreamSynchronize(d.mstream);
         for (int k = 0; k < ns; k++) (void)hipStreamSynchronize(ss[k]);
         for (int q = 0; q < kRing; q++) d.in_used[q] = false;
         for (int k = 0; k < kStage; k++) d.stage_busy[k] = false;
@@ -2034,22 +2043,31 @@ struct PipeFrame {
         d.stage_busy[k] = true;
         return CV_OK;
     }
-    // after sub-chunk j's copies into block q: compute stream j % 2 waits for them
-    int copied(int q, int j, bool start_recorded = false) {
+    // after sub-chunk j's copies into block q: compute stream j % 2 (or `on`) waits for them
+    int copied(int q, int j, bool start_recorded = false, hipStream_t on = nullptr) {
+        hipStream_t s = on ? on : ss[j % ns];
         if (tl) CV_TRY(tl_record(1 + 3 * (size_t)j, d.copy));
         CV_TRY(hipEventRecord(d.in_ready[q], d.copy));
-        CV_TRY(hipStreamWaitEvent(ss[j % ns], d.in_ready[q], 0));
-        if (tl && !start_recorded) CV_TRY(tl_record(2 + 3 * (size_t)j, ss[j % ns]));
+        if (s != d.copy) CV_TRY(hipStreamWaitEvent(s, d.in_ready[q], 0));
+        if (tl && !start_recorded) CV_TRY(tl_record(2 + 3 * (size_t)j, s));
         return CV_OK;
     }
-    // after sub-chunk j's kernels: block q is free once they are done
-    int launched(int q, int j) {
-        if (tl) CV_TRY(tl_record(3 + 3 * (size_t)j, ss[j % ns]));
-        CV_TRY(hipEventRecord(d.in_free[q], ss[j % ns]));
+    // after sub-chunk j's kernels (on compute stream j % 2, or `on`): block q is free once they are done.  A
+    // stream other than the compute and copy streams is not joined by complete(): the caller makes a joined
+    // stream wait for it.
+    int launched(int q, int j, hipStream_t on = nullptr) {
+        hipStream_t s = on ? on : ss[j % ns];
+        if (tl) CV_TRY(tl_record(3 + 3 * (size_t)j, s));
+        CV_TRY(hipEventRecord(d.in_free[q], s));
         d.in_used[q] = true;
-        used[j % ns] = true;
+        mark_used(s);
         chunks++;
         return CV_OK;
+    }
+    void mark_used(hipStream_t s) {
+        for (int k = 0; k < ns; k++)
+            if (ss[k] == s) used[k] = true;
+        if (s == d.copy) used[kPipeSlots] = true;
     }
     // completion marks per slot stream (pipe_finish joins on the host; no GPU-side join, which would hold
     // the next call's kernels on that stream until this call had finished)
@@ -2480,6 +2498,7 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
     const size_t o_bm = o_sst + (in.sig_status ? al16(ns) : 0), o_off = o_bm + al16(words * 8);
     const size_t o_len = o_off + al16(ns * 8), o_tsb = o_len + al16(ns * 4), total_out = o_tsb + al16((nt + 1) * 4);
     PipeFrame f{d, po};
+    f.ns = (int)o.pipe_slots;
     CV_TRY(hipSetDevice(d.ordinal));
     int rc = f.init();
     if (rc != CV_OK) return rc;
@@ -2527,12 +2546,32 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
     const size_t nm = mcut.size() - 1;
     size_t max_nl = 0;
     for (size_t j = 0; j < nm; j++) max_nl = std::max<size_t>(max_nl, mi.txb[mcut[j + 1]] - mi.txb[mcut[j]]);
-    for (int k = 0; k < f.ns; k++) {   // the two slots' leaf-digest workspaces
-        Slot &sl = d.slot[k];
-        if (max_nl * 32 + 32 > sl.mdig.cap) {
-            if (sl.last && sl.ev) CV_TRY(hipEventSynchronize(sl.ev));
-            CV_TRY(hipStreamSynchronize(f.ss[k]));
-            CV_TRY(sl.mdig.ensure(max_nl * 32 + 32));
+    // CV_OPT_TXS_MERKLE_STREAM: the Merkle groups on the compute streams (0: each group takes the next slot, its
+    // leaf digests in that slot's workspace), or all on one stream (1 the copy stream, behind their leaves; 2 a
+    // stream of their own) with one leaf-digest buffer, their groups running one after another there
+    hipStream_t mst = nullptr;
+    DevBuf *mdig = nullptr;
+    if (o.txs_merkle_stream == 1) {
+        mst = d.copy;
+        mdig = &d.digest;   // (the separate Merkle calls' buffer: they run on the copy stream too)
+    } else if (o.txs_merkle_stream == 2) {
+        if (!d.mstream) CV_TRY(hipStreamCreateWithFlags(&d.mstream, hipStreamNonBlocking));
+        mst = d.mstream;
+        mdig = &d.mdigest;
+    }
+    if (mst) {
+        if (max_nl * 32 + 32 > mdig->cap) {
+            CV_TRY(hipStreamSynchronize(mst));
+            CV_TRY(mdig->ensure(max_nl * 32 + 32));
+        }
+    } else {
+        for (int k = 0; k < f.ns; k++) {   // the two slots' leaf-digest workspaces
+            Slot &sl = d.slot[k];
+            if (max_nl * 32 + 32 > sl.mdig.cap) {
+                if (sl.last && sl.ev) CV_TRY(hipEventSynchronize(sl.ev));
+                CV_TRY(hipStreamSynchronize(f.ss[k]));
+                CV_TRY(sl.mdig.ensure(max_nl * 32 + 32));
+            }
         }
     }
     while (d.mev.size() < nm + 1) {
@@ -2545,6 +2584,7 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
                              : std::min(o.pipe_chunk, std::max(2 * o.pipe_first, (ns / 16 + 63) / 64 * 64));
     const size_t vmin = std::min(vch, std::max<size_t>(o.pipe_first, 4096));
     int g = 0;           // launch groups so far (group g runs on compute stream g % 2)
+    int vg = 0;          // signature groups so far (with the Merkle groups on their own stream: on stream vg % 2)
     size_t p = s0;       // the next signature to stage
     // the signature groups whose transactions all lie in Merkle sub-chunks 0..jc (to the shard's end if last)
     auto emit_sigs = [&](size_t jc, bool last) -> int {
@@ -2578,9 +2618,10 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
                 CV_TRY(hipMemcpyAsync(dv, h, bytes, hipMemcpyHostToDevice, d.copy));
                 if ((r = f.staged(sk)) != CV_OK) return r;
             }
-            if ((r = f.copied(q, g)) != CV_OK) return r;
-            Slot &sl = d.slot[g % f.ns];
-            hipStream_t s = f.ss[g % f.ns];
+            const int ks = mst ? vg++ % f.ns : g % f.ns;
+            Slot &sl = d.slot[ks];
+            hipStream_t s = f.ss[ks];
+            if ((r = f.copied(q, g, false, s)) != CV_OK) return r;
             // every Merkle group holding one of its transactions: the first one's (the largest t with tsb[t] <= p)
             // through jc — a group on the other stream may not have run yet
             const size_t tf = (size_t)(std::upper_bound(in.tsb + t0, in.tsb + t1 + 1, (uint32_t)p) - in.tsb) - 1;
@@ -2591,7 +2632,7 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
             CV_TRY(launch_verify(d, o.plan, sl, (uint32_t)m, dv, dv + o_sig, dout, doff + c0, dlen + c0, dbm + c0 / 64,
                                  in.sig_status ? dout + o_sst + c0 : nullptr, s, nullptr, false));
             if (f.tl) po.tl_merkle.push_back(0);
-            if ((r = f.launched(q, g++)) != CV_OK) return r;
+            if ((r = f.launched(q, g++, s)) != CV_OK) return r;
             f.t[3] += now_s() - tb;
             p += m;
         }
@@ -2629,37 +2670,44 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
             CV_TRY(hipMemcpyAsync(dv, h, st.total, hipMemcpyHostToDevice, d.copy));
             if ((rc = f.staged(sk)) != CV_OK) return rc;
         }
-        if ((rc = f.copied(q, g)) != CV_OK) return rc;
+        hipStream_t s = mst ? mst : f.ss[g % f.ns];
+        if ((rc = f.copied(q, g, false, s)) != CV_OK) return rc;
         {
-            Slot &sl = d.slot[g % f.ns];
-            hipStream_t s = f.ss[g % f.ns];
-            CV_TRY(ws_begin(d, sl, s));
+            Slot *sl = mst ? nullptr : &d.slot[g % f.ns];
+            if (sl) CV_TRY(ws_begin(d, *sl, s));
             const hipError_t ek = cvk_merkle((uint32_t)(st.t1 - st.t0), (uint32_t)(st.l1 - st.l0), (uint32_t)st.l0,
                                              dv + st.o_ar - st.lo, reinterpret_cast<const uint64_t *>(dv + st.o_off),
                                              reinterpret_cast<const uint32_t *>(dv + st.o_len),
-                                             reinterpret_cast<const uint32_t *>(dv + st.o_txb), sl.mdig.as<uint32_t>(),
+                                             reinterpret_cast<const uint32_t *>(dv + st.o_txb),
+                                             sl ? sl->mdig.as<uint32_t>() : mdig->as<uint32_t>(),
                                              dout + (st.t0 - t0) * 32, dout + o_mst + (st.t0 - t0), s);
-            const hipError_t e2 = ws_end(sl, s);
+            const hipError_t e2 = sl ? ws_end(*sl, s) : hipSuccess;
             CV_TRY(ek);
             CV_TRY(e2);
-            CV_TRY(hipEventRecord(d.mev[J], s));
+            if (sl) CV_TRY(hipEventRecord(d.mev[J], s));
         }
         if (f.tl) po.tl_merkle.push_back(1);
-        if ((rc = f.launched(q, g++)) != CV_OK) return rc;
+        if ((rc = f.launched(q, g++, s)) != CV_OK) return rc;
+        // (own stream: after launched()'s events, so a stream that waits for mev[J] also covers them)
+        if (mst) CV_TRY(hipEventRecord(d.mev[J], s));
         f.t[3] += now_s() - ta;
         if (J > 0 && (rc = emit_sigs(J - 1, false)) != CV_OK) return rc;
     }
     if ((rc = emit_sigs(nm - 1, true)) != CV_OK) return rc;
     // ---- per-transaction verdicts, behind both streams' last groups
     {
-        const int kl = (g - 1) % f.ns;
+        const int kl = mst ? (vg + f.ns - 1) % f.ns : (g - 1) % f.ns;
         hipStream_t s = f.ss[kl];
         for (int k = 0; k < f.ns; k++)
             if (k != kl && f.used[k]) {
                 CV_TRY(hipEventRecord(d.mev[nm], f.ss[k]));
                 CV_TRY(hipStreamWaitEvent(s, d.mev[nm], 0));
             }
+        // Merkle groups on a stream of their own: the last one (every transaction's status and id) first; the
+        // call's join on this stream then covers that stream's part of the call as well
+        if (mst && nm) CV_TRY(hipStreamWaitEvent(s, d.mev[nm - 1], 0));
         CV_TRY(cvk_tx_verdicts((uint32_t)nt, (uint32_t)s0, dtsb, dout + o_mst, dbm, dout + o_ok, s));
+        f.mark_used(s);
     }
     if ((rc = f.complete()) != CV_OK) return rc;
     drain.armed = false;

@@ -147,12 +147,23 @@ def test_verify_transactions_edges(engine):
     assert ex.value.code == -3
 
 
-def test_verify_transactions_c3_shaped(engine, oracle_c):
+@pytest.mark.parametrize("mstream", [0, 1, 2])
+def test_verify_transactions_c3_shaped(engine, oracle_c, mstream):
     """C3-shaped transactions (6 leaves, 8 signers each, workload.make_tx_batch), 200,000 of them (1.6M signatures,
     the default sub-chunk plans: signature groups that start inside the previous Merkle sub-chunk): one in 16
     with a mutated leaf, one in 32 with a bad signature; tx_ok equals the expectation and the ids the claimed
     ids wherever the leaves are intact — synchronous (the last call also timed on the GPU), and three async calls in
-    flight; the expectation itself is the C oracle's on the first 3,000 transactions."""
+    flight; the expectation itself is the C oracle's on the first 3,000 transactions.  mstream: the stream the
+    Merkle groups run on (CV_OPT_TXS_MERKLE_STREAM: the compute streams, the copy stream, their own)."""
+    saved = engine.get_option("txs_merkle_stream")
+    engine.set_option("txs_merkle_stream", mstream)
+    try:
+        _c3_shaped(engine, oracle_c)
+    finally:
+        engine.set_option("txs_merkle_stream", saved)
+
+
+def _c3_shaped(engine, oracle_c):
     ntx, signers = 200_000, 8
     tb = workload.make_tx_batch(engine, 0, ntx, signers, seed=4402)
     arena = tb.leaf_arena.cpu().numpy().copy()

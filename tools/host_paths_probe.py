@@ -7,6 +7,8 @@
   c3        the host C3 step of bench.py (1M txs x 8 signers): per-step wall time, time blocked on the Merkle
             ids and on the verdicts
   c3f       the same step through the fused cv_verify_transactions(_async), async then synchronous
+            (MERKLE_STREAMS=0,1,2 C3F_ROUNDS=2: an interleaved A/B of CV_OPT_TXS_MERKLE_STREAM, async form)
+  c3dev     the device C3 step (HBM-resident inputs), the host C3 ratios' denominator
   txsmall   notary-sized transaction batches (32 and 512 txs x 8 signers): fused call vs the separate calls, p50
 
     python tools/host_paths_probe.py [--what resolve,keyed,c3] [--reps N]
@@ -102,6 +104,17 @@ def c3(eng, reps):
     print(json.dumps({"what": "c3", **r, "pipe_stats": st}), flush=True)
 
 
+def c3dev(eng, reps):
+    """The device C3 step of bench.py (HBM-resident inputs): the denominator of the host C3 ratios, same box."""
+    import bench  # noqa: E402
+    st = torch.cuda.Stream(0)
+    torch.cuda.set_stream(st)
+    r = bench.run_c3(eng, 0, 0, 1, st.cuda_stream, torch.device("cuda", 0), 1_000_000, 4, 1)
+    torch.cuda.set_stream(torch.cuda.default_stream(0))
+    print(json.dumps({"what": "c3_device", "ms_per_step": r["elapsed"] / 4 * 1e3, "merkle_ms": r["merkle_ms"],
+                      "phase_ms": [float(x) for x in r["phases"]]}), flush=True)
+
+
 def txsmall(eng, reps):
     """A notary-sized batch of transactions (512 x 8 signers = 4,096 signatures, C3-shaped leaves) through the
     fused call against the separate Merkle + verify + cv_tx_verdicts calls: p50 per batch."""
@@ -141,16 +154,35 @@ def c3f(eng, reps):
     pcie = bench.pcie_h2d_probe(torch.device("cuda", 0))
     if os.environ.get("ASYNC_CHUNK"):                 # the async sub-chunk (CV_OPT_ASYNC_CHUNK) under test
         eng.set_option("async_chunk", int(os.environ["ASYNC_CHUNK"]))
-    for sync in (False, True) * int(os.environ.get("C3F_ROUNDS", "1")):
-        eng.stats("pipe", reset=True)
-        try:
-            r = bench.host_c3_fused_rate(eng, 0, 0, 1_000_000, reps, 1.0, pcie, sync=sync)
-        except AssertionError as e:
-            print(json.dumps({"what": "c3_fused", "sync": sync, "error": str(e)}), flush=True)
-            continue
-        r.pop("ratio_to_device_value", None)
-        print(json.dumps({"what": "c3_fused", "sync": sync, "async_chunk": eng.get_option("async_chunk"), **r,
-                          "pipe_stats": eng.stats("pipe")}), flush=True)
+    # C3F_CONFIGS="txs_merkle_stream=0;txs_merkle_stream=2,async_chunk=589824": an A/B of option sets (each config
+    # k=v,... over the defaults), interleaved over C3F_ROUNDS (async form only unless C3F_SYNC=1);
+    # MERKLE_STREAMS="0,1,2" is short for the configs txs_merkle_stream=0;...;txs_merkle_stream=2
+    if os.environ.get("C3F_CONFIGS"):
+        configs = [dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in c.split(",") if kv)
+                   for c in os.environ["C3F_CONFIGS"].split(";")]
+    elif os.environ.get("MERKLE_STREAMS"):
+        configs = [{"txs_merkle_stream": int(x)} for x in os.environ["MERKLE_STREAMS"].split(",")]
+    else:
+        configs = [{}]
+    defaults = {k: eng.get_option(k) for c in configs for k in c}
+    forms = (False, True) if os.environ.get("C3F_SYNC", "1" if len(configs) == 1 else "0") == "1" else (False,)
+    for _ in range(int(os.environ.get("C3F_ROUNDS", "1"))):
+        for cfg in configs:
+            for k, v in {**defaults, **cfg}.items():
+                eng.set_option(k, v)
+            mode = eng.get_option("txs_merkle_stream")
+            for sync in forms:
+                eng.stats("pipe", reset=True)
+                try:
+                    r = bench.host_c3_fused_rate(eng, 0, 0, 1_000_000, reps, 1.0, pcie, sync=sync)
+                except AssertionError as e:
+                    print(json.dumps({"what": "c3_fused", "sync": sync, "merkle_stream": mode, "config": cfg, "error": str(e)}),
+                          flush=True)
+                    continue
+                r.pop("ratio_to_device_value", None)
+                print(json.dumps({"what": "c3_fused", "sync": sync, "merkle_stream": mode, "config": cfg,
+                                  "async_chunk": eng.get_option("async_chunk"), **r, "pipe_stats": eng.stats("pipe")}),
+                      flush=True)
 
 
 def main():
@@ -160,7 +192,8 @@ def main():
     a = ap.parse_args()
     eng = native.Engine(1)
     for w in a.what.split(","):
-        {"resolve": resolve, "keyed": keyed, "c3": c3, "c3f": c3f, "txsmall": txsmall}[w](eng, a.reps if w not in ("c3", "c3f") else 4)
+        {"resolve": resolve, "keyed": keyed, "c3": c3, "c3f": c3f, "c3dev": c3dev,
+         "txsmall": txsmall}[w](eng, a.reps if w not in ("c3", "c3f") else 4)
     eng.close()
 
 
