@@ -455,7 +455,7 @@ static const OptDesc kOpt[CV_OPT_COUNT] = {
     {0, 0, 1},                          // CV_OPT_PIPE_OVERLAP_FIRST
     {1, 1, 16},                         // CV_OPT_MID_PIECES
     {2, 2, 3},                          // CV_OPT_PIPE_SLOTS
-    {0, 0, 2},                          // CV_OPT_TXS_MERKLE_STREAM
+    {2, 0, 2},                          // CV_OPT_TXS_MERKLE_STREAM
 };
 
 // A snapshot of a context's options, taken once per call.
@@ -2548,7 +2548,10 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
     for (size_t j = 0; j < nm; j++) max_nl = std::max<size_t>(max_nl, mi.txb[mcut[j + 1]] - mi.txb[mcut[j]]);
     // CV_OPT_TXS_MERKLE_STREAM: the Merkle groups on the compute streams (0: each group takes the next slot, its
     // leaf digests in that slot's workspace), or all on one stream (1 the copy stream, behind their leaves; 2 a
-    // stream of their own) with one leaf-digest buffer, their groups running one after another there
+    // stream of their own, the default) with one leaf-digest buffer, their groups running one after another there.
+    // Async C3 (1M txs x 8 signers) per call, interleaved on three boxes: 0 82.8 / 82.8, 80.0 / 80.3, 82.9 / 81.8 ms;
+    // 1 83.4 / 82.8; 2 80.3 / 81.6, 78.6 / 79.3, 80.8 / 80.9 (profiles/r06k_*, r06l_*, r06m_*): off the compute
+    // streams the signature groups alternate undisturbed and the Merkle kernels take CU slots between their waves
     hipStream_t mst = nullptr;
     DevBuf *mdig = nullptr;
     if (o.txs_merkle_stream == 1) {
@@ -2582,6 +2585,8 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
     // signature sub-chunks: as pipe_enqueue's plan for ns records; at least vmin unless the shard ends there
     const size_t vch = async ? async_sub_chunk(o, ns)
                              : std::min(o.pipe_chunk, std::max(2 * o.pipe_first, (ns / 16 + 63) / 64 * 64));
+    // (signature groups of whole vch units only, the records past a Merkle sub-chunk's last whole group joining the
+    // next sub-chunk's: 1-2 % slower per async C3 call, profiles/r06m_txs_whole_groups_ab.log)
     const size_t vmin = std::min(vch, std::max<size_t>(o.pipe_first, 4096));
     int g = 0;           // launch groups so far (group g runs on compute stream g % 2)
     int vg = 0;          // signature groups so far (with the Merkle groups on their own stream: on stream vg % 2)

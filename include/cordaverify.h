@@ -320,8 +320,8 @@ int cv_calibrate_cycles(cv_ctx *ctx, int device, double *out);
 #define CV_OPT_PIPE_SLOTS 21        /* compute streams (workspace slots) a pipelined verify call deals its sub-chunks over
                                        (2; 3 allowed) */
 #define CV_OPT_TXS_MERKLE_STREAM 22 /* cv_verify_transactions: the stream its Merkle groups run on — 0 the compute streams
-                                       beside the signature groups (default), 1 the copy stream behind their leaves,
-                                       2 a stream of their own */
+                                       beside the signature groups, 1 the copy stream behind their leaves, 2 a stream
+                                       of their own (default) */
 #define CV_OPT_COUNT 23
 int cv_set_option(cv_ctx *ctx, int option, int64_t value);
 int cv_get_option(cv_ctx *ctx, int option, int64_t *value);

@@ -154,7 +154,7 @@ def test_verify_transactions_c3_shaped(engine, oracle_c, mstream):
     with a mutated leaf, one in 32 with a bad signature; tx_ok equals the expectation and the ids the claimed
     ids wherever the leaves are intact — synchronous (the last call also timed on the GPU), and three async calls in
     flight; the expectation itself is the C oracle's on the first 3,000 transactions.  mstream: the stream the
-    Merkle groups run on (CV_OPT_TXS_MERKLE_STREAM: the compute streams, the copy stream, their own)."""
+    Merkle groups run on (CV_OPT_TXS_MERKLE_STREAM: the compute streams, the copy stream, their own — the default)."""
     saved = engine.get_option("txs_merkle_stream")
     engine.set_option("txs_merkle_stream", mstream)
     try:
