@@ -354,24 +354,32 @@ def host_c3_fused_rate(eng, local, sh, ntx: int, steps: int, device_value: float
         return ok_all & check(ok, rest[0])
 
     def run_steady(k_steps):
-        """A node's loop in steady state: call 0 (the pipeline's fill: its first Merkle groups' copies and the
-        binding's checks before anything runs) completes before the clock starts, with call 1 already in flight;
-        the clock then covers calls 1..K, each submitted before the previous one is taken, the last one's tail
-        included.  Returns (ok, seconds)."""
-        pend = [eng.verify_transactions_async(*args, ids=bufs[0], want_status=False),
-                eng.verify_transactions_async(*args, ids=bufs[1], want_status=False)]
-        ok, rest = eng.wait(pend.pop(0))
-        ok_all = check(ok, rest[0])
-        t0 = time.perf_counter()
-        for k in range(2, k_steps + 1):
-            pend.append(eng.verify_transactions_async(*args, ids=bufs[k % 3], want_status=False))
+        """A node's loop in steady state: the clock runs from the completion of call 1 to the completion of call
+        K + 1, and at both ends the loop is in the same state — the next call already submitted, nothing else in
+        flight — so the clock covers exactly K calls' share of a continuous loop (call 0, the pipeline's fill: the
+        binding's checks and its first Merkle groups' copies before anything runs, is outside; so is the drain of
+        call K + 2).  Returns (ok, seconds)."""
+        def submit(k):
+            return eng.verify_transactions_async(*args, ids=bufs[k % 3], want_status=False)
+
+        def finish(tk):
             tw = time.perf_counter()
-            ok, rest = eng.wait(pend.pop(0))
+            ok, rest = eng.wait(tk)
             blocked["wait_ms"] += (time.perf_counter() - tw) * 1e3
-            ok_all &= check(ok, rest[0])
-        ok, rest = eng.wait(pend.pop(0))
-        dt = time.perf_counter() - t0
-        return ok_all & check(ok, rest[0]), dt
+            return check(ok, rest[0])
+
+        pend = [submit(0), submit(1)]
+        ok_all = finish(pend.pop(0))
+        pend.append(submit(2))
+        ok_all &= finish(pend.pop(0))            # call 1 done, call 2 in flight: the clock starts
+        blocked["wait_ms"] = 0.0
+        t0 = time.perf_counter()
+        for k in range(3, k_steps + 3):          # submit calls 3 .. K + 2, take calls 2 .. K + 1
+            pend.append(submit(k))
+            ok_all &= finish(pend.pop(0))
+        dt = time.perf_counter() - t0            # call K + 1 done, call K + 2 in flight: the clock stops
+        ok_all &= finish(pend.pop(0))
+        return ok_all, dt
 
     # warm: staging, device blocks, and every one of the device's four call outputs (one per fused call, where
     # the separate form uses two per step; an output sized by smaller calls grows — a device-wide free — on
@@ -387,7 +395,6 @@ def host_c3_fused_rate(eng, local, sh, ntx: int, steps: int, device_value: float
         # the value: the loop's steady state (the K calls above include the first call's fill, reported beside it:
         # in the kernel trace of such a loop the GPU idles ~25 ms before and inside the first call, then not at all,
         # profiles/r06o_fused_trace_concurrency.txt)
-        blocked["wait_ms"] = 0.0
         ok, dt = run_steady(steps)
         assert ok, f"fused C3 step (steady state) rejected an honest transaction: {fails}"
     # where a fused call's time goes: two synchronous calls timed on the GPU (CV_OPT_TIMELINE:

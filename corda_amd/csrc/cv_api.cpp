@@ -2301,7 +2301,12 @@ struct MerkleIn {
     const uint32_t *len;
     const uint32_t *txb;   // ntx + 1 absolute leaf indices
     uint8_t *ids, *status;
+    uint64_t arena_bytes = UINT64_MAX;   // the caller's arena size (the _bounded / _ex entry points), else unbounded
 };
+// a Merkle stage's leaves inside the caller's arena (and none wrapping), checked before anything reads them
+static bool mstage_in_bounds(const MStage &st, uint64_t arena_bytes) {
+    return st.extent != UINT64_MAX && st.extent <= arena_bytes;
+}
 static int merkle_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_t t0, size_t t1, const MerkleIn &in,
                           int threads) {
     const size_t nt = t1 - t0;
@@ -2368,7 +2373,7 @@ static int merkle_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, si
         const size_t c0 = cut[j], c1 = cut[j + 1];
         double ta = now_s();
         const MStage st = mstage_plan(c0, c1, in.txb, in.off, in.len, pool);
-        if (st.extent == UINT64_MAX) return CV_E_ARGS;   // a leaf's off + len wraps
+        if (!mstage_in_bounds(st, in.arena_bytes)) return CV_E_ARGS;   // past the arena, or a leaf's off + len wraps
         const bool direct = mstage_direct(st, in.txb, in.arena, in.off, in.len);
         double tb = now_s();
         f.t[0] += tb - ta;
@@ -2657,7 +2662,7 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
     for (size_t J = 0; J < nm; J++) {
         double ta = now_s();
         const MStage st = mstage_plan(mcut[J], mcut[J + 1], mi.txb, mi.off, mi.len, pool);
-        if (st.extent == UINT64_MAX) return CV_E_ARGS;   // a leaf's off + len wraps
+        if (!mstage_in_bounds(st, mi.arena_bytes)) return CV_E_ARGS;   // past the arena, or a leaf's off + len wraps
         const bool direct = mstage_direct(st, mi.txb, mi.arena, mi.off, mi.len);
         double tb = now_s();
         f.t[0] += tb - ta;
@@ -3081,7 +3086,7 @@ int cv_ed25519_sign_batch(cv_ctx *ctx, size_t n, const uint8_t *seed, const uint
 // ---------------------------------------------------------------- Merkle (host buffers)
 static int merkle_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
                        const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, uint8_t *ids, uint8_t *tx_status,
-                       uint64_t *ticket) {
+                       uint64_t *ticket, uint64_t arena_bytes = UINT64_MAX) {
     if (!ctx) return CV_E_ARGS;
     if (ticket) *ticket = 0;
     if (ntx == 0) return CV_OK;
@@ -3097,7 +3102,7 @@ static int merkle_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const
     // leaves — transaction counts scaled so each device gets ~1/k of the leaves (C3: uniform)
     o.shard_min = std::max<size_t>(1, o.shard_min / 8);          // ~4,096 signatures' worth of transactions
     o.spread_min = std::max<size_t>(1, o.spread_min / 8);
-    MerkleIn in{leaf_arena, leaf_off, leaf_len, tx_leaf_begin, ids, tx_status};
+    MerkleIn in{leaf_arena, leaf_off, leaf_len, tx_leaf_begin, ids, tx_status, arena_bytes};
     {
         std::lock_guard<std::mutex> g(ctx->st_mu);
         ctx->stats.merkle_calls++;
@@ -3113,7 +3118,7 @@ static int merkle_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const
         if (!ticket && nlv * 12 + (t1 - t0) * 4 <= kMerkleSmall) {
             WorkerPool *pool = &d.workers(threads);
             const MStage st = mstage_plan(t0, t1, tx_leaf_begin, leaf_off, leaf_len, pool);
-            if (st.extent == UINT64_MAX) return CV_E_ARGS;   // a leaf's off + len wraps
+            if (!mstage_in_bounds(st, in.arena_bytes)) return CV_E_ARGS;   // past the arena, or off + len wraps
             if (st.total <= kMerkleSmall) return merkle_shard_small(d, st, in, pool);
         }
         int k = 0, r = CV_OK;
@@ -3154,6 +3159,13 @@ int cv_merkle_tx_ids_async(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, c
 int cv_merkle_tx_ids(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
                      const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, uint8_t *ids) {
     return merkle_call(ctx, ntx, leaf_arena, leaf_off, leaf_len, tx_leaf_begin, ids, nullptr, nullptr);
+}
+
+int cv_merkle_tx_ids_bounded(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, uint64_t leaf_arena_bytes,
+                             const uint64_t *leaf_off, const uint32_t *leaf_len, const uint32_t *tx_leaf_begin,
+                             uint8_t *ids, uint8_t *tx_status, uint64_t *ticket) {
+    return merkle_call(ctx, ntx, leaf_arena, leaf_off, leaf_len, tx_leaf_begin, ids, tx_status, ticket,
+                       leaf_arena_bytes);
 }
 
 // One shard of a small synchronous transaction call (a notary's or a resolve chain's batch: staging up to
@@ -3224,7 +3236,7 @@ static int txs_shard_small(Device &d, const Opts &o, const MStage &st, const TxI
 static int txs_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const uint64_t *leaf_off,
                     const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, const uint8_t *pk, const uint8_t *sig,
                     const uint32_t *tx_sig_begin, uint8_t *ids, uint8_t *tx_status, uint8_t *sig_status, uint8_t *tx_ok,
-                    uint64_t *ticket) {
+                    uint64_t *ticket, uint64_t arena_bytes = UINT64_MAX) {
     if (!ctx) return CV_E_ARGS;
     if (ticket) *ticket = 0;
     if (ntx == 0) return CV_OK;
@@ -3240,8 +3252,8 @@ static int txs_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const ui
     // shards of whole transactions, scaled as merkle_call's (~4,096 signatures' worth at C3's 8 per transaction)
     o.shard_min = std::max<size_t>(1, o.shard_min / 8);
     o.spread_min = std::max<size_t>(1, o.spread_min / 8);
-    TxIn in{{leaf_arena, leaf_off, leaf_len, tx_leaf_begin, ids, tx_status}, pk, sig, tx_sig_begin, sig_status, tx_ok,
-            now_s()};
+    TxIn in{{leaf_arena, leaf_off, leaf_len, tx_leaf_begin, ids, tx_status, arena_bytes}, pk, sig, tx_sig_begin, sig_status,
+            tx_ok, now_s()};
     {
         std::lock_guard<std::mutex> g(ctx->st_mu);
         ctx->stats.merkle_calls++;
@@ -3257,7 +3269,7 @@ static int txs_call(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, const ui
         if (!ticket && nlv * 12 + (t1 - t0) * 4 + ns * 96 <= kMerkleSmall) {
             WorkerPool *pool = &d.workers(threads);
             const MStage st = mstage_plan(t0, t1, tx_leaf_begin, leaf_off, leaf_len, pool);
-            if (st.extent == UINT64_MAX) return CV_E_ARGS;   // a leaf's off + len wraps
+            if (!mstage_in_bounds(st, in.m.arena_bytes)) return CV_E_ARGS;   // past the arena, or off + len wraps
             if (st.total + ns * 96 <= kMerkleSmall) return txs_shard_small(d, o, st, in, pool);
         }
         int k = 0, r = CV_OK;
@@ -3303,6 +3315,14 @@ int cv_verify_transactions_async(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_ar
     if (!ticket) return CV_E_ARGS;
     return txs_call(ctx, ntx, leaf_arena, leaf_off, leaf_len, tx_leaf_begin, pk, sig, tx_sig_begin, ids, tx_status,
                     sig_status, tx_ok, ticket);
+}
+
+int cv_verify_transactions_ex(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, uint64_t leaf_arena_bytes,
+                              const uint64_t *leaf_off, const uint32_t *leaf_len, const uint32_t *tx_leaf_begin,
+                              const uint8_t *pk, const uint8_t *sig, const uint32_t *tx_sig_begin, uint8_t *ids,
+                              uint8_t *tx_status, uint8_t *sig_status, uint8_t *tx_ok, uint64_t *ticket) {
+    return txs_call(ctx, ntx, leaf_arena, leaf_off, leaf_len, tx_leaf_begin, pk, sig, tx_sig_begin, ids, tx_status,
+                    sig_status, tx_ok, ticket, leaf_arena_bytes);
 }
 
 int cv_partial_merkle_verify(cv_ctx *ctx, size_t ntrees, size_t nnodes, const uint8_t *kind, const uint32_t *left,

@@ -33,7 +33,7 @@ EXPORTED = (
     "cv_diag_dedupe_keys", "cv_host_alloc", "cv_host_free", "cv_ed25519_verify_batch_async", "cv_wait",
     "cv_merkle_tx_ids_async", "cv_set_option", "cv_get_option", "cv_diag_stats",
     "cv_verify_transactions", "cv_verify_transactions_async", "cv_open_ex", "cv_msg_extent",
-    "cv_ed25519_verify_batch_ex",
+    "cv_ed25519_verify_batch_ex", "cv_merkle_tx_ids_bounded", "cv_verify_transactions_ex",
 )
 
 # cv_set_option names (include/cordaverify.h CV_OPT_*)
@@ -98,6 +98,12 @@ def load():
         lib.cv_verify_transactions.argtypes = [_vp, _sz] + [_vp] * 11
         lib.cv_verify_transactions.restype = ctypes.c_int
         lib.cv_verify_transactions_async.argtypes = [_vp, _sz] + [_vp] * 11 + [ctypes.POINTER(ctypes.c_uint64)]
+        lib.cv_verify_transactions_ex.argtypes = [_vp, _sz, _vp, ctypes.c_uint64] + [_vp] * 10 + \
+            [ctypes.POINTER(ctypes.c_uint64)]
+        lib.cv_verify_transactions_ex.restype = ctypes.c_int
+        lib.cv_merkle_tx_ids_bounded.argtypes = [_vp, _sz, _vp, ctypes.c_uint64] + [_vp] * 5 + \
+            [ctypes.POINTER(ctypes.c_uint64)]
+        lib.cv_merkle_tx_ids_bounded.restype = ctypes.c_int
         lib.cv_verify_transactions_async.restype = ctypes.c_int
         lib.cv_set_option.argtypes = [_vp, ctypes.c_int, ctypes.c_int64]
         lib.cv_set_option.restype = ctypes.c_int
@@ -367,7 +373,9 @@ class Engine:
         return pk, sig
 
     @staticmethod
-    def _merkle_args(arena, leaf_off, leaf_len, tx_leaf_begin):
+    def _merkle_args(arena, leaf_off, leaf_len, tx_leaf_begin, scan: bool = False):
+        """The leaf arrays as the library takes them.  scan: also check the leaves against the arena here (the
+        bounded entry points check it in the engine's own staging scan; this is their error path)."""
         tx_leaf_begin = np.ascontiguousarray(tx_leaf_begin, dtype=np.uint32)
         ntx = tx_leaf_begin.shape[0] - 1
         arena = _u8(arena) if arena is not None and np.asarray(arena).size else np.zeros(16, np.uint8)
@@ -378,10 +386,17 @@ class Engine:
             leaf_len = np.zeros(1, np.uint32)
         if leaf_off.shape[0] != leaf_len.shape[0] or (ntx > 0 and int(tx_leaf_begin[-1]) > leaf_off.shape[0]):
             raise ValueError("tx_leaf_begin reaches past the leaf arrays")
-        if ntx > 0 and int(tx_leaf_begin[-1]) and _msg_end(load(), leaf_off[:int(tx_leaf_begin[-1])],
-                                                           leaf_len[:int(tx_leaf_begin[-1])]) > arena.size:
+        if scan and ntx > 0 and int(tx_leaf_begin[-1]) and _msg_end(load(), leaf_off[:int(tx_leaf_begin[-1])],
+                                                                    leaf_len[:int(tx_leaf_begin[-1])]) > arena.size:
             raise ValueError("leaf range exceeds the arena")
         return ntx, arena, leaf_off, leaf_len, tx_leaf_begin
+
+    def _bounded_rc(self, rc: int, what: str, leaves):
+        """A bounded call's return code: CV_E_ARGS from leaves past the arena (or wrapping) as ValueError, as
+        the binding raised it when it scanned the leaves itself; any other error as CvError."""
+        if rc == -3:
+            self._merkle_args(*leaves, scan=True)   # raises ValueError for leaves past the arena
+        _check(rc, what)
 
     def merkle_tx_ids(self, arena, leaf_off, leaf_len, tx_leaf_begin, ids=None) -> Tuple[np.ndarray, np.ndarray]:
         """WireTransaction.id of every transaction -> (ids (ntx,32) u8, status u8[ntx]).  ids: an optional
@@ -389,8 +404,10 @@ class Engine:
         ntx, arena, leaf_off, leaf_len, tx_leaf_begin = self._merkle_args(arena, leaf_off, leaf_len, tx_leaf_begin)
         ids = _ids_out(ids, max(ntx, 0))
         st = np.zeros(max(ntx, 0), np.uint8)
-        _check(self._lib.cv_merkle_tx_ids_ex(self._h, ntx, _p(arena), _p(leaf_off), _p(leaf_len),
-                                             _p(tx_leaf_begin), _p(ids), _p(st)), "cv_merkle_tx_ids_ex")
+        # the leaf-arena bound is checked by the engine's staging scan (cv_merkle_tx_ids_bounded)
+        rc = self._lib.cv_merkle_tx_ids_bounded(self._h, ntx, _p(arena), arena.size, _p(leaf_off), _p(leaf_len),
+                                                _p(tx_leaf_begin), _p(ids), _p(st), None)
+        self._bounded_rc(rc, "cv_merkle_tx_ids_bounded", (arena, leaf_off, leaf_len, tx_leaf_begin))
         return ids, st
 
     def merkle_tx_ids_async(self, arena, leaf_off, leaf_len, tx_leaf_begin, ids=None) -> int:
@@ -399,9 +416,9 @@ class Engine:
         ids = _ids_out(ids, max(ntx, 0))
         st = np.zeros(max(ntx, 0), np.uint8)
         t = ctypes.c_uint64()
-        _check(self._lib.cv_merkle_tx_ids_async(self._h, ntx, _p(arena), _p(leaf_off), _p(leaf_len),
-                                                _p(tx_leaf_begin), _p(ids), _p(st), ctypes.byref(t)),
-               "cv_merkle_tx_ids_async")
+        rc = self._lib.cv_merkle_tx_ids_bounded(self._h, ntx, _p(arena), arena.size, _p(leaf_off), _p(leaf_len),
+                                                _p(tx_leaf_begin), _p(ids), _p(st), ctypes.byref(t))
+        self._bounded_rc(rc, "cv_merkle_tx_ids_bounded", (arena, leaf_off, leaf_len, tx_leaf_begin))
         with self.mu:
             self._inflight[t.value] = (ids, st, (arena, leaf_off, leaf_len, tx_leaf_begin))
         return t.value
@@ -424,17 +441,18 @@ class Engine:
         st = np.zeros(ntx, np.uint8) if want_status else None
         sst = np.zeros(nsig, np.uint8) if want_sig_status else None
         ok = np.zeros(ntx, np.uint8)
-        args = (ntx, _p(arena), _p(leaf_off), _p(leaf_len), _p(tx_leaf_begin), _p(pk), _p(sig), _p(tx_sig_begin),
-                _p(ids), _p(st), _p(sst), _p(ok))
+        args = (ntx, _p(arena), arena.size, _p(leaf_off), _p(leaf_len), _p(tx_leaf_begin), _p(pk), _p(sig),
+                _p(tx_sig_begin), _p(ids), _p(st), _p(sst), _p(ok))
         return args, (ok, ids, st, sst), (arena, leaf_off, leaf_len, tx_leaf_begin, pk, sig, tx_sig_begin)
 
     def verify_transactions(self, arena, leaf_off, leaf_len, tx_leaf_begin, pk, sig, tx_sig_begin, ids=None,
                             want_status: bool = True, want_sig_status: bool = False):
         """cv_verify_transactions (SignedTransaction.verifySignatures' id + signature checks for a batch) ->
         (tx_ok u8[ntx], ids (ntx,32) u8, tx_status u8[ntx] or None, sig_status u8[nsig] or None)."""
-        args, out, _keep = self._tx_args(arena, leaf_off, leaf_len, tx_leaf_begin, pk, sig, tx_sig_begin, ids,
-                                         want_status, want_sig_status)
-        _check(self._lib.cv_verify_transactions(self._h, *args), "cv_verify_transactions")
+        args, out, keep = self._tx_args(arena, leaf_off, leaf_len, tx_leaf_begin, pk, sig, tx_sig_begin, ids,
+                                        want_status, want_sig_status)
+        rc = self._lib.cv_verify_transactions_ex(self._h, *args, None)
+        self._bounded_rc(rc, "cv_verify_transactions_ex", keep[:4])
         return out
 
     def verify_transactions_async(self, arena, leaf_off, leaf_len, tx_leaf_begin, pk, sig, tx_sig_begin, ids=None,
@@ -444,7 +462,8 @@ class Engine:
         args, out, keep = self._tx_args(arena, leaf_off, leaf_len, tx_leaf_begin, pk, sig, tx_sig_begin, ids,
                                         want_status, want_sig_status)
         t = ctypes.c_uint64()
-        _check(self._lib.cv_verify_transactions_async(self._h, *args, ctypes.byref(t)), "cv_verify_transactions_async")
+        rc = self._lib.cv_verify_transactions_ex(self._h, *args, ctypes.byref(t))
+        self._bounded_rc(rc, "cv_verify_transactions_ex", keep[:4])
         with self.mu:
             self._inflight[t.value] = (out[0], out[1:], keep)
         return t.value

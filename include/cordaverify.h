@@ -169,6 +169,15 @@ int cv_merkle_tx_ids_async(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, c
                            const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, uint8_t *ids, uint8_t *tx_status,
                            uint64_t *ticket);
 
+/* cv_merkle_tx_ids_ex (ticket NULL) or cv_merkle_tx_ids_async (ticket non-NULL) with the leaf arena's size: a call
+ * whose leaves reach past leaf_arena[leaf_arena_bytes) (or whose off + len wraps) returns CV_E_ARGS before the
+ * engine reads past it — the check rides on the staging scan of each sub-chunk's leaves, so a binding needs no
+ * scan of its own (6M leaves: ~10 ms of host time per call).  With a ticket, leaves past the bound in a later
+ * sub-chunk may be found after earlier ones were enqueued: the call then waits for those before returning. */
+int cv_merkle_tx_ids_bounded(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, uint64_t leaf_arena_bytes,
+                             const uint64_t *leaf_off, const uint32_t *leaf_len, const uint32_t *tx_leaf_begin,
+                             uint8_t *ids, uint8_t *tx_status, uint64_t *ticket);
+
 /* Partial Merkle trees (FilteredTransaction / PartialMerkleTree.verify), one verdict per tree.
  * The shim flattens each PartialTree object in post-order and concatenates the trees: node k has
  * kind[k] (CV_PMT_LEAF 0 = PartialTree.Leaf, CV_PMT_INCLUDED 1 = IncludedLeaf, CV_PMT_NODE 2 = Node),
@@ -220,6 +229,12 @@ int cv_verify_transactions_async(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_ar
                                  const uint32_t *leaf_len, const uint32_t *tx_leaf_begin, const uint8_t *pk,
                                  const uint8_t *sig, const uint32_t *tx_sig_begin, uint8_t *ids, uint8_t *tx_status,
                                  uint8_t *sig_status, uint8_t *tx_ok, uint64_t *ticket);
+/* cv_verify_transactions (ticket NULL) or its _async form (ticket non-NULL) with the leaf arena's size, bounded as
+ * cv_merkle_tx_ids_bounded: leaves past leaf_arena[leaf_arena_bytes) or wrapping give CV_E_ARGS before any read. */
+int cv_verify_transactions_ex(cv_ctx *ctx, size_t ntx, const uint8_t *leaf_arena, uint64_t leaf_arena_bytes,
+                              const uint64_t *leaf_off, const uint32_t *leaf_len, const uint32_t *tx_leaf_begin,
+                              const uint8_t *pk, const uint8_t *sig, const uint32_t *tx_sig_begin, uint8_t *ids,
+                              uint8_t *tx_status, uint8_t *sig_status, uint8_t *tx_ok, uint64_t *ticket);
 
 /* ---------------------------------------------------------------- device-resident API
  * All pointers are device pointers on HIP device `device` (which must be in the context); work is

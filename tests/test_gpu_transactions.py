@@ -215,3 +215,55 @@ def _c3_shaped(engine, oracle_c):
         ok, (ids, st, _) = engine.wait(t)
         assert np.array_equal(ok.astype(bool), expect)
         assert np.array_equal((ids == claimed).all(axis=1), intact) and (st == 0).all()
+
+
+@pytest.mark.parametrize("ntx", [40, 30_000])
+def test_leaf_arena_bound(engine, oracle_c, corpus, ntx):
+    """cv_merkle_tx_ids_bounded / cv_verify_transactions_ex: the engine bounds the leaves by the caller's arena size in
+    its own staging scan (the binding no longer scans 12 B per leaf before every call).  At the exact extent the
+    results equal the unbounded calls'; one byte short, and with a leaf whose off + len wraps, every form returns
+    CV_E_ARGS (small one-DMA shards at 40 transactions, the pipeline at 30,000, synchronous and with a ticket), and the
+    binding raises ValueError; the engine stays exact afterwards."""
+    import ctypes
+    leaves, sigs, ref, _ = _tx_case(engine, oracle_c, corpus, 7100 + ntx, ntx)
+    arena, off, lens, begin = leaves
+    pk, sig, tsb = sigs
+    ids_ref, st_ref, _, ok_ref = ref
+    lib, p = native.load(), native._p
+    extent = int((off + lens.astype(np.uint64)).max())
+    for async_ in (False, True):
+        for bound, want in ((extent, 0), (extent - 1, -3)):
+            t = ctypes.c_uint64()
+            tk = ctypes.byref(t) if async_ else None
+            ids = np.zeros((ntx, 32), np.uint8)
+            st = np.zeros(ntx, np.uint8)
+            ok = np.zeros(ntx, np.uint8)
+            rc = lib.cv_merkle_tx_ids_bounded(engine._h, ntx, p(arena), bound, p(off), p(lens), p(begin), p(ids), p(st),
+                                              tk)
+            assert rc == want, ("merkle", async_, bound, rc)
+            if rc == 0 and async_:
+                assert lib.cv_wait(engine._h, t.value) == 0
+            if rc == 0:
+                assert np.array_equal(ids, ids_ref) and np.array_equal(st, st_ref)
+            rc = lib.cv_verify_transactions_ex(engine._h, ntx, p(arena), bound, p(off), p(lens), p(begin), p(pk), p(sig),
+                                               p(tsb), p(ids), p(st), None, p(ok), tk)
+            assert rc == want, ("txs", async_, bound, rc)
+            if rc == 0 and async_:
+                assert lib.cv_wait(engine._h, t.value) == 0
+            if rc == 0:
+                assert np.array_equal(ok, ok_ref) and np.array_equal(ids, ids_ref)
+    with pytest.raises(ValueError, match="exceeds the arena"):
+        engine.verify_transactions(arena[:extent - 1], off, lens, begin, pk, sig, tsb)
+    with pytest.raises(ValueError, match="exceeds the arena"):
+        engine.merkle_tx_ids(arena[:extent - 1], off, lens, begin)
+    wrap_off, wrap_len = off.copy(), lens.copy()
+    last = int(begin[-1]) - 1
+    wrap_off[last], wrap_len[last] = np.uint64(2 ** 64 - 8), 32
+    for bound in (arena.size, 2 ** 64 - 1):
+        rc = lib.cv_verify_transactions_ex(engine._h, ntx, p(arena), bound, p(wrap_off), p(wrap_len), p(begin), p(pk),
+                                           p(sig), p(tsb), None, None, None, p(np.zeros(ntx, np.uint8)), None)
+        assert rc == -3, bound
+    with pytest.raises(ValueError, match="exceeds the arena"):
+        engine.verify_transactions_async(arena, wrap_off, wrap_len, begin, pk, sig, tsb)
+    ok, ids, st, _ = engine.verify_transactions(arena, off, lens, begin, pk, sig, tsb)
+    assert np.array_equal(ok, ok_ref) and np.array_equal(ids, ids_ref) and np.array_equal(st, st_ref)
