@@ -171,29 +171,24 @@ def host_api_rate(eng, batch, steps: int, device_value: float, name: str, async_
                 eng.wait(pend.pop(0))
         for tk in pend:
             eng.wait(tk)
-        t = time.perf_counter()
-        pend = []
-        for _ in range(asteps):
-            pend.append(eng.verify_batch_async(*a, want_status=False))
-            if len(pend) == 2:
-                bm, _ = eng.wait(pend.pop(0))
-        for tk in pend:
-            bm, _ = eng.wait(tk)
-        dt_cold = time.perf_counter() - t
-        assert native.bitmap_to_bools(bm, n).all(), "async host API rejected an honest signature"
-        # steady state of the loop (as host_c3_fused_rate's run_steady): the clock runs between the completions of
-        # call 1 and call K + 1, each end with the next call submitted and nothing else in flight
-        pend = [eng.verify_batch_async(*a, want_status=False) for _ in range(2)]
-        eng.wait(pend.pop(0))
-        pend.append(eng.verify_batch_async(*a, want_status=False))
-        eng.wait(pend.pop(0))
-        t = time.perf_counter()
-        for _ in range(asteps):
-            pend.append(eng.verify_batch_async(*a, want_status=False))
-            bm, _ = eng.wait(pend.pop(0))
-        dt = time.perf_counter() - t
-        eng.wait(pend.pop(0))
-        assert native.bitmap_to_bools(bm, n).all(), "async host API rejected an honest signature"
+
+        def loop(k):
+            t = time.perf_counter()
+            pend = []
+            for _ in range(k):
+                pend.append(eng.verify_batch_async(*a, want_status=False))
+                if len(pend) == 2:
+                    bm, _ = eng.wait(pend.pop(0))
+            for tk in pend:
+                bm, _ = eng.wait(tk)
+            assert native.bitmap_to_bools(bm, n).all(), "async host API rejected an honest signature"
+            return time.perf_counter() - t
+
+        dt_cold = loop(asteps)
+        # the loop's steady state (as host_c3_fused_rate's): T(K + 2 calls) - T(2 calls), the first call's ramp and
+        # the last one's drain cancelling
+        t2 = loop(2)
+        dt = loop(asteps + 2) - t2
         return dt, dt_cold
 
     dt_page = timed((pk, sig, arena, off, ln))
@@ -224,7 +219,7 @@ def host_api_rate(eng, batch, steps: int, device_value: float, name: str, async_
     va = n * asteps / dt_async_page
     return {"workload": name, "value": v, "unit": "verifies/s", "ms_per_step": dt_async / asteps * 1e3, "steps": asteps,
             "cold_ms_per_step": dt_async_cold / asteps * 1e3,
-            "timing": "steady state: K calls between two completions, the next call in flight at both ends",
+            "timing": "steady state: T(K + 2 calls) - T(2 calls), two in flight (ramp and drain cancel)",
             "sigs": n, "ratio_to_device_value": v / device_value, "device_value": device_value,
             "input_bytes_per_call": in_bytes, "input_gb_per_s": in_bytes * asteps / dt_async / 1e9,
             "path": "cv_ed25519_verify_batch_async from pinned host buffers (cv_host_alloc), two calls in flight "
@@ -368,34 +363,6 @@ def host_c3_fused_rate(eng, local, sh, ntx: int, steps: int, device_value: float
         ok, rest = eng.wait(prev)
         return ok_all & check(ok, rest[0])
 
-    def run_steady(k_steps):
-        """A node's loop in steady state: the clock runs from the completion of call 1 to the completion of call
-        K + 1, and at both ends the loop is in the same state — the next call already submitted, nothing else in
-        flight — so the clock covers exactly K calls' share of a continuous loop (call 0, the pipeline's fill: the
-        binding's checks and its first Merkle groups' copies before anything runs, is outside; so is the drain of
-        call K + 2).  Returns (ok, seconds)."""
-        def submit(k):
-            return eng.verify_transactions_async(*args, ids=bufs[k % 3], want_status=False)
-
-        def finish(tk):
-            tw = time.perf_counter()
-            ok, rest = eng.wait(tk)
-            blocked["wait_ms"] += (time.perf_counter() - tw) * 1e3
-            return check(ok, rest[0])
-
-        pend = [submit(0), submit(1)]
-        ok_all = finish(pend.pop(0))
-        pend.append(submit(2))
-        ok_all &= finish(pend.pop(0))            # call 1 done, call 2 in flight: the clock starts
-        blocked["wait_ms"] = 0.0
-        t0 = time.perf_counter()
-        for k in range(3, k_steps + 3):          # submit calls 3 .. K + 2, take calls 2 .. K + 1
-            pend.append(submit(k))
-            ok_all &= finish(pend.pop(0))
-        dt = time.perf_counter() - t0            # call K + 1 done, call K + 2 in flight: the clock stops
-        ok_all &= finish(pend.pop(0))
-        return ok_all, dt
-
     # warm: staging, device blocks, and every one of the device's four call outputs (one per fused call, where
     # the separate form uses two per step; an output sized by smaller calls grows — a device-wide free — on
     # first use: 93 ms for the first timed fused steps after the separate ones against 87 ms once warm,
@@ -407,10 +374,17 @@ def host_c3_fused_rate(eng, local, sh, ntx: int, steps: int, device_value: float
     dt_cold = dt = time.perf_counter() - t
     assert ok, f"fused C3 step rejected an honest transaction: {fails}"
     if not sync:
-        # the value: the loop's steady state (the K calls above include the first call's fill, reported beside it:
-        # in the kernel trace of such a loop the GPU idles ~25 ms before and inside the first call, then not at all,
-        # profiles/r06o_fused_trace_concurrency.txt)
-        ok, dt = run_steady(steps)
+        # the value: the loop's steady state.  The K calls above include the first call's fill and the last one's
+        # drain (in the kernel trace of such a loop the GPU idles ~25 ms before and inside the first call, then not
+        # at all, profiles/r06o_fused_trace_concurrency.txt); both are the same for a loop of 2 calls and one of
+        # K + 2, so the difference of the two loops' times is K calls of a loop that runs continuously
+        t = time.perf_counter()
+        ok = run(2)
+        t2 = time.perf_counter() - t
+        blocked["wait_ms"] = 0.0
+        t = time.perf_counter()
+        ok &= run(steps + 2)
+        dt = time.perf_counter() - t - t2
         assert ok, f"fused C3 step (steady state) rejected an honest transaction: {fails}"
     # where a fused call's time goes: two synchronous calls timed on the GPU (CV_OPT_TIMELINE:
     # per launch group, Merkle and verify groups apart), outside the timed loop
@@ -434,7 +408,7 @@ def host_c3_fused_rate(eng, local, sh, ntx: int, steps: int, device_value: float
     return {"value": v, "unit": "verifies/s", "tx_ids_per_s": ntx * steps / dt, "ms_per_step": dt / steps * 1e3,
             "cold_ms_per_step": dt_cold / steps * 1e3,
             "timing": "synchronous calls" if sync else
-                      "steady state: K calls after the first one's fill, each submitted before the previous is taken",
+                      "steady state: T(K + 2 calls) - T(2 calls), two in flight (fill and drain cancel)",
             "steps": steps, "ratio_to_device_value": v / device_value, "device_value": device_value,
             "input_bytes_per_step": in_bytes, "pcie_floor_ms_per_step": in_bytes / (pcie_gbs * 1e9) * 1e3,
             "host_blocked_ms_per_step": {k: v / steps for k, v in blocked.items()}, "breakdown": breakdown,
@@ -1360,7 +1334,7 @@ def main():
                                                        "sync_call_ms")}
                 h["c3_fused"]["pcie_floor_ms_per_step"] = r3(H["c3_fused"]["pcie_floor_ms_per_step"])
                 h["c3_fused"]["cold_ms_per_step"] = r3(H["c3_fused"]["cold_ms_per_step"])
-                h["c3_fused"]["timing"] = "steady state (first call's fill outside the clock; cold_ms_per_step with it)"
+                h["c3_fused"]["timing"] = "steady state, T(K+2 calls) - T(2 calls); cold_ms_per_step: K calls from idle"
             if "keyed" in H:
                 h["keyed"]["pcie_bound_value"] = r3(H["keyed"]["pcie_bound_value"])
                 h["keyed"]["ratio_to_pcie_bound"] = r3(H["keyed"]["ratio_to_pcie_bound"])

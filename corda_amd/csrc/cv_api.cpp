@@ -2657,8 +2657,16 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
         }
         return CV_OK;
     };
-    // Merkle group J goes one step ahead of the signature groups of sub-chunk J - 1, so on its stream it queues
-    // behind older signature groups only and has usually run by the time the groups that read its ids start
+    // On the compute streams, Merkle group J goes one step ahead of the signature groups of sub-chunk J - 1, so on
+    // its stream it queues behind older signature groups only and has usually run by the time the groups that read
+    // its ids start.  On a stream of its own it waits for nothing but its leaves, so the signature groups of
+    // sub-chunk J follow it directly: the call's first signature group no longer waits for a second Merkle group's
+    // copy (the loop's fill)
+#ifdef CV_TXS_LAG   // (A/B builds only)
+    const size_t lag = CV_TXS_LAG;
+#else
+    const size_t lag = mst ? 0 : 1;
+#endif
     for (size_t J = 0; J < nm; J++) {
         double ta = now_s();
         const MStage st = mstage_plan(mcut[J], mcut[J + 1], mi.txb, mi.off, mi.len, pool);
@@ -2710,7 +2718,7 @@ static int txs_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size_
         // (own stream: after launched()'s events, so a stream that waits for mev[J] also covers them)
         if (mst) CV_TRY(hipEventRecord(d.mev[J], s));
         f.t[3] += now_s() - ta;
-        if (J > 0 && (rc = emit_sigs(J - 1, false)) != CV_OK) return rc;
+        if (J >= lag && (rc = emit_sigs(J - lag, false)) != CV_OK) return rc;
     }
     if ((rc = emit_sigs(nm - 1, true)) != CV_OK) return rc;
     // ---- per-transaction verdicts, behind both streams' last groups
