@@ -456,7 +456,6 @@ static const OptDesc kOpt[CV_OPT_COUNT] = {
     {1, 1, 16},                         // CV_OPT_MID_PIECES
     {2, 2, 3},                          // CV_OPT_PIPE_SLOTS
     {2, 0, 2},                          // CV_OPT_TXS_MERKLE_STREAM
-    {0, 0, 1},                          // CV_OPT_PIPE_ROUND
 };
 
 // A snapshot of a context's options, taken once per call.
@@ -465,7 +464,7 @@ struct Opts {
     size_t pipe_min, pipe_first, pipe_chunk, async_chunk, small_direct_min, shard_min, spread_min, merkle_chunk;
     size_t prep_overlap_min;
     size_t pipe_split, mid_pieces, pipe_slots;
-    int txs_merkle_stream, pipe_round;
+    int txs_merkle_stream;
     int threads, small_zc, auto_keyed, timeline, pipe_overlap_first;
 };
 
@@ -666,7 +665,6 @@ struct cv_ctx {
         o.mid_pieces = (size_t)opt[CV_OPT_MID_PIECES].load();
         o.pipe_slots = (size_t)opt[CV_OPT_PIPE_SLOTS].load();
         o.txs_merkle_stream = (int)opt[CV_OPT_TXS_MERKLE_STREAM].load();
-        o.pipe_round = (int)opt[CV_OPT_PIPE_ROUND].load();
         return o;
     }
 };
@@ -2177,13 +2175,10 @@ static int pipe_enqueue(cv_ctx *ctx, Device &d, const Opts &o, PipeOut &po, size
     // (tools/sync_pipe_sweep.py, two rounds on one box): 262,144-record sub-chunks 13.0-13.3 ms, 98,304 12.0,
     // 65,536 11.6, 49,152 12.9, 32,768 13.3; an 8M C5 call is compute-bound and keeps 262,144 (74 ms).
     // (keyed calls keep pipe_chunk: each of their sub-chunks carries more fixed work)
-    size_t sch = keyed ? o.pipe_chunk
-                       : std::min(o.pipe_chunk, std::max(2 * o.pipe_first, (n / o.pipe_split + 63) / 64 * 64));
-    if (!keyed && o.pipe_round) {   // CV_OPT_PIPE_ROUND: whole CV_OPT_ASYNC_CHUNK units (rounds of resident waves)
-        const size_t unit = std::max<size_t>(64, o.async_chunk / 64 * 64);
-        const size_t want = std::max(2 * o.pipe_first, (n / o.pipe_split + 63) / 64 * 64);
-        if (want >= unit) sch = want / unit * unit;
-    }
+    // (sub-chunks in whole rounds of resident waves after the ramp, 196,608 or 393,216: 10.97-11.9 ms per call
+    // against 10.38 — fewer, larger sub-chunks leave a longer tail; profiles/r06t_sync_pipe_round_sweep.log)
+    const size_t sch = keyed ? o.pipe_chunk
+                             : std::min(o.pipe_chunk, std::max(2 * o.pipe_first, (n / o.pipe_split + 63) / 64 * 64));
     const std::vector<size_t> cut = async ? pipe_cuts(b, e, ach, ach, false) : pipe_cuts(b, e, o.pipe_first, sch, true);
     size_t max_m = 1;
     for (size_t j = 0; j + 1 < cut.size(); j++) max_m = std::max(max_m, cut[j + 1] - cut[j]);

@@ -42,8 +42,7 @@ OPTIONS = {"tri_max": 1, "quad_max": 2, "drain_split": 3, "drain_split_pct": 4, 
            "auto_keyed": 12, "shard_min": 13, "spread_min": 14, "merkle_chunk": 15,
            "prep_overlap_min": 16, "timeline": 17, "pipe_split": 18,
            "pipe_overlap_first": 19, "mid_pieces": 20,
-           "pipe_slots": 21, "txs_merkle_stream": 22,
-           "pipe_round": 23}
+           "pipe_slots": 21, "txs_merkle_stream": 22}
 STATS = {"pipe": (0, ("plan_s", "pack_s", "wait_s", "enqueue_s", "sync_s", "calls", "subchunks", "direct_subchunks")),
          "small": (1, ("setup_s", "pack_s", "launch_s", "sync_s", "assemble_s", "calls")),
          "route": (2, ("calls", "routed_whole", "split_calls", "shards", "keyed_shards", "keyed_subchunks",

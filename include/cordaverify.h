@@ -337,10 +337,7 @@ int cv_calibrate_cycles(cv_ctx *ctx, int device, double *out);
 #define CV_OPT_TXS_MERKLE_STREAM 22 /* cv_verify_transactions: the stream its Merkle groups run on — 0 the compute streams
                                        beside the signature groups, 1 the copy stream behind their leaves, 2 a stream
                                        of their own (default) */
-#define CV_OPT_PIPE_ROUND 23        /* synchronous pipelined calls: the sub-chunks after the ramp in whole CV_OPT_ASYNC_CHUNK
-                                       units (rounds of resident verify waves; CV_OPT_PIPE_CHUNK does not cap them):
-                                       1 on, 0 off (default) */
-#define CV_OPT_COUNT 24
+#define CV_OPT_COUNT 23
 int cv_set_option(cv_ctx *ctx, int option, int64_t value);
 int cv_get_option(cv_ctx *ctx, int option, int64_t *value);
 
