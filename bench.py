@@ -191,7 +191,13 @@ def host_api_rate(eng, batch, steps: int, device_value: float, name: str, async_
         dt = loop(asteps + 2) - t2
         return dt, dt_cold
 
+    eng.stats("pipe", reset=True)
     dt_page = timed((pk, sig, arena, off, ln))
+    pp = eng.stats("pipe")
+    # the pageable call's host phases per call (its packing of the records into pinned staging is the part the pinned
+    # form does not have: bound by the box's host memory bandwidth)
+    page_phases = {k[:-2] + "_ms": pp[k] / max(1.0, pp["calls"]) * 1e3 for k in ("plan_s", "pack_s", "wait_s", "enqueue_s",
+                                                                                 "sync_s")}
     pinned = tuple(eng.host_copy(x) for x in (pk, sig, arena, off, ln))
     eng.stats("pipe", reset=True)
     dt_pin = timed(pinned)
@@ -231,7 +237,7 @@ def host_api_rate(eng, batch, steps: int, device_value: float, name: str, async_
                                "ratio_to_device_value": va / device_value,
                                "path": "cv_ed25519_verify_batch_async from pageable numpy buffers, two in flight"},
             "pageable": {"value": vp, "ms_per_step": dt_page / steps * 1e3, "ratio_to_device_value": vp / device_value,
-                         "input_gb_per_s": in_bytes * steps / dt_page / 1e9,
+                         "input_gb_per_s": in_bytes * steps / dt_page / 1e9, "host_phases": page_phases,
                          "path": "cv_ed25519_verify_batch (synchronous) from pageable numpy buffers (host threads "
                                  "pack pinned staging per sub-chunk)"}}
 
@@ -1342,6 +1348,7 @@ def main():
                     h[k]["sync_pinned_ratio"] = r3(H[k]["sync_pinned"]["ratio_to_device_value"])
                     h[k]["sync_pinned_ms"] = r3(H[k]["sync_pinned"]["ms_per_step"])
                     h[k]["pageable_ratio"] = r3(H[k]["pageable"]["ratio_to_device_value"])
+                    h[k]["pageable_pack_ms"] = r3(H[k]["pageable"]["host_phases"]["pack_ms"])
             if "c2" in H:
                 h["c2"]["sync_breakdown"] = {k: r3(v) for k, v in H["c2"]["sync_pinned"]["breakdown"].items()}
             if "c3_fused" in H:
