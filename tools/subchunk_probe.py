@@ -4,7 +4,7 @@
   sub S      each call cut into sub-chunks of S records dealt alternately over two streams, as the synchronous
              pipeline deals its sub-chunks — once with a device synchronize after every call (the synchronous call's
              shape, tail included), once back to back (steady state)
-beside the synchronous host call itself from pinned buffers (cv_ed25519_verify_batch).  If the sub-chunked
+(--streams: over that many streams instead) beside the synchronous host call itself from pinned buffers (cv_ed25519_verify_batch).  If the sub-chunked
 device calls are as slow as the host call, its kernel time is the sub-chunk granularity, not the DMA.
 
     python tools/subchunk_probe.py [--sizes 62528,131072,196608] [--calls 8]
@@ -29,11 +29,12 @@ def main():
     ap.add_argument("--calls", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--host", type=int, default=1)
+    ap.add_argument("--streams", type=int, default=2)
     a = ap.parse_args()
     n = a.n
     eng = native.Engine(1)
     dev = torch.device("cuda", 0)
-    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    streams = [torch.cuda.Stream(dev) for _ in range(a.streams)]
     b = workload.make_batch(eng, 0, n, 300, seed=11, stream=streams[0].cuda_stream)
     torch.cuda.synchronize(dev)
     bm = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
@@ -57,7 +58,7 @@ def main():
         t = time.perf_counter()
         for call in range(a.calls):
             for j in range(len(c) - 1):
-                verify(c[j], c[j + 1], streams[k % 2])
+                verify(c[j], c[j + 1], streams[k % len(streams)])
                 k += 1
             if sync_each:
                 torch.cuda.synchronize(dev)
@@ -77,6 +78,7 @@ def main():
             for sync_each in (True, False):
                 ms, parts = run(S, sync_each)
                 print(json.dumps({"round": rnd, "form": "whole" if not S else f"sub {S}", "first": a.first or S,
+                                  "streams": len(streams),
                                   "subchunks": parts, "sync_each_call": sync_each, "ms_per_call": round(ms, 3)}),
                       flush=True)
         if a.host:
