@@ -163,7 +163,7 @@ struct Slot {
     DevBuf head;                  // its device copy
 };
 constexpr int kSlots = 4;
-constexpr int kPipeSlots = 3;   // most compute slots a pipelined call deals its sub-chunks over (PipeFrame::ns)
+constexpr int kPipeSlots = 4;   // most compute slots a pipelined call deals its sub-chunks over (PipeFrame::ns)
 // input blocks of the host pipeline on the device: copies run up to kRing sub-chunks ahead of the kernels, so
 // a call's copies are all queued early and a Merkle call submitted behind a verify call copies its leaves
 // while that verify's kernels run (round 4: with 6 blocks the verify's copies were paced by its kernels and
@@ -454,7 +454,7 @@ static const OptDesc kOpt[CV_OPT_COUNT] = {
     {16, 1, 1024},                      // CV_OPT_PIPE_SPLIT
     {0, 0, 1},                          // CV_OPT_PIPE_OVERLAP_FIRST
     {1, 1, 16},                         // CV_OPT_MID_PIECES
-    {2, 2, 3},                          // CV_OPT_PIPE_SLOTS
+    {2, 2, 4},                          // CV_OPT_PIPE_SLOTS
     {2, 0, 2},                          // CV_OPT_TXS_MERKLE_STREAM
 };
 

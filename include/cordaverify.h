@@ -333,7 +333,7 @@ int cv_calibrate_cycles(cv_ctx *ctx, int device, double *out);
                                        the packing of the next (1 = one DMA per part, the default: measured neutral to
                                        slower at 65,536) */
 #define CV_OPT_PIPE_SLOTS 21        /* compute streams (workspace slots) a pipelined verify call deals its sub-chunks over
-                                       (2; 3 allowed) */
+                                       (2; 3 or 4 allowed) */
 #define CV_OPT_TXS_MERKLE_STREAM 22 /* cv_verify_transactions: the stream its Merkle groups run on — 0 the compute streams
                                        beside the signature groups, 1 the copy stream behind their leaves, 2 a stream
                                        of their own (default) */

@@ -97,13 +97,13 @@ def test_host_pipeline_sync_subchunk_plan_exact(engine, n):
 
 @pytest.mark.parametrize("first,chunk,overlap,slots", [(64, 64 * 17, 1, 2), (64 * 5, 64 * 3, 1, 2), (1024, 4096, 1, 2),
                                                        (1024, 4096, 0, 2), (8192, 8192, 1, 2), (64 * 5, 64 * 3, 1, 3),
-                                                       (1024, 4096, 1, 3)])
+                                                       (1024, 4096, 1, 3), (64 * 5, 64 * 3, 1, 4), (1024, 4096, 0, 4)])
 def test_host_pipeline_small_subchunks_golden(engine, corpus, first, chunk, overlap, slots):
     """The pipeline forced onto tiny sub-chunks (first / steady sizes, so one batch has hundreds of
     them, in every kernel form from tri-chain to throughput) over the golden corpus tiled to a ragged
     9,001 records in random order: every verdict and status byte equals the pinned corpus values; with and
-    without the first sub-chunk's keys-first prep overlap (CV_OPT_PIPE_OVERLAP_FIRST), over two and three compute
-    streams (CV_OPT_PIPE_SLOTS)."""
+    without the first sub-chunk's keys-first prep overlap (CV_OPT_PIPE_OVERLAP_FIRST), over two, three and four
+    compute streams (CV_OPT_PIPE_SLOTS)."""
     rng = np.random.default_rng(first + chunk)
     n = 9001
     sel = rng.integers(0, len(corpus["pk"]), n)
