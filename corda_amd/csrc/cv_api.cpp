@@ -1362,10 +1362,24 @@ struct FlatKeys {
 // Poisson tails far below 10^-6 either way.  Round 4 sampled 4,096 records at every size above 16,384 and deduped
 // every batch up to 16,384 in full: 60-100 us of host time on each distinct-keyed notary batch of 16,384-65,536
 // signatures (tools/notary_probe.py host phases), for a decision that only picks the faster path.
+// LSD radix sort of values below `bound` (passes of 11 bits up to bound's top bit): the gate's 4,096 sample
+// positions, which std::sort took ~300 us to order on this container's host (radix: 60 us for three passes) —
+// on every large call's path before its first DMA
+static void radix_sort_u32(std::vector<uint32_t> &v, uint64_t bound) {
+    std::vector<uint32_t> tmp(v.size());
+    for (int sh = 0; sh < 32 && (bound - 1) >> sh; sh += 11) {
+        uint32_t cnt[2049] = {};
+        for (uint32_t x : v) cnt[((x >> sh) & 2047) + 1]++;
+        for (int k = 0; k < 2048; k++) cnt[k + 1] += cnt[k];
+        for (uint32_t x : v) tmp[cnt[(x >> sh) & 2047]++] = x;
+        v.swap(tmp);
+    }
+}
+
 static bool dedupe_gate(size_t n, const uint8_t *pk) {
     if (n <= 4096) return true;                    // the estimate needs s << n; a full dedupe of <= 4,096 is cheap
     const uint32_t kS = (uint32_t)std::min<double>(4096.0, std::max(512.0, 4.0 * std::sqrt((double)n)));
-    FlatKeys t(2 * kS);
+    FlatKeys t(4 * kS);                            // load <= 1/4: the table never grows while sampling
     uint64_t x = 0x9E3779B97F4A7C15ull;
     uint32_t rep = 0;
     std::vector<uint32_t> pos(kS);
@@ -1373,9 +1387,12 @@ static bool dedupe_gate(size_t n, const uint8_t *pk) {
         x = x * 6364136223846793005ull + 1442695040888963407ull;
         pos[j] = (uint32_t)((x >> 32) * (uint64_t)n >> 32);
     }
-    std::sort(pos.begin(), pos.end());             // ascending positions: friendlier to the caches
+    radix_sort_u32(pos, n);                        // ascending: duplicate positions adjacent
+    constexpr uint32_t kAhead = 16;                // the key reads miss the caches: prefetched 16 samples ahead
+    for (uint32_t j = 0; j < std::min(kS, kAhead); j++) __builtin_prefetch(pk + 32 * (size_t)pos[j]);
     uint32_t prev = UINT32_MAX;
     for (uint32_t j = 0; j < kS; j++) {
+        if (j + kAhead < kS) __builtin_prefetch(pk + 32 * (size_t)pos[j + kAhead]);
         if (pos[j] == prev) continue;               // the same record twice is not a repeated key
         prev = pos[j];
         bool added;
